@@ -1,0 +1,101 @@
+"""ctypes binding of the C-ABI library ``libcmx_hip.so``.
+
+The argument/return types are derived by parsing ``include/cmx_hip.h`` (shipped inside
+the package as ``cmx_hip.h``), so the header is the single source of truth for the ABI.
+
+The library is loaded AFTER ``import torch`` so that its ``libamdhip64.so.7`` dependency
+resolves (by SONAME) to the HIP runtime torch already loaded: kernels then run on torch's
+streams and are captured by torch's HIP graphs.  There is no fallback: if the library is
+missing or fails to load, importing the product raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcmx_hip.so")
+HEADER_PATHS = [os.path.join(_HERE, "..", "include", "cmx_hip.h"), os.path.join(_HERE, "cmx_hip.h")]
+
+
+class CMXError(RuntimeError):
+    pass
+
+
+def _ctype(decl: str):
+    decl = decl.strip()
+    if "*" in decl:
+        if decl.startswith("const char") and decl.count("*") == 1 and not decl.split("*")[1].strip():
+            return ctypes.c_char_p
+        return ctypes.c_void_p
+    base = decl.rsplit(" ", 1)[0] if " " in decl else decl
+    base = base.replace("const", "").strip()
+    return {"int": ctypes.c_int32, "int64_t": ctypes.c_int64, "float": ctypes.c_float,
+            "size_t": ctypes.c_size_t, "hipStream_t": ctypes.c_void_p, "void": None}[base]
+
+
+def parse_header(path: str | None = None):
+    """Return {name: (restype, [argtypes])} for every declaration in cmx_hip.h."""
+    if path is None:
+        path = next(p for p in HEADER_PATHS if os.path.exists(p))
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    out = {}
+    for m in re.finditer(r"^\s*([A-Za-z_][\w\s\*]*?)\b(cmx_\w+)\s*\(([^)]*)\)\s*;", text, re.M):
+        ret, name, args = m.group(1), m.group(2), m.group(3).strip()
+        rt = _ctype(ret.strip() + " r") if "*" not in ret else _ctype(ret.strip() + " r")
+        if ret.strip() == "const char*":
+            rt = ctypes.c_char_p
+        argt = [] if args in ("", "void") else [_ctype(a) for a in args.split(",")]
+        out[name] = (rt, argt)
+    return out
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise CMXError(f"libcmx_hip.so not found at {LIB_PATH}; run __graft_entry__.build() "
+                       "(or `make -C rgbx_semantic_segmentation_amd/csrc`).  There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    sigs = parse_header()
+    for name, (rt, argt) in sigs.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argt
+        fn.restype = rt
+    return lib, sigs
+
+
+LIB, SIGNATURES = _load()
+
+
+def last_error() -> str:
+    return LIB.cmx_last_error().decode()
+
+
+def call(name: str, *args) -> None:
+    """Invoke an int-returning entry point; raise CMXError on a negative status."""
+    st = getattr(LIB, name)(*args)
+    if st != 0:
+        raise CMXError(f"{name} failed ({st}): {last_error()}")
+
+
+def query(name: str, *args) -> int:
+    return int(getattr(LIB, name)(*args))
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return 0
+    if t.dtype == torch.bfloat16:
+        return 1
+    raise CMXError(f"unsupported dtype {t.dtype}")

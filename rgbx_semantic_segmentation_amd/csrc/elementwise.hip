@@ -1,0 +1,198 @@
+// Vectorised elementwise + column-reduction kernels (HBM-bound; 16 B per lane per access).
+//
+//  * residual add with per-sample DropPath scale  (Block.forward, dual_segformer.py:176-180:
+//    x + drop_path(f(x)), timm DropPath = per-sample keep/keep_prob scaling)
+//  * activations (ReLU of CrossPath.channel_proj*, net_utils.py:273-274)
+//  * column sums for bias gradients of every Linear / 1x1 conv on the path
+//  * fp32 -> bf16 cast for weight shadows
+#include "cmx_common.h"
+
+template <typename T>
+__global__ void residual_add_kernel(const T* __restrict__ x, const T* __restrict__ y,
+                                    const float* __restrict__ scale, T* out, long n_per_sample,
+                                    long nvec) {
+  constexpr int V = VecT<T>::N;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
+    const long e = i * V;
+    const float s = scale ? scale[e / n_per_sample] : 1.f;
+    float a[V], b[V];
+    load_vec<T>(x + e, a);
+    load_vec<T>(y + e, b);
+#pragma unroll
+    for (int j = 0; j < V; ++j) a[j] += s * b[j];
+    store_vec<T>(out + e, a);
+  }
+}
+
+template <typename T>
+__global__ void scale_samples_kernel(const T* __restrict__ x, const float* __restrict__ scale, T* out,
+                                     long n_per_sample, long nvec) {
+  constexpr int V = VecT<T>::N;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
+    const long e = i * V;
+    const float s = scale[e / n_per_sample];
+    float a[V];
+    load_vec<T>(x + e, a);
+#pragma unroll
+    for (int j = 0; j < V; ++j) a[j] *= s;
+    store_vec<T>(out + e, a);
+  }
+}
+
+template <typename T>
+__global__ void act_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, long nvec, int act) {
+  constexpr int V = VecT<T>::N;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
+    float a[V];
+    load_vec<T>(x + i * V, a);
+#pragma unroll
+    for (int j = 0; j < V; ++j) a[j] = act_fwd(a[j], act);
+    store_vec<T>(y + i * V, a);
+  }
+}
+
+// dx = dy * act'(z); for ReLU, z may be the post-activation output (same sign pattern).
+template <typename T>
+__global__ void act_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ z, T* __restrict__ dx,
+                               long nvec, int act) {
+  constexpr int V = VecT<T>::N;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
+    float a[V], b[V];
+    load_vec<T>(dy + i * V, a);
+    load_vec<T>(z + i * V, b);
+#pragma unroll
+    for (int j = 0; j < V; ++j) a[j] *= act_grad(b[j], act);
+    store_vec<T>(dx + i * V, a);
+  }
+}
+
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ src, bf16* __restrict__ dst, long n) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    dst[i] = from_f32<bf16>(src[i]);
+}
+
+// Column sums of x (G, M, N) -> ws partials (G, nblk, N).  TPR lanes span a column tile of
+// TPR*V columns (blockIdx.z), 256/TPR row slots stride over rows.
+template <typename T, int TPR>
+__global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x, float* __restrict__ ws,
+                                                     long M, int N, long ld) {
+  constexpr int V = VecT<T>::N;
+  constexpr int RS = 256 / TPR;
+  __shared__ float red[RS][TPR * V];
+  const int g = blockIdx.y;
+  const int lane = threadIdx.x % TPR, slot = threadIdx.x / TPR;
+  const int col = (blockIdx.z * TPR + lane) * V;
+  float acc[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) acc[j] = 0.f;
+  if (col < N) {
+    const T* base = x + (long)g * M * ld + col;
+    for (long m = (long)blockIdx.x * RS + slot; m < M; m += (long)gridDim.x * RS) {
+      float v[V];
+      load_vec<T>(base + m * ld, v);
+#pragma unroll
+      for (int j = 0; j < V; ++j) acc[j] += v[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < V; ++j) red[slot][lane * V + j] = acc[j];
+  __syncthreads();
+  for (int c = threadIdx.x; c < TPR * V; c += 256) {
+    float s = 0.f;
+    for (int r = 0; r < RS; ++r) s += red[r][c];
+    const int gc = blockIdx.z * TPR * V + c;
+    if (gc < N) ws[((long)g * gridDim.x + blockIdx.x) * N + gc] = s;
+  }
+}
+
+static unsigned ew_grid(long nvec) {
+  long b = (nvec + 255) / 256;
+  return (unsigned)(b < 8192 ? (b > 0 ? b : 1) : 8192);
+}
+
+static int colsum_nblk(long M) {
+  long nb = (M + 63) / 64;
+  return (int)(nb < 256 ? nb : 256);
+}
+
+extern "C" {
+
+int cmx_residual_add(const void* x, const void* y, const float* scale, void* out, long n_per_sample,
+                     long n, int dtype, hipStream_t s) {
+  const int V = dtype == 0 ? 4 : 8;
+  CMX_REQUIRE(n % V == 0 && (!scale || n_per_sample % V == 0), CMX_ERR_SHAPE,
+              "residual_add: sizes must be multiples of %d", V);
+  if (n == 0) return CMX_OK;
+  CMX_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL(residual_add_kernel<T>, dim3(ew_grid(n / V)), dim3(256), 0, s, (const T*)x,
+                       (const T*)y, scale, (T*)out, n_per_sample, n / V);
+  });
+  return cmx_check_launch("residual_add");
+}
+
+int cmx_scale_samples(const void* x, const float* scale, void* out, long n_per_sample, long n, int dtype,
+                      hipStream_t s) {
+  const int V = dtype == 0 ? 4 : 8;
+  CMX_REQUIRE(n % V == 0 && n_per_sample % V == 0, CMX_ERR_SHAPE, "scale_samples: sizes");
+  if (n == 0) return CMX_OK;
+  CMX_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL(scale_samples_kernel<T>, dim3(ew_grid(n / V)), dim3(256), 0, s, (const T*)x,
+                       scale, (T*)out, n_per_sample, n / V);
+  });
+  return cmx_check_launch("scale_samples");
+}
+
+int cmx_act_fwd(const void* x, void* y, long n, int act, int dtype, hipStream_t s) {
+  const int V = dtype == 0 ? 4 : 8;
+  CMX_REQUIRE(n % V == 0, CMX_ERR_SHAPE, "act_fwd: n %% %d", V);
+  if (n == 0) return CMX_OK;
+  CMX_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL(act_fwd_kernel<T>, dim3(ew_grid(n / V)), dim3(256), 0, s, (const T*)x, (T*)y,
+                       n / V, act);
+  });
+  return cmx_check_launch("act_fwd");
+}
+
+int cmx_act_bwd(const void* dy, const void* z, void* dx, long n, int act, int dtype, hipStream_t s) {
+  const int V = dtype == 0 ? 4 : 8;
+  CMX_REQUIRE(n % V == 0, CMX_ERR_SHAPE, "act_bwd: n %% %d", V);
+  if (n == 0) return CMX_OK;
+  CMX_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL(act_bwd_kernel<T>, dim3(ew_grid(n / V)), dim3(256), 0, s, (const T*)dy,
+                       (const T*)z, (T*)dx, n / V, act);
+  });
+  return cmx_check_launch("act_bwd");
+}
+
+int cmx_cast_f32_bf16(const float* src, void* dst, long n, hipStream_t s) {
+  if (n == 0) return CMX_OK;
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(ew_grid(n)), dim3(256), 0, s, src, (bf16*)dst, n);
+  return cmx_check_launch("cast_f32_bf16");
+}
+
+size_t cmx_colsum_workspace(long M, int G, int N) {
+  return (size_t)G * colsum_nblk(M) * N * sizeof(float);
+}
+
+// out[g, n] (+)= alpha * sum_m x[g, m, n]; x rows have leading dimension ld (elements).
+int cmx_colsum(const void* x, float* out, float* ws, long M, int G, int N, long ld, int accumulate,
+               float alpha, int dtype, hipStream_t s) {
+  const int V = dtype == 0 ? 4 : 8;
+  CMX_REQUIRE(N % V == 0 && ld % V == 0 && M > 0, CMX_ERR_SHAPE, "colsum: N=%d ld=%ld", N, ld);
+  const int nb = colsum_nblk(M);
+  const int chunks = N / V;
+  CMX_DISPATCH(dtype, T, {
+    if (chunks <= 16) {
+      hipLaunchKernelGGL((colsum_kernel<T, 16>), dim3(nb, G, 1), dim3(256), 0, s, (const T*)x, ws, M,
+                         N, ld);
+    } else {
+      hipLaunchKernelGGL((colsum_kernel<T, 64>), dim3(nb, G, cdiv(chunks, 64)), dim3(256), 0, s,
+                         (const T*)x, ws, M, N, ld);
+    }
+  });
+  int st = cmx_check_launch("colsum");
+  if (st) return st;
+  return cmx_reduce_partials(ws, out, G, nb, N, accumulate, alpha, s);
+}
+
+}  // extern "C"

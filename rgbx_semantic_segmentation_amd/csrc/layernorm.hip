@@ -1,0 +1,281 @@
+// LayerNorm over the channel dim of token-major activations (G groups of R rows x C).
+//
+// Replaces nn.LayerNorm at: Block.norm1/norm2 + stage norms (eps 1e-6,
+// dual_segformer.py:148,155,257...), OverlapPatchEmbed.norm / Attention.norm (eps 1e-5,
+// :198,:97), CrossPath.norm1/2 (eps 1e-5, net_utils.py:270-271).  Group g has its own
+// gamma/beta (the RGB and X streams are processed in one launch).
+//
+// Layout: a row is C contiguous elements; TPR lanes own one row, each lane NCH chunks
+// of one 16-byte vector.  HBM-bound: fwd reads x once and writes y once (+8 B/row stats).
+#include "cmx_common.h"
+
+template <typename T, int TPR, int NCH>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x,
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta,
+                                                     T* __restrict__ y, float* __restrict__ mean_out,
+                                                     float* __restrict__ rstd_out, long R, int C,
+                                                     float eps) {
+  constexpr int V = VecT<T>::N;
+  constexpr int RPB = 256 / TPR;
+  const int g = blockIdx.y;
+  const int lane = threadIdx.x % TPR;
+  const long row = (long)blockIdx.x * RPB + threadIdx.x / TPR;
+  const bool live = row < R;
+  const long grow = (long)g * R + row;
+  const int nchunk = C / V;
+  float v[NCH][V];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int ch = lane + k * TPR;
+    if (live && ch < nchunk) {
+      load_vec<T>(x + grow * C + ch * V, v[k]);
+#pragma unroll
+      for (int j = 0; j < V; ++j) s += v[k][j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < V; ++j) v[k][j] = 0.f;
+    }
+  }
+  s = group_sum(s, TPR);
+  const float mu = s / C;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int ch = lane + k * TPR;
+    if (live && ch < nchunk) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) { float d = v[k][j] - mu; q += d * d; }
+    }
+  }
+  q = group_sum(q, TPR);
+  const float rstd = rsqrtf(q / C + eps);
+  if (!live) return;
+  const float* gg = gamma + (long)g * C;
+  const float* bb = beta + (long)g * C;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int ch = lane + k * TPR;
+    if (ch < nchunk) {
+      float o[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int c = ch * V + j;
+        o[j] = (v[k][j] - mu) * rstd * gg[c] + bb[c];
+      }
+      store_vec<T>(y + grow * C + ch * V, o);
+    }
+  }
+  if (lane == 0) {
+    if (mean_out) mean_out[grow] = mu;
+    if (rstd_out) rstd_out[grow] = rstd;
+  }
+}
+
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma.
+// Per-block partial column sums of dy*xhat (dgamma) and dy (dbeta) go to ws.
+template <typename T, int TPR, int NCH>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd,
+                                                     T* __restrict__ dx, float* __restrict__ ws,
+                                                     long R, int C) {
+  constexpr int V = VecT<T>::N;
+  constexpr int RPB = 256 / TPR;
+  __shared__ float red[256 / TPR][2][NCH * TPR * V > 512 ? 512 : NCH * TPR * V];
+  const int g = blockIdx.y;
+  const int lane = threadIdx.x % TPR;
+  const int rslot = threadIdx.x / TPR;
+  const int nchunk = C / V;
+  const float* gg = gamma + (long)g * C;
+  float dg[NCH][V], db[NCH][V];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k)
+#pragma unroll
+    for (int j = 0; j < V; ++j) dg[k][j] = db[k][j] = 0.f;
+
+  for (long row = (long)blockIdx.x * RPB + rslot; row < R; row += (long)gridDim.x * RPB) {
+    const long grow = (long)g * R + row;
+    const float mu = mean[grow], rs = rstd[grow];
+    float xv[NCH][V], gv[NCH][V];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch < nchunk) {
+        float dv[V];
+        load_vec<T>(x + grow * C + ch * V, xv[k]);
+        load_vec<T>(dy + grow * C + ch * V, dv);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const float xh = (xv[k][j] - mu) * rs;
+          xv[k][j] = xh;
+          gv[k][j] = dv[j] * gg[ch * V + j];
+          s1 += gv[k][j];
+          s2 += gv[k][j] * xh;
+          dg[k][j] += dv[j] * xh;
+          db[k][j] += dv[j];
+        }
+      }
+    }
+    s1 = group_sum(s1, TPR) / C;
+    s2 = group_sum(s2, TPR) / C;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch < nchunk) {
+        float o[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) o[j] = rs * (gv[k][j] - s1 - xv[k][j] * s2);
+        store_vec<T>(dx + grow * C + ch * V, o);
+      }
+    }
+  }
+  // block reduction of the column partials over the RPB row slots
+  float* out = ws + ((long)g * gridDim.x + blockIdx.x) * 2 * C;
+  for (int base = 0; base < C; base += 512) {
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int ch = lane + k * TPR;
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int c = ch * V + j - base;
+        if (ch < nchunk && c >= 0 && c < 512) {
+          red[rslot][0][c] = dg[k][j];
+          red[rslot][1][c] = db[k][j];
+        }
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < 512 && base + c < C; c += 256) {
+      float a = 0.f, b = 0.f;
+      for (int r = 0; r < RPB; ++r) { a += red[r][0][c]; b += red[r][1][c]; }
+      out[base + c] = a;
+      out[C + base + c] = b;
+    }
+    __syncthreads();
+  }
+}
+
+// out[g, w] (+)= sum_b ws[g, b, w]; used for every two-stage column reduction.
+// ws is (G, nblk, stride); columns [0, W) are reduced into out (G, W).
+__global__ void reduce_partials_kernel(const float* __restrict__ ws, float* __restrict__ out,
+                                       int nblk, int W, int stride, int accumulate, float alpha) {
+  const int g = blockIdx.y;
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= W) return;
+  float s = 0.f;
+  const float* p = ws + (long)g * nblk * stride + w;
+  for (int b = 0; b < nblk; ++b) s += p[(long)b * stride];
+  s *= alpha;
+  float* o = out + (long)g * W + w;
+  *o = accumulate ? *o + s : s;
+}
+
+int cmx_reduce_partials(const float* ws, float* out, int G, int nblk, int W, int accumulate,
+                        float alpha, hipStream_t s) {
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(cdiv(W, 256), G), dim3(256), 0, s, ws, out, nblk,
+                     W, W, accumulate, alpha);
+  return cmx_check_launch("reduce_partials");
+}
+
+static int ln_tpr(int chunks) {
+  int t = 1;
+  while (t < chunks && t < 64) t <<= 1;
+  return t < 4 ? 4 : t;
+}
+
+template <typename T>
+static int ln_fwd_launch(const void* x, const float* g, const float* b, void* y, float* mu, float* rs,
+                         long R, int G, int C, float eps, hipStream_t s) {
+  constexpr int V = VecT<T>::N;
+  const int chunks = C / V;
+  const int tpr = ln_tpr(chunks);
+  const int nch = (chunks + tpr - 1) / tpr;
+  const dim3 grid(cdiv(R, 256 / tpr), G);
+#define LNF(TPR, NCH)                                                                      \
+  if (tpr == TPR && nch == NCH) {                                                          \
+    hipLaunchKernelGGL((ln_fwd_kernel<T, TPR, NCH>), grid, dim3(256), 0, s, (const T*)x, g, b, \
+                       (T*)y, mu, rs, R, C, eps);                                          \
+    return cmx_check_launch("layernorm_fwd");                                              \
+  }
+  LNF(4, 1) LNF(8, 1) LNF(16, 1) LNF(32, 1) LNF(64, 1) LNF(64, 2) LNF(64, 4)
+#undef LNF
+  cmx_set_error("layernorm_fwd: unsupported C=%d", C);
+  return CMX_ERR_SHAPE;
+}
+
+static int ln_bwd_blocks(long R, int rpb) {
+  long nb = (R + rpb - 1) / rpb;
+  return (int)(nb < 128 ? nb : 128);
+}
+
+template <typename T>
+static int ln_bwd_launch(const void* dy, const void* x, const float* g, const float* mu,
+                         const float* rs, void* dx, float* dgamma, float* dbeta, float* ws, long R,
+                         int G, int C, int accumulate, hipStream_t s) {
+  constexpr int V = VecT<T>::N;
+  const int chunks = C / V;
+  const int tpr = ln_tpr(chunks);
+  const int nch = (chunks + tpr - 1) / tpr;
+  const int nb = ln_bwd_blocks(R, 256 / tpr);
+  const dim3 grid(nb, G);
+#define LNB(TPR, NCH)                                                                       \
+  if (tpr == TPR && nch == NCH) {                                                           \
+    hipLaunchKernelGGL((ln_bwd_kernel<T, TPR, NCH>), grid, dim3(256), 0, s, (const T*)dy,    \
+                       (const T*)x, g, mu, rs, (T*)dx, ws, R, C);                            \
+    goto reduce;                                                                            \
+  }
+  LNB(4, 1) LNB(8, 1) LNB(16, 1) LNB(32, 1) LNB(64, 1) LNB(64, 2) LNB(64, 4)
+#undef LNB
+  cmx_set_error("layernorm_bwd: unsupported C=%d", C);
+  return CMX_ERR_SHAPE;
+reduce : {
+  int st = cmx_check_launch("layernorm_bwd");
+  if (st) return st;
+  // ws layout per (g, blk): [dgamma C | dbeta C]; reduce into interleaved temp then split.
+  // dgamma and dbeta are separate (G, C) arrays: reduce each half.
+  for (int half = 0; half < 2; ++half) {
+    float* dst = half == 0 ? dgamma : dbeta;
+    if (!dst) continue;
+    // treat ws as (G, nb, 2C) and reduce columns [half*C, half*C + C)
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3(cdiv(C, 256), G), dim3(256), 0, s, ws + half * C,
+                       dst, nb, C, 2 * C, accumulate, 1.0f);
+  }
+  return CMX_OK;
+}
+}
+
+extern "C" {
+
+// y = LN(x) over C; x, y: (G*R, C) of dtype; gamma/beta: (G, C) fp32; mean/rstd: (G*R) fp32
+// (may be NULL).  Replaces nn.LayerNorm.forward (see header).
+int cmx_layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y, float* mean,
+                      float* rstd, long R, int G, int C, float eps, int dtype, hipStream_t s) {
+  CMX_REQUIRE(R >= 0 && G > 0 && C > 0, CMX_ERR_SHAPE, "layernorm_fwd: bad shape");
+  CMX_REQUIRE(C % (dtype == 0 ? 4 : 8) == 0 && C <= 1024, CMX_ERR_SHAPE,
+              "layernorm_fwd: C=%d must be a multiple of the vector width and <= 1024", C);
+  if (R == 0) return CMX_OK;
+  CMX_DISPATCH(dtype, T, return ln_fwd_launch<T>(x, gamma, beta, y, mean, rstd, R, G, C, eps, s));
+}
+
+size_t cmx_layernorm_bwd_workspace(long R, int G, int C, int dtype) {
+  const int V = dtype == 0 ? 4 : 8;
+  const int tpr = ln_tpr(C / V);
+  return (size_t)G * ln_bwd_blocks(R, 256 / tpr) * 2 * C * sizeof(float);
+}
+
+// dx (dtype), dgamma/dbeta (G, C) fp32 (overwritten, or accumulated if accumulate=1).
+int cmx_layernorm_bwd(const void* dy, const void* x, const float* gamma, const float* mean,
+                      const float* rstd, void* dx, float* dgamma, float* dbeta, float* workspace,
+                      long R, int G, int C, int accumulate, int dtype, hipStream_t s) {
+  CMX_REQUIRE(R > 0 && G > 0 && C > 0 && C <= 1024, CMX_ERR_SHAPE, "layernorm_bwd: bad shape");
+  CMX_REQUIRE(C % (dtype == 0 ? 4 : 8) == 0, CMX_ERR_SHAPE, "layernorm_bwd: C=%d", C);
+  CMX_DISPATCH(dtype, T,
+               return ln_bwd_launch<T>(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, workspace, R,
+                                       G, C, accumulate, s));
+}
+
+}  // extern "C"
