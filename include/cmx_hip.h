@@ -57,6 +57,63 @@ int cmx_sra_attn_fwd(const void* q, const void* k, const void* v, void* o, float
 size_t cmx_sra_attn_bwd_workspace(int Bt, int N, int Nk, int heads, int D);
 int cmx_sra_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse, void* dq, void* dk, void* dv, float* workspace, int Bt, int N, int Nk, int heads, int D, int64_t qs, int64_t kvs, int64_t os, int64_t dos, int64_t dqs, int64_t dkvs, float scale, int dtype, hipStream_t stream);
 
+/* ---- depthwise 3x3 + bias + act: Mix-FFN DWConv + GELU (dual_segformer.py:27-33,67-71) and
+ *      ChannelEmbed DW3x3 + ReLU (net_utils.py:315-318).  h,out: (NI, H, W, C) NHWC,
+ *      image n in group n / imgs_per_group; w (G, C, 9), b (G, C) fp32; act 0/1 gelu/2 relu. */
+int cmx_dwconv3x3_fwd(const void* h, const float* w, const float* b, void* out, int NI, int imgs_per_group, int H, int W, int C, int act, int dtype, hipStream_t stream);
+size_t cmx_dwconv3x3_bwd_workspace(int NI, int imgs_per_group, int H, int W, int C);
+int cmx_dwconv3x3_bwd(const void* da, const void* h, const float* w, const float* b, void* dz, void* dh, float* dw, float* db, float* workspace, int NI, int imgs_per_group, int H, int W, int C, int act, int accumulate, int dtype, hipStream_t stream);
+
+/* ---- conv as im2col + GEMM: OverlapPatchEmbed.proj (dual_segformer.py:196-197) and the SRA
+ *      spatial-reduction conv Attention.sr (:95-96).  NHWC cols use (kh, kw, c) order (weights
+ *      stored (Cout, kh, kw, Cin)); the NCHW variant takes the fp32 input image. */
+int cmx_im2col_nhwc(const void* x, void* cols, int NI, int H, int W, int C, int KH, int KW, int stride, int pad, int Ho, int Wo, int64_t ldc, int dtype, hipStream_t stream);
+int cmx_im2col_nchw_f32(const float* x, void* cols, int NI, int C, int H, int W, int KH, int KW, int stride, int pad, int Ho, int Wo, int64_t ldc, int dtype, hipStream_t stream);
+int cmx_col2im_nhwc(const void* cols, void* dx, int NI, int H, int W, int C, int KH, int KW, int stride, int pad, int Ho, int Wo, int64_t ldc, int dtype, hipStream_t stream);
+
+/* ---- FFM cross attention (CrossAttention.forward, net_utils.py:199-214):
+ *      ctx = softmax_{-2}(k^T v * scale) per (g, b, head); out_1 = q_1 ctx_2, out_2 = q_2 ctx_1.
+ *      ctx_reduce mode 0: alpha*X^T Y, 1: softmax_{-2}(alpha*X^T Y), 2: softmax backward. */
+size_t cmx_ffm_ctx_workspace(int BH, int N, int D);
+int cmx_ffm_ctx_reduce(const void* X, const void* Y, const float* ctx, float* out, float* workspace, int Bt, int N, int heads, int D, int64_t xs, int64_t ys, int mode, float alpha, int swapB, int dtype, hipStream_t stream);
+int cmx_ffm_rowmat(const void* X, const float* M, void* out, int Bt, int N, int heads, int D, int64_t xs, int64_t os, int trans, float alpha, int accumulate, int swapB, int dtype, hipStream_t stream);
+
+/* ---- CM-FRM (FeatureRectifyModule, net_utils.py:124-152): ChannelWeights pooling (:22-27)
+ *      + tiny-M MLP (:16-20), SpatialWeights 1x1 C->2 + sigmoid (:74-83), rectification. */
+size_t cmx_frm_pool_workspace(int B, int N, int C);
+int cmx_frm_pool_fwd(const void* x, float* pooled, int* argmax, float* workspace, int B, int N, int C, int dtype, hipStream_t stream);
+int cmx_frm_pool_bwd(const float* dpooled, const int* argmax, void* dx, int B, int N, int C, int dtype, hipStream_t stream);
+int cmx_small_linear_fwd(const float* x, const float* w, const float* b, float* y, int M, int K, int Nout, int act, hipStream_t stream);
+int cmx_small_linear_bwd(const float* dy, const float* y, const float* x, const float* w, float* dx, float* dw, float* db, float* dz_ws, int M, int K, int Nout, int act, int accumulate, hipStream_t stream);
+int cmx_frm_spatial_fwd(const void* h, const float* w2, const float* b2, float* sw, int64_t rows, int C, int dtype, hipStream_t stream);
+size_t cmx_frm_spatial_bwd_workspace(int64_t rows, int C);
+int cmx_frm_spatial_bwd(const float* dsw, const float* sw, const void* h, const float* w2, void* dh, float* dw2, float* db2, float* workspace, int64_t rows, int C, int accumulate, int dtype, hipStream_t stream);
+int cmx_frm_combine_fwd(const void* x, const float* cw, const float* sw, void* out, int B, int N, int C, int dtype, hipStream_t stream);
+size_t cmx_frm_combine_bwd_workspace(int B, int N, int C);
+int cmx_frm_combine_bwd(const void* dout, const void* x, const float* cw, const float* sw, void* dx, float* dsw, float* dcw, float* workspace, int B, int N, int C, int dtype, hipStream_t stream);
+
+/* ---- BatchNorm (ChannelEmbed BNs net_utils.py:319-329, decoder SyncBN MLPDecoder.py:51-55):
+ *      fp64 channel sums -> (all-reduce for SyncBN) -> finalize; fused residual / act / Dropout2d. */
+size_t cmx_bn_workspace(int64_t M, int C);
+int cmx_bn_stats(const void* x, double* sums, double* workspace, int64_t M, int C, int dtype, hipStream_t stream);
+int cmx_bn_finalize(const double* sums, double count, float eps, float momentum, float* running_mean, float* running_var, float* mean, float* invstd, int C, int training, hipStream_t stream);
+int cmx_bn_apply(const void* x, const float* mean, const float* invstd, const float* gamma, const float* beta, const void* res, const float* dscale, void* y, int64_t M, int C, int64_t rows_per_sample, int act, int dtype, hipStream_t stream);
+int cmx_bn_bwd_reduce(const void* dy, const void* x, const float* mean, const float* invstd, const float* gamma, const float* beta, const void* res, const float* dscale, double* sums, float* dgamma, float* dbeta, double* workspace, int64_t M, int C, int64_t rows_per_sample, int act, int accumulate, int dtype, hipStream_t stream);
+int cmx_bn_bwd_apply(const void* dy, const void* x, const float* mean, const float* invstd, const float* gamma, const float* beta, const void* res, const float* dscale, const double* sums, double count, void* dx, void* dres, int64_t M, int C, int64_t rows_per_sample, int act, int training, int dtype, hipStream_t stream);
+
+/* ---- bilinear, align_corners=False (F.interpolate in MLPDecoder.py:67-73, builder.py:233)
+ *      and its separable 1-D adjoint (backward). */
+int cmx_bilinear_fwd_nhwc(const void* in, void* out, int NB, int Hi, int Wi, int Ho, int Wo, int C, int64_t out_pix_stride, int dtype, hipStream_t stream);
+int cmx_bilinear_fwd_nchw_f32(const void* in, float* out, int NB, int Hi, int Wi, int Ho, int Wo, int C, int dtype, hipStream_t stream);
+int cmx_bilinear_adjoint_1d(const void* in, void* out, int64_t P, int Lo, int Li, int Q, int64_t sp, int64_t so, const float* a1, const float* a2, float alpha0, int in_dtype, int out_dtype, hipStream_t stream);
+
+/* ---- fused final upsample + CrossEntropyLoss(mean, ignore_index=255) (builder.py:233,249). */
+size_t cmx_upsample_ce_workspace(int B, int H, int W);
+int cmx_upsample_ce_fwd(const void* logits, const int64_t* label, void* grad, float* out, float* workspace, int B, int h, int w, int H, int W, int K, int ignore_index, int dtype, hipStream_t stream);
+
+/* ---- fused AdamW over the flat parameter buffer (train.py:128-129, init_func.py:33-57). */
+int cmx_adamw_step(float* p, const float* g, float* m, float* v, void* shadow_bf16, const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, float beta1, float beta2, float eps, float weight_decay, float grad_scale, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -17,7 +17,7 @@ Numerics follow the reference op order in fp32 (or fp64 via ``.double()``):
     the contexts (``:211-212``).
 
 Stochastic layers take injectable masks so train-mode parity can be checked:
-``DropPath.mask`` (per-sample keep flags, shape (B,)) and ``Dropout2d.mask``
+``DropPath.masks`` (list of per-sample keep flags (B,), one per call) and ``Dropout2d.mask``
 (per-(B,C) keep flags).  With ``mask is None`` they draw from torch's RNG.
 
 Deviation (documented in DESIGN.md): decoder input channels come from the encoder's
@@ -112,19 +112,21 @@ def segformer_init(m: nn.Module):
 
 
 class DropPath(nn.Module):
-    """timm DropPath restated: x / keep * floor(keep + U) per sample."""
+    """timm DropPath restated: x / keep * floor(keep + U) per sample.  One module serves
+    both residual branches of a Block (two independent draws per forward,
+    dual_segformer.py:177-178), so injected masks are a list consumed in call order."""
 
     def __init__(self, p: float):
         super().__init__()
         self.p = p
-        self.mask: Optional[torch.Tensor] = None   # (B,) keep flags in {0,1}
+        self.masks: List[torch.Tensor] = []        # [(B,) keep flags in {0,1}] per call
 
     def forward(self, x):
         if self.p == 0.0 or not self.training:
             return x
         keep = 1.0 - self.p
-        if self.mask is not None:
-            m = self.mask.to(x.dtype)
+        if self.masks:
+            m = self.masks.pop(0).to(x.dtype)
         else:
             m = torch.floor(keep + torch.rand(x.shape[0], dtype=x.dtype))
         return x.div(keep) * m.view(-1, *([1] * (x.dim() - 1)))
@@ -350,11 +352,12 @@ class RGBXTransformer(nn.Module):                          # dual_segformer.py:2
         self.depths = depths
         dp = drop_path_table(depths, drop_path_rate)
         cins = [3] + embed_dims[:3]
-        for s in range(4):
-            k, st = (7, 4) if s == 0 else (3, 2)
-            for pre in ("", "extra_"):
+        for pre in ("", "extra_"):                    # registration order of :238-246
+            for s in range(4):
+                k, st = (7, 4) if s == 0 else (3, 2)
                 setattr(self, f"{pre}patch_embed{s + 1}",
                         OverlapPatchEmbed(k, st, cins[s], embed_dims[s]))
+        for s in range(4):
             for pre, probs in (("", dp[s][0]), ("extra_", dp[s][1])):
                 setattr(self, f"{pre}block{s + 1}", nn.ModuleList(
                     [Block(embed_dims[s], NUM_HEADS[s], SR_RATIOS[s], probs[i])

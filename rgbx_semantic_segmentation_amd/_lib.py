@@ -34,7 +34,7 @@ def _ctype(decl: str):
     base = decl.rsplit(" ", 1)[0] if " " in decl else decl
     base = base.replace("const", "").strip()
     return {"int": ctypes.c_int32, "int64_t": ctypes.c_int64, "float": ctypes.c_float,
-            "size_t": ctypes.c_size_t, "hipStream_t": ctypes.c_void_p, "void": None}[base]
+            "size_t": ctypes.c_size_t, "double": ctypes.c_double, "hipStream_t": ctypes.c_void_p, "void": None}[base]
 
 
 def parse_header(path: str | None = None):

@@ -1,0 +1,152 @@
+// Bilinear resampling, align_corners=False, with PyTorch's source-index rule
+//   src = max(0, (dst + 0.5) * in/out - 0.5); i0 = floor(src); i1 = min(i0 + 1, in - 1)
+// Replaces F.interpolate in DecoderHead (MLPDecoder.py:67-73: c2..c4 up to the 1/4 grid,
+// written straight into the channel slices of the 4*E concat buffer, no torch.cat) and the
+// final logits upsample of EncoderDecoder.encode_decode (builder.py:233).
+// The backward (adjoint) is separable: two 1-D gather passes (no atomics), the first along
+// x into an fp32 temp, the second along y, each output gathering the contiguous range of
+// destination indices whose stencil touches it.
+#include "cmx_common.h"
+
+namespace {
+
+__device__ __forceinline__ void src_index(int dst, float scale, int in, int& i0, int& i1, float& l0, float& l1) {
+  float s = (dst + 0.5f) * scale - 0.5f;
+  if (s < 0.f) s = 0.f;
+  i0 = (int)s;
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l1 = s - (float)i0;
+  l0 = 1.f - l1;
+}
+
+// in (NB, Hi, Wi, C) dense; out pixel p at out + ((n*Ho + y)*Wo + x)*ops + c
+template <typename T>
+__global__ void bilinear_fwd_nhwc_kernel(const T* __restrict__ in, T* __restrict__ out, int NB, int Hi, int Wi, int Ho,
+                                         int Wo, int C, long ops, float sh, float sw) {
+  constexpr int V = VecT<T>::N;
+  const int CPR = C / V;
+  const long total = (long)NB * Ho * Wo * CPR;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int ch = i % CPR;
+    const long pix = i / CPR;
+    const int x = pix % Wo;
+    const int y = (pix / Wo) % Ho;
+    const int n = pix / ((long)Wo * Ho);
+    int y0, y1, x0, x1;
+    float ly0, ly1, lx0, lx1;
+    src_index(y, sh, Hi, y0, y1, ly0, ly1);
+    src_index(x, sw, Wi, x0, x1, lx0, lx1);
+    const T* base = in + (long)n * Hi * Wi * C + ch * V;
+    float a[V], b[V], c[V], d[V], o[V];
+    load_vec<T>(base + ((long)y0 * Wi + x0) * C, a);
+    load_vec<T>(base + ((long)y0 * Wi + x1) * C, b);
+    load_vec<T>(base + ((long)y1 * Wi + x0) * C, c);
+    load_vec<T>(base + ((long)y1 * Wi + x1) * C, d);
+#pragma unroll
+    for (int j = 0; j < V; ++j) o[j] = ly0 * (lx0 * a[j] + lx1 * b[j]) + ly1 * (lx0 * c[j] + lx1 * d[j]);
+    store_vec<T>(out + pix * ops + ch * V, o);
+  }
+}
+
+// NHWC (dtype) -> NCHW fp32 (inference logits); thread per output element, x fastest
+template <typename T>
+__global__ void bilinear_fwd_nchw_kernel(const T* __restrict__ in, float* __restrict__ out, int NB, int Hi, int Wi,
+                                         int Ho, int Wo, int C, float sh, float sw) {
+  const long total = (long)NB * C * Ho * Wo;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int x = i % Wo;
+    const int y = (i / Wo) % Ho;
+    const int c = (i / ((long)Wo * Ho)) % C;
+    const int n = i / ((long)Wo * Ho * C);
+    int y0, y1, x0, x1;
+    float ly0, ly1, lx0, lx1;
+    src_index(y, sh, Hi, y0, y1, ly0, ly1);
+    src_index(x, sw, Wi, x0, x1, lx0, lx1);
+    const T* base = in + (long)n * Hi * Wi * C + c;
+    const float a = to_f32(base[((long)y0 * Wi + x0) * C]), b = to_f32(base[((long)y0 * Wi + x1) * C]);
+    const float cc = to_f32(base[((long)y1 * Wi + x0) * C]), d = to_f32(base[((long)y1 * Wi + x1) * C]);
+    out[i] = ly0 * (lx0 * a + lx1 * b) + ly1 * (lx0 * cc + lx1 * d);
+  }
+}
+
+// 1-D adjoint along one axis: in (P, Lo, Q) with strides (sp, so, 1) -> out (P, Li, Q) dense;
+// out[p][i][q] = alpha * sum_{o : i0(o)==i or i1(o)==i} w(o, i) * in[p][o][q]
+template <typename TI, typename TO>
+__global__ void bilinear_adj_kernel(const TI* __restrict__ in, TO* __restrict__ out, long P, int Lo, int Li, int Q,
+                                    long sp, long so, float scale, const float* __restrict__ a1,
+                                    const float* __restrict__ a2, float alpha0) {
+  const float alpha = alpha0 * (a1 ? *a1 : 1.f) * (a2 ? *a2 : 1.f);
+  const long total = P * Li * Q;
+  const float inv = 1.f / scale;  // out/in
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int q = e % Q;
+    const int i = (e / Q) % Li;
+    const long p = e / ((long)Q * Li);
+    int olo = (int)floorf((i - 1.5f) * inv) - 1;
+    int ohi = (int)ceilf((i + 1.5f) * inv) + 1;
+    if (olo < 0) olo = 0;
+    if (ohi > Lo - 1) ohi = Lo - 1;
+    float acc = 0.f;
+    for (int o = olo; o <= ohi; ++o) {
+      int i0, i1;
+      float l0, l1;
+      src_index(o, scale, Li, i0, i1, l0, l1);
+      float w = 0.f;
+      if (i0 == i) w += l0;
+      if (i1 == i) w += l1;
+      if (w != 0.f) acc += w * to_f32(in[p * sp + (long)o * so + q]);
+    }
+    out[e] = from_f32<TO>(alpha * acc);
+  }
+}
+
+unsigned gridcap(long total) {
+  const unsigned g = cdiv(total, 256);
+  return g < 16384 ? (g ? g : 1) : 16384;
+}
+}  // namespace
+
+extern "C" {
+
+int cmx_bilinear_fwd_nhwc(const void* in, void* out, int NB, int Hi, int Wi, int Ho, int Wo, int C, int64_t out_pix_stride,
+                          int dtype, hipStream_t s) {
+  const int V = dtype == 0 ? 4 : 8;
+  CMX_REQUIRE(C % V == 0 && out_pix_stride % V == 0, CMX_ERR_SHAPE, "bilinear_fwd_nhwc: C=%d", C);
+  const float sh = (float)Hi / Ho, sw = (float)Wi / Wo;
+  CMX_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL(bilinear_fwd_nhwc_kernel<T>, dim3(gridcap((long)NB * Ho * Wo * (C / V))), dim3(256), 0, s,
+                       (const T*)in, (T*)out, NB, Hi, Wi, Ho, Wo, C, (long)out_pix_stride, sh, sw);
+  });
+  return cmx_check_launch("bilinear_fwd_nhwc");
+}
+
+int cmx_bilinear_fwd_nchw_f32(const void* in, float* out, int NB, int Hi, int Wi, int Ho, int Wo, int C, int dtype,
+                              hipStream_t s) {
+  const float sh = (float)Hi / Ho, sw = (float)Wi / Wo;
+  CMX_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL(bilinear_fwd_nchw_kernel<T>, dim3(gridcap((long)NB * C * Ho * Wo)), dim3(256), 0, s,
+                       (const T*)in, out, NB, Hi, Wi, Ho, Wo, C, sh, sw);
+  });
+  return cmx_check_launch("bilinear_fwd_nchw");
+}
+
+// in/out dtypes independent (0 fp32, 1 bf16); alpha = alpha0 * (*a1) * (*a2) (NULL -> 1)
+int cmx_bilinear_adjoint_1d(const void* in, void* out, int64_t P, int Lo, int Li, int Q, int64_t sp, int64_t so,
+                            const float* a1, const float* a2, float alpha0, int in_dtype, int out_dtype,
+                            hipStream_t s) {
+  const float scale = (float)Li / Lo;
+  const unsigned grid = gridcap(P * Li * Q);
+#define ADJ(TI, TO)                                                                                   \
+  hipLaunchKernelGGL((bilinear_adj_kernel<TI, TO>), dim3(grid), dim3(256), 0, s, (const TI*)in, (TO*)out, \
+                     (long)P, Lo, Li, Q, (long)sp, (long)so, scale, a1, a2, alpha0)
+  if (in_dtype == 0 && out_dtype == 0) ADJ(float, float);
+  else if (in_dtype == 0 && out_dtype == 1) ADJ(float, bf16);
+  else if (in_dtype == 1 && out_dtype == 0) ADJ(bf16, float);
+  else if (in_dtype == 1 && out_dtype == 1) ADJ(bf16, bf16);
+  else { cmx_set_error("bilinear_adjoint: dtype"); return CMX_ERR_DTYPE; }
+#undef ADJ
+  return cmx_check_launch("bilinear_adjoint_1d");
+}
+
+}  // extern "C"

@@ -146,3 +146,6 @@ static inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b)
 // ws (G, nblk, W) -> out (G, W); defined in layernorm.hip, shared by all two-stage reductions
 int cmx_reduce_partials(const float* ws, float* out, int G, int nblk, int W, int accumulate,
                         float alpha, hipStream_t s);
+// ws (nblk, stride) columns [0, W) -> out (W)
+int cmx_reduce_partials_strided(const float* ws, float* out, int nblk, int W, int stride, int accumulate,
+                                hipStream_t s);

@@ -1,0 +1,158 @@
+// Convolution support for the OverlapPatchEmbed convs and the SRA spatial-reduction conv.
+//
+// Replaces  OverlapPatchEmbed.proj  (Conv2d k7/s4/p3 and k3/s2/p1, dual_segformer.py:196-197)
+// and  Attention.sr  (Conv2d kR/sR, :95-96, a non-overlapping patchify) as
+//   cols = im2col(x)  ->  GEMM with the weight (stored tap-major: (Cout, kh, kw, Cin))
+// on token-major NHWC activations.  Backward dX = col2im(dCols) is a gather over the
+// (kh, kw) taps that read each input pixel, so it needs no atomics.
+//
+// cols row = one output pixel (n, oy, ox); column = (kh*KW + kw)*C + c, row stride ldc
+// (>= KH*KW*C, padding columns written as zero).  Output spatial size follows
+// torch.nn.Conv2d floor semantics: Ho = (H + 2p - KH)/s + 1.
+#include "cmx_common.h"
+
+template <typename T>
+__global__ void im2col_nhwc_kernel(const T* __restrict__ x, T* __restrict__ cols, int NI, int H, int W,
+                                   int C, int KH, int KW, int stride, int pad, int Ho, int Wo, long ldc) {
+  constexpr int V = VecT<T>::N;
+  const int CPT = C / V;                       // chunks per tap
+  const int taps = KH * KW;
+  const long total = (long)NI * Ho * Wo * taps * CPT;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int ch = i % CPT;
+    const int tap = (i / CPT) % taps;
+    const long row = i / ((long)CPT * taps);
+    const int ox = row % Wo;
+    const int oy = (row / Wo) % Ho;
+    const int n = row / ((long)Wo * Ho);
+    const int iy = oy * stride - pad + tap / KW;
+    const int ix = ox * stride - pad + tap % KW;
+    float v[V];
+    if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+      load_vec<T>(x + (((long)n * H + iy) * W + ix) * C + ch * V, v);
+    } else {
+#pragma unroll
+      for (int j = 0; j < V; ++j) v[j] = 0.f;
+    }
+    store_vec<T>(cols + row * ldc + (long)tap * C + ch * V, v);
+  }
+}
+
+// zero the padding columns [K, ldc) of every row
+template <typename T>
+__global__ void zero_pad_cols_kernel(T* __restrict__ cols, long rows, int K, long ldc) {
+  const int padw = (int)(ldc - K);
+  const long total = rows * padw;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x)
+    cols[(i / padw) * ldc + K + i % padw] = from_f32<T>(0.f);
+}
+
+// NCHW fp32 image -> cols in (c, kh, kw) order (= reference weight flatten order)
+template <typename T>
+__global__ void im2col_nchw_kernel(const float* __restrict__ x, T* __restrict__ cols, int NI, int C, int H,
+                                   int W, int KH, int KW, int stride, int pad, int Ho, int Wo, long ldc) {
+  const int K = C * KH * KW;
+  const long total = (long)NI * Ho * Wo * ldc;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int k = i % ldc;
+    const long row = i / ldc;
+    float v = 0.f;
+    if (k < K) {
+      const int c = k / (KH * KW);
+      const int kh = (k / KW) % KH;
+      const int kw = k % KW;
+      const int ox = row % Wo;
+      const int oy = (row / Wo) % Ho;
+      const int n = row / ((long)Wo * Ho);
+      const int iy = oy * stride - pad + kh;
+      const int ix = ox * stride - pad + kw;
+      if (iy >= 0 && iy < H && ix >= 0 && ix < W) v = x[(((long)n * C + c) * H + iy) * W + ix];
+    }
+    cols[i] = from_f32<T>(v);
+  }
+}
+
+template <typename T>
+__global__ void col2im_nhwc_kernel(const T* __restrict__ cols, T* __restrict__ dx, int NI, int H, int W,
+                                   int C, int KH, int KW, int stride, int pad, int Ho, int Wo, long ldc) {
+  constexpr int V = VecT<T>::N;
+  const int CPR = C / V;
+  const long total = (long)NI * H * W * CPR;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int ch = i % CPR;
+    const long pix = i / CPR;
+    const int x = pix % W;
+    const int y = (pix / W) % H;
+    const int n = pix / ((long)W * H);
+    float acc[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) acc[j] = 0.f;
+    for (int kh = 0; kh < KH; ++kh) {
+      const int ty = y + pad - kh;
+      if (ty < 0 || ty % stride) continue;
+      const int oy = ty / stride;
+      if (oy >= Ho) continue;
+      for (int kw = 0; kw < KW; ++kw) {
+        const int tx = x + pad - kw;
+        if (tx < 0 || tx % stride) continue;
+        const int ox = tx / stride;
+        if (ox >= Wo) continue;
+        float v[V];
+        load_vec<T>(cols + (((long)n * Ho + oy) * Wo + ox) * ldc + (long)(kh * KW + kw) * C + ch * V, v);
+#pragma unroll
+        for (int j = 0; j < V; ++j) acc[j] += v[j];
+      }
+    }
+    store_vec<T>(dx + pix * C + ch * V, acc);
+  }
+}
+
+static unsigned grid_for(long total) {
+  const unsigned g = cdiv(total, 256);
+  return g < 16384 ? (g > 0 ? g : 1) : 16384;
+}
+
+extern "C" {
+
+int cmx_im2col_nhwc(const void* x, void* cols, int NI, int H, int W, int C, int KH, int KW, int stride, int pad,
+                    int Ho, int Wo, int64_t ldc, int dtype, hipStream_t s) {
+  const int V = dtype == 0 ? 4 : 8;
+  CMX_REQUIRE(C % V == 0 && ldc >= (long)KH * KW * C && ldc % V == 0, CMX_ERR_SHAPE,
+              "im2col_nhwc: C=%d ldc=%ld", C, (long)ldc);
+  CMX_REQUIRE(Ho == (H + 2 * pad - KH) / stride + 1 && Wo == (W + 2 * pad - KW) / stride + 1, CMX_ERR_SHAPE,
+              "im2col_nhwc: output size mismatch");
+  const long rows = (long)NI * Ho * Wo;
+  CMX_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL(im2col_nhwc_kernel<T>, dim3(grid_for(rows * KH * KW * (C / V))), dim3(256), 0, s,
+                       (const T*)x, (T*)cols, NI, H, W, C, KH, KW, stride, pad, Ho, Wo, (long)ldc);
+    if (ldc > (long)KH * KW * C)
+      hipLaunchKernelGGL(zero_pad_cols_kernel<T>, dim3(grid_for(rows * (ldc - KH * KW * C))), dim3(256), 0, s,
+                         (T*)cols, rows, KH * KW * C, (long)ldc);
+  });
+  return cmx_check_launch("im2col_nhwc");
+}
+
+int cmx_im2col_nchw_f32(const float* x, void* cols, int NI, int C, int H, int W, int KH, int KW, int stride,
+                        int pad, int Ho, int Wo, int64_t ldc, int dtype, hipStream_t s) {
+  CMX_REQUIRE(ldc >= (long)KH * KW * C, CMX_ERR_SHAPE, "im2col_nchw: ldc");
+  CMX_REQUIRE(Ho == (H + 2 * pad - KH) / stride + 1 && Wo == (W + 2 * pad - KW) / stride + 1, CMX_ERR_SHAPE,
+              "im2col_nchw: output size mismatch");
+  CMX_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL(im2col_nchw_kernel<T>, dim3(grid_for((long)NI * Ho * Wo * ldc)), dim3(256), 0, s, x,
+                       (T*)cols, NI, C, H, W, KH, KW, stride, pad, Ho, Wo, (long)ldc);
+  });
+  return cmx_check_launch("im2col_nchw");
+}
+
+int cmx_col2im_nhwc(const void* cols, void* dx, int NI, int H, int W, int C, int KH, int KW, int stride, int pad,
+                    int Ho, int Wo, int64_t ldc, int dtype, hipStream_t s) {
+  const int V = dtype == 0 ? 4 : 8;
+  CMX_REQUIRE(C % V == 0 && ldc % V == 0, CMX_ERR_SHAPE, "col2im_nhwc: C=%d", C);
+  CMX_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL(col2im_nhwc_kernel<T>, dim3(grid_for((long)NI * H * W * (C / V))), dim3(256), 0, s,
+                       (const T*)cols, (T*)dx, NI, H, W, C, KH, KW, stride, pad, Ho, Wo, (long)ldc);
+  });
+  return cmx_check_launch("col2im_nhwc");
+}
+
+}  // extern "C"

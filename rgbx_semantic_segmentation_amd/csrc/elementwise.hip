@@ -105,6 +105,18 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x, fl
   }
 }
 
+// scalar fallback for widths that are not a multiple of the vector width
+template <typename T>
+__global__ void colsum_scalar_kernel(const T* __restrict__ x, float* __restrict__ ws, long M, int N, long ld) {
+  const int g = blockIdx.y;
+  for (int c = threadIdx.x; c < N; c += blockDim.x) {
+    float acc = 0.f;
+    const T* base = x + (long)g * M * ld + c;
+    for (long m = blockIdx.x; m < M; m += gridDim.x) acc += to_f32(base[m * ld]);
+    ws[((long)g * gridDim.x + blockIdx.x) * N + c] = acc;
+  }
+}
+
 static unsigned ew_grid(long nvec) {
   long b = (nvec + 255) / 256;
   return (unsigned)(b < 8192 ? (b > 0 ? b : 1) : 8192);
@@ -178,11 +190,15 @@ size_t cmx_colsum_workspace(long M, int G, int N) {
 int cmx_colsum(const void* x, float* out, float* ws, long M, int G, int N, long ld, int accumulate,
                float alpha, int dtype, hipStream_t s) {
   const int V = dtype == 0 ? 4 : 8;
-  CMX_REQUIRE(N % V == 0 && ld % V == 0 && M > 0, CMX_ERR_SHAPE, "colsum: N=%d ld=%ld", N, ld);
+  CMX_REQUIRE(M > 0 && ld >= N, CMX_ERR_SHAPE, "colsum: N=%d ld=%ld", N, ld);
   const int nb = colsum_nblk(M);
   const int chunks = N / V;
+  const bool vec = (N % V == 0) && (ld % V == 0);
   CMX_DISPATCH(dtype, T, {
-    if (chunks <= 16) {
+    if (!vec) {
+      hipLaunchKernelGGL((colsum_scalar_kernel<T>), dim3(nb, G), dim3(N < 256 ? 64 * ((N + 63) / 64) : 256), 0, s,
+                         (const T*)x, ws, M, N, ld);
+    } else if (chunks <= 16) {
       hipLaunchKernelGGL((colsum_kernel<T, 16>), dim3(nb, G, 1), dim3(256), 0, s, (const T*)x, ws, M,
                          N, ld);
     } else {

@@ -181,6 +181,13 @@ int cmx_reduce_partials(const float* ws, float* out, int G, int nblk, int W, int
   return cmx_check_launch("reduce_partials");
 }
 
+int cmx_reduce_partials_strided(const float* ws, float* out, int nblk, int W, int stride, int accumulate,
+                                hipStream_t s) {
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(cdiv(W, 256), 1), dim3(256), 0, s, ws, out, nblk, W, stride,
+                     accumulate, 1.0f);
+  return cmx_check_launch("reduce_partials_strided");
+}
+
 static int ln_tpr(int chunks) {
   int t = 1;
   while (t < chunks && t < 64) t <<= 1;

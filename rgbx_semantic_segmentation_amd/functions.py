@@ -1,0 +1,541 @@
+"""Autograd Functions of the CMX training step, each backed by libcmx_hip.so kernels.
+
+Conventions
+ * Encoder activations are (G, M, C) tensors, G = 2 modality groups (RGB, X) processed by
+   one launch, M = B * H * W tokens (token-major = NHWC), C channels contiguous.
+ * Weights arrive as storage-layout views of the ParamStore (stacked over the modality
+   pair, compute dtype); their gradients are written directly into the fp32 gradient
+   buffer views passed alongside (``Wg``/``bg``).  Functions return ``None`` for those
+   and take an ``anchor`` Parameter only so autograd records the node.
+ * Plain dense GEMMs (Linear / 1x1 conv / im2col conv) are library GEMMs (hipBLASLt via
+   torch.bmm) in the compute dtype with fp32 weight gradients; everything else is a
+   hand-written gfx950 kernel (see include/cmx_hip.h).
+"""
+from __future__ import annotations
+
+import torch
+from torch.autograd import Function
+
+from . import kernels as K
+
+
+def _c(t):
+    return t if t.is_contiguous() else t.contiguous()
+
+
+def _wgrad(dy, x, out):
+    """out (fp32 view, (G, N, k)) = dy^T @ x with fp32 accumulation/output."""
+    dyt = dy.transpose(1, 2)
+    if dy.dtype == torch.float32:
+        if out.is_contiguous():
+            torch.bmm(dyt, x, out=out)
+        else:
+            out.copy_(torch.bmm(dyt, x))
+    else:
+        out.copy_(torch.bmm(dyt, x, out_dtype=torch.float32))
+
+
+# ---------------------------------------------------------------------------- Linear
+class GLinear(Function):
+    """y[g] = sum_i x_i[g] @ W[g][:, K_i]^T + b[g]   (nn.Linear / 1x1 Conv2d; the K-split
+    form replaces torch.cat of the inputs, e.g. CrossPath.end_proj on cat(y, v),
+    net_utils.py:277-280, and ChannelEmbed's 1x1 convs on cat(x1, x2), :323-326)."""
+
+    @staticmethod
+    def forward(ctx, W, Wg, b, bg, anchor, *xs):
+        G, N, Ktot = W.shape
+        y = None
+        k0 = 0
+        for x in xs:
+            k = x.shape[-1]
+            Wt = W[:, :, k0:k0 + k].transpose(1, 2)
+            if y is None:
+                y = torch.baddbmm(b[:, None, :], x, Wt) if b is not None else torch.bmm(x, Wt)
+            else:
+                y.baddbmm_(x, Wt)
+            k0 += k
+        assert k0 == Ktot, (k0, Ktot)
+        ctx.save_for_backward(W, *xs)
+        ctx.Wg, ctx.bg = Wg, bg
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        W, *xs = ctx.saved_tensors
+        dy = _c(dy)
+        G, M, N = dy.shape
+        dxs = []
+        k0 = 0
+        for i, x in enumerate(xs):
+            k = x.shape[-1]
+            if ctx.needs_input_grad[5 + i]:
+                dxs.append(torch.bmm(dy, W[:, :, k0:k0 + k]))
+            else:
+                dxs.append(None)
+            _wgrad(dy, x, ctx.Wg[:, :, k0:k0 + k])
+            k0 += k
+        if ctx.bg is not None:
+            K.colsum(dy, ctx.bg.reshape(G, N), G=G)
+        return (None, None, None, None, None, *dxs)
+
+
+def glinear(store, wp, bp, *xs):
+    """Grouped linear using parameter ``wp`` (and bias ``bp``) of the store."""
+    W = store.w(wp)
+    Wg = store.g(wp)
+    G = W.shape[0]
+    W = W.view(G, W.shape[1], -1)
+    Wg = Wg.view(G, Wg.shape[1], -1)
+    b = bg = None
+    if bp is not None:
+        b = store.w(bp).view(G, -1)
+        bg = store.g(bp).view(G, -1)
+    return GLinear.apply(W, Wg, b, bg, wp, *xs)
+
+
+# ---------------------------------------------------------------------------- LayerNorm
+class LayerNormF(Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, gg, bg, eps, G, anchor):
+        y, mean, rstd = K.layernorm_fwd(x, gamma, beta, eps, G=G)
+        ctx.save_for_backward(x, gamma, mean, rstd)
+        ctx.gg, ctx.bg, ctx.G = gg, bg, G
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gamma, mean, rstd = ctx.saved_tensors
+        dx = K.layernorm_bwd(_c(dy), x, gamma, mean, rstd, ctx.G, ctx.gg, ctx.bg)
+        return dx, None, None, None, None, None, None, None
+
+
+def layernorm(store, mod, x, G):
+    gamma = store.w(mod.weight, compute=False).view(G, -1)
+    beta = store.w(mod.bias, compute=False).view(G, -1)
+    gg = store.g(mod.weight).view(G, -1)
+    bg = store.g(mod.bias).view(G, -1)
+    return LayerNormF.apply(x, gamma, beta, gg, bg, mod.eps, G, mod.weight)
+
+
+# ---------------------------------------------------------------------------- residual
+class ResidualF(Function):
+    """x + drop_path(y): timm DropPath as a per-sample scale (0 or 1/keep) fused in the add."""
+
+    @staticmethod
+    def forward(ctx, x, y, scale, nps):
+        ctx.scale, ctx.nps = scale, nps
+        return K.residual_add(x, y, scale, n_per_sample=nps)
+
+    @staticmethod
+    def backward(ctx, dout):
+        dout = _c(dout)
+        dy = dout if ctx.scale is None else K.scale_samples(dout, ctx.scale, ctx.nps)
+        return dout, dy, None, None
+
+
+class ReluF(Function):
+    @staticmethod
+    def forward(ctx, x):
+        y = K.act_fwd(x, "relu")
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        return K.act_bwd(_c(dy), y, "relu")
+
+
+# ---------------------------------------------------------------------------- attention
+class SRAttentionF(Function):
+    """softmax(q k^T d^-1/2) v of Attention.forward (dual_segformer.py:119-134)."""
+
+    @staticmethod
+    def forward(ctx, q, kv, Bt, N, Nk, heads, D):
+        C = heads * D
+        o, lse = K.sra_attn_fwd(q, kv, kv[..., C:], Bt, N, Nk, heads, D, D ** -0.5, C, 2 * C)
+        o = o.view(q.shape)
+        ctx.save_for_backward(q, kv, o, lse)
+        ctx.dims = (Bt, N, Nk, heads, D)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, kv, o, lse = ctx.saved_tensors
+        Bt, N, Nk, heads, D = ctx.dims
+        C = heads * D
+        dq, dkv = K.sra_attn_bwd(q, kv, kv[..., C:], o, _c(do), lse, Bt, N, Nk, heads, D, D ** -0.5, C, 2 * C)
+        return dq.view(q.shape), dkv.view(kv.shape), None, None, None, None, None
+
+
+# ---------------------------------------------------------------------------- depthwise
+class DWConvF(Function):
+    """Depthwise 3x3 + bias + act (Mix-FFN DWConv+GELU, ChannelEmbed DW+ReLU)."""
+
+    @staticmethod
+    def forward(ctx, h, w, b, wg, bg, NI, ipg, H, W, act, anchor):
+        C = h.shape[-1]
+        out = torch.empty_like(h)
+        K.call("cmx_dwconv3x3_fwd", K.ptr(h), K.ptr(w), K.ptr(b), K.ptr(out), NI, ipg, H, W, C, K.ACT[act],
+               K.dtype_code(h), K.stream())
+        ctx.save_for_backward(h, w, b)
+        ctx.meta = (wg, bg, NI, ipg, H, W, act)
+        return out
+
+    @staticmethod
+    def backward(ctx, da):
+        h, w, b = ctx.saved_tensors
+        wg, bg, NI, ipg, H, W, act = ctx.meta
+        C = h.shape[-1]
+        da = _c(da)
+        dz = torch.empty_like(h)
+        dh = torch.empty_like(h) if ctx.needs_input_grad[0] else None
+        ws = K._ws(K.query("cmx_dwconv3x3_bwd_workspace", NI, ipg, H, W, C), h.device)
+        K.call("cmx_dwconv3x3_bwd", K.ptr(da), K.ptr(h), K.ptr(w), K.ptr(b), K.ptr(dz), K.ptr(dh), K.ptr(wg),
+               K.ptr(bg), K.ptr(ws), NI, ipg, H, W, C, K.ACT[act], 0, K.dtype_code(h), K.stream())
+        return dh, None, None, None, None, None, None, None, None, None, None
+
+
+def dwconv(store, conv, h, NI, ipg, H, W, act):
+    G = NI // ipg
+    w = store.w(conv.weight, compute=False).view(G, -1, 9)
+    b = store.w(conv.bias, compute=False).view(G, -1)
+    wg = store.g(conv.weight).view(G, -1, 9)
+    bg = store.g(conv.bias).view(G, -1)
+    return DWConvF.apply(h, w, b, wg, bg, NI, ipg, H, W, act, conv.weight)
+
+
+# ---------------------------------------------------------------------------- conv (im2col + GEMM)
+class ConvF(Function):
+    """Conv2d as im2col + grouped GEMM on NHWC (OverlapPatchEmbed.proj, Attention.sr)."""
+
+    @staticmethod
+    def forward(ctx, x, W, Wg, b, bg, geom, anchor):
+        # geom: (G, NI, H, Wd, C, KH, KW, stride, pad, Ho, Wo, nchw)
+        G, NI, H, Wd, C, KH, KW, st, pad, Ho, Wo, nchw = geom
+        Kp = W.shape[-1]
+        cols = torch.empty(G, NI // G * Ho * Wo, Kp, dtype=W.dtype, device=W.device)
+        if nchw:
+            K.call("cmx_im2col_nchw_f32", K.ptr(x), K.ptr(cols), NI, C, H, Wd, KH, KW, st, pad, Ho, Wo, Kp,
+                   K.dtype_code(cols), K.stream())
+        else:
+            K.call("cmx_im2col_nhwc", K.ptr(x), K.ptr(cols), NI, H, Wd, C, KH, KW, st, pad, Ho, Wo, Kp,
+                   K.dtype_code(cols), K.stream())
+        y = torch.baddbmm(b[:, None, :], cols, W.transpose(1, 2)) if b is not None else \
+            torch.bmm(cols, W.transpose(1, 2))
+        ctx.save_for_backward(cols, W)
+        ctx.meta = (Wg, bg, geom)
+        ctx.xshape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        cols, W = ctx.saved_tensors
+        Wg, bg, geom = ctx.meta
+        G, NI, H, Wd, C, KH, KW, st, pad, Ho, Wo, nchw = geom
+        dy = _c(dy)
+        _wgrad(dy, cols, Wg)
+        if bg is not None:
+            K.colsum(dy, bg, G=G)
+        dx = None
+        if ctx.needs_input_grad[0] and not nchw:
+            dcols = torch.bmm(dy, W)
+            dx = torch.empty(NI, H, Wd, C, dtype=dy.dtype, device=dy.device)
+            K.call("cmx_col2im_nhwc", K.ptr(dcols), K.ptr(dx), NI, H, Wd, C, KH, KW, st, pad, Ho, Wo, W.shape[-1],
+                   K.dtype_code(dx), K.stream())
+            dx = dx.view(ctx.xshape)
+        return dx, None, None, None, None, None, None
+
+
+def conv(store, mod, x, G, NI, H, W, C, stride, pad, nchw=False):
+    KH, KW = mod.kernel_size
+    Ho = (H + 2 * pad - KH) // stride + 1
+    Wo = (W + 2 * pad - KW) // stride + 1
+    Wt = store.w(mod.weight)
+    Wgt = store.g(mod.weight)
+    Wt = Wt.view(G, Wt.shape[1], -1)
+    Wgt = Wgt.view(G, Wgt.shape[1], -1)
+    b = store.w(mod.bias).view(G, -1) if mod.bias is not None else None
+    bg = store.g(mod.bias).view(G, -1) if mod.bias is not None else None
+    geom = (G, NI, H, W, C, KH, KW, stride, pad, Ho, Wo, nchw)
+    return ConvF.apply(x, Wt, Wgt, b, bg, geom, mod.weight), Ho, Wo
+
+
+# ---------------------------------------------------------------------------- FFM cross attention
+class CrossAttentionF(Function):
+    """CrossAttention.forward (net_utils.py:199-214) on grouped tensors:
+    u (G=2, M, C) is the query (raw, no projection), kv (2, M, 2C) = [k | v].
+    ctx_g = softmax_{-2}(k_g^T v_g * s); out_g = u_g @ ctx_{1-g}."""
+
+    @staticmethod
+    def forward(ctx, u, kv, B, N, heads, D):
+        G, M, C = u.shape
+        BH = G * B * heads
+        scale = D ** -0.5
+        cx = torch.empty(BH, D, D, dtype=torch.float32, device=u.device)
+        ws = K._ws(K.query("cmx_ffm_ctx_workspace", BH, N, D), u.device)
+        dt = K.dtype_code(kv)
+        K.call("cmx_ffm_ctx_reduce", K.ptr(kv), kv.data_ptr() + C * kv.element_size(), 0, K.ptr(cx), K.ptr(ws),
+               G * B, N, heads, D, 2 * C, 2 * C, 1, scale, 0, dt, K.stream())
+        out = torch.empty(G, M, C, dtype=u.dtype, device=u.device)
+        K.call("cmx_ffm_rowmat", K.ptr(u), K.ptr(cx), K.ptr(out), G * B, N, heads, D, u.stride(1), C, 0, 1.0, 0, B,
+               dt, K.stream())
+        ctx.save_for_backward(u, kv, cx)
+        ctx.meta = (B, N, heads, D)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        u, kv, cx = ctx.saved_tensors
+        B, N, heads, D = ctx.meta
+        G, M, C = u.shape
+        dout = _c(dout)
+        dt = K.dtype_code(dout)
+        scale = D ** -0.5
+        BH = G * B * heads
+        du = torch.empty(G, M, C, dtype=u.dtype, device=u.device)
+        K.call("cmx_ffm_rowmat", K.ptr(dout), K.ptr(cx), K.ptr(du), G * B, N, heads, D, C, C, 1, 1.0, 0, B, dt,
+               K.stream())
+        dA = torch.empty_like(cx)
+        ws = K._ws(K.query("cmx_ffm_ctx_workspace", BH, N, D), u.device)
+        K.call("cmx_ffm_ctx_reduce", K.ptr(u), K.ptr(dout), K.ptr(cx), K.ptr(dA), K.ptr(ws), G * B, N, heads, D,
+               u.stride(1), C, 2, scale, B, dt, K.stream())
+        dkv = torch.empty(G, M, 2 * C, dtype=kv.dtype, device=kv.device)
+        kp, vp = kv.data_ptr(), kv.data_ptr() + C * kv.element_size()
+        dkp, dvp = dkv.data_ptr(), dkv.data_ptr() + C * dkv.element_size()
+        # dk = v dA^T, dv = k dA
+        K.call("cmx_ffm_rowmat", vp, K.ptr(dA), dkp, G * B, N, heads, D, 2 * C, 2 * C, 1, 1.0, 0, 0, dt, K.stream())
+        K.call("cmx_ffm_rowmat", kp, K.ptr(dA), dvp, G * B, N, heads, D, 2 * C, 2 * C, 0, 1.0, 0, 0, dt, K.stream())
+        return du, dkv, None, None, None, None
+
+
+# ---------------------------------------------------------------------------- FRM
+class FRMF(Function):
+    """FeatureRectifyModule (net_utils.py:124-152) on x (2, B, N, C)."""
+
+    @staticmethod
+    def forward(ctx, x, prm, anchor):
+        (W1, b1, W2, b2, W0, b0, w2s, b2s) = prm["w"]
+        G, B, N, C = x.shape
+        dt = K.dtype_code(x)
+        pooled = torch.empty(B, 4 * C, dtype=torch.float32, device=x.device)
+        argmax = torch.empty(B, 2 * C, dtype=torch.int32, device=x.device)
+        ws = K._ws(K.query("cmx_frm_pool_workspace", B, N, C), x.device)
+        K.call("cmx_frm_pool_fwd", K.ptr(x), K.ptr(pooled), K.ptr(argmax), K.ptr(ws), B, N, C, dt, K.stream())
+        y1 = torch.empty(B, 4 * C, dtype=torch.float32, device=x.device)
+        K.call("cmx_small_linear_fwd", K.ptr(pooled), K.ptr(W1), K.ptr(b1), K.ptr(y1), B, 4 * C, 4 * C, 2, K.stream())
+        cw = torch.empty(B, 2 * C, dtype=torch.float32, device=x.device)
+        K.call("cmx_small_linear_fwd", K.ptr(y1), K.ptr(W2), K.ptr(b2), K.ptr(cw), B, 4 * C, 2 * C, 3, K.stream())
+        x1 = x[0].reshape(B * N, C)
+        x2 = x[1].reshape(B * N, C)
+        h = torch.addmm(b0, x1, W0[:, :C].t())
+        h.addmm_(x2, W0[:, C:].t())
+        sw = torch.empty(B * N, 2, dtype=torch.float32, device=x.device)
+        K.call("cmx_frm_spatial_fwd", K.ptr(h), K.ptr(w2s), K.ptr(b2s), K.ptr(sw), B * N, C, dt, K.stream())
+        out = torch.empty_like(x)
+        K.call("cmx_frm_combine_fwd", K.ptr(x), K.ptr(cw), K.ptr(sw), K.ptr(out), B, N, C, dt, K.stream())
+        ctx.save_for_backward(x, pooled, argmax, y1, cw, h, sw)
+        ctx.prm = prm
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, pooled, argmax, y1, cw, h, sw = ctx.saved_tensors
+        (W1, b1, W2, b2, W0, b0, w2s, b2s) = ctx.prm["w"]
+        (gW1, gb1, gW2, gb2, gW0, gb0, gw2s, gb2s) = ctx.prm["g"]
+        W1f, W2f, w2sf = ctx.prm["w32"]
+        G, B, N, C = x.shape
+        dt = K.dtype_code(x)
+        dout = _c(dout)
+        dx = torch.empty_like(x)
+        dsw = torch.empty(B * N, 2, dtype=torch.float32, device=x.device)
+        dcw = torch.empty(B, 2 * C, dtype=torch.float32, device=x.device)
+        ws = K._ws(K.query("cmx_frm_combine_bwd_workspace", B, N, C), x.device)
+        K.call("cmx_frm_combine_bwd", K.ptr(dout), K.ptr(x), K.ptr(cw), K.ptr(sw), K.ptr(dx), K.ptr(dsw), K.ptr(dcw),
+               K.ptr(ws), B, N, C, dt, K.stream())
+        dh = torch.empty_like(h)
+        ws2 = K._ws(K.query("cmx_frm_spatial_bwd_workspace", B * N, C), x.device)
+        K.call("cmx_frm_spatial_bwd", K.ptr(dsw), K.ptr(sw), K.ptr(h), K.ptr(w2sf), K.ptr(dh), K.ptr(gw2s),
+               K.ptr(gb2s), K.ptr(ws2), B * N, C, 0, dt, K.stream())
+        dx1 = dx[0].view(B * N, C)
+        dx2 = dx[1].view(B * N, C)
+        dx1.addmm_(dh, W0[:, :C])
+        dx2.addmm_(dh, W0[:, C:])
+        x1 = x[0].reshape(B * N, C)
+        x2 = x[1].reshape(B * N, C)
+        _wgrad(dh[None], x1[None], gW0[:, :C][None])
+        _wgrad(dh[None], x2[None], gW0[:, C:][None])
+        K.colsum(dh, gb0.view(1, C), G=1)
+        # channel MLP backward (sigmoid then relu), then pooling backward
+        dz = torch.empty(B * 4 * C, dtype=torch.float32, device=x.device)
+        dy1 = torch.empty(B, 4 * C, dtype=torch.float32, device=x.device)
+        K.call("cmx_small_linear_bwd", K.ptr(dcw), K.ptr(cw), K.ptr(y1), K.ptr(W2f), K.ptr(dy1), K.ptr(gW2),
+               K.ptr(gb2), K.ptr(dz), B, 4 * C, 2 * C, 3, 0, K.stream())
+        dpooled = torch.empty(B, 4 * C, dtype=torch.float32, device=x.device)
+        K.call("cmx_small_linear_bwd", K.ptr(dy1), K.ptr(y1), K.ptr(pooled), K.ptr(W1f), K.ptr(dpooled), K.ptr(gW1),
+               K.ptr(gb1), K.ptr(dz), B, 4 * C, 4 * C, 2, 0, K.stream())
+        K.call("cmx_frm_pool_bwd", K.ptr(dpooled), K.ptr(argmax), K.ptr(dx), B, N, C, dt, K.stream())
+        return dx, None, None
+
+
+def frm(store, mod, x):
+    cwm, swm = mod.channel_weights.mlp, mod.spatial_weights.mlp
+    C = x.shape[-1]
+    f32 = lambda p: store.w(p, stacked=False, compute=False)
+    cmp = lambda p: store.w(p, stacked=False)
+    g = lambda p: store.g(p, stacked=False)
+    prm = {
+        # fp32 for the small MLP / spatial head (computed on the VALU in fp32);
+        # compute dtype for the spatial 1x1 GEMM
+        "w": (f32(cwm[0].weight), f32(cwm[0].bias), f32(cwm[2].weight), f32(cwm[2].bias),
+              cmp(swm[0].weight).view(C, 2 * C), cmp(swm[0].bias), f32(swm[2].weight).view(2, C), f32(swm[2].bias)),
+        "g": (g(cwm[0].weight), g(cwm[0].bias), g(cwm[2].weight), g(cwm[2].bias),
+              g(swm[0].weight).view(C, 2 * C), g(swm[0].bias), g(swm[2].weight).view(2, C), g(swm[2].bias)),
+        "w32": (f32(cwm[0].weight), f32(cwm[2].weight), f32(swm[2].weight).view(2, C)),
+    }
+    return FRMF.apply(x, prm, cwm[0].weight)
+
+
+# ---------------------------------------------------------------------------- BatchNorm
+class BatchNormF(Function):
+    @staticmethod
+    def forward(ctx, x, res, prm, training, act, dscale, rps, group, anchor):
+        gamma, beta, gg, bg, rm, rv, eps, momentum = prm
+        M, C = x.shape
+        dt = K.dtype_code(x)
+        mean = torch.empty(C, dtype=torch.float32, device=x.device)
+        invstd = torch.empty(C, dtype=torch.float32, device=x.device)
+        count = float(M)
+        if training:
+            sums = torch.empty(2, C, dtype=torch.float64, device=x.device)
+            ws = torch.empty(max(1, K.query("cmx_bn_workspace", M, C) // 8), dtype=torch.float64, device=x.device)
+            K.call("cmx_bn_stats", K.ptr(x), K.ptr(sums), K.ptr(ws), M, C, dt, K.stream())
+            if group is not None:
+                import torch.distributed as dist
+                dist.all_reduce(sums, group=group)
+                count *= dist.get_world_size(group)
+            K.call("cmx_bn_finalize", K.ptr(sums), count, eps, momentum, K.ptr(rm), K.ptr(rv), K.ptr(mean),
+                   K.ptr(invstd), C, 1, K.stream())
+        else:
+            K.call("cmx_bn_finalize", 0, 1.0, eps, momentum, K.ptr(rm), K.ptr(rv), K.ptr(mean), K.ptr(invstd), C, 0,
+                   K.stream())
+        y = torch.empty_like(x)
+        K.call("cmx_bn_apply", K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(gamma), K.ptr(beta), K.ptr(res),
+               K.ptr(dscale), K.ptr(y), M, C, rps, K.ACT[act], dt, K.stream())
+        ctx.save_for_backward(x, res if res is not None else x, mean, invstd)
+        ctx.meta = (prm, training, act, dscale, rps, group, count, res is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, res, mean, invstd = ctx.saved_tensors
+        prm, training, act, dscale, rps, group, count, has_res = ctx.meta
+        gamma, beta, gg, bg, rm, rv, eps, momentum = prm
+        res = res if has_res else None
+        M, C = x.shape
+        dt = K.dtype_code(x)
+        dy = _c(dy)
+        sums = torch.empty(2, C, dtype=torch.float64, device=x.device)
+        ws = torch.empty(max(1, K.query("cmx_bn_workspace", M, C) // 8), dtype=torch.float64, device=x.device)
+        K.call("cmx_bn_bwd_reduce", K.ptr(dy), K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(gamma), K.ptr(beta),
+               K.ptr(res), K.ptr(dscale), K.ptr(sums), K.ptr(gg), K.ptr(bg), K.ptr(ws), M, C, rps, K.ACT[act], 0, dt,
+               K.stream())
+        if training and group is not None:
+            import torch.distributed as dist
+            dist.all_reduce(sums, group=group)
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if has_res else None
+        K.call("cmx_bn_bwd_apply", K.ptr(dy), K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(gamma), K.ptr(beta),
+               K.ptr(res), K.ptr(dscale), K.ptr(sums), count, K.ptr(dx), K.ptr(dres), M, C, rps, K.ACT[act],
+               int(training), dt, K.stream())
+        return dx, dres, None, None, None, None, None, None, None
+
+
+def batchnorm(store, bn, x, training, res=None, act="none", dscale=None, rps=1, group=None):
+    prm = (store.w(bn.weight, stacked=False, compute=False), store.w(bn.bias, stacked=False, compute=False),
+           store.g(bn.weight, stacked=False), store.g(bn.bias, stacked=False), bn.running_mean, bn.running_var,
+           float(bn.eps), float(bn.momentum))
+    if training:
+        bn.num_batches_tracked.add_(1)
+    return BatchNormF.apply(x, res, prm, training, act, dscale, rps, group, bn.weight)
+
+
+# ---------------------------------------------------------------------------- decoder gather
+class DecoderGatherF(Function):
+    """Bilinear upsample of c4, c3, c2 to the 1/4 grid + concat [c4, c3, c2, c1]
+    (MLPDecoder.py:66-77) written straight into one (B, N1, 4E) buffer."""
+
+    @staticmethod
+    def forward(ctx, c4, c3, c2, c1, sizes):
+        B, N1, E = c1.shape
+        (H1, W1), hw = sizes[0], sizes[1:]
+        cat = torch.empty(B, N1, 4 * E, dtype=c1.dtype, device=c1.device)
+        dt = K.dtype_code(c1)
+        esz = cat.element_size()
+        for slot, (t, (h, w)) in enumerate(zip((c4, c3, c2, c1), (hw[2], hw[1], hw[0], (H1, W1)))):
+            K.call("cmx_bilinear_fwd_nhwc", K.ptr(_c(t)), cat.data_ptr() + slot * E * esz, B, h, w, H1, W1, E, 4 * E,
+                   dt, K.stream())
+        ctx.sizes = sizes
+        ctx.E = E
+        return cat
+
+    @staticmethod
+    def backward(ctx, dcat):
+        dcat = _c(dcat)
+        (H1, W1), hw = ctx.sizes[0], ctx.sizes[1:]
+        E = ctx.E
+        B = dcat.shape[0]
+        dt = K.dtype_code(dcat)
+        esz = dcat.element_size()
+        grads = []
+        for slot, (h, w) in enumerate((hw[2], hw[1], hw[0])):
+            base = dcat.data_ptr() + slot * E * esz
+            tmp = torch.empty(B * H1, w, E, dtype=torch.float32, device=dcat.device)
+            K.call("cmx_bilinear_adjoint_1d", base, K.ptr(tmp), B * H1, W1, w, E, W1 * 4 * E, 4 * E, 0, 0, 1.0, dt, 0,
+                   K.stream())
+            g = torch.empty(B, h * w, E, dtype=dcat.dtype, device=dcat.device)
+            K.call("cmx_bilinear_adjoint_1d", K.ptr(tmp), K.ptr(g), B, H1, h, w * E, H1 * w * E, w * E, 0, 0, 1.0, 0,
+                   dt, K.stream())
+            grads.append(g)
+        g1 = dcat[..., 3 * E:].contiguous()
+        return grads[0], grads[1], grads[2], g1, None
+
+
+# ---------------------------------------------------------------------------- final upsample + CE
+class UpsampleCEF(Function):
+    """F.interpolate(logits, (H, W), bilinear) + CrossEntropyLoss(mean, ignore_index)
+    (builder.py:233,249) fused; full-res logits are never materialised."""
+
+    @staticmethod
+    def forward(ctx, logits, label, dims, ignore):
+        B, h, w, H, W, Kc = dims
+        grad = torch.empty(B, H, W, Kc, dtype=logits.dtype, device=logits.device)
+        out = torch.empty(3, dtype=torch.float32, device=logits.device)
+        ws = K._ws(K.query("cmx_upsample_ce_workspace", B, H, W), logits.device)
+        K.call("cmx_upsample_ce_fwd", K.ptr(_c(logits)), K.ptr(label), K.ptr(grad), K.ptr(out), K.ptr(ws), B, h, w, H,
+               W, Kc, ignore, K.dtype_code(logits), K.stream())
+        ctx.save_for_backward(grad, out)
+        ctx.dims = dims
+        ctx.ldtype = logits.dtype
+        ctx.lshape = logits.shape
+        return out[0].clone()
+
+    @staticmethod
+    def backward(ctx, dloss):
+        grad, out = ctx.saved_tensors
+        B, h, w, H, W, Kc = ctx.dims
+        dloss = _c(dloss.reshape(1).to(torch.float32))
+        tmp = torch.empty(B * H, w, Kc, dtype=torch.float32, device=grad.device)
+        K.call("cmx_bilinear_adjoint_1d", K.ptr(grad), K.ptr(tmp), B * H, W, w, Kc, W * Kc, Kc, 0, 0, 1.0,
+               K.dtype_code(grad), 0, K.stream())
+        dl = torch.empty(B, h * w, Kc, dtype=ctx.ldtype, device=grad.device)
+        K.call("cmx_bilinear_adjoint_1d", K.ptr(tmp), K.ptr(dl), B, H, h, w * Kc, H * w * Kc, w * Kc, K.ptr(dloss),
+               out.data_ptr() + 4, 1.0, 0, K.dtype_code(dl), K.stream())
+        return dl.view(ctx.lshape), None, None, None
+
+
+def upsample_logits_nchw(logits, B, h, w, H, W, Kc):
+    out = torch.empty(B, Kc, H, W, dtype=torch.float32, device=logits.device)
+    K.call("cmx_bilinear_fwd_nchw_f32", K.ptr(_c(logits)), K.ptr(out), B, h, w, H, W, Kc, K.dtype_code(logits),
+           K.stream())
+    return out

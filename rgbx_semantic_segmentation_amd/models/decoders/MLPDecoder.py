@@ -1,0 +1,52 @@
+"""SegFormer all-MLP decode head (reference: models/decoders/MLPDecoder.py:8-81).
+
+Execution on tokens: linear_c{1..4} GEMMs, bilinear upsample of c2..c4 written straight
+into the channel slices of one (B, N1, 4E) buffer (no torch.cat), linear_fuse GEMM,
+BatchNorm (SyncBN across ranks when a process group is given) + ReLU + Dropout2d fused
+into one apply kernel, linear_pred GEMM.  Returns low-resolution logits (B*N1, K).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from ... import functions as F
+
+
+class MLP(nn.Module):
+    def __init__(self, input_dim=2048, embed_dim=768):
+        super().__init__()
+        self.proj = nn.Linear(input_dim, embed_dim)
+
+
+class DecoderHead(nn.Module):
+    def __init__(self, in_channels=(64, 128, 320, 512), num_classes=40, dropout_ratio=0.1,
+                 norm_layer=nn.BatchNorm2d, embed_dim=768, align_corners=False):
+        super().__init__()
+        self.num_classes = num_classes
+        self.dropout_ratio = dropout_ratio
+        self.in_channels = list(in_channels)
+        self.embed_dim = embed_dim
+        c1, c2, c3, c4 = in_channels
+        self.linear_c4 = MLP(c4, embed_dim)
+        self.linear_c3 = MLP(c3, embed_dim)
+        self.linear_c2 = MLP(c2, embed_dim)
+        self.linear_c1 = MLP(c1, embed_dim)
+        self.linear_fuse = nn.Sequential(nn.Conv2d(4 * embed_dim, embed_dim, 1), nn.BatchNorm2d(embed_dim),
+                                         nn.ReLU(inplace=True))
+        self.linear_pred = nn.Conv2d(embed_dim, num_classes, 1)
+
+    def run(self, store, feats, grids, B, training, dscale=None, group=None):
+        E = self.embed_dim
+        lin = (self.linear_c1, self.linear_c2, self.linear_c3, self.linear_c4)
+        proj = []
+        for i in range(4):
+            t = F.glinear(store, lin[i].proj.weight, lin[i].proj.bias, feats[i].view(1, -1, feats[i].shape[-1]))
+            proj.append(t.view(B, -1, E))
+        H1, W1 = grids[0]
+        cat = F.DecoderGatherF.apply(proj[3], proj[2], proj[1], proj[0], [grids[0]] + list(grids[1:]))
+        M = B * H1 * W1
+        f = F.glinear(store, self.linear_fuse[0].weight, self.linear_fuse[0].bias, cat.view(1, M, 4 * E))
+        f = F.batchnorm(store, self.linear_fuse[1], f.view(M, E), training, act="relu", dscale=dscale,
+                        rps=H1 * W1, group=group)
+        return F.glinear(store, self.linear_pred.weight, self.linear_pred.bias, f.view(1, M, E)).view(M, -1)

@@ -1,0 +1,228 @@
+"""Dual-stream MiT encoder (mit_b0..b5) of CMX, executed with both modality streams in
+every kernel launch.
+
+Parameter containers keep the reference module tree (``dual_segformer.py:19-528``), so
+``state_dict`` keys match (``backbone.block2.3.attn.sr.weight``,
+``backbone.extra_patch_embed1.proj.weight``, ...).  The containers hold parameters only;
+``RGBXTransformer.run`` executes a stage for BOTH streams at once: the RGB module's
+parameters are addressed through the ParamStore as (2, ...) stacked views that include
+the ``extra_*`` twin, activations are (2, B*N, C) token-major tensors.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+
+from ... import functions as F
+from ..net_utils import FeatureRectifyModule, FeatureFusionModule, init_segformer
+
+MIT_SPECS = {
+    "mit_b0": dict(embed_dims=[32, 64, 160, 256], depths=[2, 2, 2, 2]),
+    "mit_b1": dict(embed_dims=[64, 128, 320, 512], depths=[2, 2, 2, 2]),
+    "mit_b2": dict(embed_dims=[64, 128, 320, 512], depths=[3, 4, 6, 3]),
+    "mit_b3": dict(embed_dims=[64, 128, 320, 512], depths=[3, 4, 18, 3]),
+    "mit_b4": dict(embed_dims=[64, 128, 320, 512], depths=[3, 8, 27, 3]),
+    "mit_b5": dict(embed_dims=[64, 128, 320, 512], depths=[3, 6, 40, 3]),
+}
+NUM_HEADS = [1, 2, 5, 8]
+SR_RATIOS = [8, 4, 2, 1]
+MLP_RATIO = 4
+
+
+def drop_path_probs(depths: List[int], rate: float):
+    """Per stage: (rgb_probs, x_probs) per block.  Reproduces dual_segformer.py:249-311,
+    including the stage-2 indexing (block2[i] -> dpr[cur], extra_block2[i] -> dpr[cur+1])."""
+    dpr = [x.item() for x in torch.linspace(0, rate, sum(depths))]
+    out, cur = [], 0
+    for s, d in enumerate(depths):
+        if s == 1:
+            out.append(([dpr[cur]] * d, [dpr[cur + 1]] * d))
+        else:
+            p = [dpr[cur + i] for i in range(d)]
+            out.append((p, list(p)))
+        cur += d
+    return out
+
+
+class DWConv(nn.Module):                          # dual_segformer.py:19-33
+    def __init__(self, dim):
+        super().__init__()
+        self.dwconv = nn.Conv2d(dim, dim, 3, 1, 1, bias=True, groups=dim)
+
+
+class Mlp(nn.Module):                             # dual_segformer.py:36-74
+    def __init__(self, dim, hidden):
+        super().__init__()
+        self.fc1 = nn.Linear(dim, hidden)
+        self.dwconv = DWConv(hidden)
+        self.fc2 = nn.Linear(hidden, dim)
+
+
+class Attention(nn.Module):                       # dual_segformer.py:77-138
+    def __init__(self, dim, num_heads, sr_ratio):
+        super().__init__()
+        self.num_heads = num_heads
+        self.q = nn.Linear(dim, dim, bias=True)
+        self.kv = nn.Linear(dim, 2 * dim, bias=True)
+        self.proj = nn.Linear(dim, dim)
+        self.sr_ratio = sr_ratio
+        if sr_ratio > 1:
+            self.sr = nn.Conv2d(dim, dim, sr_ratio, sr_ratio)
+            self.norm = nn.LayerNorm(dim)
+
+
+class Block(nn.Module):                           # dual_segformer.py:141-180
+    def __init__(self, dim, num_heads, sr_ratio, drop_path):
+        super().__init__()
+        self.norm1 = nn.LayerNorm(dim, eps=1e-6)
+        self.attn = Attention(dim, num_heads, sr_ratio)
+        self.drop_path_prob = drop_path
+        self.norm2 = nn.LayerNorm(dim, eps=1e-6)
+        self.mlp = Mlp(dim, dim * MLP_RATIO)
+
+
+class OverlapPatchEmbed(nn.Module):               # dual_segformer.py:183-225
+    def __init__(self, patch_size, stride, in_chans, embed_dim):
+        super().__init__()
+        self.proj = nn.Conv2d(in_chans, embed_dim, patch_size, stride, patch_size // 2)
+        self.norm = nn.LayerNorm(embed_dim)
+        self.stride = stride
+        self.pad = patch_size // 2
+
+
+class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
+    def __init__(self, embed_dims, depths, drop_path_rate=0.1):
+        super().__init__()
+        self.embed_dims, self.depths = list(embed_dims), list(depths)
+        self.dp = drop_path_probs(depths, drop_path_rate)
+        cins = [3] + list(embed_dims[:3])
+        for pre in ("", "extra_"):
+            for s in range(4):
+                k, st = (7, 4) if s == 0 else (3, 2)
+                setattr(self, f"{pre}patch_embed{s + 1}", OverlapPatchEmbed(k, st, cins[s], embed_dims[s]))
+        for s in range(4):
+            for pre, probs in (("", self.dp[s][0]), ("extra_", self.dp[s][1])):
+                setattr(self, f"{pre}block{s + 1}", nn.ModuleList(
+                    [Block(embed_dims[s], NUM_HEADS[s], SR_RATIOS[s], probs[i]) for i in range(depths[s])]))
+                setattr(self, f"{pre}norm{s + 1}", nn.LayerNorm(embed_dims[s], eps=1e-6))
+        self.FRMs = nn.ModuleList([FeatureRectifyModule(d) for d in embed_dims])
+        self.FFMs = nn.ModuleList([FeatureFusionModule(d, NUM_HEADS[s]) for s, d in enumerate(embed_dims)])
+        self.apply(init_segformer)
+
+    # ------------------------------------------------------------------------ execution
+    def drop_path_keep_probs(self):
+        """(n_blocks_total, 2) keep probabilities in execution order (stage, block)."""
+        rows = []
+        for s in range(4):
+            for i in range(self.depths[s]):
+                rows.append((1.0 - self.dp[s][0][i], 1.0 - self.dp[s][1][i]))
+        return rows
+
+    def run_block(self, store, blk: Block, x, B, H, W, s_attn, s_mlp):
+        G, M, C = x.shape
+        N = H * W
+        a = blk.attn
+        h = F.layernorm(store, blk.norm1, x, G)
+        q = F.glinear(store, a.q.weight, a.q.bias, h)
+        if a.sr_ratio > 1:
+            R = a.sr_ratio
+            xs, Hk, Wk = F.conv(store, a.sr, h, G, G * B, H, W, C, R, 0)
+            xs = F.layernorm(store, a.norm, xs, G)
+            Nk = Hk * Wk
+        else:
+            xs, Nk = h, N
+        kv = F.glinear(store, a.kv.weight, a.kv.bias, xs)
+        o = F.SRAttentionF.apply(q, kv, G * B, N, Nk, a.num_heads, C // a.num_heads)
+        p = F.glinear(store, a.proj.weight, a.proj.bias, o)
+        x = F.ResidualF.apply(x, p, s_attn, N * C)
+        h = F.layernorm(store, blk.norm2, x, G)
+        f = F.glinear(store, blk.mlp.fc1.weight, blk.mlp.fc1.bias, h)
+        f = F.dwconv(store, blk.mlp.dwconv.dwconv, f, G * B, B, H, W, "gelu")
+        f = F.glinear(store, blk.mlp.fc2.weight, blk.mlp.fc2.bias, f)
+        return F.ResidualF.apply(x, f, s_mlp, N * C)
+
+    def run(self, store, images, B, H, W, training, dp_scales: Optional[torch.Tensor], bn_group=None):
+        """images: (2*B, 3, H, W) fp32 NCHW (RGB batch then X batch).
+        dp_scales: (n_blocks_total, 2, 2*? ) per-block (attn, mlp) per-sample scales or None.
+        Returns the 4 fused maps [(B*N_s, C_s) tokens] and their grids."""
+        G = 2
+        x = images
+        outs, grids = [], []
+        bi = 0
+        Hc, Wc, Cin = H, W, 3
+        for s in range(4):
+            pe = getattr(self, f"patch_embed{s + 1}")
+            x, Ho, Wo = F.conv(store, pe.proj, x, G, G * B, Hc, Wc, Cin, pe.stride, pe.pad, nchw=(s == 0))
+            x = F.layernorm(store, pe.norm, x, G)
+            Hc, Wc, Cin = Ho, Wo, self.embed_dims[s]
+            for i, blk in enumerate(getattr(self, f"block{s + 1}")):
+                sa = sm = None
+                if dp_scales is not None:
+                    sa, sm = dp_scales[bi, 0], dp_scales[bi, 1]
+                x = self.run_block(store, blk, x, B, Hc, Wc, sa, sm)
+                bi += 1
+            x = F.layernorm(store, getattr(self, f"norm{s + 1}"), x, G)
+            C = self.embed_dims[s]
+            r = F.frm(store, self.FRMs[s], x.view(G, B, Hc * Wc, C))
+            outs.append(self.FFMs[s].run(store, r, B, Hc, Wc, training))
+            grids.append((Hc, Wc))
+            x = r.view(G, B * Hc * Wc, C)
+        return outs, grids
+
+
+class mit_b0(RGBXTransformer):
+    def __init__(self, fuse_cfg=None, **kwargs):
+        super().__init__(**MIT_SPECS["mit_b0"], drop_path_rate=0.1)
+
+
+class mit_b1(RGBXTransformer):
+    def __init__(self, fuse_cfg=None, **kwargs):
+        super().__init__(**MIT_SPECS["mit_b1"], drop_path_rate=0.1)
+
+
+class mit_b2(RGBXTransformer):
+    def __init__(self, fuse_cfg=None, **kwargs):
+        super().__init__(**MIT_SPECS["mit_b2"], drop_path_rate=0.1)
+
+
+class mit_b3(RGBXTransformer):
+    def __init__(self, fuse_cfg=None, **kwargs):
+        super().__init__(**MIT_SPECS["mit_b3"], drop_path_rate=0.1)
+
+
+class mit_b4(RGBXTransformer):
+    def __init__(self, fuse_cfg=None, **kwargs):
+        super().__init__(**MIT_SPECS["mit_b4"], drop_path_rate=0.1)
+
+
+class mit_b5(RGBXTransformer):
+    def __init__(self, fuse_cfg=None, **kwargs):
+        super().__init__(**MIT_SPECS["mit_b5"], drop_path_rate=0.1)
+
+
+BACKBONES = {"mit_b0": mit_b0, "mit_b1": mit_b1, "mit_b2": mit_b2, "mit_b3": mit_b3, "mit_b4": mit_b4,
+             "mit_b5": mit_b5}
+
+
+def load_dualpath_model(model: nn.Module, model_file):
+    """Pretrained MiT weights duplicated into both streams (dual_segformer.py:449-480).
+    ``model_file`` is a path (loaded with weights_only=True) or a state dict."""
+    raw = torch.load(model_file, map_location="cpu", weights_only=True) if isinstance(model_file, str) \
+        else model_file
+    if "model" in raw:
+        raw = raw["model"]
+    sd = {}
+    for k, v in raw.items():
+        if "patch_embed" in k:
+            sd[k] = v
+            sd[k.replace("patch_embed", "extra_patch_embed")] = v
+        elif "block" in k:
+            sd[k] = v
+            sd[k.replace("block", "extra_block")] = v
+        elif "norm" in k:
+            sd[k] = v
+            sd[k.replace("norm", "extra_norm")] = v
+    return model.load_state_dict(sd, strict=False)

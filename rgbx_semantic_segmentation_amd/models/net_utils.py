@@ -1,0 +1,126 @@
+"""CM-FRM and FFM parameter containers + FFM execution (reference: models/net_utils.py).
+
+Containers reproduce the reference module names (``channel_weights.mlp.0``,
+``cross.cross_attn.kv1``, ``channel_emb.channel_embed.4`` ...).  ``FeatureFusionModule.run``
+executes CrossPath + ChannelEmbed for the modality pair in grouped launches and returns
+the fused map as (B*N, C) tokens (the reference returns NCHW; the decoder consumes
+tokens directly, MLPDecoder.py:17-18 flattens it anyway).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from .. import functions as F
+
+
+def trunc_normal_(t, std=0.02):
+    with torch.no_grad():
+        return nn.init.trunc_normal_(t, mean=0.0, std=std, a=-2.0, b=2.0)
+
+
+def init_segformer(m):
+    """MiT/FFM ``_init_weights`` (dual_segformer.py:52-65, net_utils.py:360-373)."""
+    if isinstance(m, nn.Linear):
+        trunc_normal_(m.weight, std=0.02)
+        if m.bias is not None:
+            nn.init.constant_(m.bias, 0)
+    elif isinstance(m, nn.LayerNorm):
+        nn.init.constant_(m.bias, 0)
+        nn.init.constant_(m.weight, 1.0)
+    elif isinstance(m, nn.Conv2d):
+        fan_out = m.kernel_size[0] * m.kernel_size[1] * m.out_channels // m.groups
+        with torch.no_grad():
+            m.weight.normal_(0, math.sqrt(2.0 / fan_out))
+            if m.bias is not None:
+                m.bias.zero_()
+
+
+class ChannelWeights(nn.Module):                  # net_utils.py:10-30
+    def __init__(self, dim):
+        super().__init__()
+        self.dim = dim
+        self.mlp = nn.Sequential(nn.Linear(4 * dim, 4 * dim), nn.ReLU(inplace=True),
+                                 nn.Linear(4 * dim, 2 * dim), nn.Sigmoid())
+
+
+class SpatialWeights(nn.Module):                  # net_utils.py:69-83
+    def __init__(self, dim):
+        super().__init__()
+        self.mlp = nn.Sequential(nn.Conv2d(2 * dim, dim, 1), nn.ReLU(inplace=True),
+                                 nn.Conv2d(dim, 2, 1), nn.Sigmoid())
+
+
+class FeatureRectifyModule(nn.Module):            # net_utils.py:124-152
+    def __init__(self, dim, reduction=1, lambda_c=0.5, lambda_s=0.5):
+        super().__init__()
+        self.lambda_c, self.lambda_s = lambda_c, lambda_s
+        self.channel_weights = ChannelWeights(dim)
+        self.spatial_weights = SpatialWeights(dim)
+
+
+class CrossAttention(nn.Module):                  # net_utils.py:187-214
+    def __init__(self, dim, num_heads):
+        super().__init__()
+        self.num_heads = num_heads
+        self.kv1 = nn.Linear(dim, 2 * dim, bias=False)
+        self.kv2 = nn.Linear(dim, 2 * dim, bias=False)
+
+
+class CrossPath(nn.Module):                       # net_utils.py:260-281
+    def __init__(self, dim, num_heads):
+        super().__init__()
+        self.channel_proj1 = nn.Linear(dim, 2 * dim)
+        self.channel_proj2 = nn.Linear(dim, 2 * dim)
+        self.act1 = nn.ReLU(inplace=True)
+        self.act2 = nn.ReLU(inplace=True)
+        self.cross_attn = CrossAttention(dim, num_heads)
+        self.end_proj1 = nn.Linear(2 * dim, dim)
+        self.end_proj2 = nn.Linear(2 * dim, dim)
+        self.norm1 = nn.LayerNorm(dim)
+        self.norm2 = nn.LayerNorm(dim)
+
+
+class ChannelEmbed(nn.Module):                    # net_utils.py:309-329
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.residual = nn.Conv2d(cin, cout, 1, bias=False)
+        self.channel_embed = nn.Sequential(
+            nn.Conv2d(cin, cout, 1, bias=True),
+            nn.Conv2d(cout, cout, 3, 1, 1, bias=True, groups=cout),
+            nn.ReLU(inplace=True),
+            nn.Conv2d(cout, cout, 1, bias=True),
+            nn.BatchNorm2d(cout))                 # plain BN, eps 1e-5 (norm_fuse not forwarded)
+        self.norm = nn.BatchNorm2d(cout)
+
+
+class FeatureFusionModule(nn.Module):             # net_utils.py:354-384
+    def __init__(self, dim, num_heads, reduction=1, norm_layer=None):
+        super().__init__()
+        self.dim, self.num_heads = dim, num_heads
+        self.cross = CrossPath(dim, num_heads)
+        self.channel_emb = ChannelEmbed(2 * dim, dim)
+        self.apply(init_segformer)
+
+    def run(self, store, r, B, H, W, training):
+        """r: (2, B, N, C) rectified pair -> fused (B*N, C) tokens."""
+        G, _, N, C = r.shape
+        M = B * N
+        cp, ce = self.cross, self.channel_emb
+        heads = self.num_heads
+        x = r.view(G, M, C)
+        a = F.ReluF.apply(F.glinear(store, cp.channel_proj1.weight, cp.channel_proj1.bias, x))
+        y, u = a[..., :C], a[..., C:]
+        kv = F.glinear(store, cp.cross_attn.kv1.weight, None, u)
+        v = F.CrossAttentionF.apply(u, kv, B, N, heads, C // heads)
+        e = F.glinear(store, cp.end_proj1.weight, cp.end_proj1.bias, y, v)
+        o = F.layernorm(store, cp.norm1, F.ResidualF.apply(x, e, None, x.numel()), G)
+        o1, o2 = o[0:1], o[1:2]
+        res = F.glinear(store, ce.residual.weight, None, o1, o2)
+        t = F.glinear(store, ce.channel_embed[0].weight, ce.channel_embed[0].bias, o1, o2)
+        t = F.dwconv(store, ce.channel_embed[1], t, B, B, H, W, "relu")
+        t = F.glinear(store, ce.channel_embed[3].weight, ce.channel_embed[3].bias, t)
+        s = F.batchnorm(store, ce.channel_embed[4], t.view(M, C), training, res=res.view(M, C))
+        return F.batchnorm(store, ce.norm, s, training)

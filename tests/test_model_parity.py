@@ -1,0 +1,146 @@
+"""End-to-end parity of the HIP EncoderDecoder with the CPU oracle (oracle/cmx_ref.py).
+
+* eval logits, fp32 compute: max|diff| / max|ref| < 1e-3 (BASELINE.json north star)
+* train mode with injected DropPath / Dropout2d masks, fp32: loss, every parameter
+  gradient and the BN running statistics
+* bf16 compute: logits within 5e-2 relative (bf16 storage of activations)
+The oracle runs in fp64 on the CPU on the same weights (state_dict copied)."""
+import pytest
+import torch
+
+from oracle.cmx_ref import EncoderDecoder as RefModel, CMXConfig, DropPath, Dropout2d
+
+pytestmark = pytest.mark.gpu
+
+
+def relerr(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+def make_pair(backbone, K, dtype, seed=0):
+    from rgbx_semantic_segmentation_amd.models.builder import EncoderDecoder
+    torch.manual_seed(seed)
+    ref = RefModel(CMXConfig(backbone=backbone, num_classes=K))
+    # non-trivial BN running statistics
+    g = torch.Generator().manual_seed(seed + 1)
+    for n, b in ref.named_buffers():
+        if n.endswith("running_mean"):
+            b.copy_(torch.rand(b.shape, generator=g) * 0.2 - 0.1)
+        elif n.endswith("running_var"):
+            b.copy_(torch.rand(b.shape, generator=g) + 0.5)
+    cfg = dict(backbone=backbone, num_classes=K, compute_dtype=dtype, decoder_embed_dim=512)
+    model = EncoderDecoder(cfg).cuda()
+    missing = model.load_state_dict(ref.state_dict(), strict=True)
+    return ref.double(), model
+
+
+def inputs(B, H, W, K, seed=3):
+    g = torch.Generator().manual_seed(seed)
+    rgb = torch.randn(B, 3, H, W, generator=g)
+    x = torch.randn(B, 1, H, W, generator=g).expand(B, 3, H, W).contiguous()
+    lab = torch.randint(0, K, (B, H, W), generator=g)
+    lab[:, 5:20, 7:30] = 255
+    return rgb, x, lab
+
+
+@pytest.mark.parametrize("backbone,H,W", [("mit_b0", 128, 160), ("mit_b2", 96, 128)])
+def test_eval_logits_fp32(dev, backbone, H, W):
+    K = 9
+    ref, model = make_pair(backbone, K, "float32")
+    ref.eval(); model.eval()
+    rgb, x, _ = inputs(2, H, W, K)
+    with torch.no_grad():
+        out_ref = ref(rgb.double(), x.double())
+        out = model(rgb.cuda(), x.cuda())
+    torch.cuda.synchronize()
+    assert out.shape == out_ref.shape and out.dtype == torch.float32
+    e = relerr(out, out_ref)
+    print(backbone, "eval logits rel err", e)
+    assert e < 1e-3
+
+
+def test_eval_logits_bf16(dev):
+    K = 9
+    ref, model = make_pair("mit_b0", K, "bfloat16")
+    ref.eval(); model.eval()
+    rgb, x, _ = inputs(2, 128, 160, K)
+    with torch.no_grad():
+        out_ref = ref(rgb.double(), x.double())
+        out = model(rgb.cuda(), x.cuda())
+    e = relerr(out, out_ref)
+    print("bf16 eval logits rel err", e)
+    assert e < 5e-2
+
+
+def _inject(ref, model, B, seed=7):
+    """Same stochastic masks in oracle and product."""
+    g = torch.Generator().manual_seed(seed)
+    bb = model.backbone
+    nb = sum(bb.depths)
+    flags = torch.ones(nb, 2, 2 * B)
+    bi = 0
+    for s in range(4):
+        for i in range(bb.depths[s]):
+            for stream, pre in enumerate(("", "extra_")):
+                rblk = getattr(ref.backbone, f"{pre}block{s + 1}")[i]
+                if isinstance(rblk.drop_path, DropPath):
+                    mk = [(torch.rand(B, generator=g) > 0.3).double() for _ in range(2)]
+                    rblk.drop_path.masks = [m.clone() for m in mk]
+                    for br in range(2):
+                        flags[bi, br, stream * B:(stream + 1) * B] = mk[br].float()
+            bi += 1
+    d2 = (torch.rand(B, 512, generator=g) > 0.1).double()
+    ref.decode_head.dropout.mask = d2
+    model.forced_masks = {"droppath": flags, "dropout2d": d2.float()}
+
+
+@pytest.mark.parametrize("backbone,H,W", [("mit_b0", 128, 160), ("mit_b2", 96, 128)])
+def test_train_step_grads_fp32(dev, backbone, H, W):
+    """Per-parameter gradient error e = max|g - g64| / max(max|g64|, 1e-6 * gmax) must be
+    <= 2e-3, or <= 10x the error of the same oracle run in plain fp32 on the CPU (sums over
+    thousands of tokens of gradients that are mathematically ~0, e.g. a bias feeding a
+    BatchNorm, have no meaningful relative error in any fp32 implementation)."""
+    K = 9
+    ref, model = make_pair(backbone, K, "float32")
+    ref32 = RefModel(CMXConfig(backbone=backbone, num_classes=K))
+    ref32.load_state_dict(ref.state_dict())
+    ref.train(); model.train(); ref32.train()
+    B = 2
+    rgb, x, lab = inputs(B, H, W, K)
+    _inject(ref, model, B)
+    model.forced_masks = None
+    _inject(ref32, model, B)
+    loss_ref = ref(rgb.double(), x.double(), lab)
+    loss_ref.backward()
+    ref32(rgb, x, lab).backward()
+    loss = model(rgb.cuda(), x.cuda(), lab.cuda())
+    loss.backward()
+    torch.cuda.synchronize()
+    assert abs(loss.item() - loss_ref.item()) / abs(loss_ref.item()) < 1e-4, (loss.item(), loss_ref.item())
+    ref_params = dict(ref.named_parameters())
+    r32 = dict(ref32.named_parameters())
+    gmax = max(p.grad.abs().max().item() for p in ref.parameters())
+    bad = []
+    worst = []
+    for n, p in model.named_parameters():
+        gr = ref_params[n].grad
+        assert gr is not None, n
+        den = max(gr.abs().max().item(), 1e-6 * gmax)
+        e = (p.grad.detach().double().cpu() - gr).abs().max().item() / den
+        e32 = (r32[n].grad.double() - gr).abs().max().item() / den
+        worst.append((e, e32, n))
+        if e > max(2e-3, 10 * e32):
+            bad.append((e, e32, n, gr.abs().max().item()))
+    worst.sort(reverse=True)
+    print("worst grads (gpu err, cpu-fp32 err, name)", worst[:6])
+    # ReLU kinks: a pre-activation within fp32 rounding of 0 (seen: +3.6e-9 in fp64, -1.8e-8
+    # in fp32) flips one mask element and moves a cancellation-dominated weight gradient by a
+    # few percent.  Allow a bounded number of such outliers, each still < 5e-2.
+    n_allowed = max(2, len(worst) // 100)
+    assert len(bad) <= n_allowed and all(b[0] < 5e-2 for b in bad), bad[:8]
+    for (n, b) in model.named_buffers():
+        if "running" in n:
+            e = relerr(b, dict(ref.named_buffers())[n])
+            assert e < 1e-4, (n, e)
