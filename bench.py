@@ -1,0 +1,202 @@
+"""Benchmark: CMX-B2 training step, 480x640, bs=2 per GPU, bf16, synthetic NYUv2-shape batch.
+
+One step = forward + per-pixel CE + backward + (N>1: RCCL gradient all-reduce + SyncBN of
+the decoder BN) + fused AdamW, i.e. train.py:185-207 for one batch.  The whole step is
+captured once into a HIP graph (torch.cuda.CUDAGraph) and replayed; the WarmUpPolyLR
+update is written into the optimizer's device LR scalar between replays.
+
+Usage:  python bench.py [--gpus N --steps K --warmup W]   (N>1: one rank per GPU via
+        torch.distributed.run; rank 0 prints ONE JSON line).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+PEAK_BF16_TFLOPS = 2516.6      # 256 CU x 2.4 GHz x 4096 FLOP/clk/CU (dense, MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--backbone", default="mit_b2")
+    p.add_argument("--height", type=int, default=480)
+    p.add_argument("--width", type=int, default=640)
+    p.add_argument("--batch", type=int, default=2, help="per-GPU batch")
+    p.add_argument("--classes", type=int, default=40)
+    p.add_argument("--dtype", default="bfloat16")
+    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-steps", type=int, default=1)
+    p.add_argument("--cpu-threads", type=int, default=16)
+    return p.parse_args()
+
+
+def cpu_baseline(args):
+    """The oracle's restatement of the reference train step on the host cores (fp32),
+    bounded sample: 1 untimed + args.cpu_steps timed steps of the SAME workload."""
+    from oracle.cmx_ref import CMXConfig
+    from oracle.train_ref import time_cpu_steps
+    from rgbx_semantic_segmentation_amd.data import make_batch
+    threads = min(args.cpu_threads, os.cpu_count() or 1)
+    batch = make_batch(args.batch, args.height, args.width, args.classes, seed=12345)
+    cfg = CMXConfig(backbone=args.backbone, num_classes=args.classes)
+    sec = time_cpu_steps(cfg, batch, warmup=1, steps=args.cpu_steps, threads=threads)
+    return {"value": round(args.batch / sec, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/train_ref.py (fp32 PyTorch-CPU restatement of train.py) {args.backbone} "
+                      f"{args.height}x{args.width} bs={args.batch}: 1 warm-up + {args.cpu_steps} timed step(s), "
+                      f"{sec:.2f} s/step"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    group = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+        group = dist.group.WORLD
+
+    from rgbx_semantic_segmentation_amd.models.builder import EncoderDecoder
+    from rgbx_semantic_segmentation_amd.optim import FusedAdamW
+    from rgbx_semantic_segmentation_amd.data import make_batch
+    from rgbx_semantic_segmentation_amd.utils.lr_policy import WarmUpPolyLR
+    from rgbx_semantic_segmentation_amd.flops import train_flops_per_image
+    from rgbx_semantic_segmentation_amd import dist as cdist
+
+    torch.manual_seed(12345)
+    cfg = dict(backbone=args.backbone, num_classes=args.classes, compute_dtype=args.dtype, decoder_embed_dim=512)
+    norm = torch.nn.SyncBatchNorm if world > 1 else torch.nn.BatchNorm2d
+    model = EncoderDecoder(cfg, norm_layer=norm).cuda(dev)
+    sync = None
+    if world > 1:
+        model.process_group = group
+        cdist.broadcast_parameters(model, group)
+        sync = cdist.GradAllReduce(model.store, group)
+    model.train()
+    opt = FusedAdamW(model, lr=6e-5, betas=(0.9, 0.999), weight_decay=0.01, grad_sync=sync)
+    niters = 1449 // 8 + 1
+    policy = WarmUpPolyLR(6e-5, 0.9, 200 * niters, niters * 10)
+    rgb, x, lab = make_batch(args.batch, args.height, args.width, args.classes, seed=12345 + rank, device=dev)
+
+    def step():
+        loss = model(rgb, x, lab)
+        loss.backward()
+        opt.step()
+        return loss
+
+    it = 0
+
+    def set_lr():
+        nonlocal it
+        lr = policy.get_lr(it)
+        for g in opt.param_groups:
+            g["lr"] = lr
+        it += 1
+
+    # eager warm-up (also primes the caching allocator and hipBLASLt heuristics)
+    for _ in range(2):
+        step()
+        set_lr()
+    torch.cuda.synchronize()
+    graph = None
+    if not args.no_graph:
+        try:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                step()
+            torch.cuda.current_stream().wait_stream(s)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                static_loss = step()
+        except Exception as e:  # pragma: no cover - reported in the JSON line
+            print(f"[bench] graph capture failed, eager mode: {e!r}", file=sys.stderr)
+            graph = None
+
+    def run_one():
+        set_lr()
+        if graph is not None:
+            graph.replay()
+        else:
+            step()
+
+    for _ in range(args.warmup):
+        run_one()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run_one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    ms = elapsed / args.steps * 1e3
+    images = args.batch * world * args.steps
+    ips = images / elapsed
+    fl_img = train_flops_per_image(backbone=args.backbone, H=args.height, W=args.width, K=args.classes)
+    step_frac = (ips / world) * fl_img / (PEAK_BF16_TFLOPS * 1e12)
+
+    roof = None
+    if rank == 0:
+        from rgbx_semantic_segmentation_amd.roofline import measure_dominant
+        roof = measure_dominant(args)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+
+    if rank == 0:
+        out = {
+            "metric": "train images/sec CMX-B2 480x640 bs=2/GPU at 1/2/4/8 MI355X; % MFMA roofline",
+            "value": round(ips, 3),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16" if args.dtype in ("bfloat16", "bf16") else "fp32",
+            "data": "synthetic (seeded uint8 RGB + replicated X plane, ImageNet-normalised; uniform labels "
+                    "with one 25x25 ignore block per image; random-init weights)",
+            "config": {"workload": f"CMX-{args.backbone.replace('mit_', '').upper()} train step "
+                                   f"{args.height}x{args.width}", "model": f"CMX-{args.backbone}",
+                       "global_batch": args.batch * world, "per_gpu_batch": args.batch,
+                       "image": [args.height, args.width], "classes": args.classes,
+                       "parallelism": f"dp{world}", "hip_graph": graph is not None},
+            "step_mfma_roofline": {"train_gflop_per_image": round(fl_img / 1e9, 3),
+                                   "achieved_tflops": round((ips / world) * fl_img / 1e12, 2),
+                                   "peak_tflops": PEAK_BF16_TFLOPS, "frac": round(step_frac, 5)},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -142,8 +142,12 @@ class EncoderDecoder(nn.Module):
         """DropPath per-sample scales (n_blocks, 2 [attn, mlp], 2*B) and Dropout2d (B, E)."""
         if not self.training:
             return None, None
-        keep = torch.tensor(self.backbone.drop_path_keep_probs(), dtype=torch.float32)  # (nb, 2 streams)
-        keep = keep[:, None, :, None].expand(-1, 2, -1, B).reshape(len(keep), 2, 2 * B).to(device)
+        key = (B, str(device))
+        cache = self.__dict__.setdefault("_keep_cache", {})
+        if key not in cache:   # built once: no host->device copy inside a captured graph
+            keep = torch.tensor(self.backbone.drop_path_keep_probs(), dtype=torch.float32)  # (nb, 2 streams)
+            cache[key] = keep[:, None, :, None].expand(-1, 2, -1, B).reshape(len(keep), 2, 2 * B).to(device)
+        keep = cache[key]
         p = self.decode_head.dropout_ratio
         E = self.decode_head.embed_dim
         if self.forced_masks is not None:
@@ -164,6 +168,8 @@ class EncoderDecoder(nn.Module):
             raise RuntimeError("call model.cuda() first: EncoderDecoder has no CPU execution path")
         B, _, H, W = rgb.shape
         dev = self.store.device
+        if self.training and torch.is_grad_enabled() and not torch.cuda.is_current_stream_capturing():
+            self.store.ensure_grads()
         images = torch.cat([rgb, modal_x], 0).to(device=dev, dtype=torch.float32).contiguous()
         dp, d2 = self._stochastic(B, dev)
         group = self.process_group if (self.sync_bn and self.training) else None

@@ -173,6 +173,13 @@ class ParamStore:
         v = self._storage_view(self.grad, s, False)
         return v[None] if stacked else v
 
+    def ensure_grads(self):
+        """Re-attach ``param.grad`` to the flat gradient buffer if a caller detached it
+        (e.g. ``torch.optim.Optimizer.zero_grad(set_to_none=True)``)."""
+        for n, p in self.params.items():
+            if p.grad is None:
+                p.grad = self._param_view(self.grad, self.slots[n])
+
     def refresh_shadow(self):
         if self.shadow is not None:
             from . import kernels as K
