@@ -84,6 +84,7 @@ size_t cmx_frm_pool_workspace(int B, int N, int C);
 int cmx_frm_pool_fwd(const void* x, float* pooled, int* argmax, float* workspace, int B, int N, int C, int dtype, hipStream_t stream);
 int cmx_frm_pool_bwd(const float* dpooled, const int* argmax, void* dx, int B, int N, int C, int dtype, hipStream_t stream);
 int cmx_small_linear_fwd(const float* x, const float* w, const float* b, float* y, int M, int K, int Nout, int act, hipStream_t stream);
+size_t cmx_small_linear_bwd_workspace(int M, int K, int Nout);
 int cmx_small_linear_bwd(const float* dy, const float* y, const float* x, const float* w, float* dx, float* dw, float* db, float* dz_ws, int M, int K, int Nout, int act, int accumulate, hipStream_t stream);
 int cmx_frm_spatial_fwd(const void* h, const float* w2, const float* b2, float* sw, int64_t rows, int C, int dtype, hipStream_t stream);
 size_t cmx_frm_spatial_bwd_workspace(int64_t rows, int C);

@@ -51,13 +51,21 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, 
   }
 }
 
-// sums (2, C) = sum over blocks of ws (nblk, 2, C)
-__global__ void bn_sum_blocks_kernel(const double* __restrict__ ws, double* __restrict__ sums, int nblk, int C) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= 2 * C) return;
-  double a = 0.0;
-  for (int b = 0; b < nblk; ++b) a += ws[(long)b * 2 * C + e];
-  sums[e] = a;
+// sums (2, C) = sum over blocks of ws (nblk, 2, C); 64 columns x 4 row slices per block
+__global__ __launch_bounds__(256) void bn_sum_blocks_kernel(const double* __restrict__ ws, double* __restrict__ sums,
+                                                            int nblk, int C) {
+  __shared__ double red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + tx;
+  double a0 = 0.0, a1 = 0.0;
+  if (e < 2 * C) {
+    int b = ty;
+    for (; b + 4 < nblk; b += 8) { a0 += ws[(long)b * 2 * C + e]; a1 += ws[(long)(b + 4) * 2 * C + e]; }
+    for (; b < nblk; b += 4) a0 += ws[(long)b * 2 * C + e];
+  }
+  red[ty][tx] = a0 + a1;
+  __syncthreads();
+  if (ty == 0 && e < 2 * C) sums[e] = ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx];
 }
 
 __global__ void bn_finalize_kernel(const double* __restrict__ sums, double count, float eps, float momentum,
@@ -227,7 +235,7 @@ int cmx_bn_stats(const void* x, double* sums, double* workspace, int64_t M, int 
     hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(nb, cdiv(C / V, TPR)), dim3(256), 0, s, (const T*)x, workspace,
                        (long)M, C);
   });
-  hipLaunchKernelGGL(bn_sum_blocks_kernel, dim3(cdiv(2 * C, 256)), dim3(256), 0, s, workspace, sums, nb, C);
+  hipLaunchKernelGGL(bn_sum_blocks_kernel, dim3(cdiv(2 * C, 64)), dim3(256), 0, s, workspace, sums, nb, C);
   return cmx_check_launch("bn_stats");
 }
 
@@ -270,7 +278,7 @@ int cmx_bn_bwd_reduce(const void* dy, const void* x, const float* mean, const fl
                        (const T*)x, mean, invstd, gamma, beta, (const T*)res, dscale, workspace, (long)M, C,
                        (long)rows_per_sample, act);
   });
-  hipLaunchKernelGGL(bn_sum_blocks_kernel, dim3(cdiv(2 * C, 256)), dim3(256), 0, s, workspace, sums, nb, C);
+  hipLaunchKernelGGL(bn_sum_blocks_kernel, dim3(cdiv(2 * C, 64)), dim3(256), 0, s, workspace, sums, nb, C);
   hipLaunchKernelGGL(bn_param_grad_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, sums, dgamma, dbeta, C, accumulate);
   return cmx_check_launch("bn_bwd_reduce");
 }

@@ -196,7 +196,7 @@ int ctx_nchunk(int N, int BH) {
 extern "C" {
 
 size_t cmx_ffm_ctx_workspace(int BH, int N, int D) {
-  return (size_t)ctx_nchunk(N, BH) * BH * D * D * sizeof(float);
+  return ((size_t)ctx_nchunk(N, BH) + 1) * BH * D * D * sizeof(float);
 }
 
 // out (BH, D, D) fp32 = finalize(sum_n X^T Y); mode 0: alpha*sum; 1: softmax over dim -2 of
@@ -211,9 +211,12 @@ int cmx_ffm_ctx_reduce(const void* X, const void* Y, const float* ctx, float* ou
   const int nc = ctx_nchunk(N, BH);
   const int chunk = (N + nc - 1) / nc;
   CTX_D_DISPATCH(D, CMX_DISPATCH(dtype, T, {
+    float* sum = workspace + (size_t)nc * BH * DD * DD;
     hipLaunchKernelGGL((ctx_reduce_kernel<T, DD>), dim3(nc, BH), dim3(256), 0, s, (const T*)X, (const T*)Y,
                        workspace, N, heads, (long)xs, (long)ys, chunk, nc, BH);
-    hipLaunchKernelGGL((ctx_finalize_kernel<DD>), dim3(BH), dim3(64), 0, s, workspace, ctx, out, nc, BH, mode,
+    const int st = cmx_reduce_partials(workspace, sum, 1, nc, BH * DD * DD, 0, 1.f, s);
+    if (st) return st;
+    hipLaunchKernelGGL((ctx_finalize_kernel<DD>), dim3(BH), dim3(64), 0, s, sum, ctx, out, 1, BH, mode,
                        alpha, swapB, heads);
   }));
   return cmx_check_launch("ffm_ctx_reduce");

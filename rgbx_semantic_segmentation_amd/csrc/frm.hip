@@ -84,15 +84,34 @@ __global__ void small_linear_dz_kernel(const float* __restrict__ dy, const float
     dz[i] = dy[i] * act_grad_from_out(y[i], act);
 }
 
-// dx[m][k] = sum_n dz[m][n] w[n][k]
-__global__ void small_linear_dx_kernel(const float* __restrict__ dz, const float* __restrict__ w, float* __restrict__ dx,
-                                       int M, int K, int Nout) {
-  const long total = (long)M * K;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int k = i % K, m = i / K;
-    float s = 0.f;
-    for (int n = 0; n < Nout; ++n) s += dz[(long)m * Nout + n] * w[(long)n * K + k];
-    dx[i] = s;
+// partial dx over an n-slice: ws[slice][m][k] = sum_{n in slice} dz[m][n] w[n][k].
+// Block = 64 k-columns x 4 n-subslices (coalesced W rows), grid = (K/64, NSLICE).
+constexpr int DX_NSLICE = 16;
+constexpr int DX_MMAX = 8;
+__global__ __launch_bounds__(256) void small_linear_dx_kernel(const float* __restrict__ dz, const float* __restrict__ w,
+                                                              float* __restrict__ ws, int M, int K, int Nout) {
+  __shared__ float red[4][DX_MMAX][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + tx;
+  const int per = (Nout + DX_NSLICE - 1) / DX_NSLICE;
+  const int n0 = blockIdx.y * per, n1 = min(Nout, n0 + per);
+  float acc[DX_MMAX];
+#pragma unroll
+  for (int m = 0; m < DX_MMAX; ++m) acc[m] = 0.f;
+  if (k < K) {
+    for (int n = n0 + ty; n < n1; n += 4) {
+      const float wv = w[(long)n * K + k];
+#pragma unroll
+      for (int m = 0; m < DX_MMAX; ++m)
+        if (m < M) acc[m] += dz[(long)m * Nout + n] * wv;
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < DX_MMAX; ++m) red[ty][m][tx] = acc[m];
+  __syncthreads();
+  if (ty == 0 && k < K) {
+    for (int m = 0; m < M; ++m)
+      ws[((long)blockIdx.y * M + m) * K + k] = ((red[0][m][tx] + red[1][m][tx]) + red[2][m][tx]) + red[3][m][tx];
   }
 }
 
@@ -321,6 +340,11 @@ int spatial_nblk(long rows) {
 
 extern "C" {
 
+// dz_ws of cmx_small_linear_bwd: M*Nout + 16*M*K floats
+size_t cmx_small_linear_bwd_workspace(int M, int K, int Nout) {
+  return ((size_t)M * Nout + (size_t)DX_NSLICE * M * K) * sizeof(float);
+}
+
 size_t cmx_frm_pool_workspace(int B, int N, int C) {
   const int nc = pool_nchunk(N, 2 * B);
   return (size_t)2 * B * nc * C * 3 * sizeof(float);
@@ -363,8 +387,14 @@ int cmx_small_linear_bwd(const float* dy, const float* y, const float* x, const 
                          float* db, float* dz_ws, int M, int K, int Nout, int act, int accumulate, hipStream_t s) {
   hipLaunchKernelGGL(small_linear_dz_kernel, dim3(gridcap((long)M * Nout)), dim3(256), 0, s, dy, y, dz_ws,
                      (long)M * Nout, act);
-  if (dx)
-    hipLaunchKernelGGL(small_linear_dx_kernel, dim3(gridcap((long)M * K)), dim3(256), 0, s, dz_ws, w, dx, M, K, Nout);
+  CMX_REQUIRE(M <= DX_MMAX, CMX_ERR_SHAPE, "small_linear_bwd: M=%d > %d", M, DX_MMAX);
+  if (dx) {
+    float* part = dz_ws + (size_t)M * Nout;   // DX_NSLICE * M * K floats after dz
+    hipLaunchKernelGGL(small_linear_dx_kernel, dim3(cdiv(K, 64), DX_NSLICE), dim3(256), 0, s, dz_ws, w, part, M, K,
+                       Nout);
+    const int st = cmx_reduce_partials(part, dx, 1, DX_NSLICE, M * K, 0, 1.f, s);
+    if (st) return st;
+  }
   hipLaunchKernelGGL(small_linear_dw_kernel, dim3(gridcap((long)Nout * K)), dim3(256), 0, s, dz_ws, x, dw, db, M, K,
                      Nout, accumulate);
   return cmx_check_launch("small_linear_bwd");

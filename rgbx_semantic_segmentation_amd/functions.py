@@ -367,7 +367,7 @@ class FRMF(Function):
         _wgrad(dh[None], x2[None], gW0[:, C:][None])
         K.colsum(dh, gb0.view(1, C), G=1)
         # channel MLP backward (sigmoid then relu), then pooling backward
-        dz = torch.empty(B * 4 * C, dtype=torch.float32, device=x.device)
+        dz = K._ws(K.query("cmx_small_linear_bwd_workspace", B, 4 * C, 4 * C), x.device)
         dy1 = torch.empty(B, 4 * C, dtype=torch.float32, device=x.device)
         K.call("cmx_small_linear_bwd", K.ptr(dcw), K.ptr(cw), K.ptr(y1), K.ptr(W2f), K.ptr(dy1), K.ptr(gW2),
                K.ptr(gb2), K.ptr(dz), B, 4 * C, 2 * C, 3, 0, K.stream())
@@ -397,6 +397,17 @@ def frm(store, mod, x):
 
 
 # ---------------------------------------------------------------------------- BatchNorm
+def sync_bn_sums(sums: torch.Tensor, count: float, group) -> float:
+    """SyncBatchNorm exchange (MLPDecoder.py:53 under train.py:64-65): all-reduce the fp64
+    per-channel sums over the ranks of ``group`` in place; return the global row count
+    (equal per-rank batches, dataloader.py:155).  No-op without a group."""
+    if group is None:
+        return count
+    import torch.distributed as dist
+    dist.all_reduce(sums, group=group)
+    return count * dist.get_world_size(group)
+
+
 class BatchNormF(Function):
     @staticmethod
     def forward(ctx, x, res, prm, training, act, dscale, rps, group, anchor):
@@ -410,10 +421,7 @@ class BatchNormF(Function):
             sums = torch.empty(2, C, dtype=torch.float64, device=x.device)
             ws = torch.empty(max(1, K.query("cmx_bn_workspace", M, C) // 8), dtype=torch.float64, device=x.device)
             K.call("cmx_bn_stats", K.ptr(x), K.ptr(sums), K.ptr(ws), M, C, dt, K.stream())
-            if group is not None:
-                import torch.distributed as dist
-                dist.all_reduce(sums, group=group)
-                count *= dist.get_world_size(group)
+            count = sync_bn_sums(sums, count, group)
             K.call("cmx_bn_finalize", K.ptr(sums), count, eps, momentum, K.ptr(rm), K.ptr(rv), K.ptr(mean),
                    K.ptr(invstd), C, 1, K.stream())
         else:
@@ -440,9 +448,8 @@ class BatchNormF(Function):
         K.call("cmx_bn_bwd_reduce", K.ptr(dy), K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(gamma), K.ptr(beta),
                K.ptr(res), K.ptr(dscale), K.ptr(sums), K.ptr(gg), K.ptr(bg), K.ptr(ws), M, C, rps, K.ACT[act], 0, dt,
                K.stream())
-        if training and group is not None:
-            import torch.distributed as dist
-            dist.all_reduce(sums, group=group)
+        if training:
+            sync_bn_sums(sums, count, group)
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if has_res else None
         K.call("cmx_bn_bwd_apply", K.ptr(dy), K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(gamma), K.ptr(beta),

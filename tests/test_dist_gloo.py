@@ -1,0 +1,67 @@
+"""Multi-process (world_size 2, gloo, CPU) tests of the data-parallel host logic:
+* the flat-gradient all-reduce + 1/P scale equals DDP's average of per-rank gradients of the
+  per-rank mean loss (train.py:141-149);
+* SyncBN statistics from all-reduced fp64 sums equal the global-batch statistics.
+"""
+import os
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rgbx_semantic_segmentation_amd.dist import GradAllReduce, all_reduce_tensor
+        from rgbx_semantic_segmentation_amd.functions import sync_bn_sums
+        torch.manual_seed(0)
+        # a tiny model, per-rank data slices of one global batch
+        w = torch.randn(6, 4, dtype=torch.float64)
+        X = torch.randn(world * 5, 4, dtype=torch.float64)
+        Y = torch.randn(world * 5, 6, dtype=torch.float64)
+        xs, ys = X[rank * 5:(rank + 1) * 5], Y[rank * 5:(rank + 1) * 5]
+        wr = w.clone().requires_grad_(True)
+        ((xs @ wr.t() - ys) ** 2).mean().backward()
+
+        class Store:
+            pass
+        st = Store()
+        st.grad = wr.grad.flatten().clone()
+        scale = GradAllReduce(st, None)(st.grad)
+        ours = st.grad * scale
+        # DDP reference: mean over ranks of per-rank gradients
+        ref = torch.zeros_like(w)
+        for r in range(world):
+            wr2 = w.clone().requires_grad_(True)
+            ((X[r * 5:(r + 1) * 5] @ wr2.t() - Y[r * 5:(r + 1) * 5]) ** 2).mean().backward()
+            ref += wr2.grad / world
+        ok1 = torch.allclose(ours.view_as(w), ref)
+        # SyncBN sums
+        feats = torch.randn(world * 7, 3, dtype=torch.float64)
+        mine = feats[rank * 7:(rank + 1) * 7]
+        sums = torch.stack([mine.sum(0), (mine * mine).sum(0)])
+        count = sync_bn_sums(sums, 7.0, dist.group.WORLD)
+        mean = sums[0] / count
+        var = sums[1] / count - mean ** 2
+        ok2 = count == world * 7 and torch.allclose(mean, feats.mean(0)) and torch.allclose(var, feats.var(0, unbiased=False))
+        loss = all_reduce_tensor(torch.tensor([float(rank)]), world_size=world)
+        ok3 = abs(loss.item() - (world - 1) / 2) < 1e-12
+        q.put((rank, bool(ok1), bool(ok2), bool(ok3)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_semantics_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + (os.getpid() % 1000)
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[1] and r[2] and r[3] for r in res), res
