@@ -46,6 +46,7 @@ int cmx_residual_add(const void* x, const void* y, const float* sample_scale, vo
 int cmx_scale_samples(const void* x, const float* sample_scale, void* out, int64_t n_per_sample, int64_t n, int dtype, hipStream_t stream);
 int cmx_act_fwd(const void* x, void* y, int64_t n, int act, int dtype, hipStream_t stream);
 int cmx_act_bwd(const void* dy, const void* z, void* dx, int64_t n, int act, int dtype, hipStream_t stream);
+int cmx_partials_sum(const float* ws, float* out, int G, int nblk, int W, int accumulate, float alpha, hipStream_t stream);
 int cmx_cast_f32_bf16(const float* src, void* dst, int64_t n, hipStream_t stream);
 size_t cmx_colsum_workspace(int64_t M, int G, int N);
 int cmx_colsum(const void* x, float* out, float* workspace, int64_t M, int G, int N, int64_t ld, int accumulate, float alpha, int dtype, hipStream_t stream);

@@ -23,7 +23,7 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
   const float bc2s = sqrtf(1.f - powf(b2, t));
   const float step_size = lr / bc1;
   const long nv = n / 4;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (long)gridDim.x * blockDim.x) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)nv; i += gridDim.x * blockDim.x) {
     const long e = i * 4;
     float4 pp = *reinterpret_cast<float4*>(p + e);
     float4 gg = *reinterpret_cast<const float4*>(g + e);

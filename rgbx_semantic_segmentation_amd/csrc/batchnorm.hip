@@ -114,13 +114,13 @@ __global__ void bn_apply_kernel(const T* __restrict__ x, const float* __restrict
                                 const float* __restrict__ dscale, T* __restrict__ y, long M, int C, long rps, int act) {
   constexpr int V = VecT<T>::N;
   const long nvec = M * C / V;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
-    const long e = i * V;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)nvec; i += gridDim.x * blockDim.x) {
+    const int e = i * V;
     const int c0 = e % C;
     float xh[V], pre[V];
     bn_pre<T>(x, res, mean, invstd, gamma, beta, e, c0, xh, pre);
     float o[V];
-    const long b = (e / C) / rps;
+    const int b = (e / C) / (int)rps;
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       o[j] = act_fwd(pre[j], act);
@@ -191,13 +191,13 @@ __global__ void bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restric
                                     int training) {
   constexpr int V = VecT<T>::N;
   const long nvec = M * C / V;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
-    const long e = i * V;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)nvec; i += gridDim.x * blockDim.x) {
+    const int e = i * V;
     const int c0 = e % C;
     float xh[V], pre[V], d[V], o[V], gr[V];
     bn_pre<T>(x, res, mean, invstd, gamma, beta, e, c0, xh, pre);
     load_vec<T>(dy + e, d);
-    const long b = (e / C) / rps;
+    const int b = (e / C) / (int)rps;
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       const int c = c0 + j;

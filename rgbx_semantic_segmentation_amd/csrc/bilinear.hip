@@ -27,12 +27,12 @@ __global__ void bilinear_fwd_nhwc_kernel(const T* __restrict__ in, T* __restrict
   constexpr int V = VecT<T>::N;
   const int CPR = C / V;
   const long total = (long)NB * Ho * Wo * CPR;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)total; i += gridDim.x * blockDim.x) {
     const int ch = i % CPR;
-    const long pix = i / CPR;
+    const int pix = i / CPR;
     const int x = pix % Wo;
     const int y = (pix / Wo) % Ho;
-    const int n = pix / ((long)Wo * Ho);
+    const int n = pix / (Wo * Ho);
     int y0, y1, x0, x1;
     float ly0, ly1, lx0, lx1;
     src_index(y, sh, Hi, y0, y1, ly0, ly1);
@@ -54,11 +54,11 @@ template <typename T>
 __global__ void bilinear_fwd_nchw_kernel(const T* __restrict__ in, float* __restrict__ out, int NB, int Hi, int Wi,
                                          int Ho, int Wo, int C, float sh, float sw) {
   const long total = (long)NB * C * Ho * Wo;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)total; i += gridDim.x * blockDim.x) {
     const int x = i % Wo;
     const int y = (i / Wo) % Ho;
-    const int c = (i / ((long)Wo * Ho)) % C;
-    const int n = i / ((long)Wo * Ho * C);
+    const int c = (i / (Wo * Ho)) % C;
+    const int n = i / (Wo * Ho * C);
     int y0, y1, x0, x1;
     float ly0, ly1, lx0, lx1;
     src_index(y, sh, Hi, y0, y1, ly0, ly1);
@@ -79,10 +79,10 @@ __global__ void bilinear_adj_kernel(const TI* __restrict__ in, TO* __restrict__ 
   const float alpha = alpha0 * (a1 ? *a1 : 1.f) * (a2 ? *a2 : 1.f);
   const long total = P * Li * Q;
   const float inv = 1.f / scale;  // out/in
-  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < (int)total; e += gridDim.x * blockDim.x) {
     const int q = e % Q;
     const int i = (e / Q) % Li;
-    const long p = e / ((long)Q * Li);
+    const int p = e / (Q * Li);
     int olo = (int)floorf((i - 1.5f) * inv) - 1;
     int ohi = (int)ceilf((i + 1.5f) * inv) + 1;
     if (olo < 0) olo = 0;

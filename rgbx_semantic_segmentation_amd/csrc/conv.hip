@@ -18,13 +18,13 @@ __global__ void im2col_nhwc_kernel(const T* __restrict__ x, T* __restrict__ cols
   const int CPT = C / V;                       // chunks per tap
   const int taps = KH * KW;
   const long total = (long)NI * Ho * Wo * taps * CPT;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)total; i += gridDim.x * blockDim.x) {
     const int ch = i % CPT;
     const int tap = (i / CPT) % taps;
-    const long row = i / ((long)CPT * taps);
+    const int row = i / (CPT * taps);
     const int ox = row % Wo;
     const int oy = (row / Wo) % Ho;
-    const int n = row / ((long)Wo * Ho);
+    const int n = row / (Wo * Ho);
     const int iy = oy * stride - pad + tap / KW;
     const int ix = ox * stride - pad + tap % KW;
     float v[V];
@@ -43,7 +43,7 @@ template <typename T>
 __global__ void zero_pad_cols_kernel(T* __restrict__ cols, long rows, int K, long ldc) {
   const int padw = (int)(ldc - K);
   const long total = rows * padw;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x)
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)total; i += gridDim.x * blockDim.x)
     cols[(i / padw) * ldc + K + i % padw] = from_f32<T>(0.f);
 }
 
@@ -53,9 +53,9 @@ __global__ void im2col_nchw_kernel(const float* __restrict__ x, T* __restrict__ 
                                    int W, int KH, int KW, int stride, int pad, int Ho, int Wo, long ldc) {
   const int K = C * KH * KW;
   const long total = (long)NI * Ho * Wo * ldc;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int k = i % ldc;
-    const long row = i / ldc;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)total; i += gridDim.x * blockDim.x) {
+    const int k = i % (int)ldc;
+    const int row = i / (int)ldc;
     float v = 0.f;
     if (k < K) {
       const int c = k / (KH * KW);
@@ -63,7 +63,7 @@ __global__ void im2col_nchw_kernel(const float* __restrict__ x, T* __restrict__ 
       const int kw = k % KW;
       const int ox = row % Wo;
       const int oy = (row / Wo) % Ho;
-      const int n = row / ((long)Wo * Ho);
+      const int n = row / (Wo * Ho);
       const int iy = oy * stride - pad + kh;
       const int ix = ox * stride - pad + kw;
       if (iy >= 0 && iy < H && ix >= 0 && ix < W) v = x[(((long)n * C + c) * H + iy) * W + ix];
@@ -78,12 +78,12 @@ __global__ void col2im_nhwc_kernel(const T* __restrict__ cols, T* __restrict__ d
   constexpr int V = VecT<T>::N;
   const int CPR = C / V;
   const long total = (long)NI * H * W * CPR;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)total; i += gridDim.x * blockDim.x) {
     const int ch = i % CPR;
-    const long pix = i / CPR;
+    const int pix = i / CPR;
     const int x = pix % W;
     const int y = (pix / W) % H;
-    const int n = pix / ((long)W * H);
+    const int n = pix / (W * H);
     float acc[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) acc[j] = 0.f;

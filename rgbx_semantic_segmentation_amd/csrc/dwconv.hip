@@ -74,10 +74,10 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ h, co
   const long gpix = (long)ipg * H * W;
   const T* base = h + (long)g * gpix * C + c0;
   T* obase = out + (long)g * gpix * C + c0;
-  for (long p = slot; p < gpix; p += P) {
+  for (int p = slot; p < (int)gpix; p += P) {
     const int x = p % W;
     const int y = (p / W) % H;
-    const long img = p / ((long)W * H);
+    const int img = p / (W * H);
     const T* ib = base + img * H * W * C;
     float acc[4] = {bias[0], bias[1], bias[2], bias[3]};
 #pragma unroll
@@ -125,10 +125,10 @@ __global__ __launch_bounds__(256) void dw_bwd_dz_kernel(const T* __restrict__ da
   }
   const long gpix = (long)ipg * H * W;
   const T* base = h + (long)g * gpix * C + c0;
-  for (long p = slot; p < gpix; p += P) {
+  for (int p = slot; p < (int)gpix; p += P) {
     const int x = p % W;
     const int y = (p / W) % H;
-    const long img = p / ((long)W * H);
+    const int img = p / (W * H);
     const T* ib = base + img * H * W * C;
     float hv[9][4];
     float z[4] = {bias[0], bias[1], bias[2], bias[3]};
@@ -178,9 +178,9 @@ __global__ __launch_bounds__(256) void dw_bwd_dz_kernel(const T* __restrict__ da
 __global__ void dw_scatter_kernel(const float* __restrict__ tmp, float* __restrict__ dw, float* __restrict__ db, int G,
                                   int C, int accumulate) {
   const long total = (long)G * C * 10;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)total; i += gridDim.x * blockDim.x) {
     const int k = i % 10;
-    const long gc = i / 10;
+    const int gc = i / 10;
     const float s = tmp[i];
     float* o = k < 9 ? &dw[gc * 9 + k] : (db ? &db[gc] : nullptr);
     if (o) *o = accumulate ? *o + s : s;

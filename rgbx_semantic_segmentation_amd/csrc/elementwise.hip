@@ -12,8 +12,8 @@ __global__ void residual_add_kernel(const T* __restrict__ x, const T* __restrict
                                     const float* __restrict__ scale, T* out, long n_per_sample,
                                     long nvec) {
   constexpr int V = VecT<T>::N;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
-    const long e = i * V;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)nvec; i += gridDim.x * blockDim.x) {
+    const int e = i * V;
     const float s = scale ? scale[e / n_per_sample] : 1.f;
     float a[V], b[V];
     load_vec<T>(x + e, a);
@@ -28,8 +28,8 @@ template <typename T>
 __global__ void scale_samples_kernel(const T* __restrict__ x, const float* __restrict__ scale, T* out,
                                      long n_per_sample, long nvec) {
   constexpr int V = VecT<T>::N;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
-    const long e = i * V;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)nvec; i += gridDim.x * blockDim.x) {
+    const int e = i * V;
     const float s = scale[e / n_per_sample];
     float a[V];
     load_vec<T>(x + e, a);
@@ -42,7 +42,7 @@ __global__ void scale_samples_kernel(const T* __restrict__ x, const float* __res
 template <typename T>
 __global__ void act_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, long nvec, int act) {
   constexpr int V = VecT<T>::N;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)nvec; i += gridDim.x * blockDim.x) {
     float a[V];
     load_vec<T>(x + i * V, a);
 #pragma unroll
@@ -56,7 +56,7 @@ template <typename T>
 __global__ void act_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ z, T* __restrict__ dx,
                                long nvec, int act) {
   constexpr int V = VecT<T>::N;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)nvec; i += gridDim.x * blockDim.x) {
     float a[V], b[V];
     load_vec<T>(dy + i * V, a);
     load_vec<T>(z + i * V, b);
@@ -67,7 +67,7 @@ __global__ void act_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ z
 }
 
 __global__ void cast_f32_bf16_kernel(const float* __restrict__ src, bf16* __restrict__ dst, long n) {
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)n; i += gridDim.x * blockDim.x)
     dst[i] = from_f32<bf16>(src[i]);
 }
 

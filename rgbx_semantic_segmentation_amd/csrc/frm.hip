@@ -38,7 +38,7 @@ __global__ void pool_final_kernel(const float* __restrict__ psum, const float* _
                                   const int* __restrict__ pidx, float* __restrict__ pooled, int* __restrict__ argmax,
                                   int B, int N, int C, int nchunk) {
   const long total = 2L * B * C;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)total; i += gridDim.x * blockDim.x) {
     const int c = i % C;
     const int gb = i / C;
     const int g = gb / B, b = gb % B;
@@ -80,7 +80,7 @@ __device__ __forceinline__ float act_grad_from_out(float y, int act) {
 
 __global__ void small_linear_dz_kernel(const float* __restrict__ dy, const float* __restrict__ y, float* __restrict__ dz,
                                        long n, int act) {
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)n; i += gridDim.x * blockDim.x)
     dz[i] = dy[i] * act_grad_from_out(y[i], act);
 }
 
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256) void small_linear_dx_kernel(const float* __res
 __global__ void small_linear_dw_kernel(const float* __restrict__ dz, const float* __restrict__ x, float* __restrict__ dw,
                                        float* __restrict__ db, int M, int K, int Nout, int accumulate) {
   const long total = (long)Nout * K;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)total; i += gridDim.x * blockDim.x) {
     const int k = i % K, n = i / K;
     float s = 0.f;
     for (int m = 0; m < M; ++m) s += dz[(long)m * Nout + n] * x[(long)m * K + k];
@@ -166,10 +166,10 @@ __global__ void combine_fwd_kernel(const T* __restrict__ x, const float* __restr
   constexpr int V = VecT<T>::N;
   const long per = (long)B * N * C;
   const long nvec = per / V;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
-    const long e = i * V;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)nvec; i += gridDim.x * blockDim.x) {
+    const int e = i * V;
     const int c0 = e % C;
-    const long row = e / C;        // b*N + n
+    const int row = e / C;        // b*N + n
     const int b = row / N;
     float a[V], bb[V], o1[V], o2[V];
     load_vec<T>(x + e, a);
@@ -307,10 +307,10 @@ template <typename T>
 __global__ void pool_bwd_kernel(const float* __restrict__ dpooled, const int* __restrict__ argmax, T* __restrict__ dx,
                                 int B, int N, int C) {
   const long total = 2L * B * N * C;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)total; i += gridDim.x * blockDim.x) {
     const int c = i % C;
     const int n = (i / C) % N;
-    const long gb = i / ((long)C * N);
+    const int gb = i / (C * N);
     const int g = gb / B, b = gb % B;
     float v = dpooled[(long)b * 4 * C + g * C + c] / N;
     if (argmax[(long)b * 2 * C + g * C + c] == n) v += dpooled[(long)b * 4 * C + 2 * C + g * C + c];

@@ -302,3 +302,13 @@ int cmx_layernorm_bwd(const void* dy, const void* x, const float* gamma, const f
 }
 
 }  // extern "C"
+
+extern "C" {
+// out (G, W) (+)= alpha * sum over nblk of ws (G, nblk, W): the split-K combine of the
+// chunked weight-gradient GEMMs and every other two-stage column reduction.
+int cmx_partials_sum(const float* ws, float* out, int G, int nblk, int W, int accumulate, float alpha,
+                     hipStream_t s) {
+  CMX_REQUIRE(G > 0 && nblk > 0 && W > 0, CMX_ERR_SHAPE, "partials_sum: shape");
+  return cmx_reduce_partials(ws, out, G, nblk, W, accumulate, alpha, s);
+}
+}

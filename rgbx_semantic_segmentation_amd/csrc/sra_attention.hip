@@ -383,11 +383,11 @@ __global__ void sra_dkv_reduce_kernel(const float* __restrict__ ws_dk, const flo
                                       T* __restrict__ dk, T* __restrict__ dv, int Bt, int Nk, int heads,
                                       int D, long kvs, int nchunk) {
   const long total = (long)Bt * heads * Nk * D;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)total; i += gridDim.x * blockDim.x) {
     const int d = i % D;
     const int key = (i / D) % Nk;
-    const int head = (i / ((long)D * Nk)) % heads;
-    const int b = i / ((long)D * Nk * heads);
+    const int head = (i / (D * Nk)) % heads;
+    const int b = i / (D * Nk * heads);
     float sk = 0.f, sv = 0.f;
     for (int c = 0; c < nchunk; ++c) {
       sk += ws_dk[(long)c * total + i];

@@ -32,10 +32,10 @@ __global__ __launch_bounds__(256) void upsample_ce_kernel(const T* __restrict__ 
   const float sh = (float)h / H, sw = (float)w / W;
   const long total = (long)B * H * W;
   float lsum = 0.f, lcnt = 0.f;
-  for (long p = (long)blockIdx.x * blockDim.x + threadIdx.x; p < total; p += (long)gridDim.x * blockDim.x) {
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < (int)total; p += gridDim.x * blockDim.x) {
     const int x = p % W;
     const int y = (p / W) % H;
-    const int b = p / ((long)W * H);
+    const int b = p / (W * H);
     const long lab = label[p];
     T* gp = grad + p * K;
     if (lab == ignore || lab < 0 || lab >= K) {
