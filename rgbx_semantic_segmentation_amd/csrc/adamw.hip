@@ -45,8 +45,8 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
     *reinterpret_cast<float4*>(m + e) = make_float4(ma[0], ma[1], ma[2], ma[3]);
     *reinterpret_cast<float4*>(v + e) = make_float4(va[0], va[1], va[2], va[3]);
     if (shadow) {
-      uint32_t a = (uint32_t)from_f32<bf16>(pa[0]).x | ((uint32_t)from_f32<bf16>(pa[1]).x << 16);
-      uint32_t b = (uint32_t)from_f32<bf16>(pa[2]).x | ((uint32_t)from_f32<bf16>(pa[3]).x << 16);
+      uint32_t a = pack2_bf16(pa[0], pa[1]);
+      uint32_t b = pack2_bf16(pa[2], pa[3]);
       *reinterpret_cast<uint2*>(shadow + e) = make_uint2(a, b);
     }
   }

@@ -90,8 +90,8 @@ __device__ __forceinline__ void store4(T* p, const float* v) {
   if constexpr (sizeof(T) == 4) {
     *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
   } else {
-    uint32_t a = (uint32_t)from_f32<bf16>(v[0]).x | ((uint32_t)from_f32<bf16>(v[1]).x << 16);
-    uint32_t b = (uint32_t)from_f32<bf16>(v[2]).x | ((uint32_t)from_f32<bf16>(v[3]).x << 16);
+    uint32_t a = pack2_bf16(v[0], v[1]);
+    uint32_t b = pack2_bf16(v[2], v[3]);
     *reinterpret_cast<uint2*>(p) = make_uint2(a, b);
   }
 }

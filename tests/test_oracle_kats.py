@@ -154,3 +154,31 @@ def test_group_weight_partition():
 
 def test_param_count_b2():
     assert R.count_params(R.EncoderDecoder(R.CMXConfig(backbone="mit_b2", num_classes=40))) == 66581424
+
+
+def test_fast_erf_table():
+    """cmx_erf (csrc/cmx_common.h) evaluated in float32 with the coefficients parsed from
+    the header: max |erf error| <= 5e-7 on [-6, 6] (the GELU kernels' accuracy budget)."""
+    import math
+    import os
+    import re
+    import numpy as np
+    src = open(os.path.join(os.path.dirname(__file__), "..", "rgbx_semantic_segmentation_amd", "csrc",
+                            "cmx_common.h")).read()
+    body = src[src.index("float cmx_erf(float x)"):]
+    body = body[:body.index("return x * p")]
+    lits = [np.float32(v) for v in re.findall(r"(-?\d\.\d+e-\d+)f", body)]
+    assert len(lits) == 12
+    f = np.float32
+    x = np.linspace(-6, 6, 40001).astype(f)
+    xc = np.clip(x, f(-4), f(4))
+    x2 = xc * xc
+    p = np.full_like(x2, lits[0])
+    for a in lits[1:7]:
+        p = p * x2 + a
+    q = np.full_like(x2, lits[7])
+    for b in lits[8:]:
+        q = q * x2 + b
+    r = xc * p * (f(1) / q)
+    ref = np.array([math.erf(float(v)) for v in x])
+    assert np.abs(r.astype(np.float64) - ref).max() < 5e-7
