@@ -1,0 +1,67 @@
+"""Engine / loader drop-in surface (reference engine/engine.py, dataloader/dataloader.py)."""
+import os
+
+import pytest
+import torch
+
+from rgbx_semantic_segmentation_amd.engine.engine import Engine
+from rgbx_semantic_segmentation_amd.dataloader import SyntheticRGBXDataset, get_train_loader
+from rgbx_semantic_segmentation_amd.utils.pyt_utils import parse_devices
+
+
+def test_parse_devices():
+    assert parse_devices("0,2-3") == [0, 2, 3]
+    assert parse_devices("") == []
+    with pytest.raises(ValueError):
+        parse_devices("3-1")
+
+
+def test_engine_checkpoint_roundtrip(tmp_path, monkeypatch):
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(4, 3), torch.nn.BatchNorm1d(3))
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-3)
+    m(torch.randn(5, 4)).sum().backward()
+    opt.step()
+    with Engine(argv=[]) as e:
+        assert not e.distributed and e.world_size == 1 and e.continue_state_object is None
+        e.register_state(model=m, optimizer=opt)
+        e.update_iteration(3, 7)
+        e.save_and_link_checkpoint(str(tmp_path / "ckpt"), str(tmp_path / "log"), str(tmp_path / "log_last"))
+        with pytest.raises(KeyError):
+            e.register_state(bogus=1)
+    ck = tmp_path / "ckpt" / "epoch-3.pth"
+    assert ck.exists() and os.path.islink(tmp_path / "ckpt" / "epoch-last.pth")
+    sd = torch.load(ck, weights_only=True)
+    assert set(sd) == {"model", "optimizer", "epoch", "iteration"} and sd["iteration"] == 7
+    # a DDP-style 'module.' prefix is stripped on restore even without DDP
+    sd["model"] = {"module." + k: v for k, v in sd["model"].items()}
+    torch.save(sd, tmp_path / "ddp.pth")
+    m2 = torch.nn.Sequential(torch.nn.Linear(4, 3), torch.nn.BatchNorm1d(3))
+    opt2 = torch.optim.AdamW(m2.parameters(), lr=1e-3)
+    with Engine(argv=["-c", str(tmp_path / "ddp.pth")]) as e2:
+        e2.register_state(model=m2, optimizer=opt2)
+        e2.restore_checkpoint()
+        assert e2.state.epoch == 4 and e2.state.iteration == 7
+    for a, b in zip(m.state_dict().values(), m2.state_dict().values()):
+        assert torch.equal(a, b)
+    assert torch.equal(opt.state_dict()["state"][0]["exp_avg"], opt2.state_dict()["state"][0]["exp_avg"])
+
+
+def test_train_loader_minibatch_dict(monkeypatch):
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+
+    class Cfg:
+        batch_size = 2
+        num_workers = 0
+
+    with Engine(argv=[]) as e:
+        loader, sampler = get_train_loader(e, SyntheticRGBXDataset(4, 32, 48, 9), Cfg)
+    assert sampler is None
+    mb = next(iter(loader))
+    assert set(mb) == {"data", "label", "modal_x", "fn", "n"}
+    assert mb["data"].shape == (2, 3, 32, 48) and mb["data"].dtype == torch.float32
+    assert mb["label"].dtype == torch.int64 and (mb["label"] == 255).any()
+    from rgbx_semantic_segmentation_amd.data import MEAN, STD
+    raw = mb["modal_x"].double() * STD[None, :, None, None] + MEAN[None, :, None, None]
+    assert torch.allclose(raw[:, 0], raw[:, 1], atol=1e-6)        # one X plane replicated, then normalised
