@@ -113,6 +113,18 @@ int cmx_bilinear_adjoint_1d(const void* in, void* out, int64_t P, int Lo, int Li
 size_t cmx_upsample_ce_workspace(int B, int H, int W);
 int cmx_upsample_ce_fwd(const void* logits, const int64_t* label, void* grad, float* out, float* workspace, int B, int h, int w, int H, int W, int K, int ignore_index, int dtype, hipStream_t stream);
 
+/* ---- dense layers: batched MFMA GEMM with fused epilogues -----------------------------
+ * Replaces every nn.Linear and 1x1 Conv2d of the path (dual_segformer.py:42-43, 87-96, 110;
+ * net_utils.py:14-17, 72-75, 196-198, 265-269, 316-326; MLPDecoder.py:13-19, 63-70), the
+ * im2col'd OverlapPatchEmbed / SR convs (dual_segformer.py:95, 196) and their dgrad / wgrad.
+ * C[g](i,j) = epi(sum_k A(i,k) B(j,k)); A(i,k) = A[i*lda+k] (transA=0) or A[k*lda+i] (1); k >= K1
+ * reads A2 (cat-free two-input Linear).  epi: v = act(acc + bias[g*sbias+j]); residual R (layout
+ * of C): v = R + rscale[(g*M+i)/rows_per_sample]*v; out_mode 0: C = dtype(v), 1: C = fp32(v), 2: C += v.
+ * ones_col: B row N-1 is virtual ones and column N-1 of the result goes to dbias (bias gradient).
+ * splitk > 1: K split over blocks into a workspace of cmx_gemm_workspace() bytes, then reduced. */
+size_t cmx_gemm_workspace(int G, int M, int N, int splitk);
+int cmx_gemm(const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R, const float* rscale, float* dbias, float* workspace, int G, int M, int N, int K, int K1, int64_t lda, int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias, int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode, int ones_col, int splitk, int dtype, hipStream_t stream);
+
 /* ---- fused AdamW over the flat parameter buffer (train.py:128-129, init_func.py:33-57). */
 int cmx_adamw_step(float* p, const float* g, float* m, float* v, void* shadow_bf16, const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, float beta1, float beta2, float eps, float weight_decay, float grad_scale, hipStream_t stream);
 

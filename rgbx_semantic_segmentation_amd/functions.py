@@ -13,6 +13,8 @@ Conventions
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch.autograd import Function
 
@@ -58,51 +60,93 @@ def _wgrad(dy, x, out):
 
 
 # ---------------------------------------------------------------------------- Linear
+# Dense layers run on cmx_gemm (csrc/gemm.hip).  CMX_GEMM=0 routes them through hipBLASLt
+# (torch.bmm) instead -- an A/B switch for measurements only.
+USE_CMX_GEMM = os.environ.get("CMX_GEMM", "1") != "0"
+
+
+def _dgrad(dz, W_slice, out):
+    """out (G, M, k) = dz (G, M, N) @ W_slice (G, N, k)."""
+    if USE_CMX_GEMM:
+        K.gemm(dz, W_slice.transpose(1, 2), out)
+    else:
+        torch.bmm(dz, W_slice, out=out)
+    return out
+
+
+def _wgrad_into(dz, x, Wg_slice, bg=None):
+    """Wg_slice (fp32 view (G, N, k)) = dz^T x;  bg (G, N) = column sums of dz."""
+    if USE_CMX_GEMM:
+        K.gemm(dz.transpose(1, 2), x.transpose(1, 2), Wg_slice, out_mode=1, dbias=bg, splitk=0)
+        return
+    _wgrad(dz, x, Wg_slice)
+    if bg is not None:
+        K.colsum(dz, bg, G=dz.shape[0])
+
+
+def _fwd_gemm(x, W, b, y, act="none", res=None, rscale=None, rps=1, x2=None):
+    if USE_CMX_GEMM:
+        K.gemm(x, W, y, bias=b, residual=res, rscale=rscale, rows_per_sample=rps, act=act, A2=x2)
+        return y
+    k1 = x.shape[-1]
+    if b is not None:
+        torch.baddbmm(b[:, None, :].to(y.dtype), x, W[:, :, :k1].transpose(1, 2), out=y)
+    else:
+        torch.bmm(x, W[:, :, :k1].transpose(1, 2), out=y)
+    if x2 is not None:
+        y.baddbmm_(x2, W[:, :, k1:].transpose(1, 2))
+    if act != "none":
+        y.copy_(K.act_fwd(y, act))
+    if res is not None:
+        y.copy_(K.residual_add(res, y, rscale, n_per_sample=rps * y.shape[-1]))
+    return y
+
+
 class GLinear(Function):
-    """y[g] = sum_i x_i[g] @ W[g][:, K_i]^T + b[g]   (nn.Linear / 1x1 Conv2d; the K-split
-    form replaces torch.cat of the inputs, e.g. CrossPath.end_proj on cat(y, v),
-    net_utils.py:277-280, and ChannelEmbed's 1x1 convs on cat(x1, x2), :323-326)."""
+    """y[g] = act(x1[g] @ W[g][:, :k1]^T (+ x2[g] @ W[g][:, k1:]^T) + b[g]), optionally
+    y = res + rscale[sample] * (...)  (nn.Linear / 1x1 Conv2d; the two-input form replaces
+    torch.cat of the inputs, e.g. CrossPath.end_proj on cat(y, v), net_utils.py:277-280,
+    ChannelEmbed's 1x1 convs on cat(x1, x2), :323-326; the residual form is Block's
+    x + drop_path(proj/fc2(...)), dual_segformer.py:168-169)."""
 
     @staticmethod
-    def forward(ctx, W, Wg, b, bg, anchor, *xs):
+    def forward(ctx, W, Wg, b, bg, anchor, act, res, rscale, rps, x1, x2):
         G, N, Ktot = W.shape
-        y = None
-        k0 = 0
-        for x in xs:
-            k = x.shape[-1]
-            Wt = W[:, :, k0:k0 + k].transpose(1, 2)
-            if y is None:
-                y = torch.baddbmm(b[:, None, :], x, Wt) if b is not None else torch.bmm(x, Wt)
-            else:
-                y.baddbmm_(x, Wt)
-            k0 += k
-        assert k0 == Ktot, (k0, Ktot)
-        ctx.save_for_backward(W, *xs)
-        ctx.Wg, ctx.bg = Wg, bg
+        M = x1.shape[1]
+        assert x1.shape[-1] + (x2.shape[-1] if x2 is not None else 0) == Ktot, (x1.shape, W.shape)
+        y = torch.empty(G, M, N, dtype=x1.dtype, device=x1.device)
+        _fwd_gemm(x1, W, b, y, act=act, res=res, rscale=rscale, rps=rps, x2=x2)
+        ctx.save_for_backward(W, x1, x2, y if act == "relu" else None)
+        ctx.meta = (Wg, bg, act, res is not None, rscale, rps)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        W, *xs = ctx.saved_tensors
+        W, x1, x2, y = ctx.saved_tensors
+        Wg, bg, act, has_res, rscale, rps = ctx.meta
         dy = _c(dy)
         G, M, N = dy.shape
-        dxs = []
-        k0 = 0
-        for i, x in enumerate(xs):
-            k = x.shape[-1]
-            if ctx.needs_input_grad[5 + i]:
-                dxs.append(torch.bmm(dy, W[:, :, k0:k0 + k]))
-            else:
-                dxs.append(None)
-            _wgrad(dy, x, ctx.Wg[:, :, k0:k0 + k])
-            k0 += k
-        if ctx.bg is not None:
-            K.colsum(dy, ctx.bg.reshape(G, N), G=G)
-        return (None, None, None, None, None, *dxs)
+        dres = dy if has_res else None
+        dz = dy
+        if rscale is not None:
+            dz = K.scale_samples(dz, rscale, rps * N)
+        if act == "relu":
+            dz = K.act_bwd(dz, y, "relu")
+        k1 = x1.shape[-1]
+        dx1 = dx2 = None
+        if ctx.needs_input_grad[9]:
+            dx1 = _dgrad(dz, W[:, :, :k1], torch.empty_like(x1))
+        if x2 is not None and ctx.needs_input_grad[10]:
+            dx2 = _dgrad(dz, W[:, :, k1:], torch.empty_like(x2))
+        _wgrad_into(dz, x1, Wg[:, :, :k1], bg)
+        if x2 is not None:
+            _wgrad_into(dz, x2, Wg[:, :, k1:])
+        return (None, None, None, None, None, None, dres, None, None, dx1, dx2)
 
 
-def glinear(store, wp, bp, *xs):
-    """Grouped linear using parameter ``wp`` (and bias ``bp``) of the store."""
+def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1):
+    """Grouped linear using parameter ``wp`` (and bias ``bp``) of the store; x2 = second
+    input segment (cat-free), res/rscale/rps = fused DropPath residual (rps = rows per sample)."""
     W = store.w(wp)
     Wg = store.g(wp)
     G = W.shape[0]
@@ -110,9 +154,9 @@ def glinear(store, wp, bp, *xs):
     Wg = Wg.view(G, Wg.shape[1], -1)
     b = bg = None
     if bp is not None:
-        b = store.w(bp).view(G, -1)
+        b = store.w(bp, compute=False).view(G, -1)
         bg = store.g(bp).view(G, -1)
-    return GLinear.apply(W, Wg, b, bg, wp, *xs)
+    return GLinear.apply(W, Wg, b, bg, wp, act, res, rscale, rps, x1, x2)
 
 
 # ---------------------------------------------------------------------------- LayerNorm
@@ -243,8 +287,7 @@ class ConvF(Function):
         else:
             K.call("cmx_im2col_nhwc", K.ptr(x), K.ptr(cols), NI, H, Wd, C, KH, KW, st, pad, Ho, Wo, Kp,
                    K.dtype_code(cols), K.stream())
-        y = torch.baddbmm(b[:, None, :], cols, W.transpose(1, 2)) if b is not None else \
-            torch.bmm(cols, W.transpose(1, 2))
+        y = _fwd_gemm(cols, W, b, torch.empty(G, cols.shape[1], W.shape[1], dtype=cols.dtype, device=cols.device))
         ctx.save_for_backward(cols, W)
         ctx.meta = (Wg, bg, geom)
         ctx.xshape = x.shape
@@ -256,12 +299,10 @@ class ConvF(Function):
         Wg, bg, geom = ctx.meta
         G, NI, H, Wd, C, KH, KW, st, pad, Ho, Wo, nchw = geom
         dy = _c(dy)
-        _wgrad(dy, cols, Wg)
-        if bg is not None:
-            K.colsum(dy, bg, G=G)
+        _wgrad_into(dy, cols, Wg, bg)
         dx = None
         if ctx.needs_input_grad[0] and not nchw:
-            dcols = torch.bmm(dy, W)
+            dcols = _dgrad(dy, W, torch.empty_like(cols))
             dx = torch.empty(NI, H, Wd, C, dtype=dy.dtype, device=dy.device)
             K.call("cmx_col2im_nhwc", K.ptr(dcols), K.ptr(dx), NI, H, Wd, C, KH, KW, st, pad, Ho, Wo, W.shape[-1],
                    K.dtype_code(dx), K.stream())
@@ -277,7 +318,7 @@ def conv(store, mod, x, G, NI, H, W, C, stride, pad, nchw=False):
     Wgt = store.g(mod.weight)
     Wt = Wt.view(G, Wt.shape[1], -1)
     Wgt = Wgt.view(G, Wgt.shape[1], -1)
-    b = store.w(mod.bias).view(G, -1) if mod.bias is not None else None
+    b = store.w(mod.bias, compute=False).view(G, -1) if mod.bias is not None else None
     bg = store.g(mod.bias).view(G, -1) if mod.bias is not None else None
     geom = (G, NI, H, W, C, KH, KW, stride, pad, Ho, Wo, nchw)
     return ConvF.apply(x, Wt, Wgt, b, bg, geom, mod.weight), Ho, Wo
@@ -348,10 +389,14 @@ class FRMF(Function):
         K.call("cmx_small_linear_fwd", K.ptr(pooled), K.ptr(W1), K.ptr(b1), K.ptr(y1), B, 4 * C, 4 * C, 2, K.stream())
         cw = torch.empty(B, 2 * C, dtype=torch.float32, device=x.device)
         K.call("cmx_small_linear_fwd", K.ptr(y1), K.ptr(W2), K.ptr(b2), K.ptr(cw), B, 4 * C, 2 * C, 3, K.stream())
-        x1 = x[0].reshape(B * N, C)
-        x2 = x[1].reshape(B * N, C)
-        h = torch.addmm(b0, x1, W0[:, :C].t())
-        h.addmm_(x2, W0[:, C:].t())
+        # h = cat(x1, x2) W0^T + b0 (SpatialWeights' first 1x1 conv, net_utils.py:72-73), cat-free
+        h = torch.empty(1, B * N, C, dtype=x.dtype, device=x.device)
+        if USE_CMX_GEMM:
+            K.gemm(x[0].view(1, B * N, C), W0[None], h, bias=b0[None], A2=x[1].view(1, B * N, C))
+        else:
+            torch.addmm(b0.to(x.dtype), x[0].reshape(B * N, C), W0[:, :C].t(), out=h[0])
+            h[0].addmm_(x[1].reshape(B * N, C), W0[:, C:].t())
+        h = h[0]
         sw = torch.empty(B * N, 2, dtype=torch.float32, device=x.device)
         K.call("cmx_frm_spatial_fwd", K.ptr(h), K.ptr(w2s), K.ptr(b2s), K.ptr(sw), B * N, C, dt, K.stream())
         out = torch.empty_like(x)
@@ -379,15 +424,14 @@ class FRMF(Function):
         ws2 = K._ws(K.query("cmx_frm_spatial_bwd_workspace", B * N, C), x.device)
         K.call("cmx_frm_spatial_bwd", K.ptr(dsw), K.ptr(sw), K.ptr(h), K.ptr(w2sf), K.ptr(dh), K.ptr(gw2s),
                K.ptr(gb2s), K.ptr(ws2), B * N, C, 0, dt, K.stream())
-        dx1 = dx[0].view(B * N, C)
-        dx2 = dx[1].view(B * N, C)
-        dx1.addmm_(dh, W0[:, :C])
-        dx2.addmm_(dh, W0[:, C:])
-        x1 = x[0].reshape(B * N, C)
-        x2 = x[1].reshape(B * N, C)
-        _wgrad(dh[None], x1[None], gW0[:, :C][None])
-        _wgrad(dh[None], x2[None], gW0[:, C:][None])
-        K.colsum(dh, gb0.view(1, C), G=1)
+        for i in range(2):          # dx_i += dh @ W0[:, iC:(i+1)C] (residual epilogue, in place)
+            dxi = dx[i].view(1, B * N, C)
+            if USE_CMX_GEMM:
+                K.gemm(dh[None], W0[None, :, i * C:(i + 1) * C].transpose(1, 2), dxi, residual=dxi)
+            else:
+                dxi[0].addmm_(dh, W0[:, i * C:(i + 1) * C])
+        _wgrad_into(dh[None], x[0].view(1, B * N, C), gW0[None, :, :C], gb0.view(1, C))
+        _wgrad_into(dh[None], x[1].view(1, B * N, C), gW0[None, :, C:])
         # channel MLP backward (sigmoid then relu), then pooling backward
         dz = K._ws(K.query("cmx_small_linear_bwd_workspace", B, 4 * C, 4 * C), x.device)
         dy1 = torch.empty(B, 4 * C, dtype=torch.float32, device=x.device)
@@ -410,7 +454,7 @@ def frm(store, mod, x):
         # fp32 for the small MLP / spatial head (computed on the VALU in fp32);
         # compute dtype for the spatial 1x1 GEMM
         "w": (f32(cwm[0].weight), f32(cwm[0].bias), f32(cwm[2].weight), f32(cwm[2].bias),
-              cmp(swm[0].weight).view(C, 2 * C), cmp(swm[0].bias), f32(swm[2].weight).view(2, C), f32(swm[2].bias)),
+              cmp(swm[0].weight).view(C, 2 * C), f32(swm[0].bias), f32(swm[2].weight).view(2, C), f32(swm[2].bias)),
         "g": (g(cwm[0].weight), g(cwm[0].bias), g(cwm[2].weight), g(cwm[2].bias),
               g(swm[0].weight).view(C, 2 * C), g(swm[0].bias), g(swm[2].weight).view(2, C), g(swm[2].bias)),
         "w32": (f32(cwm[0].weight), f32(cwm[2].weight), f32(swm[2].weight).view(2, C)),

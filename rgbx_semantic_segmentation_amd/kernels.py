@@ -92,6 +92,67 @@ def colsum(x: torch.Tensor, out: torch.Tensor, G: int = 1, accumulate: bool = Fa
     return out
 
 
+# ------------------------------------------------------------------------------ GEMM
+def _operand(t: torch.Tensor, name: str):
+    """(G, rows, k) logical view -> (trans, ld, batch stride)."""
+    if t.stride(2) == 1:
+        return 0, t.stride(1), t.stride(0)
+    if t.stride(1) == 1:
+        return 1, t.stride(2), t.stride(0)
+    raise ValueError(f"gemm: operand {name} needs a unit stride along rows or k, got strides {t.stride()}")
+
+
+def gemm_auto_split(G: int, M: int, N: int, K: int) -> int:
+    """Split-K factor: aim for ~1024 blocks (4 per CU) with >= 8 k-tiles of 32 per split;
+    only the wgrad shapes (small M x N output, K = tokens) end up split."""
+    tiles = -(-M // (64 if M <= 64 else 128)) * -(-N // (64 if N <= 64 else 128))
+    nk = -(-K // 32)
+    s = max(1, min(64, nk // 8, 1024 // max(1, tiles * G)))
+    return s
+
+
+def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, bias: torch.Tensor | None = None,
+         residual: torch.Tensor | None = None, rscale: torch.Tensor | None = None, rows_per_sample: int = 1,
+         act: str = "none", out_mode: int = 0, A2: torch.Tensor | None = None, dbias: torch.Tensor | None = None,
+         splitk: int = 1) -> torch.Tensor:
+    """C[g] = epi([A[g] | A2[g]] @ B[g]^T) on logical views A (G, M, K1), A2 (G, M, K-K1),
+    B (G, N, K), C (G, M, N).
+
+    A transposed operand is just a transposed view (unit stride along rows instead of k):
+    the kernel reads it in place.  out_mode: 0 store in C's dtype (= A's), 1 store fp32,
+    2 accumulate into fp32 C.  bias (G, N) fp32 (any batch stride, unit inner stride);
+    residual has C's layout: C = residual + rscale[(g*M + i) // rows_per_sample] * act(acc + bias).
+    dbias (G, M) fp32: also produce sum_k A(i, k) (the bias gradient of a wgrad, via a
+    virtual ones column of B).  splitk > 1 splits K over blocks (wgrad over tokens); 0 = auto."""
+    G, M, K1 = A.shape
+    Kd = K1 + (A2.shape[2] if A2 is not None else 0)
+    N = B.shape[1]
+    assert B.shape == (G, N, Kd) and C.shape == (G, M, N) and C.stride(2) == 1, (A.shape, B.shape, C.shape)
+    assert A.dtype == B.dtype and C.dtype == (A.dtype if out_mode == 0 else torch.float32), (A.dtype, C.dtype)
+    tA, lda, sA = _operand(A, "A")
+    tA2, lda2, sA2 = _operand(A2, "A2") if A2 is not None else (0, 0, 0)
+    assert tA2 == 0 and (A2 is None or (tA == 0 and A2.shape[:2] == (G, M) and A2.dtype == A.dtype))
+    tB, ldb, sB = _operand(B, "B")
+    sbias = 0
+    if bias is not None:
+        assert bias.dtype == torch.float32 and bias.shape[-1] == N and bias.stride(-1) == 1
+        sbias = bias.stride(0) if bias.dim() == 2 else 0
+    sdb = 0
+    if dbias is not None:
+        assert dbias.dtype == torch.float32 and dbias.shape[-1] == M and dbias.stride(-1) == 1
+        sdb = dbias.stride(0) if dbias.dim() == 2 else 0
+    if residual is not None:
+        assert residual.shape == C.shape and residual.stride() == C.stride() and residual.dtype == C.dtype
+    Nk = N + (1 if dbias is not None else 0)
+    if splitk == 0:
+        splitk = gemm_auto_split(G, M, Nk, Kd)
+    ws = _ws(query("cmx_gemm_workspace", G, M, Nk, splitk), A.device) if splitk > 1 else None
+    call("cmx_gemm", ptr(A), ptr(A2), ptr(B), ptr(C), ptr(bias), ptr(residual), ptr(rscale), ptr(dbias), ptr(ws),
+         G, M, Nk, Kd, K1, lda, lda2, ldb, C.stride(1), sA, sA2, sB, C.stride(0), sbias, sdb, int(rows_per_sample),
+         tA, tB, ACT[act], int(out_mode), int(dbias is not None), int(splitk), dtype_code(A), stream())
+    return C
+
+
 # ------------------------------------------------------------------------------ SRA attention
 def sra_attn_fwd(q, k, v, Bt, N, Nk, heads, D, scale, qs, kvs, save_lse=True):
     """q: base pointer tensor of (Bt, N, *) rows with stride qs; k/v: views into the kv

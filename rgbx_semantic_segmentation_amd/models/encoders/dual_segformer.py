@@ -136,13 +136,12 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
             xs, Nk = h, N
         kv = F.glinear(store, a.kv.weight, a.kv.bias, xs)
         o = F.SRAttentionF.apply(q, kv, G * B, N, Nk, a.num_heads, C // a.num_heads)
-        p = F.glinear(store, a.proj.weight, a.proj.bias, o)
-        x = F.ResidualF.apply(x, p, s_attn, N * C)
+        # x + drop_path(proj(o)): residual and DropPath scale fused into the proj GEMM epilogue
+        x = F.glinear(store, a.proj.weight, a.proj.bias, o, res=x, rscale=s_attn, rps=N)
         h = F.layernorm(store, blk.norm2, x, G)
         f = F.glinear(store, blk.mlp.fc1.weight, blk.mlp.fc1.bias, h)
         f = F.dwconv(store, blk.mlp.dwconv.dwconv, f, G * B, B, H, W, "gelu")
-        f = F.glinear(store, blk.mlp.fc2.weight, blk.mlp.fc2.bias, f)
-        return F.ResidualF.apply(x, f, s_mlp, N * C)
+        return F.glinear(store, blk.mlp.fc2.weight, blk.mlp.fc2.bias, f, res=x, rscale=s_mlp, rps=N)
 
     def run(self, store, images, B, H, W, training, dp_scales: Optional[torch.Tensor], bn_group=None):
         """images: (2*B, 3, H, W) fp32 NCHW (RGB batch then X batch).

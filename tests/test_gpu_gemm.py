@@ -1,0 +1,120 @@
+"""cmx_gemm (csrc/gemm.hip) against a plain PyTorch fp32 reference of the same op.
+
+Covers the three GEMMs of a layer (forward NT, dgrad with a transposed B, wgrad with both
+operands transposed), ragged M / N / K (K = 152 is the padded 7x7x3 patch-embed K,
+N = 40 the NYUv2 classifier), every epilogue (bias, GELU / ReLU, DropPath-scaled residual,
+fp32 store / accumulate) and both storage dtypes.  Tolerances: fp32 mode 1e-5 relative
+(exact fp32 MFMA, summation order differs); bf16 mode 1e-2 relative (bf16 output
+rounding, fp32 accumulation)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    return ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-30)).item()
+
+
+def ref_epi(acc, bias, act, residual, rscale, rps):
+    v = acc + (bias[:, None, :] if bias is not None else 0)
+    v = {"none": v, "gelu": F.gelu(v), "relu": F.relu(v)}[act]
+    if residual is not None:
+        G, M = v.shape[:2]
+        s = torch.ones(G * M, device=v.device) if rscale is None else rscale.repeat_interleave(rps)
+        v = residual.float() + s.view(G, M, 1) * v
+    return v
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("G,M,N,K", [(2, 300, 64, 64), (2, 1000, 128, 152), (1, 777, 40, 512), (2, 256, 320, 1280),
+                                     (1, 130, 520, 24)])
+@pytest.mark.parametrize("tA,tB", [(0, 0), (0, 1), (1, 1), (1, 0)])
+def test_gemm_layouts(dev, dtype, G, M, N, K, tA, tB):
+    torch.manual_seed(0)
+    if (tA and M % 8) or (tB and N % 8):
+        pytest.skip("transposed operand needs its contiguous dim % 8 == 0")
+    A = torch.randn(G, M, K, device="cuda").to(dtype)
+    B = torch.randn(G, N, K, device="cuda").to(dtype)
+    Av = A.transpose(1, 2).contiguous().transpose(1, 2) if tA else A
+    Bv = B.transpose(1, 2).contiguous().transpose(1, 2) if tB else B
+    from rgbx_semantic_segmentation_amd import kernels as Kn
+    C = torch.empty(G, M, N, device="cuda", dtype=dtype)
+    Kn.gemm(Av, Bv, C)
+    ref = torch.bmm(A.float(), B.float().transpose(1, 2))
+    assert rel(C, ref) < (1e-5 if dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("act", ["none", "gelu", "relu"])
+@pytest.mark.parametrize("res", [False, True])
+def test_gemm_epilogues(dev, dtype, act, res):
+    torch.manual_seed(1)
+    from rgbx_semantic_segmentation_amd import kernels as Kn
+    G, M, N, K, rps = 2, 600, 192, 96, 300
+    A = torch.randn(G, M, K, device="cuda").to(dtype)
+    B = torch.randn(G, N, K, device="cuda").to(dtype) * 0.1
+    bias = torch.randn(G, N, device="cuda")
+    R = torch.randn(G, M, N, device="cuda").to(dtype) if res else None
+    s = torch.tensor([0.0, 1.25, 1.25, 0.0], device="cuda") if res else None
+    C = torch.empty(G, M, N, device="cuda", dtype=dtype)
+    Kn.gemm(A, B, C, bias=bias, residual=R, rscale=s, rows_per_sample=rps, act=act)
+    ref = ref_epi(torch.bmm(A.float(), B.float().transpose(1, 2)), bias, act, R, s, rps)
+    assert rel(C, ref) < (1e-5 if dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_fp32_out_and_accumulate(dev, dtype):
+    torch.manual_seed(2)
+    from rgbx_semantic_segmentation_amd import kernels as Kn
+    G, M, N, K = 2, 4800, 64, 256          # wgrad-shaped: dW (N x K) = dy^T x over M tokens
+    dy = torch.randn(G, M, N, device="cuda").to(dtype)
+    x = torch.randn(G, M, K, device="cuda").to(dtype)
+    W = torch.empty(G, N, K, device="cuda")
+    Kn.gemm(dy.transpose(1, 2), x.transpose(1, 2), W, out_mode=1)
+    ref = torch.bmm(dy.float().transpose(1, 2), x.float())
+    assert rel(W, ref) < 1e-5
+    Kn.gemm(dy.transpose(1, 2), x.transpose(1, 2), W, out_mode=2)
+    assert rel(W, 2 * ref) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_two_segment_A(dev, dtype):
+    """Linear on cat(x1, x2) without the cat (end_proj / ChannelEmbed)."""
+    torch.manual_seed(3)
+    from rgbx_semantic_segmentation_amd import kernels as Kn
+    G, M, N, K1, K2 = 2, 700, 160, 64, 96
+    x1 = torch.randn(G, M, K1, device="cuda").to(dtype)
+    x2 = torch.randn(G, M, K2, device="cuda").to(dtype)
+    W = torch.randn(G, N, K1 + K2, device="cuda").to(dtype)
+    b = torch.randn(G, N, device="cuda")
+    C = torch.empty(G, M, N, device="cuda", dtype=dtype)
+    Kn.gemm(x1, W, C, bias=b, A2=x2)
+    ref = torch.bmm(torch.cat([x1, x2], -1).float(), W.float().transpose(1, 2)) + b[:, None, :]
+    assert rel(C, ref) < (1e-5 if dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("splitk", [1, 7, 32])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_gemm_wgrad_splitk_bias_grad(dev, dtype, splitk, accumulate):
+    """dW = dy^T x split over tokens, written into a column slice of a wider gradient
+    buffer (K-split Linear), with the bias gradient from the virtual ones column."""
+    torch.manual_seed(4)
+    from rgbx_semantic_segmentation_amd import kernels as Kn
+    G, Mtok, N, Kx, Ktot, k0 = 2, 9600, 64, 128, 320, 64
+    dy = torch.randn(G, Mtok, N, device="cuda").to(dtype)
+    x = torch.randn(G, Mtok, Kx, device="cuda").to(dtype)
+    Wg = torch.randn(G, N, Ktot, device="cuda")
+    bg = torch.randn(G, N, device="cuda")
+    W0, b0 = Wg.clone(), bg.clone()
+    Kn.gemm(dy.transpose(1, 2), x.transpose(1, 2), Wg[:, :, k0:k0 + Kx], out_mode=2 if accumulate else 1,
+            dbias=bg, splitk=splitk)
+    refW = torch.bmm(dy.float().transpose(1, 2), x.float())
+    refb = dy.float().sum(1)
+    if accumulate:
+        refW, refb = refW + W0[:, :, k0:k0 + Kx], refb + b0
+    assert rel(Wg[:, :, k0:k0 + Kx], refW) < 1e-5
+    assert rel(bg, refb) < 1e-5
+    assert torch.equal(Wg[:, :, :k0], W0[:, :, :k0]) and torch.equal(Wg[:, :, k0 + Kx:], W0[:, :, k0 + Kx:])
