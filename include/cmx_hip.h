@@ -121,8 +121,10 @@ int cmx_upsample_ce_fwd(const void* logits, const int64_t* label, void* grad, fl
  * reads A2 (cat-free two-input Linear).  epi: v = act(acc + bias[g*sbias+j]); residual R (layout
  * of C): v = R + rscale[(g*M+i)/rows_per_sample]*v; out_mode 0: C = dtype(v), 1: C = fp32(v), 2: C += v.
  * ones_col: B row N-1 is virtual ones and column N-1 of the result goes to dbias (bias gradient).
- * splitk > 1: K split over blocks into a workspace of cmx_gemm_workspace() bytes, then reduced. */
+ * splitk > 1: K split over blocks into a workspace of cmx_gemm_workspace() bytes, then reduced (the
+ * reducer applies the epilogue); splitk <= 0: the library's choice, cmx_gemm_splitk(). */
 size_t cmx_gemm_workspace(int G, int M, int N, int splitk);
+int cmx_gemm_splitk(int G, int M, int N, int K, int ones_col, int dtype);
 int cmx_gemm(const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R, const float* rscale, float* dbias, float* workspace, int G, int M, int N, int K, int K1, int64_t lda, int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias, int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode, int ones_col, int splitk, int dtype, hipStream_t stream);
 
 /* ---- fused AdamW over the flat parameter buffer (train.py:128-129, init_func.py:33-57). */

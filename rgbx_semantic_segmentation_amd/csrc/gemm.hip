@@ -12,53 +12,406 @@
 // Extras that remove whole passes / launches from the step:
 //  * two-segment A along k (k < K1 from A, k >= K1 from A2): Linear on cat(x1, x2) without
 //    the cat (CrossPath.end_proj, ChannelEmbed, net_utils.py:277-280, 323-326);
-//  * `ones_col`: B gets a virtual column j = N - 1 of ones, so the wgrad's last output
-//    column is sum_m dy[m][n] = the bias gradient, routed to `dbias` (no colsum launch);
-//  * split-K over blockIdx.z into fp32 partial slabs + a reducer that writes the (possibly
-//    strided, possibly accumulating) fp32 output: the wgrad reduces over up to 76800 tokens
-//    into a 64 x 256 result, which has no parallelism without it.
+//  * `ones_col`: column N - 1 of the result is sum_k A(i, k) (the bias gradient of a wgrad,
+//    sum over tokens of dy), routed to `dbias` -- no colsum launch;
+//  * split-K over blockIdx.z into fp32 partial slabs + a reducer that applies the full
+//    epilogue: the wgrads reduce over up to 76800 tokens into a 64 x 256 result, and the
+//    stage-4 layers (600 tokens) have only ~20 output tiles; both need K parallelism.
 //
 // Epilogue (per output element, fp32):  v = acc + bias[j];  v = act(v);
 //   out_mode 0: C = T(v)            out_mode 1: C = fp32(v)        out_mode 2: C += v (fp32)
 //   residual R (same layout as C):  C = R + s[(g*M + i) / rows_per_sample] * v  (DropPath-scaled
 //   residual, s may be NULL = 1) -- the Block's `x + drop_path(f(x))` (dual_segformer.py:168-169).
 //
-// Tiling (gfx950, wave64): 256 threads = 4 waves in a 2 x 2 grid over a BM x BN block tile;
-// each wave owns (BM/2) x (BN/2) as 32x32 MFMA tiles (v_mfma_f32_32x32x16_bf16, or the exact
-// fp32 v_mfma_f32_32x32x2_f32 in fp32 parity mode).  BK = 32 per stage, two LDS buffers;
-// the next stage's global loads are issued into registers before the current stage's
-// MFMAs and written to LDS after them (one barrier per stage).  Transposed operands are
-// transposed during the LDS write.  Block -> tile mapping is XCD-aware: consecutive block
-// ids land on different XCDs, so each XCD's L2 sees consecutive tiles of one A row-panel.
+// Two kernels:
+//  * gemm_bf16_kernel -- the bf16 path of the step.  256 threads = 4 waves (2 x 2) over a
+//    BM x BN tile (64 or 128 each), v_mfma_f32_32x32x16_bf16, BK = 64.  Operand tiles move
+//    HBM -> LDS by buffer_load_dwordx4 ... lds (LDS-DMA, no register staging), double
+//    buffered: tile t+1 is in flight while tile t is multiplied.  Out-of-range rows / k come
+//    back as zeros from the buffer descriptor's range check (offset 0x80000000), so ragged
+//    edges need no branches.  A k-contiguous operand is imaged [rows][64] (128-B rows) and
+//    read with ds_read_b128; a row-contiguous (transposed) operand is imaged [64][rows] and
+//    read with gfx950's ds_read_b64_tr_b16, which transposes 4 x 16 blocks on the way to the
+//    registers -- no transposing LDS writes.  Both images are XOR-swizzled on 16-B chunks so
+//    every fragment read is bank-conflict-free; the LDS-DMA writes linearly, so the inverse
+//    swizzle is applied to the per-lane global source address.
+//  * gemm_generic_kernel -- fp32 parity mode (exact v_mfma_f32_32x32x2_f32) and any bf16
+//    problem whose strides / dims do not allow 16-B chunks; register staged, BK = 32.
 #include "cmx_mfma.h"
 
 namespace {
 
+struct GemmArgs {
+  const void* A; const void* A2; const void* B; void* C; const float* bias; const void* R; const float* rscale;
+  float* dbias; float* ws;
+  int G, M, N, K, K1, kt_per_split, rows_per_sample, act, out_mode, tiles_m, tiles_n, ones_col, nsplit, vec, cvec;
+  long lda, lda2, ldb, ldc, sA, sA2, sB, sC, sbias, sdb;
+};
+
+// block id -> tile id, giving each of the 8 XCDs (hardware deals block b to XCD b % 8) a
+// contiguous range of tiles so neighbouring tiles share an L2.  Bijective for any count.
+__device__ __forceinline__ int xcd_tile(int b, int nt) {
+  const int q = nt >> 3, r = nt & 7, x = b & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
+// ---------------------------------------------------------------------------- epilogue
+template <typename T>
+__device__ __forceinline__ void epi_store(const GemmArgs& p, int g, int i, int j, float acc) {
+  const float bj = p.bias ? p.bias[(long)g * p.sbias + j] : 0.f;
+  float v = act_fwd(acc + bj, p.act);
+  const long off = (long)g * p.sC + (long)i * p.ldc + j;
+  if (p.R) {
+    const float sc = p.rscale ? p.rscale[((long)g * p.M + i) / p.rows_per_sample] : 1.f;
+    v = to_f32(reinterpret_cast<const T*>(p.R)[off]) + sc * v;
+  }
+  if (p.out_mode == 0) reinterpret_cast<T*>(p.C)[off] = from_f32<T>(v);
+  else if (p.out_mode == 1) reinterpret_cast<float*>(p.C)[off] = v;
+  else reinterpret_cast<float*>(p.C)[off] += v;
+}
+
+__device__ __forceinline__ void dbias_store(const GemmArgs& p, int g, int i, float v) {
+  float* d = p.dbias + (long)g * p.sdb + i;
+  *d = p.out_mode == 2 ? *d + v : v;
+}
+
+// 8 consecutive columns j..j+nv-1 of row i (nv <= 8).  p.vec8: C / R rows are 16-B aligned
+// chunks, so a full group moves with one 16-B (bf16) or two 16-B (fp32) accesses.
+template <typename T>
+__device__ __forceinline__ void epi_store8(const GemmArgs& p, int g, int i, int j, int nv, float* v) {
+  if (nv < 8 || !p.cvec) {
+    for (int e = 0; e < nv; ++e) epi_store<T>(p, g, i, j + e, v[e]);
+    return;
+  }
+  if (p.bias) {
+    const float* bp = p.bias + (long)g * p.sbias + j;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += bp[e];
+  }
+  if (p.act) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = act_fwd(v[e], p.act);
+  }
+  const long off = (long)g * p.sC + (long)i * p.ldc + j;
+  if (p.R) {
+    const float sc = p.rscale ? p.rscale[((long)g * p.M + i) / p.rows_per_sample] : 1.f;
+    float rv[8];
+    load_vec<T>(reinterpret_cast<const T*>(p.R) + off, rv);
+    if constexpr (sizeof(T) == 4) load_vec<T>(reinterpret_cast<const T*>(p.R) + off + 4, rv + 4);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = rv[e] + sc * v[e];
+  }
+  if (p.out_mode == 0) {
+    store_vec<T>(reinterpret_cast<T*>(p.C) + off, v);
+    if constexpr (sizeof(T) == 4) store_vec<T>(reinterpret_cast<T*>(p.C) + off + 4, v + 4);
+  } else {
+    float4* d = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + off);
+    if (p.out_mode == 2) {
+      const float4 o0 = d[0], o1 = d[1];
+      v[0] += o0.x; v[1] += o0.y; v[2] += o0.z; v[3] += o0.w; v[4] += o1.x; v[5] += o1.y; v[6] += o1.z; v[7] += o1.w;
+    }
+    d[0] = make_float4(v[0], v[1], v[2], v[3]);
+    d[1] = make_float4(v[4], v[5], v[6], v[7]);
+  }
+}
+
+// split-K slabs: real columns ws[((g*S + z)*M + i)*Nr + j], bias-gradient column after them
+// at ws[G*S*M*Nr + (g*S + z)*M + i]  (total G*S*M*N floats, N counting the ones column)
+__device__ __forceinline__ float* slab(const GemmArgs& p, int g, int z) {
+  const int Nr = p.ones_col ? p.N - 1 : p.N;
+  return p.ws + (((long)g * p.nsplit + z) * p.M) * Nr;
+}
+__device__ __forceinline__ float* slab_db(const GemmArgs& p, int G, int g, int z) {
+  const int Nr = p.N - 1;
+  return p.ws + (long)G * p.nsplit * p.M * Nr + ((long)g * p.nsplit + z) * p.M;
+}
+
+// ============================================================================ bf16 fast path
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+// One LDS-DMA wave-instruction: 64 lanes x 16 B from rsrc + voffset[lane] to LDS bytes
+// [lds, lds + 1024) in lane order.  Inline asm on purpose: through the compiler intrinsic,
+// hipcc cannot tell the DMA's LDS range from the buffer being read and waits vmcnt(0)
+// before every ds_read, which serialises the prefetch with the MFMAs.  The kernel orders
+// the DMA itself: `s_waitcnt vmcnt(0)` + barrier before a staged buffer is read.
+__device__ __forceinline__ void dma16(const i32x4 rsrc, uint32_t lds, int voffset) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :: "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voffset), "s"(rsrc) : "memory");   // m0 is reserved: hipcc uses it for nothing else in these kernels
+}
+
+constexpr int FBK = 64;                         // k per pipeline stage
+constexpr int OOB = (int)0x80000000;            // voffset past num_records -> the load returns 0
+
+__device__ __forceinline__ i32x4 make_rsrc(const void* base) {
+  const uint64_t a = (uint64_t)base;
+  i32x4 r;
+  r.x = (int)(uint32_t)a;
+  r.y = (int)(uint32_t)(a >> 32);               // stride 0 (raw buffer)
+  r.z = 0x7ffffff0;                             // num_records: every in-range offset is < 2^31 - 16
+  r.w = 0x00020000;                             // gfx9 data format dword
+  return r;
+}
+
+// s_waitcnt vmcnt(N) with expcnt / lgkmcnt left alone (gfx9 encoding: vmcnt[3:0] | [15:14])
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const char* p) {
+  return (uint32_t)reinterpret_cast<uintptr_t>(p);
+}
+
+// swizzle of the transposed image [64][ROWS]: 16-B chunk position of chunk c in k-row kk
+template <int ROWS>
+__device__ __forceinline__ int tr_swz(int kk) {
+  if constexpr (ROWS == 128) return ((kk & 3) << 2) | ((kk >> 2) & 3);   // 256-B rows, 16 chunks
+  else return ((kk >> 1) & 1) << 2;                                        // 128-B rows, 8 chunks
+}
+
+// k-contiguous operand tile -> image [ROWS][64] (128-B rows), chunk c of row r at position
+// c ^ ((r >> 1) & 7).  ROWS / 32 LDS-DMA instructions per wave (8 rows each).
+template <int ROWS>
+__device__ __forceinline__ void stage_k(const i32x4 rsrc, char* img, long ld, int row0, int nrows, int k0, int kend,
+                                        int w, int lane) {
+  constexpr int NI = ROWS / 32;
+#pragma unroll
+  for (int n = 0; n < NI; ++n) {
+    const int row = (w * NI + n) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    const int gr = row0 + row, gk = k0 + c * 8;
+    const int off = (gr < nrows && gk < kend) ? (int)(((long)gr * ld + gk) * 2) : OOB;
+    dma16(rsrc, lds_addr(img + (w * NI + n) * 1024), off);
+  }
+}
+
+// row-contiguous operand tile -> image [64][ROWS] (ROWS*2-B k-rows), chunk c of k-row kk at
+// position c ^ tr_swz(kk).  ROWS / 32 instructions per wave.
+template <int ROWS>
+__device__ __forceinline__ void stage_r(const i32x4 rsrc, char* img, long ld, int row0, int nrows, int k0, int kend,
+                                        int w, int lane) {
+  constexpr int NI = ROWS / 32;
+  constexpr int CPR = ROWS / 8;                 // chunks per k-row
+  constexpr int KPI = 64 / CPR;                 // k-rows per instruction
+#pragma unroll
+  for (int n = 0; n < NI; ++n) {
+    const int kk = (w * NI + n) * KPI + lane / CPR;
+    const int c = (lane % CPR) ^ tr_swz<ROWS>(kk);
+    const int gk = k0 + kk, gr = row0 + c * 8;
+    const int off = (gk < kend && gr < nrows) ? (int)(((long)gk * ld + gr) * 2) : OOB;
+    dma16(rsrc, lds_addr(img + (w * NI + n) * 1024), off);
+  }
+}
+
+// fragment of sub-tile rows [rb, rb + 32), k16-step s, from a [ROWS][64] image
+__device__ __forceinline__ bf16x8 frag_k(const char* img, int rb, int s, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+  const int row = rb + r;
+  const int pos = (2 * s + h) ^ ((row >> 1) & 7);
+  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(img + row * 128 + pos * 16));
+}
+
+// same fragment from a transposed [64][ROWS] image: two ds_read_b64_tr_b16 (k 0-3, 4-7 of
+// the lane's 8), each delivering column (16*g16 + i) of a 4 x 16 block
+template <int ROWS>
+__device__ __forceinline__ bf16x8 frag_r(const char* img, int rb, int s, int lane) {
+  const int h = lane >> 5, g16 = (lane >> 4) & 1, i = lane & 15, q = i >> 2, pp = i & 3;
+  const int col = rb + 16 * g16 + 4 * pp;
+  const int chunk = col >> 3;
+  s16x4 v[2];
+#pragma unroll
+  for (int rd = 0; rd < 2; ++rd) {
+    const int kk = 16 * s + 8 * h + 4 * rd + q;
+    const int off = kk * (ROWS * 2) + ((chunk ^ tr_swz<ROWS>(kk)) << 4) + ((pp & 1) << 3);
+    v[rd] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        reinterpret_cast<__attribute__((address_space(3))) s16x4*>(reinterpret_cast<uintptr_t>(img + off)));
+  }
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 c = __builtin_shufflevector(v[0], v[1], 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, c);
+}
+
+// NS = LDS stages in the DMA ring: 2 for grids of >= 2 blocks per CU (the co-resident block
+// hides the DMA latency), 4 for grids of at most one block per CU (the ring must hide it).
+template <int BM, int BN, bool TA, bool TB, int NS>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const GemmArgs p) {
+  constexpr int A_BYTES = BM * FBK * 2, STAGE = (BM + BN) * FBK * 2;
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int EPI = BM * (BN + 4) * 4;        // fp32 output tile for the epilogue
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE > EPI ? NS * STAGE : EPI];
+
+  // 1-D grid over (split, group, tile); each XCD gets a contiguous run of that order, i.e.
+  // neighbouring tiles of one (split, group): they share A row panels and the B k-slice in L2
+  const int ntile = p.tiles_m * p.tiles_n;
+  const int lin = xcd_tile(blockIdx.x, ntile * p.G * p.nsplit);
+  const int t = lin % ntile, g = (lin / ntile) % p.G, z = lin / (ntile * p.G);
+  const int tm = t / p.tiles_n, tn = t % p.tiles_n;
+  const bf16* Ag = reinterpret_cast<const bf16*>(p.A) + (long)g * p.sA;
+  const bf16* A2g = p.A2 ? reinterpret_cast<const bf16*>(p.A2) + (long)g * p.sA2 : Ag;
+  const bf16* Bg = reinterpret_cast<const bf16*>(p.B) + (long)g * p.sB;
+  const i32x4 rA = make_rsrc(Ag), rA2 = make_rsrc(A2g), rB = make_rsrc(Bg);
+  const int i0 = tm * BM, j0 = tn * BN;
+  const int nreal = p.ones_col ? p.N - 1 : p.N;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const bool do_db = p.ones_col && tn == 0 && wn == 0;   // this wave also sums its A rows
+
+  f32x16 acc[TM][TN], accd[TM];
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+    accd[a] = zero16();
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[a][b] = zero16();
+  }
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u));
+
+  const int nk = (p.K + FBK - 1) / FBK;
+  const int kt0 = z * p.kt_per_split;
+  const int kt1 = min(nk, kt0 + p.kt_per_split);
+
+  auto stage = [&](int kt, char* buf) {
+    const int k0 = kt * FBK;
+    if constexpr (TA) {
+      stage_r<BM>(rA, buf, p.lda, i0, p.M, k0, p.K, w, lane);
+    } else {
+      if (k0 < p.K1) stage_k<BM>(rA, buf, p.lda, i0, p.M, k0, p.K1, w, lane);
+      else stage_k<BM>(rA2, buf, p.lda2, i0, p.M, k0 - p.K1, p.K - p.K1, w, lane);
+    }
+    if constexpr (TB) stage_r<BN>(rB, buf + A_BYTES, p.ldb, j0, nreal, k0, p.K, w, lane);
+    else stage_k<BN>(rB, buf + A_BYTES, p.ldb, j0, nreal, k0, p.K, w, lane);
+  };
+
+  auto compute = [&](const char* buf) {
+    const char* ai = buf;
+    const char* bi = buf + A_BYTES;
+#pragma unroll
+    for (int s = 0; s < FBK / 16; ++s) {
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+        const int rb = wm * (BM / 2) + a * 32;
+        if constexpr (TA) fa[a] = frag_r<BM>(ai, rb, s, lane);
+        else fa[a] = frag_k(ai, rb, s, lane);
+      }
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int rb = wn * (BN / 2) + b * 32;
+        if constexpr (TB) fb[b] = frag_r<BN>(bi, rb, s, lane);
+        else fb[b] = frag_k(bi, rb, s, lane);
+      }
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[b], fa[a], acc[a][b], 0, 0, 0);
+      if (do_db) {
+#pragma unroll
+        for (int a = 0; a < TM; ++a) accd[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fa[a], accd[a], 0, 0, 0);
+      }
+    }
+  };
+
+  // NS-deep ring of LDS stages: tile t + NS - 1 is issued before tile t is multiplied; the
+  // counted wait before each barrier retires exactly the next tile (the DMA of the tiles after
+  // it stays in flight across the barrier).  The WAR distance is one barrier: the stage being
+  // refilled was last read in the previous iteration, which every wave has left.
+  constexpr int PER = BM / 32 + BN / 32;        // LDS-DMA instructions per stage per wave
+  auto wait_keep = [](int keep) {               // all but the `keep` most recent tiles landed
+    if (keep >= 2) vm_wait<2 * PER>();
+    else if (keep == 1) vm_wait<PER>();
+    else vm_wait<0>();
+  };
+  const int pro = min(NS - 1, kt1 - kt0);
+#pragma unroll
+  for (int q = 0; q < NS - 1; ++q)
+    if (q < pro) stage(kt0 + q, smem + q * STAGE);
+  wait_keep(pro - 1);
+  __syncthreads();
+  int cur = 0;
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int nxt = cur == 0 ? NS - 1 : cur - 1;
+    if (kt + NS - 1 < kt1) stage(kt + NS - 1, smem + nxt * STAGE);
+    compute(smem + cur * STAGE);
+    // tiles kt+1 .. kt+ahead are in flight; retire tile kt+1, keep the rest
+    const int ahead = min(NS - 1, kt1 - 1 - kt);
+    wait_keep(ahead - 1);
+    __syncthreads();
+    cur = cur + 1 == NS ? 0 : cur + 1;
+  }
+
+  // epilogue through LDS.  acc[a][b] holds C^T (B fragment fed as the MFMA's A operand), so
+  // lane (r, h) register q is C(i = r, j = accrow(q, h)) of its 32x32 sub-tile and registers
+  // 4g..4g+3 are 4 consecutive j: one ds_write_b128 each into a row-major fp32 tile (pitch
+  // BN + 4 floats: the 8 lanes of a write group hit 8 distinct 4-bank slots).  The tile is
+  // then read back 8 consecutive columns per thread and stored with 16-B (bf16) / 32-B
+  // (fp32) row-contiguous stores, the epilogue applied on the way.
+  const int r = lane & 31, h = lane >> 5;
+  constexpr int CP = BN + 4;
+  float* cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int il = wm * (BM / 2) + a * 32 + r, jl = wn * (BN / 2) + b * 32 + 8 * g4 + 4 * h;
+        *reinterpret_cast<float4*>(cs + il * CP + jl) =
+            make_float4(acc[a][b][4 * g4], acc[a][b][4 * g4 + 1], acc[a][b][4 * g4 + 2], acc[a][b][4 * g4 + 3]);
+      }
+  if (do_db && h == 0) {        // accd[a] = ones * A^T: every register of lane r is sum_k A(r, k)
+    float* wd = p.nsplit > 1 ? slab_db(p, p.G, g, z) : nullptr;
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      const int i = i0 + wm * (BM / 2) + a * 32 + r;
+      if (i < p.M) {
+        if (wd) wd[i] = accd[a][0];
+        else dbias_store(p, g, i, accd[a][0]);
+      }
+    }
+  }
+  __syncthreads();
+  constexpr int TPR = BN / 8, RPP = 256 / TPR;
+  const int jl = (threadIdx.x % TPR) * 8;
+  const int j = j0 + jl;
+  if (j >= nreal) return;
+  const int nv = min(8, nreal - j);
+  float* wsz = p.nsplit > 1 ? slab(p, g, z) : nullptr;
+#pragma unroll 2
+  for (int pass = 0; pass < BM / RPP; ++pass) {
+    const int il = pass * RPP + threadIdx.x / TPR;
+    const int i = i0 + il;
+    if (i >= p.M) break;
+    float v[8];
+    const float4 u0 = *reinterpret_cast<const float4*>(cs + il * CP + jl);
+    const float4 u1 = *reinterpret_cast<const float4*>(cs + il * CP + jl + 4);
+    v[0] = u0.x; v[1] = u0.y; v[2] = u0.z; v[3] = u0.w; v[4] = u1.x; v[5] = u1.y; v[6] = u1.z; v[7] = u1.w;
+    if (wsz) {
+      float* d = wsz + (long)i * nreal + j;
+      if (nv == 8 && (nreal & 3) == 0) {
+        reinterpret_cast<float4*>(d)[0] = u0;
+        reinterpret_cast<float4*>(d)[1] = u1;
+      } else {
+        for (int e = 0; e < nv; ++e) d[e] = v[e];
+      }
+    } else {
+      epi_store8<bf16>(p, g, i, j, nv, v);
+    }
+  }
+}
+
+// ============================================================================ generic path
 constexpr int BK = 32;
 
 template <typename T> struct Stage;
 template <> struct Stage<bf16> { static constexpr int V = 8, PAD = 8; typedef uint4 raw; };
 template <> struct Stage<float> { static constexpr int V = 4, PAD = 4; typedef float4 raw; };
 
-template <typename T>
-__device__ __forceinline__ typename Stage<T>::raw ones_first() {   // {1, 0, 0, ...}
-  typename Stage<T>::raw v{};
-  if constexpr (sizeof(T) == 4) v.x = 1.f;
-  else v.x = 0x3f80u;                                              // bf16(1.0) in the low half
-  return v;
-}
-
-struct GemmArgs {
-  const void* A; const void* A2; const void* B; void* C; const float* bias; const void* R; const float* rscale;
-  float* dbias; float* ws;
-  int M, N, K, K1, kt_per_split, rows_per_sample, act, out_mode, tiles_m, tiles_n, ones_col, nsplit;
-  long lda, lda2, ldb, ldc, sA, sA2, sB, sC, sbias, sdb;
-};
-
 template <typename T, int ROWS>
 struct TileLoader {
   // One operand tile: ROWS (i or j) x BK (k).  Per thread: CH chunks of V contiguous
-  // elements along the operand's contiguous dim.
+  // elements along the operand's contiguous dim (element-wise when !vec: ragged dims).
   static constexpr int V = Stage<T>::V;
   static constexpr int CHUNKS = ROWS * BK / V;
   static constexpr int CH = CHUNKS / 256;
@@ -69,7 +422,7 @@ struct TileLoader {
   // ones_row >= 0: that (virtual) row is all ones for valid k
   template <bool TRANS>
   __device__ __forceinline__ void load(const T* __restrict__ P, long ld, int row0, int nrows, int k0, int kend,
-                                       int ones_row) {
+                                       int ones_row, bool vec) {
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int q = threadIdx.x + c * 256;
@@ -83,12 +436,24 @@ struct TileLoader {
       }
       const int gr = row0 + row, gk = k0 + k;
       r[c] = typename Stage<T>::raw{};
-      if (gk < kend) {
-        if (gr < nrows) {
-          const T* p = !TRANS ? P + (long)gr * ld + gk : P + (long)gk * ld + gr;
-          r[c] = *reinterpret_cast<const typename Stage<T>::raw*>(p);
-        } else if (TRANS && gr == ones_row) {
-          r[c] = ones_first<T>();
+      if (vec) {
+        if (gk < kend) {
+          if (gr < nrows) {
+            const T* p = !TRANS ? P + (long)gr * ld + gk : P + (long)gk * ld + gr;
+            r[c] = *reinterpret_cast<const typename Stage<T>::raw*>(p);
+          } else if (TRANS && gr == ones_row) {
+            reinterpret_cast<T*>(&r[c])[0] = from_f32<T>(1.f);
+          }
+        }
+      } else {
+        T* e = reinterpret_cast<T*>(&r[c]);
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const int rr = TRANS ? gr + v : gr, kk = TRANS ? gk : gk + v;
+          if (kk < kend) {
+            if (rr < nrows) e[v] = !TRANS ? P[(long)rr * ld + kk] : P[(long)kk * ld + rr];
+            else if (TRANS && rr == ones_row) e[v] = from_f32<T>(1.f);
+          }
         }
       }
     }
@@ -114,18 +479,14 @@ struct TileLoader {
 };
 
 template <typename T, int BM, int BN, bool TA, bool TB>
-__global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
+__global__ __launch_bounds__(256) void gemm_generic_kernel(const GemmArgs p) {
   typedef MF<T> mf;
   constexpr int LD = BK + Stage<T>::PAD;
   constexpr int TM = BM / 64, TN = BN / 64;     // 32x32 MFMA tiles per wave
   __shared__ __attribute__((aligned(16))) T As[2][BM * LD];
   __shared__ __attribute__((aligned(16))) T Bs[2][BN * LD];
 
-  // XCD-aware tile order: hardware dispatches block b to XCD b % 8; give XCD x the
-  // contiguous tile range [x * per, (x + 1) * per) so one XCD walks one A row-panel.
-  const int ntiles = p.tiles_m * p.tiles_n;
-  int t = blockIdx.x;
-  if (ntiles % 8 == 0) t = (t % 8) * (ntiles / 8) + t / 8;
+  const int t = xcd_tile(blockIdx.x, p.tiles_m * p.tiles_n);
   const int tm = t / p.tiles_n, tn = t % p.tiles_n;
   const int g = blockIdx.y, z = blockIdx.z;
   const T* Ag = reinterpret_cast<const T*>(p.A) + (long)g * p.sA;
@@ -134,6 +495,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
   const int i0 = tm * BM, j0 = tn * BN;
   const int nreal = p.ones_col ? p.N - 1 : p.N;     // real B rows (the ones row is virtual)
   const int ones_row = p.ones_col ? p.N - 1 : -1;
+  const bool vec = p.vec;
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = w >> 1, wn = w & 1;
@@ -153,9 +515,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
 
   auto load_tile = [&](int kt) {
     const int k0 = kt * BK;
-    if (k0 < p.K1) la.template load<TA>(Ag, p.lda, i0, p.M, k0, p.K1, -1);
-    else la.template load<TA>(A2g, p.lda2, i0, p.M, k0 - p.K1, p.K - p.K1, -1);
-    lb.template load<TB>(Bg, p.ldb, j0, nreal, k0, p.K, ones_row);
+    if (k0 < p.K1) la.template load<TA>(Ag, p.lda, i0, p.M, k0, p.K1, -1, vec);
+    else la.template load<TA>(A2g, p.lda2, i0, p.M, k0 - p.K1, p.K - p.K1, -1, vec);
+    lb.template load<TB>(Bg, p.ldb, j0, nreal, k0, p.K, ones_row, vec);
   };
 
   if (kt0 < kt1) {
@@ -195,100 +557,159 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
   for (int b = 0; b < TN; ++b) {
     const int j = j0 + wn * (BN / 2) + b * 32 + r;
     if (j >= p.N) continue;
-    if (p.nsplit > 1) {        // raw fp32 partial slab (g, z, i, j), N columns incl. ones column
-      float* wsz = p.ws + (((long)g * p.nsplit + z) * p.M) * p.N;
-#pragma unroll
-      for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int i = i0 + wm * (BM / 2) + a * 32 + accrow(q, h);
-          if (i < p.M) wsz[(long)i * p.N + j] = acc[a][b][q];
-        }
-      continue;
-    }
-    if (j == ones_row) {       // bias gradient column
+    const bool dbcol = j == ones_row;
+    if (p.nsplit > 1) {
+      float* wsz = dbcol ? slab_db(p, p.G, g, z) : slab(p, g, z);
 #pragma unroll
       for (int a = 0; a < TM; ++a)
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
           const int i = i0 + wm * (BM / 2) + a * 32 + accrow(q, h);
           if (i < p.M) {
-            float* d = p.dbias + (long)g * p.sdb + i;
-            *d = p.out_mode == 2 ? *d + acc[a][b][q] : acc[a][b][q];
+            if (dbcol) wsz[i] = acc[a][b][q];
+            else wsz[(long)i * nreal + j] = acc[a][b][q];
           }
         }
       continue;
     }
-    const float bj = p.bias ? p.bias[(long)g * p.sbias + j] : 0.f;
 #pragma unroll
     for (int a = 0; a < TM; ++a) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int i = i0 + wm * (BM / 2) + a * 32 + accrow(q, h);
         if (i >= p.M) continue;
-        float v = act_fwd(acc[a][b][q] + bj, p.act);
-        const long off = (long)g * p.sC + (long)i * p.ldc + j;
-        if (p.R) {
-          const float sc = p.rscale ? p.rscale[((long)g * p.M + i) / p.rows_per_sample] : 1.f;
-          v = to_f32(reinterpret_cast<const T*>(p.R)[off]) + sc * v;
-        }
-        if (p.out_mode == 0) {
-          reinterpret_cast<T*>(p.C)[off] = from_f32<T>(v);
-        } else if (p.out_mode == 1) {
-          reinterpret_cast<float*>(p.C)[off] = v;
-        } else {
-          reinterpret_cast<float*>(p.C)[off] += v;
-        }
+        if (dbcol) dbias_store(p, g, i, acc[a][b][q]);
+        else epi_store<T>(p, g, i, j, acc[a][b][q]);
       }
     }
   }
 }
 
-// sum the nsplit partial slabs; fp32 output (out_mode 1 store / 2 accumulate), strided C;
-// column N-1 goes to dbias when ones_col.  4 columns per thread.
+// ============================================================================ split-K reducer
+// Sums the nsplit slabs and applies the full epilogue.  A thread owns one group of 8
+// consecutive output columns and every ZL-th slab (ZL z-lanes per group: the wgrads carry up
+// to 64 slabs, and a lone thread walking them serially is latency-bound); the z-lanes meet
+// in LDS and lane 0 finishes the group.  Groups past M x ceil(Nr/8) are bias-gradient rows.
+template <typename T, int ZL>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs p) {
+  constexpr int GPB = 256 / ZL;                 // groups per block
+  __shared__ float4 red[ZL > 1 ? ZL - 1 : 1][GPB][2];
   const int g = blockIdx.y;
-  const long MN = (long)p.M * p.N;
-  const long e = ((long)blockIdx.x * 256 + threadIdx.x);
-  if (e >= MN) return;
-  const float* src = p.ws + (long)g * p.nsplit * MN + e;
-  float s = 0.f;
-  for (int z = 0; z < p.nsplit; ++z) s += src[(long)z * MN];
-  const int i = (int)(e / p.N), j = (int)(e % p.N);
-  float* d;
-  if (p.ones_col && j == p.N - 1) d = p.dbias + (long)g * p.sdb + i;
-  else d = reinterpret_cast<float*>(p.C) + (long)g * p.sC + (long)i * p.ldc + j;
-  *d = p.out_mode == 2 ? *d + s : s;
+  const int Nr = p.ones_col ? p.N - 1 : p.N;
+  const int ng = (Nr + 7) >> 3;
+  const long MN = (long)p.M * Nr;
+  const long work = (long)p.M * ng;
+  const int gl = threadIdx.x % GPB, zl = threadIdx.x / GPB;
+  const long e = (long)blockIdx.x * GPB + gl;
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int i = 0, j = 0, nv = 0;
+  if (e < work) {
+    i = (int)(e / ng); j = (int)(e % ng) * 8; nv = min(8, Nr - j);
+    const float* src = slab(p, g, 0) + (long)i * Nr + j;
+    if (nv == 8 && (Nr & 3) == 0) {
+      int z = zl;
+#pragma unroll 4
+      for (; z < p.nsplit; z += ZL) {
+        const float4 a = reinterpret_cast<const float4*>(src + (long)z * MN)[0];
+        const float4 b = reinterpret_cast<const float4*>(src + (long)z * MN)[1];
+        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+      }
+    } else {
+      for (int z = zl; z < p.nsplit; z += ZL)
+        for (int c = 0; c < nv; ++c) v[c] += src[(long)z * MN + c];
+    }
+  } else if (p.ones_col && e < work + p.M) {
+    const float* src = slab_db(p, p.G, g, 0) + (e - work);
+#pragma unroll 4
+    for (int z = zl; z < p.nsplit; z += ZL) v[0] += src[(long)z * p.M];
+  }
+  if constexpr (ZL > 1) {
+    if (zl > 0) {
+      red[zl - 1][gl][0] = make_float4(v[0], v[1], v[2], v[3]);
+      red[zl - 1][gl][1] = make_float4(v[4], v[5], v[6], v[7]);
+    }
+    __syncthreads();
+    if (zl > 0) return;
+#pragma unroll
+    for (int q = 0; q < ZL - 1; ++q) {
+      const float4 a = red[q][gl][0], b = red[q][gl][1];
+      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    }
+  }
+  if (e < work) epi_store8<T>(p, g, i, j, nv, v);
+  else if (p.ones_col && e < work + p.M) dbias_store(p, g, (int)(e - work), v[0]);
 }
 
-template <typename T, int BM, int BN>
-void launch(const GemmArgs& a, int G, int nsplit, int transA, int transB, hipStream_t s) {
-  dim3 grid(a.tiles_m * a.tiles_n, G, nsplit);
-#define CMX_GEMM_LAUNCH(TA, TB) hipLaunchKernelGGL((gemm_kernel<T, BM, BN, TA, TB>), grid, dim3(256), 0, s, a)
-  if (!transA && !transB) CMX_GEMM_LAUNCH(false, false);
-  else if (!transA && transB) CMX_GEMM_LAUNCH(false, true);
-  else if (transA && transB) CMX_GEMM_LAUNCH(true, true);
+template <typename T>
+void launch_reduce(const GemmArgs& a, int G, long groups, hipStream_t s) {
+  if (a.nsplit >= 32) hipLaunchKernelGGL((splitk_reduce_kernel<T, 16>), dim3(cdiv(groups, 16), G), dim3(256), 0, s, a);
+  else if (a.nsplit >= 8) hipLaunchKernelGGL((splitk_reduce_kernel<T, 4>), dim3(cdiv(groups, 64), G), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((splitk_reduce_kernel<T, 1>), dim3(cdiv(groups, 256), G), dim3(256), 0, s, a);
+}
+
+// ============================================================================ host side
+template <int BM, int BN, int NS>
+void launch_bf16(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream_t s) {
+  dim3 grid(a.tiles_m * a.tiles_n * G * nsplit);
+#define CMX_GEMM_LAUNCH(TA, TB) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, TA, TB, NS>), grid, dim3(256), 0, s, a)
+  if (!tA && !tB) CMX_GEMM_LAUNCH(false, false);
+  else if (!tA && tB) CMX_GEMM_LAUNCH(false, true);
+  else if (tA && tB) CMX_GEMM_LAUNCH(true, true);
   else CMX_GEMM_LAUNCH(true, false);
 #undef CMX_GEMM_LAUNCH
 }
 
-template <typename T>
-void dispatch_tile(GemmArgs& a, int G, int nsplit, int transA, int transB, hipStream_t s) {
-  // tile shape: the output's narrow side gets 64 (stage-1 C = 64 outputs, 64-row wgrads)
-  const bool m64 = a.M <= 64, n64 = a.N <= 64;
-  if (m64 && n64) {
-    a.tiles_m = (a.M + 63) / 64; a.tiles_n = (a.N + 63) / 64;
-    launch<T, 64, 64>(a, G, nsplit, transA, transB, s);
-  } else if (m64) {
-    a.tiles_m = (a.M + 63) / 64; a.tiles_n = (a.N + 127) / 128;
-    launch<T, 64, 128>(a, G, nsplit, transA, transB, s);
-  } else if (n64) {
-    a.tiles_m = (a.M + 127) / 128; a.tiles_n = (a.N + 63) / 64;
-    launch<T, 128, 64>(a, G, nsplit, transA, transB, s);
-  } else {
-    a.tiles_m = (a.M + 127) / 128; a.tiles_n = (a.N + 127) / 128;
-    launch<T, 128, 128>(a, G, nsplit, transA, transB, s);
-  }
+template <int BM, int BN>
+void launch_bf16_ns(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream_t s) {
+  const long blocks = (long)a.tiles_m * a.tiles_n * G * nsplit;
+  if (blocks <= 256) launch_bf16<BM, BN, 4>(a, G, nsplit, tA, tB, s);
+  else launch_bf16<BM, BN, 2>(a, G, nsplit, tA, tB, s);
+}
+
+template <typename T, int BM, int BN>
+void launch_generic(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream_t s) {
+  dim3 grid(a.tiles_m * a.tiles_n, G, nsplit);
+#define CMX_GEMM_LAUNCH(TA, TB) hipLaunchKernelGGL((gemm_generic_kernel<T, BM, BN, TA, TB>), grid, dim3(256), 0, s, a)
+  if (!tA && !tB) CMX_GEMM_LAUNCH(false, false);
+  else if (!tA && tB) CMX_GEMM_LAUNCH(false, true);
+  else if (tA && tB) CMX_GEMM_LAUNCH(true, true);
+  else CMX_GEMM_LAUNCH(true, false);
+#undef CMX_GEMM_LAUNCH
+}
+
+// the bf16 fast path needs every operand row to be whole 16-B chunks on 16-B boundaries
+// and every per-group operand to be addressable with 31-bit byte offsets
+bool fast_ok(const void* A, const void* A2, const void* B, int M, int N, int K, int K1, long lda, long lda2, long ldb,
+             long sA, long sA2, long sB, int tA, int tB, int ones_col) {
+  const int nb = ones_col ? N - 1 : N;
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (!al(A) || !al(B) || (A2 && !al(A2))) return false;
+  if (lda % 8 || ldb % 8 || sA % 8 || sB % 8 || K % 8) return false;
+  if (tA ? M % 8 : false) return false;
+  if (tB ? nb % 8 : false) return false;
+  if (A2 && (K1 % FBK || lda2 % 8 || sA2 % 8 || tA)) return false;
+  const long extA = tA ? (long)K * lda : (long)M * lda;
+  const long extB = tB ? (long)K * ldb : (long)nb * ldb;
+  const long extA2 = A2 ? (long)M * lda2 : 0;
+  const long lim = (1L << 30) - 64;             // elements (bf16) -> < 2^31 bytes
+  return extA < lim && extB < lim && extA2 < lim;
+}
+
+int tile_dim(int n) { return n <= 64 ? 64 : 128; }
+
+// split factor for the bf16 path: one block per CU when the output has few tiles (each split
+// keeps >= 4 k-tiles of 64; the slabs cost 8 B of HBM traffic per output element and split)
+int auto_split(int G, int M, int N, int K, int ones_col) {
+  const int nb = ones_col ? N - 1 : N;
+  const long tiles = (long)cdiv(M, tile_dim(M)) * cdiv(nb, tile_dim(nb)) * G;
+  const int nk = (K + FBK - 1) / FBK;
+  if (tiles >= 200 || nk < 8) return 1;
+  long s = (256 + tiles - 1) / tiles;
+  s = s < nk / 4 ? s : nk / 4;
+  if (s > 128) s = 128;
+  if (s < 1) s = 1;
+  const int per = (nk + (int)s - 1) / (int)s;
+  return (nk + per - 1) / per;
 }
 
 }  // namespace
@@ -299,45 +720,86 @@ size_t cmx_gemm_workspace(int G, int M, int N, int splitk) {
   return splitk > 1 ? (size_t)G * splitk * M * N * sizeof(float) : 0;
 }
 
+int cmx_gemm_splitk(int G, int M, int N, int K, int ones_col, int dtype) {
+  if (G <= 0 || M <= 0 || N <= 0 || K <= 0) return 1;
+  if (dtype == 1) return auto_split(G, M, N, K, ones_col);
+  // generic path: BK = 32, aim for ~1024 blocks with >= 8 k-tiles per split
+  const int nb = ones_col ? N : N;
+  const long tiles = (long)cdiv(M, M <= 64 ? 64 : 128) * cdiv(nb, nb <= 64 ? 64 : 128) * G;
+  const int nk = (K + BK - 1) / BK;
+  long s = 1024 / (tiles > 0 ? tiles : 1);
+  if (s > nk / 8) s = nk / 8;
+  if (s > 64) s = 64;
+  return s < 1 ? 1 : (int)s;
+}
+
 int cmx_gemm(const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R,
              const float* rscale, float* dbias, float* workspace, int G, int M, int N, int K, int K1, int64_t lda,
              int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias,
              int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode, int ones_col, int splitk,
              int dtype, hipStream_t s) {
-  const int V = dtype == 0 ? 4 : 8;
   CMX_REQUIRE(G > 0 && M > 0 && N > 0 && K > 0, CMX_ERR_SHAPE, "gemm: empty problem G=%d M=%d N=%d K=%d", G, M, N, K);
+  CMX_REQUIRE(dtype == 0 || dtype == 1, CMX_ERR_DTYPE, "gemm: unsupported dtype %d", dtype);
   CMX_REQUIRE(out_mode >= 0 && out_mode <= 2 && act >= 0 && act <= 3, CMX_ERR_ARG, "gemm: out_mode/act");
   CMX_REQUIRE(!(R && out_mode == 2), CMX_ERR_ARG, "gemm: residual with accumulate");
   if (!A2) K1 = K;
-  CMX_REQUIRE(K1 > 0 && K1 <= K && (K1 == K || (K1 % BK == 0 && !transA)), CMX_ERR_SHAPE,
-              "gemm: second A segment needs K1 %% %d == 0 and transA = 0 (K1=%d K=%d)", BK, K1, K);
-  // vector staging: the contiguous dim of each operand moves in chunks of V elements
-  const int nb = ones_col ? N - 1 : N;
-  CMX_REQUIRE((transA ? M : K) % V == 0 && (transB ? nb : K) % V == 0 && (K - K1) % V == 0, CMX_ERR_SHAPE,
-              "gemm: contiguous operand dims must be multiples of %d (M=%d N=%d K=%d tA=%d tB=%d)", V, M, N, K,
-              transA, transB);
-  CMX_REQUIRE(lda % V == 0 && ldb % V == 0 && sA % V == 0 && sB % V == 0 && (!A2 || (lda2 % V == 0 && sA2 % V == 0)),
-              CMX_ERR_SHAPE, "gemm: operand strides must be multiples of %d", V);
+  CMX_REQUIRE(K1 > 0 && K1 <= K && (K1 == K || !transA), CMX_ERR_SHAPE,
+              "gemm: a second A segment needs transA = 0 (K1=%d K=%d)", K1, K);
   CMX_REQUIRE(!R || rows_per_sample > 0, CMX_ERR_ARG, "gemm: rows_per_sample");
   CMX_REQUIRE(!ones_col || (transB && dbias && N >= 2 && out_mode != 0 && !bias && !R && act == 0), CMX_ERR_ARG,
               "gemm: ones_col (bias gradient) needs transB, dbias, fp32 output and no epilogue");
-  CMX_REQUIRE(splitk >= 1 && (splitk == 1 || (workspace && out_mode != 0 && !bias && !R && act == 0)), CMX_ERR_ARG,
-              "gemm: split-K needs a workspace, fp32 output and no epilogue");
   CMX_REQUIRE((long)M * N < (1L << 31) && (long)M * K < (1L << 40), CMX_ERR_SHAPE, "gemm: problem too large");
+  const bool fast = dtype == 1 && fast_ok(A, A2, B, M, N, K, K1, lda, lda2, ldb, sA, sA2, sB, transA, transB, ones_col);
+  const int V = dtype == 0 ? 4 : 8;
+  const int nb = ones_col ? N - 1 : N;
+  const bool vec = (transA ? M : K) % V == 0 && (transB ? nb : K) % V == 0 && (K - K1) % V == 0 && (K1 == K || K1 % V == 0) &&
+                   lda % V == 0 && ldb % V == 0 && sA % V == 0 && sB % V == 0 && (!A2 || (lda2 % V == 0 && sA2 % V == 0)) &&
+                   ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && (!A2 || (uintptr_t)A2 % 16 == 0);
+  CMX_REQUIRE(fast || K1 == K || K1 % BK == 0, CMX_ERR_SHAPE, "gemm: second A segment needs K1 %% %d == 0", BK);
+  if (splitk <= 0) splitk = fast ? auto_split(G, M, N, K, ones_col) : cmx_gemm_splitk(G, M, N, K, ones_col, 0);
+  CMX_REQUIRE(splitk == 1 || workspace, CMX_ERR_ARG, "gemm: split-K needs a workspace");
   GemmArgs a{};
   a.A = A; a.A2 = A2; a.B = B; a.C = C; a.bias = bias; a.R = R; a.rscale = rscale; a.dbias = dbias; a.ws = workspace;
-  a.M = M; a.N = N; a.K = K; a.K1 = K1; a.rows_per_sample = rows_per_sample > 0 ? rows_per_sample : 1;
-  a.act = act; a.out_mode = out_mode; a.ones_col = ones_col; a.nsplit = splitk;
+  a.G = G; a.M = M; a.N = N; a.K = K; a.K1 = K1; a.rows_per_sample = rows_per_sample > 0 ? rows_per_sample : 1;
+  a.act = act; a.out_mode = out_mode; a.ones_col = ones_col; a.vec = vec;
+  // 8-column epilogue groups as aligned vectors: C (and R) rows start on 16-B boundaries
+  const long esz = out_mode == 0 ? (dtype == 1 ? 2 : 4) : 4;
+  a.cvec = ((uintptr_t)C % 16 == 0) && (ldc * esz) % 16 == 0 && (sC * esz) % 16 == 0 &&
+           (!R || (uintptr_t)R % 16 == 0);
   a.lda = lda; a.lda2 = lda2; a.ldb = ldb; a.ldc = ldc; a.sA = sA; a.sA2 = sA2; a.sB = sB; a.sC = sC;
   a.sbias = sbias; a.sdb = sdb;
-  const int nk = (K + BK - 1) / BK;
+  const int kstep = fast ? FBK : BK;
+  const int nk = (K + kstep - 1) / kstep;
   a.kt_per_split = (nk + splitk - 1) / splitk;
-  if (dtype == 1) dispatch_tile<bf16>(a, G, splitk, transA, transB, s);
-  else if (dtype == 0) dispatch_tile<float>(a, G, splitk, transA, transB, s);
-  else { cmx_set_error("gemm: unsupported dtype %d", dtype); return CMX_ERR_DTYPE; }
+  splitk = (nk + a.kt_per_split - 1) / a.kt_per_split;      // no empty splits
+  a.nsplit = splitk;
+  if (fast) {
+    const int bm = tile_dim(M), bn = tile_dim(nb);
+    a.tiles_m = cdiv(M, bm); a.tiles_n = cdiv(nb, bn);
+    if (bm == 64 && bn == 64) launch_bf16_ns<64, 64>(a, G, splitk, transA, transB, s);
+    else if (bm == 64) launch_bf16_ns<64, 128>(a, G, splitk, transA, transB, s);
+    else if (bn == 64) launch_bf16_ns<128, 64>(a, G, splitk, transA, transB, s);
+    else launch_bf16_ns<128, 128>(a, G, splitk, transA, transB, s);
+  } else {
+    // tile shape: the output's narrow side gets 64 (stage-1 C = 64 outputs, 64-row wgrads)
+    const bool m64 = M <= 64, n64 = N <= 64;
+    a.tiles_m = cdiv(M, m64 ? 64 : 128); a.tiles_n = cdiv(N, n64 ? 64 : 128);
+    if (dtype == 1) {
+      if (m64 && n64) launch_generic<bf16, 64, 64>(a, G, splitk, transA, transB, s);
+      else if (m64) launch_generic<bf16, 64, 128>(a, G, splitk, transA, transB, s);
+      else if (n64) launch_generic<bf16, 128, 64>(a, G, splitk, transA, transB, s);
+      else launch_generic<bf16, 128, 128>(a, G, splitk, transA, transB, s);
+    } else {
+      if (m64 && n64) launch_generic<float, 64, 64>(a, G, splitk, transA, transB, s);
+      else if (m64) launch_generic<float, 64, 128>(a, G, splitk, transA, transB, s);
+      else if (n64) launch_generic<float, 128, 64>(a, G, splitk, transA, transB, s);
+      else launch_generic<float, 128, 128>(a, G, splitk, transA, transB, s);
+    }
+  }
   if (splitk > 1) {
-    const long MN = (long)M * N;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(cdiv(MN, 256), G), dim3(256), 0, s, a);
+    const long work = (long)M * ((nb + 7) / 8) + (ones_col ? M : 0);
+    if (dtype == 1) launch_reduce<bf16>(a, G, work, s);
+    else launch_reduce<float>(a, G, work, s);
   }
   return cmx_check_launch("gemm");
 }

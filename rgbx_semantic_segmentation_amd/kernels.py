@@ -102,19 +102,10 @@ def _operand(t: torch.Tensor, name: str):
     raise ValueError(f"gemm: operand {name} needs a unit stride along rows or k, got strides {t.stride()}")
 
 
-def gemm_auto_split(G: int, M: int, N: int, K: int) -> int:
-    """Split-K factor: aim for ~1024 blocks (4 per CU) with >= 8 k-tiles of 32 per split;
-    only the wgrad shapes (small M x N output, K = tokens) end up split."""
-    tiles = -(-M // (64 if M <= 64 else 128)) * -(-N // (64 if N <= 64 else 128))
-    nk = -(-K // 32)
-    s = max(1, min(64, nk // 8, 1024 // max(1, tiles * G)))
-    return s
-
-
 def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, bias: torch.Tensor | None = None,
          residual: torch.Tensor | None = None, rscale: torch.Tensor | None = None, rows_per_sample: int = 1,
          act: str = "none", out_mode: int = 0, A2: torch.Tensor | None = None, dbias: torch.Tensor | None = None,
-         splitk: int = 1) -> torch.Tensor:
+         splitk: int = 0) -> torch.Tensor:
     """C[g] = epi([A[g] | A2[g]] @ B[g]^T) on logical views A (G, M, K1), A2 (G, M, K-K1),
     B (G, N, K), C (G, M, N).
 
@@ -122,8 +113,9 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, bias: torch.Tensor |
     the kernel reads it in place.  out_mode: 0 store in C's dtype (= A's), 1 store fp32,
     2 accumulate into fp32 C.  bias (G, N) fp32 (any batch stride, unit inner stride);
     residual has C's layout: C = residual + rscale[(g*M + i) // rows_per_sample] * act(acc + bias).
-    dbias (G, M) fp32: also produce sum_k A(i, k) (the bias gradient of a wgrad, via a
-    virtual ones column of B).  splitk > 1 splits K over blocks (wgrad over tokens); 0 = auto."""
+    dbias (G, M) fp32: also produce sum_k A(i, k) (the bias gradient of a wgrad).
+    splitk > 1 splits K over blocks into fp32 slabs reduced with the epilogue applied;
+    0 = the library's choice (cmx_gemm_splitk: fill the chip when the output has few tiles)."""
     G, M, K1 = A.shape
     Kd = K1 + (A2.shape[2] if A2 is not None else 0)
     N = B.shape[1]
@@ -144,8 +136,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, bias: torch.Tensor |
     if residual is not None:
         assert residual.shape == C.shape and residual.stride() == C.stride() and residual.dtype == C.dtype
     Nk = N + (1 if dbias is not None else 0)
-    if splitk == 0:
-        splitk = gemm_auto_split(G, M, Nk, Kd)
+    if splitk <= 0:
+        splitk = query("cmx_gemm_splitk", G, M, Nk, Kd, int(dbias is not None), dtype_code(A))
     ws = _ws(query("cmx_gemm_workspace", G, M, Nk, splitk), A.device) if splitk > 1 else None
     call("cmx_gemm", ptr(A), ptr(A2), ptr(B), ptr(C), ptr(bias), ptr(residual), ptr(rscale), ptr(dbias), ptr(ws),
          G, M, Nk, Kd, K1, lda, lda2, ldb, C.stride(1), sA, sA2, sB, C.stride(0), sbias, sdb, int(rows_per_sample),

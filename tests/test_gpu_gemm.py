@@ -49,12 +49,15 @@ def test_gemm_layouts(dev, dtype, G, M, N, K, tA, tB):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("act", ["none", "gelu", "relu"])
 @pytest.mark.parametrize("res", [False, True])
-def test_gemm_epilogues(dev, dtype, act, res):
+@pytest.mark.parametrize("K", [96, 2048])
+def test_gemm_epilogues(dev, dtype, act, res, K):
+    """K = 2048 on a 600 x 192 output takes the auto split-K path: the epilogue then runs in
+    the slab reducer."""
     torch.manual_seed(1)
     from rgbx_semantic_segmentation_amd import kernels as Kn
-    G, M, N, K, rps = 2, 600, 192, 96, 300
+    G, M, N, rps = 2, 600, 192, 300
     A = torch.randn(G, M, K, device="cuda").to(dtype)
-    B = torch.randn(G, N, K, device="cuda").to(dtype) * 0.1
+    B = torch.randn(G, N, K, device="cuda").to(dtype) * (1.0 / K ** 0.5)
     bias = torch.randn(G, N, device="cuda")
     R = torch.randn(G, M, N, device="cuda").to(dtype) if res else None
     s = torch.tensor([0.0, 1.25, 1.25, 0.0], device="cuda") if res else None
@@ -118,3 +121,39 @@ def test_gemm_wgrad_splitk_bias_grad(dev, dtype, splitk, accumulate):
     assert rel(Wg[:, :, k0:k0 + Kx], refW) < 1e-5
     assert rel(bg, refb) < 1e-5
     assert torch.equal(Wg[:, :, :k0], W0[:, :, :k0]) and torch.equal(Wg[:, :, k0 + Kx:], W0[:, :, k0 + Kx:])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("tA,tB", [(0, 0), (0, 1)])
+def test_gemm_unaligned_dims(dev, dtype, tA, tB):
+    """Row strides / reduction lengths that are not whole 16-B chunks (K = 9 classes of the
+    B0 classifier's dgrad, lda = 9) take the element-wise generic path."""
+    torch.manual_seed(5)
+    from rgbx_semantic_segmentation_amd import kernels as Kn
+    G, M, N, K = 1, 768, 512, 9
+    A = torch.randn(G, M, K, device="cuda").to(dtype)
+    B = torch.randn(G, N, K, device="cuda").to(dtype)
+    Bv = B.transpose(1, 2).contiguous().transpose(1, 2) if tB else B
+    C = torch.empty(G, M, N, device="cuda", dtype=dtype)
+    Kn.gemm(A, Bv, C)
+    ref = torch.bmm(A.float(), B.float().transpose(1, 2))
+    assert rel(C, ref) < (1e-5 if dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("G,M,N,K", [(2, 38400, 256, 64), (1, 38400, 512, 2048), (2, 600, 64, 4096),
+                                     (2, 2400, 320, 1280), (2, 64, 256, 38400)])
+@pytest.mark.parametrize("tA,tB", [(0, 0), (0, 1), (1, 1)])
+def test_gemm_step_shapes_bf16(dev, G, M, N, K, tA, tB):
+    """The bf16 LDS-DMA path on the shapes of the B2 step (census in scripts/gemm_census.py):
+    large-M forward / dgrad tiles, small-output split-K and token-reduction wgrads."""
+    torch.manual_seed(6)
+    from rgbx_semantic_segmentation_amd import kernels as Kn
+    dt = torch.bfloat16
+    A = torch.randn(G, M, K, device="cuda").to(dt)
+    B = torch.randn(G, N, K, device="cuda").to(dt)
+    Av = A.transpose(1, 2).contiguous().transpose(1, 2) if tA else A
+    Bv = B.transpose(1, 2).contiguous().transpose(1, 2) if tB else B
+    C = torch.empty(G, M, N, device="cuda", dtype=torch.float32)
+    Kn.gemm(Av, Bv, C, out_mode=1)
+    ref = torch.bmm(A.float(), B.float().transpose(1, 2))
+    assert rel(C, ref) < 1e-5

@@ -138,8 +138,12 @@ def test_train_step_grads_fp32(dev, backbone, H, W):
     # ReLU kinks: a pre-activation within fp32 rounding of 0 (seen: +3.6e-9 in fp64, -1.8e-8
     # in fp32) flips one mask element and moves a cancellation-dominated weight gradient by a
     # few percent.  Allow a bounded number of such outliers, each still < 5e-2.
+    # The FFM channel_proj Linear feeds a ReLU directly (net_utils.py:265-269) and at 96x128
+    # its stage-3/4 weight gradient sums over only 96 / 24 tokens, so one flipped mask element
+    # moves it by up to ~6 % (seen with the hipBLASLt path and the cmx GEMM alike, at
+    # different stages): those may reach 1e-1.
     n_allowed = max(2, len(worst) // 100)
-    assert len(bad) <= n_allowed and all(b[0] < 5e-2 for b in bad), bad[:8]
+    assert len(bad) <= n_allowed and all(b[0] < (1e-1 if "channel_proj" in b[2] else 5e-2) for b in bad), bad[:8]
     for (n, b) in model.named_buffers():
         if "running" in n:
             e = relerr(b, dict(ref.named_buffers())[n])
