@@ -17,6 +17,8 @@
 // in flight together.  Lanes of a wave are consecutive quads: every load / store is a
 // coalesced 8-byte (bf16) / 16-byte (fp32) segment of a channel-contiguous NHWC row.
 // The activation is a template argument: the GELU kernels carry no dead ReLU/sigmoid code.
+// (That strip path now serves only channel counts that are not multiples of 32; see the
+// LDS-tiled path below for every layer of B0 / B2.)
 #include "cmx_common.h"
 
 namespace {
@@ -253,6 +255,289 @@ __global__ void dw_scatter_kernel(const float* __restrict__ tmp, float* __restri
   }
 }
 
+// ============================================================================ LDS-tiled path
+// Block = one tile of TY x TX output pixels x CB channels (CB = 32 or 64) of one image.
+// Input tiles (with halo) are staged in LDS by fully coalesced 16-B-per-lane loads (8
+// consecutive lanes = one pixel's CB channels); each thread then owns ONE group of 8
+// channels -- its 72 taps and 8 biases stay in registers -- and walks tile pixels, reading
+// the 3x3 neighbourhood from LDS (lanes on consecutive pixels: conflict-free).
+//
+// The backward is one kernel: dz = da * act'(z) is recomputed (z from the h tile) on the
+// tile plus a 1-pixel halo into LDS, then dh = conv^T(dz) and the dW / db partial sums of
+// the inner pixels come from that LDS image.  dz never goes to HBM (the old path wrote it,
+// read it back for dh, and re-read h for dW).  Per-block dW / db partials are summed across
+// the threads of a channel group by a butterfly reduce-scatter (80 -> 5 values per lane)
+// and written to a (group, tile) slab that reduce_partials folds.
+constexpr int TY2 = 8, TX2 = 16;                 // inner tile
+constexpr int EY = TY2 + 2, EX = TX2 + 2;         // + 1-pixel halo
+constexpr int HY = TY2 + 4, HX = TX2 + 4;         // + 2-pixel halo (backward h tile)
+
+template <typename T> struct V8;                  // 8 channels as stored
+template <> struct V8<bf16> { uint4 a; };
+template <> struct V8<float> { float4 a, b; };
+
+template <typename T>
+__device__ __forceinline__ V8<T> v8_load(const T* p) {
+  V8<T> v;
+  if constexpr (sizeof(T) == 2) v.a = *reinterpret_cast<const uint4*>(p);
+  else { v.a = reinterpret_cast<const float4*>(p)[0]; v.b = reinterpret_cast<const float4*>(p)[1]; }
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ void v8_store(T* p, const V8<T>& v) {
+  if constexpr (sizeof(T) == 2) *reinterpret_cast<uint4*>(p) = v.a;
+  else { reinterpret_cast<float4*>(p)[0] = v.a; reinterpret_cast<float4*>(p)[1] = v.b; }
+}
+template <typename T>
+__device__ __forceinline__ V8<T> v8_zero() {
+  V8<T> v;
+  if constexpr (sizeof(T) == 2) v.a = make_uint4(0, 0, 0, 0);
+  else { v.a = make_float4(0.f, 0.f, 0.f, 0.f); v.b = v.a; }
+  return v;
+}
+// unpack to 4 packed pairs
+template <typename T>
+__device__ __forceinline__ void v8_unpack(const V8<T>& v, cmx_f2 (&o)[4]) {
+  if constexpr (sizeof(T) == 2) {
+    const uint32_t w[4] = {v.a.x, v.a.y, v.a.z, v.a.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = (cmx_f2){__uint_as_float(w[i] << 16), __uint_as_float(w[i] & 0xffff0000u)};
+  } else {
+    o[0] = (cmx_f2){v.a.x, v.a.y}; o[1] = (cmx_f2){v.a.z, v.a.w};
+    o[2] = (cmx_f2){v.b.x, v.b.y}; o[3] = (cmx_f2){v.b.z, v.b.w};
+  }
+}
+template <typename T>
+__device__ __forceinline__ V8<T> v8_pack(const cmx_f2 (&o)[4]) {
+  V8<T> v;
+  if constexpr (sizeof(T) == 2) {
+    v.a = make_uint4(pack2_bf16(o[0].x, o[0].y), pack2_bf16(o[1].x, o[1].y), pack2_bf16(o[2].x, o[2].y),
+                     pack2_bf16(o[3].x, o[3].y));
+  } else {
+    v.a = make_float4(o[0].x, o[0].y, o[1].x, o[1].y);
+    v.b = make_float4(o[2].x, o[2].y, o[3].x, o[3].y);
+  }
+  return v;
+}
+
+// 8 channels' 9 taps (72 contiguous floats) as pairs: w2[pair][tap] = {w[2p][tap], w[2p+1][tap]}
+__device__ __forceinline__ void load_w72(const float* wg, cmx_f2 (&w2)[4][9]) {
+  cmx_f2 (&a)[2][9] = *reinterpret_cast<cmx_f2 (*)[2][9]>(&w2[0]);
+  cmx_f2 (&b)[2][9] = *reinterpret_cast<cmx_f2 (*)[2][9]>(&w2[2]);
+  load_w36(wg, a);
+  load_w36(wg + 36, b);
+}
+
+struct Tile2 {
+  int g, img, ty0, tx0, cb0, sp;
+};
+__device__ __forceinline__ Tile2 tile2_of(int CB, int ipg, int tiles_x, int tiles_y, int ncb) {
+  Tile2 t;
+  int b = blockIdx.x;
+  const int cb = b % ncb; b /= ncb;
+  t.sp = b;                                        // spatial tile index within the group
+  const int tx = b % tiles_x; b /= tiles_x;
+  const int ty = b % tiles_y; b /= tiles_y;
+  t.img = b;
+  t.g = blockIdx.y;
+  t.ty0 = ty * TY2; t.tx0 = tx * TX2; t.cb0 = cb * CB;
+  return t;
+}
+
+// stage a (RY x RX)-pixel region with origin (y0, x0) of image `base` (channels cb0..cb0+CB)
+// into img[cg][px][8]; zeros outside the image
+template <typename T, int CB, int RY_, int RX_>
+__device__ __forceinline__ void stage_region(const T* __restrict__ base, T* img, int y0, int x0, int H, int W, int C) {
+  constexpr int NCG = CB / 8, NPX = RY_ * RX_;
+  for (int it = threadIdx.x; it < NCG * NPX; it += 256) {
+    const int cg = it % NCG, px = it / NCG;
+    const int y = y0 + px / RX_, x = x0 + px % RX_;
+    V8<T> v = v8_zero<T>();
+    if (y >= 0 && y < H && x >= 0 && x < W) v = v8_load<T>(base + ((long)y * W + x) * C + cg * 8);
+    v8_store<T>(img + (cg * NPX + px) * 8, v);
+  }
+}
+
+template <typename T, int CB, int ACT, bool FLIP>
+__global__ __launch_bounds__(256) void dw2_fwd_kernel(const T* __restrict__ h, const float* __restrict__ w,
+                                                      const float* __restrict__ b, T* __restrict__ out, int ipg, int H,
+                                                      int W, int C, int tiles_x, int tiles_y, int ncb) {
+  constexpr int NCG = CB / 8, TPC = 256 / NCG;
+  __shared__ __attribute__((aligned(16))) T hs[NCG * EY * EX * 8];
+  const Tile2 t = tile2_of(CB, ipg, tiles_x, tiles_y, ncb);
+  const long ibase = ((long)t.g * ipg + t.img) * H * W * C + t.cb0;
+  stage_region<T, CB, EY, EX>(h + ibase, hs, t.ty0 - 1, t.tx0 - 1, H, W, C);
+  const int cg = threadIdx.x / TPC, pl = threadIdx.x % TPC;
+  const int c0 = t.cb0 + cg * 8;
+  cmx_f2 wr[4][9], bias[4];
+  load_w72(w + ((long)t.g * C + c0) * 9, wr);
+  if (b) {
+    const float4 b0 = *reinterpret_cast<const float4*>(b + (long)t.g * C + c0);
+    const float4 b1 = *reinterpret_cast<const float4*>(b + (long)t.g * C + c0 + 4);
+    bias[0] = (cmx_f2){b0.x, b0.y}; bias[1] = (cmx_f2){b0.z, b0.w};
+    bias[2] = (cmx_f2){b1.x, b1.y}; bias[3] = (cmx_f2){b1.z, b1.w};
+  } else {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) bias[u] = pk_splat(0.f);
+  }
+  __syncthreads();
+  const T* hc = hs + cg * EY * EX * 8;
+  for (int it = pl; it < TY2 * TX2; it += TPC) {
+    const int r = it / TX2, c = it % TX2;
+    const int y = t.ty0 + r, x = t.tx0 + c;
+    if (y >= H || x >= W) continue;
+    cmx_f2 acc[4] = {bias[0], bias[1], bias[2], bias[3]};
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        cmx_f2 v[4];
+        v8_unpack<T>(v8_load<T>(hc + ((r + i) * EX + c + j) * 8), v);
+        const int tap = FLIP ? 8 - (i * 3 + j) : i * 3 + j;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[u] = pk_fma(wr[u][tap], v[u], acc[u]);
+      }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = act2_fwd<ACT>(acc[u]);
+    v8_store<T>(out + ibase + ((long)y * W + x) * C + cg * 8, v8_pack<T>(acc));
+  }
+}
+
+// butterfly reduce-scatter of N values over the lanes (xor offsets o): lanes with bit o set
+// keep the upper half
+template <int N>
+__device__ __forceinline__ void rs_step(const float (&v)[N], float (&o)[N / 2], int off, bool up) {
+#pragma unroll
+  for (int k = 0; k < N / 2; ++k) {
+    const float send = up ? v[k] : v[k + N / 2];
+    const float keep = up ? v[k + N / 2] : v[k];
+    o[k] = keep + __shfl_xor(send, off, 64);
+  }
+}
+
+template <typename T, int CB, int ACT>
+__global__ __launch_bounds__(256, 2) void dw2_bwd_kernel(const T* __restrict__ da, const T* __restrict__ h,
+                                                      const float* __restrict__ w, const float* __restrict__ b,
+                                                      T* __restrict__ dh, float* __restrict__ part, int ipg, int H,
+                                                      int W, int C, int tiles_x, int tiles_y, int ncb, int nsp) {
+  constexpr int NCG = CB / 8, TPC = 256 / NCG;
+  __shared__ __attribute__((aligned(16))) T hs[NCG * HY * HX * 8];
+  __shared__ __attribute__((aligned(16))) T das[NCG * EY * EX * 8];
+  __shared__ __attribute__((aligned(16))) T dzs[NCG * EY * EX * 8];
+  const Tile2 t = tile2_of(CB, ipg, tiles_x, tiles_y, ncb);
+  const long ibase = ((long)t.g * ipg + t.img) * H * W * C + t.cb0;
+  stage_region<T, CB, HY, HX>(h + ibase, hs, t.ty0 - 2, t.tx0 - 2, H, W, C);
+  stage_region<T, CB, EY, EX>(da + ibase, das, t.ty0 - 1, t.tx0 - 1, H, W, C);
+  const int cg = threadIdx.x / TPC, pl = threadIdx.x % TPC;
+  const int c0 = t.cb0 + cg * 8;
+  cmx_f2 wr[4][9], bias[4];
+  load_w72(w + ((long)t.g * C + c0) * 9, wr);
+  if (b) {
+    const float4 b0 = *reinterpret_cast<const float4*>(b + (long)t.g * C + c0);
+    const float4 b1 = *reinterpret_cast<const float4*>(b + (long)t.g * C + c0 + 4);
+    bias[0] = (cmx_f2){b0.x, b0.y}; bias[1] = (cmx_f2){b0.z, b0.w};
+    bias[2] = (cmx_f2){b1.x, b1.y}; bias[3] = (cmx_f2){b1.z, b1.w};
+  } else {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) bias[u] = pk_splat(0.f);
+  }
+  __syncthreads();
+  const T* hc = hs + cg * HY * HX * 8;
+  const T* dac = das + cg * EY * EX * 8;
+  T* dzc = dzs + cg * EY * EX * 8;
+  // dz on the tile + 1-pixel halo (zero outside the image: no such output pixel)
+  for (int it = pl; it < EY * EX; it += TPC) {
+    const int r = it / EX, c = it % EX;
+    const int y = t.ty0 - 1 + r, x = t.tx0 - 1 + c;
+    V8<T> dzv = v8_zero<T>();
+    if (y >= 0 && y < H && x >= 0 && x < W) {
+      cmx_f2 z[4] = {bias[0], bias[1], bias[2], bias[3]};
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          cmx_f2 v[4];
+          v8_unpack<T>(v8_load<T>(hc + ((r + i) * HX + c + j) * 8), v);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) z[u] = pk_fma(wr[u][i * 3 + j], v[u], z[u]);
+        }
+      cmx_f2 d[4];
+      v8_unpack<T>(v8_load<T>(dac + it * 8), d);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) d[u] = d[u] * act2_grad<ACT>(z[u]);
+      dzv = v8_pack<T>(d);
+    }
+    v8_store<T>(dzc + it * 8, dzv);
+  }
+  __syncthreads();
+  // dh = conv^T(dz) on the inner tile (needs the taps; they die after this loop)
+  if (dh) {
+    for (int it = pl; it < TY2 * TX2; it += TPC) {
+      const int r = it / TX2, c = it % TX2;
+      const int y = t.ty0 + r, x = t.tx0 + c;
+      if (y >= H || x >= W) continue;
+      cmx_f2 g[4] = {pk_splat(0.f), pk_splat(0.f), pk_splat(0.f), pk_splat(0.f)};
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          cmx_f2 dv[4];           // dh[y][x] += w[i][j] dz[y-i+1][x-j+1]
+          v8_unpack<T>(v8_load<T>(dzc + ((r + 2 - i) * EX + c + 2 - j) * 8), dv);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) g[u] = pk_fma(wr[u][i * 3 + j], dv[u], g[u]);
+        }
+      v8_store<T>(dh + ibase + ((long)y * W + x) * C + cg * 8, v8_pack<T>(g));
+    }
+  }
+  // dW[i][j] += dz[y][x] h[y+i-1][x+j-1], db += dz over the inner tile
+  cmx_f2 acc[4][10];                                // [channel pair][9 taps + bias]
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) acc[u][k] = pk_splat(0.f);
+  for (int it = pl; it < TY2 * TX2; it += TPC) {
+    const int r = it / TX2, c = it % TX2;
+    if (t.ty0 + r >= H || t.tx0 + c >= W) continue;
+    cmx_f2 dz0[4];
+    v8_unpack<T>(v8_load<T>(dzc + ((r + 1) * EX + c + 1) * 8), dz0);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        cmx_f2 hv[4];
+        v8_unpack<T>(v8_load<T>(hc + ((r + 1 + i) * HX + c + 1 + j) * 8), hv);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[u][i * 3 + j] = pk_fma(dz0[u], hv[u], acc[u][i * 3 + j]);
+      }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u][9] += dz0[u];
+  }
+  // reduce the 80 partials over the TPC lanes of this channel group (TPC = 32 or 64)
+  const int lane = threadIdx.x & 63;
+  float flat[80], r40[40], r20[20], r10[10], r5[5];   // flat[ch * 10 + k]
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      flat[(2 * u) * 10 + k] = acc[u][k].x;
+      flat[(2 * u + 1) * 10 + k] = acc[u][k].y;
+    }
+  int seg = 0, s_off = TPC >> 1;
+  rs_step<80>(flat, r40, s_off, (lane & s_off) != 0); seg = seg * 2 + ((lane & s_off) != 0); s_off >>= 1;
+  rs_step<40>(r40, r20, s_off, (lane & s_off) != 0); seg = seg * 2 + ((lane & s_off) != 0); s_off >>= 1;
+  rs_step<20>(r20, r10, s_off, (lane & s_off) != 0); seg = seg * 2 + ((lane & s_off) != 0); s_off >>= 1;
+  rs_step<10>(r10, r5, s_off, (lane & s_off) != 0); seg = seg * 2 + ((lane & s_off) != 0); s_off >>= 1;
+  for (; s_off > 0; s_off >>= 1) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) r5[k] += __shfl_xor(r5[k], s_off, 64);
+  }
+  if ((lane & (TPC / 16 - 1)) == 0) {              // one lane per 5-value segment
+    float* o = part + ((long)t.g * nsp + t.sp) * C * 10 + (long)c0 * 10 + seg * 5;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) o[k] = r5[k];
+  }
+}
+
 int bwd_slots(int CQ, int nstrips) {
   int pmax = DW_BWD_THREADS / CQ;
   if (pmax < 1) pmax = 1;
@@ -262,6 +547,10 @@ int bwd_slots(int CQ, int nstrips) {
 }
 }  // namespace
 
+// LDS-tiled path when the channel count splits into 32-channel blocks (every B0/B2 layer)
+// (fp32 parity mode: 32-channel blocks, so the backward's three tiles fit twice per CU)
+static int tile_cb(int C, int dtype) { return (C % 64 == 0 && dtype == 1) ? 64 : C % 32 == 0 ? 32 : 0; }
+
 extern "C" {
 
 int cmx_dwconv3x3_fwd(const void* h, const float* w, const float* b, void* out, int NI, int imgs_per_group, int H,
@@ -269,6 +558,23 @@ int cmx_dwconv3x3_fwd(const void* h, const float* w, const float* b, void* out, 
   CMX_REQUIRE(C % 4 == 0 && NI % imgs_per_group == 0, CMX_ERR_SHAPE, "dwconv_fwd: C=%d", C);
   CMX_REQUIRE((long)NI * H * W * C < (1L << 31), CMX_ERR_SHAPE, "dwconv_fwd: tensor too large for 32-bit indexing");
   const int G = NI / imgs_per_group;
+  const int CB = tile_cb(C, dtype);
+  if (CB) {
+    const int tx = cdiv(W, TX2), ty = cdiv(H, TY2), ncb = C / CB;
+    const dim3 grid((unsigned)imgs_per_group * ty * tx * ncb, G);
+    CMX_DISPATCH(dtype, T, {
+      CMX_ACT_DISPATCH(act, A, {
+        if (CB == 32) {
+          hipLaunchKernelGGL((dw2_fwd_kernel<T, 32, A, false>), grid, dim3(256), 0, s, (const T*)h, w, b, (T*)out,
+                             imgs_per_group, H, W, C, tx, ty, ncb);
+        } else if constexpr (sizeof(T) == 2) {
+          hipLaunchKernelGGL((dw2_fwd_kernel<T, 64, A, false>), grid, dim3(256), 0, s, (const T*)h, w, b, (T*)out,
+                             imgs_per_group, H, W, C, tx, ty, ncb);
+        }
+      });
+    });
+    return cmx_check_launch("dwconv_fwd");
+  }
   const int NXS = cdiv(W, RXF), NYS = cdiv(H, RY);
   const long threads = (long)(C / 4) * NXS * NYS * imgs_per_group;
   CMX_DISPATCH(dtype, T, {
@@ -282,33 +588,55 @@ int cmx_dwconv3x3_fwd(const void* h, const float* w, const float* b, void* out, 
 
 size_t cmx_dwconv3x3_bwd_workspace(int NI, int imgs_per_group, int H, int W, int C) {
   const int G = NI / imgs_per_group;
-  const int P = bwd_slots(C / 4, cdiv(W, RXB) * cdiv(H, RY) * imgs_per_group);
+  const int P = tile_cb(C, 0) ? imgs_per_group * cdiv(H, TY2) * cdiv(W, TX2)
+                           : bwd_slots(C / 4, cdiv(W, RXB) * cdiv(H, RY) * imgs_per_group);
   return ((size_t)G * P * C * 10 + (size_t)G * C * 10) * sizeof(float);
 }
 
-// da: upstream grad of the activation output; dz (sized like h, dtype) receives
-// da * act'(z); dh = conv^T(dz) (may be NULL); dw (G,C,9), db (G,C) fp32 (db may be NULL).
+// da: upstream grad of the activation output; dh = conv^T(dz) (may be NULL) with
+// dz = da * act'(z); dw (G,C,9), db (G,C) fp32 (db may be NULL).  dz (sized like h, dtype)
+// receives dz on the strip path only; the LDS-tiled path keeps dz on chip (dz may be NULL).
 int cmx_dwconv3x3_bwd(const void* da, const void* h, const float* w, const float* b, void* dz, void* dh, float* dw,
                       float* db, float* workspace, int NI, int imgs_per_group, int H, int W, int C, int act,
                       int accumulate, int dtype, hipStream_t s) {
   CMX_REQUIRE(C % 4 == 0 && NI % imgs_per_group == 0, CMX_ERR_SHAPE, "dwconv_bwd: C=%d", C);
   CMX_REQUIRE((long)NI * H * W * C < (1L << 31), CMX_ERR_SHAPE, "dwconv_bwd: tensor too large for 32-bit indexing");
   const int G = NI / imgs_per_group;
-  const int CQ = C / 4;
-  const int NXB = cdiv(W, RXB), NXS = cdiv(W, RXF), NYS = cdiv(H, RY);
-  const int P = bwd_slots(CQ, NXB * NYS * imgs_per_group);
-  float* tmp = workspace + (size_t)G * P * C * 10;
-  CMX_DISPATCH(dtype, T, {
-    CMX_ACT_DISPATCH(act, A, {
-      hipLaunchKernelGGL((dw_bwd_dz_kernel<T, A>), dim3(cdiv((long)CQ * P, 256), G), dim3(256), 0, s, (const T*)da,
-                         (const T*)h, w, b, (T*)dz, workspace, imgs_per_group, H, W, C, NXB, NYS, P);
+  const int CB = tile_cb(C, dtype);
+  int P;
+  if (CB) {
+    const int tx = cdiv(W, TX2), ty = cdiv(H, TY2), ncb = C / CB;
+    P = imgs_per_group * ty * tx;
+    const dim3 grid((unsigned)P * ncb, G);
+    CMX_DISPATCH(dtype, T, {
+      CMX_ACT_DISPATCH(act, A, {
+        if (CB == 32) {
+          hipLaunchKernelGGL((dw2_bwd_kernel<T, 32, A>), grid, dim3(256), 0, s, (const T*)da, (const T*)h, w, b,
+                             (T*)dh, workspace, imgs_per_group, H, W, C, tx, ty, ncb, P);
+        } else if constexpr (sizeof(T) == 2) {
+          hipLaunchKernelGGL((dw2_bwd_kernel<T, 64, A>), grid, dim3(256), 0, s, (const T*)da, (const T*)h, w, b,
+                             (T*)dh, workspace, imgs_per_group, H, W, C, tx, ty, ncb, P);
+        }
+      });
     });
-    if (dh) {
-      const long threads = (long)CQ * NXS * NYS * imgs_per_group;
-      hipLaunchKernelGGL((dw_fwd_kernel<T, true, 0>), dim3(cdiv(threads, 256), G), dim3(256), 0, s, (const T*)dz, w,
-                         (const float*)nullptr, (T*)dh, imgs_per_group, H, W, C, NXS, NYS);
-    }
-  });
+  } else {
+    CMX_REQUIRE(dz, CMX_ERR_ARG, "dwconv_bwd: C=%d takes the strip path, which needs a dz buffer", C);
+    const int CQ = C / 4;
+    const int NXB = cdiv(W, RXB), NXS = cdiv(W, RXF), NYS = cdiv(H, RY);
+    P = bwd_slots(CQ, NXB * NYS * imgs_per_group);
+    CMX_DISPATCH(dtype, T, {
+      CMX_ACT_DISPATCH(act, A, {
+        hipLaunchKernelGGL((dw_bwd_dz_kernel<T, A>), dim3(cdiv((long)CQ * P, 256), G), dim3(256), 0, s, (const T*)da,
+                           (const T*)h, w, b, (T*)dz, workspace, imgs_per_group, H, W, C, NXB, NYS, P);
+      });
+      if (dh) {
+        const long threads = (long)CQ * NXS * NYS * imgs_per_group;
+        hipLaunchKernelGGL((dw_fwd_kernel<T, true, 0>), dim3(cdiv(threads, 256), G), dim3(256), 0, s, (const T*)dz, w,
+                           (const float*)nullptr, (T*)dh, imgs_per_group, H, W, C, NXS, NYS);
+      }
+    });
+  }
+  float* tmp = workspace + (size_t)G * P * C * 10;
   int st = cmx_reduce_partials(workspace, tmp, G, P, C * 10, 0, 1.f, s);
   if (st) return st;
   const long tot = (long)G * C * 10;

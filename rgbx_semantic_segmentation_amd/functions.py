@@ -254,7 +254,8 @@ class DWConvF(Function):
         wg, bg, NI, ipg, H, W, act = ctx.meta
         C = h.shape[-1]
         da = _c(da)
-        dz = torch.empty_like(h)
+        # the LDS-tiled backward (C % 32 == 0) keeps dz on chip; the strip path writes it
+        dz = torch.empty_like(h) if C % 32 else None
         dh = torch.empty_like(h) if ctx.needs_input_grad[0] else None
         ws = K._ws(K.query("cmx_dwconv3x3_bwd_workspace", NI, ipg, H, W, C), h.device)
         K.call("cmx_dwconv3x3_bwd", K.ptr(da), K.ptr(h), K.ptr(w), K.ptr(b), K.ptr(dz), K.ptr(dh), K.ptr(wg),
