@@ -19,6 +19,7 @@ import torch
 from torch.autograd import Function
 
 from . import kernels as K
+from .streams import run_side
 
 
 def _c(t):
@@ -138,9 +139,11 @@ class GLinear(Function):
             dx1 = _dgrad(dz, W[:, :, :k1], torch.empty_like(x1))
         if x2 is not None and ctx.needs_input_grad[10]:
             dx2 = _dgrad(dz, W[:, :, k1:], torch.empty_like(x2))
-        _wgrad_into(dz, x1, Wg[:, :, :k1], bg)
-        if x2 is not None:
-            _wgrad_into(dz, x2, Wg[:, :, k1:])
+        def wgrads():
+            _wgrad_into(dz, x1, Wg[:, :, :k1], bg)
+            if x2 is not None:
+                _wgrad_into(dz, x2, Wg[:, :, k1:])
+        run_side(wgrads, dz, x1, x2)
         return (None, None, None, None, None, None, dres, None, None, dx1, dx2)
 
 
@@ -300,7 +303,7 @@ class ConvF(Function):
         Wg, bg, geom = ctx.meta
         G, NI, H, Wd, C, KH, KW, st, pad, Ho, Wo, nchw = geom
         dy = _c(dy)
-        _wgrad_into(dy, cols, Wg, bg)
+        run_side(lambda: _wgrad_into(dy, cols, Wg, bg), dy, cols)
         dx = None
         if ctx.needs_input_grad[0] and not nchw:
             dcols = _dgrad(dy, W, torch.empty_like(cols))
@@ -431,8 +434,10 @@ class FRMF(Function):
                 K.gemm(dh[None], W0[None, :, i * C:(i + 1) * C].transpose(1, 2), dxi, residual=dxi)
             else:
                 dxi[0].addmm_(dh, W0[:, i * C:(i + 1) * C])
-        _wgrad_into(dh[None], x[0].view(1, B * N, C), gW0[None, :, :C], gb0.view(1, C))
-        _wgrad_into(dh[None], x[1].view(1, B * N, C), gW0[None, :, C:])
+        def wgrads():
+            _wgrad_into(dh[None], x[0].view(1, B * N, C), gW0[None, :, :C], gb0.view(1, C))
+            _wgrad_into(dh[None], x[1].view(1, B * N, C), gW0[None, :, C:])
+        run_side(wgrads, dh, x)
         # channel MLP backward (sigmoid then relu), then pooling backward
         dz = K._ws(K.query("cmx_small_linear_bwd_workspace", B, 4 * C, 4 * C), x.device)
         dy1 = torch.empty(B, 4 * C, dtype=torch.float32, device=x.device)
