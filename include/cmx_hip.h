@@ -32,10 +32,14 @@ typedef struct ihipStream_t* hipStream_t;
 /* ---- housekeeping ------------------------------------------------------------------ */
 int cmx_abi_version(void);
 const char* cmx_last_error(void);
+/* pinned host -> device copy of a packed record table on `stream` (see grouped launches) */
+int cmx_upload(void* dst, const void* src, size_t nbytes, hipStream_t stream);
 
 /* ---- LayerNorm: nn.LayerNorm in Block.norm1/norm2, stage norms (eps 1e-6,
  *      dual_segformer.py:148,155,257), OverlapPatchEmbed.norm (:198), Attention.norm (:97),
- *      CrossPath.norm1/2 (net_utils.py:270-271), eps 1e-5.  x,y: (G*R, C); gamma,beta (G,C). */
+ *      CrossPath.norm1/2 (net_utils.py:270-271), eps 1e-5.  x,y: (G*R, C); gamma,beta (G,C).
+ *      Backward with dgamma = dbeta = NULL leaves the per-block partials (G, nb, 2C) =
+ *      [dgamma | dbeta] in the workspace (nb = workspace bytes / (8 G C)) for cmx_reduce_grouped. */
 int cmx_layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y, float* mean, float* rstd, int64_t R, int G, int C, float eps, int dtype, hipStream_t stream);
 size_t cmx_layernorm_bwd_workspace(int64_t R, int G, int C, int dtype);
 int cmx_layernorm_bwd(const void* dy, const void* x, const float* gamma, const float* mean, const float* rstd, void* dx, float* dgamma, float* dbeta, float* workspace, int64_t R, int G, int C, int accumulate, int dtype, hipStream_t stream);
@@ -60,7 +64,9 @@ int cmx_sra_attn_bwd(const void* q, const void* k, const void* v, const void* o,
 
 /* ---- depthwise 3x3 + bias + act: Mix-FFN DWConv + GELU (dual_segformer.py:27-33,67-71) and
  *      ChannelEmbed DW3x3 + ReLU (net_utils.py:315-318).  h,out: (NI, H, W, C) NHWC,
- *      image n in group n / imgs_per_group; w (G, C, 9), b (G, C) fp32; act 0/1 gelu/2 relu. */
+ *      image n in group n / imgs_per_group; w (G, C, 9), b (G, C) fp32; act 0/1 gelu/2 relu.
+ *      Backward with dw = db = NULL leaves the partials (G, P, C*10) = [9 taps | bias] per channel
+ *      in the workspace (P = workspace bytes / (40 G C) - 1) for cmx_reduce_grouped. */
 int cmx_dwconv3x3_fwd(const void* h, const float* w, const float* b, void* out, int NI, int imgs_per_group, int H, int W, int C, int act, int dtype, hipStream_t stream);
 size_t cmx_dwconv3x3_bwd_workspace(int NI, int imgs_per_group, int H, int W, int C);
 int cmx_dwconv3x3_bwd(const void* da, const void* h, const float* w, const float* b, void* dz, void* dh, float* dw, float* db, float* workspace, int NI, int imgs_per_group, int H, int W, int C, int act, int accumulate, int dtype, hipStream_t stream);
@@ -126,6 +132,21 @@ int cmx_upsample_ce_fwd(const void* logits, const int64_t* label, void* grad, fl
 size_t cmx_gemm_workspace(int G, int M, int N, int splitk);
 int cmx_gemm_splitk(int G, int M, int N, int K, int ones_col, int dtype);
 int cmx_gemm(const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R, const float* rscale, float* dbias, float* workspace, int G, int M, int N, int K, int K1, int64_t lda, int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias, int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode, int ones_col, int splitk, int dtype, hipStream_t stream);
+
+/* ---- grouped (deferred) launches: the weight gradients of a backward segment in ONE GEMM
+ *      launch and every partial-sum reduction (split-K slabs, LayerNorm dgamma/dbeta, DWConv
+ *      dW/db partials) in ONE reduce launch, issued when the segment's backward is done.
+ *      Replaces the per-layer weight-gradient half of autograd's Linear/Conv2d/LayerNorm
+ *      backward (the DDP reducer consumes those gradients, train.py:145-146).  The host packs
+ *      records (cmx_*_pack, host memory of cmx_*_record_size() bytes each, blk0 = first block of
+ *      the record, returns its block count), copies them to device memory, then launches. */
+size_t cmx_gemm_group_record_size(void);
+int cmx_gemm_grouped_splitk(int G, int M, int N, int K, int ones_col);
+int cmx_gemm_group_pack(void* rec, const void* A, const void* B, void* C, float* dbias, float* workspace, int G, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t sA, int64_t sB, int64_t sC, int64_t sdb, int transA, int transB, int out_mode, int ones_col, int splitk, int blk0);
+int cmx_gemm_grouped(const void* recs, int nrec, int total_blocks, hipStream_t stream);
+size_t cmx_reduce_record_size(void);
+int cmx_reduce_pack(void* rec, const float* src, float* dst, float* dst2, int G, int nblk, int64_t sg, int64_t sb, int rows, int cols, int csplit, int64_t dg, int ldd, int64_t dg2, int ldd2, int accumulate, int blk0);
+int cmx_reduce_grouped(const void* recs, int nrec, int total_blocks, hipStream_t stream);
 
 /* ---- fused AdamW over the flat parameter buffer (train.py:128-129, init_func.py:33-57). */
 int cmx_adamw_step(float* p, const float* g, float* m, float* v, void* shadow_bf16, const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, float beta1, float beta2, float eps, float weight_decay, float grad_scale, hipStream_t stream);

@@ -23,3 +23,13 @@ int cmx_check_launch(const char* what) {
 
 extern "C" int cmx_abi_version(void) { return CMX_ABI_VERSION; }
 extern "C" const char* cmx_last_error(void) { return g_err; }
+
+// Host -> device copy of a packed launch-record table (cmx_*_pack) on the caller's stream.
+// `src` must be pinned host memory that stays unmodified until the copy has run (inside a
+// HIP-graph capture: for the graph's lifetime, since every replay re-reads it).
+extern "C" int cmx_upload(void* dst, const void* src, size_t nbytes, hipStream_t s) {
+  CMX_REQUIRE(dst && src, CMX_ERR_ARG, "upload: null pointer");
+  const hipError_t e = hipMemcpyAsync(dst, src, nbytes, hipMemcpyHostToDevice, s);
+  CMX_REQUIRE(e == hipSuccess, CMX_ERR_LAUNCH, "upload: %s", hipGetErrorString(e));
+  return CMX_OK;
+}

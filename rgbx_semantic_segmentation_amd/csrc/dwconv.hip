@@ -636,6 +636,7 @@ int cmx_dwconv3x3_bwd(const void* da, const void* h, const float* w, const float
       }
     });
   }
+  if (!dw && !db) return cmx_check_launch("dwconv_bwd");   // partials (G, P, C*10) left for a deferred reduce
   float* tmp = workspace + (size_t)G * P * C * 10;
   int st = cmx_reduce_partials(workspace, tmp, G, P, C * 10, 0, 1.f, s);
   if (st) return st;

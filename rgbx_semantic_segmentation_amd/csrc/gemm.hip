@@ -38,6 +38,7 @@
 //  * gemm_generic_kernel -- fp32 parity mode (exact v_mfma_f32_32x32x2_f32) and any bf16
 //    problem whose strides / dims do not allow 16-B chunks; register staged, BK = 32.
 #include "cmx_mfma.h"
+#include <string.h>
 
 namespace {
 
@@ -236,17 +237,20 @@ __device__ __forceinline__ bf16x8 frag_r(const char* img, int rb, int s, int lan
 
 // NS = LDS stages in the DMA ring: 2 for grids of >= 2 blocks per CU (the co-resident block
 // hides the DMA latency), 4 for grids of at most one block per CU (the ring must hide it).
+// LDS bytes of one block: the NS-stage DMA ring, reused by the fp32 epilogue tile
+template <int BM, int BN, int NS>
+constexpr int gemm_smem_bytes() {
+  return NS * (BM + BN) * FBK * 2 > BM * (BN + 4) * 4 ? NS * (BM + BN) * FBK * 2 : BM * (BN + 4) * 4;
+}
+
+// One output tile (of one split / group) of problem p.  `lin` = the block's linear index
+// within the problem, in (split, group, tile) order; smem = gemm_smem_bytes<BM, BN, NS>().
 template <int BM, int BN, bool TA, bool TB, int NS>
-__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const GemmArgs p) {
+__device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin, char* smem) {
   constexpr int A_BYTES = BM * FBK * 2, STAGE = (BM + BN) * FBK * 2;
   constexpr int TM = BM / 64, TN = BN / 64;
-  constexpr int EPI = BM * (BN + 4) * 4;        // fp32 output tile for the epilogue
-  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE > EPI ? NS * STAGE : EPI];
 
-  // 1-D grid over (split, group, tile); each XCD gets a contiguous run of that order, i.e.
-  // neighbouring tiles of one (split, group): they share A row panels and the B k-slice in L2
   const int ntile = p.tiles_m * p.tiles_n;
-  const int lin = xcd_tile(blockIdx.x, ntile * p.G * p.nsplit);
   const int t = lin % ntile, g = (lin / ntile) % p.G, z = lin / (ntile * p.G);
   const int tm = t / p.tiles_n, tn = t % p.tiles_n;
   const bf16* Ag = reinterpret_cast<const bf16*>(p.A) + (long)g * p.sA;
@@ -399,6 +403,99 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const GemmArgs p) {
       epi_store8<bf16>(p, g, i, j, nv, v);
     }
   }
+}
+
+// 1-D grid over (split, group, tile); each XCD gets a contiguous run of that order, i.e.
+// neighbouring tiles of one (split, group): they share A row panels and the B k-slice in L2
+template <int BM, int BN, bool TA, bool TB, int NS>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const GemmArgs p) {
+  __shared__ __attribute__((aligned(1024))) char smem[gemm_smem_bytes<BM, BN, NS>()];
+  gemm_bf16_body<BM, BN, TA, TB, NS>(p, xcd_tile(blockIdx.x, p.tiles_m * p.tiles_n * p.G * p.nsplit), smem);
+}
+
+// ============================================================================ grouped launch
+// Many independent problems in ONE launch (the weight gradients of a whole backward segment,
+// which nothing reads before the optimizer): record r owns blocks [blk0, blk0 + nblk) of the
+// grid.  The XCD remap runs over the whole grid, so each XCD takes a contiguous run of
+// (problem, split, group, tile) and neighbouring tiles of one problem still share L2.  The
+// tile shape is chosen per problem (the output's narrow side gets 64), so a 64 x 64 stage-1
+// weight gradient and a 512 x 2048 decoder one share the launch without padding waste.
+struct GroupRec {
+  GemmArgs a;
+  int bm, bn, blk0, nblk;
+};
+
+__global__ __launch_bounds__(256, 2) void gemm_grouped_kernel(const GroupRec* __restrict__ recs, int nrec) {
+  __shared__ __attribute__((aligned(1024))) char smem[gemm_smem_bytes<128, 128, 2>()];
+  const int lin = xcd_tile(blockIdx.x, gridDim.x);
+  int lo = 0, hi = nrec - 1;                    // last record with blk0 <= lin
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (recs[mid].blk0 <= lin) lo = mid; else hi = mid - 1;
+  }
+  const GroupRec& r = recs[lo];
+  const GemmArgs p = r.a;
+  const int local = lin - r.blk0;
+  if (r.bm == 128 && r.bn == 128) gemm_bf16_body<128, 128, true, true, 2>(p, local, smem);
+  else if (r.bm == 128) gemm_bf16_body<128, 64, true, true, 2>(p, local, smem);
+  else if (r.bn == 128) gemm_bf16_body<64, 128, true, true, 2>(p, local, smem);
+  else gemm_bf16_body<64, 64, true, true, 2>(p, local, smem);
+}
+
+// ============================================================================ grouped reduce
+// out (+)= sum over nblk partial rows, for many reductions in one launch: the split-K slabs of
+// the grouped weight gradients, the per-block dgamma / dbeta partials of LayerNorm backward and
+// the dW / db partials of the depthwise conv backward.  Element w < rows * cols of group g is
+// sum_b src[g*sg + b*sb + w]; it lands at dst[g*dg + r*ldd + c] (c < csplit) or
+// dst2[g*dg2 + r*ldd2 + c - csplit] (r = w / cols, c = w % cols): e.g. LN's [dgamma | dbeta]
+// rows, DWConv's [9 taps | bias] rows, a GEMM slab's row pitch vs the gradient view's ldc.
+// zl threads share one output along b (long partial columns), meeting in LDS.
+struct RedRec {
+  const float* src; float* dst; float* dst2;
+  long sg, sb, dg, dg2;
+  int ldd, ldd2, G, nblk, rows, cols, csplit, accumulate, zl, cpg, blk0, pad;
+};
+
+__global__ __launch_bounds__(256) void reduce_grouped_kernel(const RedRec* __restrict__ recs, int nrec) {
+  __shared__ float red[256];
+  const int b = blockIdx.x;
+  int lo = 0, hi = nrec - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (recs[mid].blk0 <= b) lo = mid; else hi = mid - 1;
+  }
+  const RedRec& r = recs[lo];
+  const int zl = r.zl, opb = 256 / zl;
+  const int local = b - r.blk0;
+  const int g = local / r.cpg, ch = local % r.cpg;
+  const int o = threadIdx.x % opb, sl = threadIdx.x / opb;
+  const long W = (long)r.rows * r.cols;
+  const long w = (long)ch * opb + o;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (w < W) {
+    const float* p = r.src + (long)g * r.sg + w;
+    const long sb = r.sb;
+    int k = sl;
+    for (; k + 3 * zl < r.nblk; k += 4 * zl) {
+      s0 += p[(long)k * sb];
+      s1 += p[(long)(k + zl) * sb];
+      s2 += p[(long)(k + 2 * zl) * sb];
+      s3 += p[(long)(k + 3 * zl) * sb];
+    }
+    for (; k < r.nblk; k += zl) s0 += p[(long)k * sb];
+  }
+  float v = (s0 + s1) + (s2 + s3);
+  if (zl > 1) {
+    red[threadIdx.x] = v;
+    __syncthreads();
+    if (sl) return;
+    for (int q = 1; q < zl; ++q) v += red[o + q * opb];
+  }
+  if (w >= W) return;
+  const int row = (int)(w / r.cols), c = (int)(w % r.cols);
+  float* d = c < r.csplit ? r.dst + (long)g * r.dg + (long)row * r.ldd + c
+                          : r.dst2 + (long)g * r.dg2 + (long)row * r.ldd2 + (c - r.csplit);
+  *d = r.accumulate ? *d + v : v;
 }
 
 // ============================================================================ generic path
@@ -802,6 +899,83 @@ int cmx_gemm(const void* A, const void* A2, const void* B, void* C, const float*
     else launch_reduce<float>(a, G, work, s);
   }
   return cmx_check_launch("gemm");
+}
+
+
+// ---------------------------------------------------------------- grouped (deferred) launches
+size_t cmx_gemm_group_record_size(void) { return sizeof(GroupRec); }
+
+// split for a problem inside a grouped launch: the launch is filled by many problems, so a
+// split only bounds the k-loop of one block (<= 32 k-tiles of 64 = 2048 tokens per block)
+int cmx_gemm_grouped_splitk(int G, int M, int N, int K, int ones_col) {
+  if (G <= 0 || M <= 0 || N <= 0 || K <= 0) return 1;
+  const int nk = (K + FBK - 1) / FBK;
+  int s = (nk + 31) / 32;
+  if (s > 64) s = 64;
+  const int per = (nk + s - 1) / s;
+  return (nk + per - 1) / per;
+}
+
+int cmx_gemm_group_pack(void* rec, const void* A, const void* B, void* C, float* dbias, float* workspace, int G, int M,
+                        int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t sA, int64_t sB, int64_t sC,
+                        int64_t sdb, int transA, int transB, int out_mode, int ones_col, int splitk, int blk0) {
+  CMX_REQUIRE(rec && G > 0 && M > 0 && N > 0 && K > 0 && blk0 >= 0, CMX_ERR_SHAPE, "gemm_group_pack: bad problem");
+  CMX_REQUIRE(transA && transB, CMX_ERR_ARG, "gemm_group_pack: grouped launches take transA = transB = 1 (weight gradients)");
+  CMX_REQUIRE(out_mode == 1 || out_mode == 2, CMX_ERR_ARG, "gemm_group_pack: fp32 output only");
+  CMX_REQUIRE(!ones_col || (dbias && N >= 2), CMX_ERR_ARG, "gemm_group_pack: ones_col needs dbias");
+  CMX_REQUIRE((long)M * N < (1L << 31), CMX_ERR_SHAPE, "gemm_group_pack: problem too large");
+  CMX_REQUIRE(fast_ok(A, nullptr, B, M, N, K, K, lda, 0, ldb, sA, 0, sB, transA, transB, ones_col), CMX_ERR_ARG,
+              "gemm_group_pack: operands not eligible for the bf16 LDS-DMA path");
+  if (splitk <= 0) splitk = cmx_gemm_grouped_splitk(G, M, N, K, ones_col);
+  CMX_REQUIRE(splitk == 1 || workspace, CMX_ERR_ARG, "gemm_group_pack: split-K needs a workspace");
+  GroupRec r{};
+  GemmArgs& a = r.a;
+  a.A = A; a.A2 = nullptr; a.B = B; a.C = C; a.dbias = dbias; a.ws = workspace;
+  a.G = G; a.M = M; a.N = N; a.K = K; a.K1 = K; a.rows_per_sample = 1;
+  a.act = 0; a.out_mode = out_mode; a.ones_col = ones_col; a.vec = 1;
+  a.cvec = ((uintptr_t)C % 16 == 0) && (ldc * 4) % 16 == 0 && (sC * 4) % 16 == 0;
+  a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.sA = sA; a.sB = sB; a.sC = sC; a.sdb = sdb;
+  const int nk = (K + FBK - 1) / FBK;
+  a.kt_per_split = (nk + splitk - 1) / splitk;
+  a.nsplit = (nk + a.kt_per_split - 1) / a.kt_per_split;
+  const int nb = ones_col ? N - 1 : N;
+  r.bm = tile_dim(M); r.bn = tile_dim(nb);
+  a.tiles_m = cdiv(M, r.bm); a.tiles_n = cdiv(nb, r.bn);
+  r.blk0 = blk0;
+  r.nblk = a.tiles_m * a.tiles_n * G * a.nsplit;
+  memcpy(rec, &r, sizeof(r));
+  return r.nblk;
+}
+
+int cmx_gemm_grouped(const void* recs, int nrec, int total_blocks, hipStream_t s) {
+  CMX_REQUIRE(recs && nrec > 0 && total_blocks > 0, CMX_ERR_ARG, "gemm_grouped: empty launch");
+  hipLaunchKernelGGL(gemm_grouped_kernel, dim3(total_blocks), dim3(256), 0, s, (const GroupRec*)recs, nrec);
+  return cmx_check_launch("gemm_grouped");
+}
+
+size_t cmx_reduce_record_size(void) { return sizeof(RedRec); }
+
+int cmx_reduce_pack(void* rec, const float* src, float* dst, float* dst2, int G, int nblk, int64_t sg, int64_t sb,
+                    int rows, int cols, int csplit, int64_t dg, int ldd, int64_t dg2, int ldd2, int accumulate,
+                    int blk0) {
+  CMX_REQUIRE(rec && src && dst && G > 0 && nblk > 0 && rows > 0 && cols > 0 && blk0 >= 0, CMX_ERR_SHAPE,
+              "reduce_pack: bad reduction");
+  CMX_REQUIRE(csplit >= cols || (dst2 && csplit >= 0), CMX_ERR_ARG, "reduce_pack: columns past csplit need dst2");
+  RedRec r{};
+  r.src = src; r.dst = dst; r.dst2 = dst2; r.sg = sg; r.sb = sb; r.dg = dg; r.dg2 = dg2;
+  r.ldd = ldd; r.ldd2 = ldd2; r.G = G; r.nblk = nblk; r.rows = rows; r.cols = cols; r.csplit = csplit;
+  r.accumulate = accumulate;
+  r.zl = nblk <= 8 ? 1 : (nblk <= 64 ? 4 : 16);
+  r.cpg = (int)cdiv((long)rows * cols, 256 / r.zl);
+  r.blk0 = blk0;
+  memcpy(rec, &r, sizeof(r));
+  return r.cpg * G;
+}
+
+int cmx_reduce_grouped(const void* recs, int nrec, int total_blocks, hipStream_t s) {
+  CMX_REQUIRE(recs && nrec > 0 && total_blocks > 0, CMX_ERR_ARG, "reduce_grouped: empty launch");
+  hipLaunchKernelGGL(reduce_grouped_kernel, dim3(total_blocks), dim3(256), 0, s, (const RedRec*)recs, nrec);
+  return cmx_check_launch("reduce_grouped");
 }
 
 }  // extern "C"

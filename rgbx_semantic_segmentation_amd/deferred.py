@@ -1,0 +1,219 @@
+"""Deferred weight-gradient work of the backward pass, issued as grouped launches.
+
+In the reference every ``nn.Linear`` / ``nn.Conv2d`` / ``nn.LayerNorm`` backward computes its
+weight gradient right away (autograd, ``train.py:192``) and DDP's reducer picks the gradients
+up as they complete (``train.py:145-146``).  Nothing on the backward's critical path reads a
+weight gradient, though: only the optimizer (and the gradient all-reduce) does.  On MI355X
+the per-layer weight-gradient GEMMs, their split-K combines and the LayerNorm / DWConv
+partial-sum reductions were ~550 small launches per CMX-B2 step, each a few microseconds of
+mostly idle chip.  Here they are queued while the backward runs and issued as
+
+  * ONE grouped GEMM launch (``cmx_gemm_grouped``): every queued weight-gradient problem of
+    the segment, each with its own tile shape and split, in one grid;
+  * ONE grouped reduce launch (``cmx_reduce_grouped``): the split-K slabs of those problems
+    plus the queued LayerNorm dgamma/dbeta and DWConv dW/db partials;
+
+when the segment's backward is done (``flush()``; ``arm()`` queues a flush at the end of
+the backward pass as an autograd-engine callback).  Queued operands stay alive until the
+flush, which costs HBM (the saved activations and upstream gradients of a segment), not
+time -- 288 GB per GPU leaves room for it.
+
+Records are packed on the host by the library (``cmx_*_pack``) into pinned memory and copied
+to the device on the launch stream (``cmx_upload``).  Inside a HIP-graph capture the pinned
+table must outlive the graph (every replay re-reads it): it is kept for the process lifetime.
+Outside a capture it is released once an event recorded after the copy has completed.
+
+``CMX_DEFER=0`` runs every weight gradient immediately instead (A/B switch for measurements).
+"""
+from __future__ import annotations
+
+import collections
+import ctypes
+import os
+
+import torch
+
+from . import _lib
+from ._lib import LIB, call, query, ptr, stream
+
+ENABLED = os.environ.get("CMX_DEFER", "1") == "1"
+
+_GREC = query("cmx_gemm_group_record_size")
+_RREC = query("cmx_reduce_record_size")
+
+
+class _Queue:
+    def __init__(self):
+        self.gemms = []        # argument tuples of cmx_gemm_group_pack (minus rec / ws / splitk / blk0)
+        self.reds = []         # argument tuples of cmx_reduce_pack (minus rec / blk0)
+        self.keep = []         # tensors the queued work reads or writes
+        self.armed = False
+
+
+_q = _Queue()
+_graph_tables = []             # pinned tables referenced by captured graphs (never freed)
+_inflight = collections.deque()   # (event, pinned table) of eager uploads
+
+
+def pending() -> bool:
+    return bool(_q.gemms or _q.reds)
+
+
+def arm() -> None:
+    """Flush at the end of the running backward pass (idempotent per pass).  Outside a
+    backward pass (direct callers, tests) the caller flushes explicitly."""
+    if not _q.armed and torch._C._current_autograd_node() is not None:
+        _q.armed = True
+        torch.autograd.Variable._execution_engine.queue_callback(flush)
+
+
+def _operand(t: torch.Tensor):
+    if t.stride(2) == 1:
+        return 0, t.stride(1), t.stride(0)
+    if t.stride(1) == 1:
+        return 1, t.stride(2), t.stride(0)
+    return None
+
+
+def wgrad(dz: torch.Tensor, x: torch.Tensor, Wg: torch.Tensor, bg: torch.Tensor | None = None) -> bool:
+    """Queue Wg (fp32 (G, N, k) view) = dz^T x and bg (G, N) = column sums of dz, with
+    dz (G, M, N), x (G, M, k) bf16.  Returns False (nothing queued) when the problem is not
+    eligible for the grouped bf16 path; the caller then runs it immediately."""
+    if not ENABLED or dz.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or not dz.is_cuda:
+        return False
+    if not _free:
+        reserve()
+    A, B = dz.transpose(1, 2), x.transpose(1, 2)           # (G, N, M), (G, k, M)
+    G, N, M = A.shape
+    k = B.shape[1]
+    if Wg.shape != (G, N, k) or Wg.dtype != torch.float32 or Wg.stride(2) != 1:
+        return False
+    oa, ob = _operand(A), _operand(B)
+    if oa is None or ob is None or oa[0] != 1 or ob[0] != 1:
+        return False
+    if bg is not None and (bg.dtype != torch.float32 or bg.shape[-1] != N or bg.stride(-1) != 1):
+        return False
+    Nk = k + (1 if bg is not None else 0)
+    sdb = (bg.stride(0) if bg.dim() == 2 else 0) if bg is not None else 0
+    args = (A, B, Wg, bg, G, N, Nk, M, oa[1], ob[1], Wg.stride(1), oa[2], ob[2], Wg.stride(0), sdb)
+    # validate now (shape / alignment / 31-bit extents) so a refusal falls back immediately
+    rec = (ctypes.c_uint8 * _GREC)()
+    st = LIB.cmx_gemm_group_pack(ctypes.addressof(rec), ptr(A), ptr(B), ptr(Wg), ptr(bg), 1, G, N, Nk, M,
+                                 oa[1], ob[1], Wg.stride(1), oa[2], ob[2], Wg.stride(0), sdb, 1, 1, 1,
+                                 int(bg is not None), 1, 0)
+    if st <= 0:
+        return False
+    _q.gemms.append(args)
+    _q.keep.extend((dz, x))
+    arm()
+    return True
+
+
+def reduce(src: torch.Tensor, dst: torch.Tensor, dst2: torch.Tensor | None, G: int, nblk: int, sg: int, sb: int,
+           rows: int, cols: int, csplit: int, dg: int, ldd: int, dg2: int = 0, ldd2: int = 0,
+           accumulate: bool = False) -> None:
+    """Queue dst/dst2 (+)= sum over nblk partial rows of src (see cmx_reduce_pack)."""
+    if not _free:
+        reserve()
+    _q.reds.append((src.data_ptr(), dst.data_ptr(), ptr(dst2), G, nblk, sg, sb, rows, cols, csplit, dg, ldd, dg2,
+                    ldd2, int(accumulate)))
+    _q.keep.append(src)
+    arm()
+
+
+_TABLE_BYTES = 256 * 1024        # one pinned record table (> 1000 records)
+_free = []                        # pinned tables ready for reuse
+
+
+def reserve(n: int = 16) -> None:
+    """Pre-allocate pinned record tables.  Pinned allocation is not permitted while a stream
+    is capturing, so a HIP-graph capture draws on this pool (EncoderDecoder.cuda() and every
+    eager flush top it up)."""
+    if torch.cuda.is_current_stream_capturing():
+        return
+    _drain()
+    while len(_free) < n:
+        _free.append(torch.empty(_TABLE_BYTES, dtype=torch.uint8, pin_memory=True))
+
+
+def _drain() -> None:
+    if torch.cuda.is_current_stream_capturing():      # event queries are not permitted then
+        return
+    while _inflight and _inflight[0][0].query():
+        _free.append(_inflight.popleft()[1])
+
+
+def _table(nbytes: int) -> torch.Tensor:
+    if nbytes > _TABLE_BYTES:
+        if torch.cuda.is_current_stream_capturing():
+            raise _lib.CMXError(f"deferred: record table of {nbytes} B exceeds the pinned table size inside a capture")
+        return torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    _drain()
+    if not _free:
+        if torch.cuda.is_current_stream_capturing():
+            raise _lib.CMXError("deferred: pinned table pool exhausted inside a HIP-graph capture; "
+                                "call deferred.reserve(n) before capturing")
+        reserve(4)
+    return _free.pop()
+
+
+def _upload(table: torch.Tensor, nbytes: int, device) -> torch.Tensor:
+    dev = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    call("cmx_upload", dev.data_ptr(), table.data_ptr(), nbytes, stream())
+    if torch.cuda.is_current_stream_capturing():
+        _graph_tables.append(table)          # every replay re-reads it
+    else:
+        ev = torch.cuda.Event()
+        ev.record()
+        _inflight.append((ev, table))
+    return dev
+
+
+def flush() -> None:
+    """Issue the queued weight-gradient GEMMs (one launch) and reductions (one launch)."""
+    q = _q
+    q.armed = False
+    if not (q.gemms or q.reds):
+        return
+    gemms, reds, keep = q.gemms, list(q.reds), q.keep
+    q.gemms, q.reds, q.keep = [], [], []
+    device = keep[0].device
+    if gemms:
+        splits = [query("cmx_gemm_grouped_splitk", a[4], a[5], a[6], a[7], int(a[3] is not None)) for a in gemms]
+        sizes = [query("cmx_gemm_workspace", a[4], a[5], a[6], s) if s > 1 else 0 for a, s in zip(gemms, splits)]
+        arena = torch.empty(max(1, sum((z + 255) // 256 * 64 for z in sizes)), dtype=torch.float32, device=device)
+        table = _table(len(gemms) * _GREC)
+        base = table.data_ptr()
+        blk, off = 0, 0
+        for i, (a, s, sz) in enumerate(zip(gemms, splits, sizes)):
+            A, B, Wg, bg, G, M, N, K, lda, ldb, ldc, sA, sB, sC, sdb = a
+            ws = arena.data_ptr() + off if s > 1 else 0
+            nb = LIB.cmx_gemm_group_pack(base + i * _GREC, ptr(A), ptr(B), ptr(Wg), ptr(bg), ws, G, M, N, K, lda, ldb,
+                                         ldc, sA, sB, sC, sdb, 1, 1, 1, int(bg is not None), s, blk)
+            if nb <= 0:
+                raise _lib.CMXError(f"cmx_gemm_group_pack failed ({nb}): {_lib.last_error()}")
+            blk += nb
+            if s > 1:
+                # slabs: (G, s, M, Nr) fp32, Nr = real columns; then the bias-gradient column (G, s, M)
+                Nr = N - 1 if bg is not None else N
+                reds.append((ws, Wg.data_ptr(), 0, G, s, s * M * Nr, M * Nr, M, Nr, Nr, sC, ldc, 0, 0, 0))
+                if bg is not None:
+                    reds.append((ws + 4 * G * s * M * Nr, bg.data_ptr(), 0, G, s, s * M, M, 1, M, M, sdb, M, 0, 0, 0))
+                off += (sz + 255) // 256 * 256
+        dev = _upload(table, len(gemms) * _GREC, device)
+        call("cmx_gemm_grouped", dev.data_ptr(), len(gemms), blk, stream())
+        keep.append(arena)
+    if reds:
+        table = _table(len(reds) * _RREC)
+        base = table.data_ptr()
+        blk = 0
+        for i, r in enumerate(reds):
+            nb = LIB.cmx_reduce_pack(base + i * _RREC, *r, blk)
+            if nb <= 0:
+                raise _lib.CMXError(f"cmx_reduce_pack failed ({nb}): {_lib.last_error()}")
+            blk += nb
+        dev = _upload(table, len(reds) * _RREC, device)
+        call("cmx_reduce_grouped", dev.data_ptr(), len(reds), blk, stream())
+    # the caching allocator may hand the queued buffers out again once this stream has
+    # passed the launches above (stream-ordered reuse): dropping `keep` here is safe
+    del keep

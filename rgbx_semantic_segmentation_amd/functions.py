@@ -18,6 +18,7 @@ import os
 import torch
 from torch.autograd import Function
 
+from . import deferred
 from . import kernels as K
 from .streams import run_side
 
@@ -76,7 +77,10 @@ def _dgrad(dz, W_slice, out):
 
 
 def _wgrad_into(dz, x, Wg_slice, bg=None):
-    """Wg_slice (fp32 view (G, N, k)) = dz^T x;  bg (G, N) = column sums of dz."""
+    """Wg_slice (fp32 view (G, N, k)) = dz^T x;  bg (G, N) = column sums of dz.  bf16: queued
+    for the segment's grouped weight-gradient launch (deferred.py); otherwise run now."""
+    if USE_CMX_GEMM and deferred.wgrad(dz, x, Wg_slice, bg):
+        return
     if USE_CMX_GEMM:
         K.gemm(dz.transpose(1, 2), x.transpose(1, 2), Wg_slice, out_mode=1, dbias=bg, splitk=0)
         return
@@ -174,8 +178,25 @@ class LayerNormF(Function):
     @staticmethod
     def backward(ctx, dy):
         x, gamma, mean, rstd = ctx.saved_tensors
-        dx = K.layernorm_bwd(_c(dy), x, gamma, mean, rstd, ctx.G, ctx.gg, ctx.bg)
+        if deferred.ENABLED:
+            dx = _layernorm_bwd_deferred(_c(dy), x, gamma, mean, rstd, ctx.G, ctx.gg, ctx.bg)
+        else:
+            dx = K.layernorm_bwd(_c(dy), x, gamma, mean, rstd, ctx.G, ctx.gg, ctx.bg)
         return dx, None, None, None, None, None, None, None
+
+
+def _layernorm_bwd_deferred(dy, x, gamma, mean, rstd, G, gg, bg):
+    """dx now; dgamma / dbeta partials (G, nb, 2C) reduced by the segment's grouped reduce."""
+    C = x.shape[-1]
+    R = x.numel() // C // G
+    dx = torch.empty_like(x)
+    nbytes = K.query("cmx_layernorm_bwd_workspace", R, G, C, K.dtype_code(x))
+    ws = K._ws(nbytes, x.device)
+    K.call("cmx_layernorm_bwd", K.ptr(dy), K.ptr(x), K.ptr(gamma), K.ptr(mean), K.ptr(rstd), K.ptr(dx), 0, 0,
+           K.ptr(ws), R, G, C, 0, K.dtype_code(x), K.stream())
+    nb = nbytes // (8 * G * C)
+    deferred.reduce(ws, gg, bg, G, nb, nb * 2 * C, 2 * C, 1, 2 * C, C, gg.stride(0), 0, bg.stride(0), 0)
+    return dx
 
 
 def layernorm(store, mod, x, G):
@@ -260,9 +281,16 @@ class DWConvF(Function):
         # the LDS-tiled backward (C % 32 == 0) keeps dz on chip; the strip path writes it
         dz = torch.empty_like(h) if C % 32 else None
         dh = torch.empty_like(h) if ctx.needs_input_grad[0] else None
-        ws = K._ws(K.query("cmx_dwconv3x3_bwd_workspace", NI, ipg, H, W, C), h.device)
-        K.call("cmx_dwconv3x3_bwd", K.ptr(da), K.ptr(h), K.ptr(w), K.ptr(b), K.ptr(dz), K.ptr(dh), K.ptr(wg),
-               K.ptr(bg), K.ptr(ws), NI, ipg, H, W, C, K.ACT[act], 0, K.dtype_code(h), K.stream())
+        nbytes = K.query("cmx_dwconv3x3_bwd_workspace", NI, ipg, H, W, C)
+        ws = K._ws(nbytes, h.device)
+        defer = deferred.ENABLED
+        K.call("cmx_dwconv3x3_bwd", K.ptr(da), K.ptr(h), K.ptr(w), K.ptr(b), K.ptr(dz), K.ptr(dh),
+               0 if defer else K.ptr(wg), 0 if defer else K.ptr(bg), K.ptr(ws), NI, ipg, H, W, C, K.ACT[act], 0,
+               K.dtype_code(h), K.stream())
+        if defer:       # dW / db partials (G, P, C*10) = [9 taps | bias] per channel
+            G = NI // ipg
+            P = nbytes // (40 * G * C) - 1
+            deferred.reduce(ws, wg, bg, G, P, P * C * 10, C * 10, C, 10, 9, wg.stride(0), 9, bg.stride(0), 1)
         return dh, None, None, None, None, None, None, None, None, None, None
 
 

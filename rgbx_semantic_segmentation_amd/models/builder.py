@@ -118,6 +118,8 @@ class EncoderDecoder(nn.Module):
             self.store = ParamStore(self, device, self.compute_dtype,
                                     conv_pad={"backbone.patch_embed1.proj.weight": PE1_KPAD,
                                               "backbone.extra_patch_embed1.proj.weight": PE1_KPAD})
+        from .. import deferred
+        deferred.reserve()          # pinned launch-record tables for captured backward passes
         return self
 
     def cuda(self, device=None):
