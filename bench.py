@@ -158,10 +158,9 @@ def main():
     fl_img = train_flops_per_image(backbone=args.backbone, H=args.height, W=args.width, K=args.classes)
     step_frac = (ips / world) * fl_img / (PEAK_BF16_TFLOPS * 1e12)
 
-    roof = None
-    if rank == 0:
-        from rgbx_semantic_segmentation_amd.roofline import measure_dominant
-        roof = measure_dominant(args)
+    # every rank runs the roofline step (its SyncBN collectives need all ranks); rank 0 reports
+    from rgbx_semantic_segmentation_amd.roofline import measure_dominant
+    roof = measure_dominant(model, (rgb, x, lab))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

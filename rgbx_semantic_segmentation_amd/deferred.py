@@ -51,6 +51,9 @@ class _Queue:
 
 
 _q = _Queue()
+# observer(dev_table, nrec, blocks, problems, keep) is called after each grouped GEMM launch
+# (bench.py's roofline re-times that launch standalone); None in normal operation
+observer = None
 _graph_tables = []             # pinned tables referenced by captured graphs (never freed)
 _inflight = collections.deque()   # (event, pinned table) of eager uploads
 
@@ -203,6 +206,8 @@ def flush() -> None:
         dev = _upload(table, len(gemms) * _GREC, device)
         call("cmx_gemm_grouped", dev.data_ptr(), len(gemms), blk, stream())
         keep.append(arena)
+        if observer is not None:
+            observer(dev, len(gemms), blk, gemms, keep)
     if reds:
         table = _table(len(reds) * _RREC)
         base = table.data_ptr()
