@@ -43,6 +43,10 @@ int cmx_upload(void* dst, const void* src, size_t nbytes, hipStream_t stream);
 int cmx_layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y, float* mean, float* rstd, int64_t R, int G, int C, float eps, int dtype, hipStream_t stream);
 size_t cmx_layernorm_bwd_workspace(int64_t R, int G, int C, int dtype);
 int cmx_layernorm_bwd(const void* dy, const void* x, const float* gamma, const float* mean, const float* rstd, void* dx, float* dgamma, float* dbeta, float* workspace, int64_t R, int G, int C, int accumulate, int dtype, hipStream_t stream);
+/* backward of a norm whose input also feeds a residual (Block.forward x + drop_path(..), dual_segformer.py:168-169)
+ * and whose output has two consumers (Attention.q and .sr, :114-121): upstream gradient dy + dy2,
+ * dx = dres + LN_bwd(dy + dy2) and the DropPath-scaled copy dxs = sscale[(g*R+row)/rows_per_sample] * dx (NULLable). */
+int cmx_layernorm_bwd_res(const void* dy, const void* dy2, const void* x, const float* gamma, const float* mean, const float* rstd, const void* dres, const float* sscale, void* dxs, void* dx, float* dgamma, float* dbeta, float* workspace, int64_t R, int G, int C, int64_t rows_per_sample, int accumulate, int dtype, hipStream_t stream);
 
 /* ---- elementwise: residual + DropPath (Block.forward, dual_segformer.py:177-178),
  *      activations (CrossPath ReLU net_utils.py:273-274), bias-grad column sums, casts. */

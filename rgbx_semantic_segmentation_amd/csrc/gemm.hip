@@ -38,6 +38,7 @@
 //  * gemm_generic_kernel -- fp32 parity mode (exact v_mfma_f32_32x32x2_f32) and any bf16
 //    problem whose strides / dims do not allow 16-B chunks; register staged, BK = 32.
 #include "cmx_mfma.h"
+#include "cmx_dma.h"
 #include <string.h>
 
 namespace {
@@ -128,44 +129,7 @@ __device__ __forceinline__ float* slab_db(const GemmArgs& p, int G, int g, int z
 }
 
 // ============================================================================ bf16 fast path
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
-
-// One LDS-DMA wave-instruction: 64 lanes x 16 B from rsrc + voffset[lane] to LDS bytes
-// [lds, lds + 1024) in lane order.  Inline asm on purpose: through the compiler intrinsic,
-// hipcc cannot tell the DMA's LDS range from the buffer being read and waits vmcnt(0)
-// before every ds_read, which serialises the prefetch with the MFMAs.  The kernel orders
-// the DMA itself: `s_waitcnt vmcnt(0)` + barrier before a staged buffer is read.
-__device__ __forceinline__ void dma16(const i32x4 rsrc, uint32_t lds, int voffset) {
-  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
-               :: "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voffset), "s"(rsrc) : "memory");   // m0 is reserved: hipcc uses it for nothing else in these kernels
-}
-
 constexpr int FBK = 64;                         // k per pipeline stage
-constexpr int OOB = (int)0x80000000;            // voffset past num_records -> the load returns 0
-
-__device__ __forceinline__ i32x4 make_rsrc(const void* base) {
-  const uint64_t a = (uint64_t)base;
-  i32x4 r;
-  r.x = (int)(uint32_t)a;
-  r.y = (int)(uint32_t)(a >> 32);               // stride 0 (raw buffer)
-  r.z = 0x7ffffff0;                             // num_records: every in-range offset is < 2^31 - 16
-  r.w = 0x00020000;                             // gfx9 data format dword
-  return r;
-}
-
-// s_waitcnt vmcnt(N) with expcnt / lgkmcnt left alone (gfx9 encoding: vmcnt[3:0] | [15:14])
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
-}
-
-__device__ __forceinline__ uint32_t lds_addr(const char* p) {
-  return (uint32_t)reinterpret_cast<uintptr_t>(p);
-}
-
 // swizzle of the transposed image [64][ROWS]: 16-B chunk position of chunk c in k-row kk
 template <int ROWS>
 __device__ __forceinline__ int tr_swz(int kk) {

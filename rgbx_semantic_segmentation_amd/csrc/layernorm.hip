@@ -73,7 +73,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x,
   }
 }
 
-// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma.
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma  (+ dres: the gradient
+// of a residual branch that bypasses the norm, Block.forward's x + drop_path(...),
+// dual_segformer.py:168-169, summed here instead of by a separate add).  dxs (optional) =
+// sscale[row / rps] * dx: the DropPath-scaled copy the residual branch's own backward needs.
 // Per-block partial column sums of dy*xhat (dgamma) and dy (dbeta) go to ws.
 template <typename T, int TPR, int NCH>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
@@ -81,7 +84,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
                                                      const float* __restrict__ mean,
                                                      const float* __restrict__ rstd,
                                                      T* __restrict__ dx, float* __restrict__ ws,
-                                                     long R, int C) {
+                                                     long R, int C, const T* __restrict__ dres,
+                                                     const float* __restrict__ sscale, T* __restrict__ dxs,
+                                                     long rps, const T* __restrict__ dy2) {
   constexpr int V = VecT<T>::N;
   constexpr int RPB = 256 / TPR;
   __shared__ float red[256 / TPR][2][NCH * TPR * V > 512 ? 512 : NCH * TPR * V];
@@ -108,6 +113,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
         float dv[V];
         load_vec<T>(x + grow * C + ch * V, xv[k]);
         load_vec<T>(dy + grow * C + ch * V, dv);
+        if (dy2) {              // second consumer of y (q and the SR conv both read norm1's output)
+          float d2[V];
+          load_vec<T>(dy2 + grow * C + ch * V, d2);
+#pragma unroll
+          for (int j = 0; j < V; ++j) dv[j] += d2[j];
+        }
 #pragma unroll
         for (int j = 0; j < V; ++j) {
           const float xh = (xv[k][j] - mu) * rs;
@@ -129,7 +140,19 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
         float o[V];
 #pragma unroll
         for (int j = 0; j < V; ++j) o[j] = rs * (gv[k][j] - s1 - xv[k][j] * s2);
+        if (dres) {
+          float rv[V];
+          load_vec<T>(dres + grow * C + ch * V, rv);
+#pragma unroll
+          for (int j = 0; j < V; ++j) o[j] += rv[j];
+        }
         store_vec<T>(dx + grow * C + ch * V, o);
+        if (dxs) {
+          const float sc = sscale[grow / rps];
+#pragma unroll
+          for (int j = 0; j < V; ++j) o[j] *= sc;
+          store_vec<T>(dxs + grow * C + ch * V, o);
+        }
       }
     }
   }
@@ -230,15 +253,16 @@ static int ln_fwd_launch(const void* x, const float* g, const float* b, void* y,
   return CMX_ERR_SHAPE;
 }
 
-static int ln_bwd_blocks(long R, int rpb) {
+static int ln_bwd_blocks(long R, int rpb) {     // <= 512 blocks per group: ~2 rows per thread at stage 1
   long nb = (R + rpb - 1) / rpb;
-  return (int)(nb < 128 ? nb : 128);
+  return (int)(nb < 512 ? nb : 512);
 }
 
 template <typename T>
 static int ln_bwd_launch(const void* dy, const void* x, const float* g, const float* mu,
                          const float* rs, void* dx, float* dgamma, float* dbeta, float* ws, long R,
-                         int G, int C, int accumulate, hipStream_t s) {
+                         int G, int C, int accumulate, const void* dres, const float* sscale, void* dxs,
+                         long rps, const void* dy2, hipStream_t s) {
   constexpr int V = VecT<T>::N;
   const int chunks = C / V;
   const int tpr = ln_tpr(chunks);
@@ -248,7 +272,8 @@ static int ln_bwd_launch(const void* dy, const void* x, const float* g, const fl
 #define LNB(TPR, NCH)                                                                       \
   if (tpr == TPR && nch == NCH) {                                                           \
     hipLaunchKernelGGL((ln_bwd_kernel<T, TPR, NCH>), grid, dim3(256), 0, s, (const T*)dy,    \
-                       (const T*)x, g, mu, rs, (T*)dx, ws, R, C);                            \
+                       (const T*)x, g, mu, rs, (T*)dx, ws, R, C, (const T*)dres, sscale,     \
+                       (T*)dxs, rps, (const T*)dy2);                                         \
     goto reduce;                                                                            \
   }
   LNB(4, 1) LNB(8, 1) LNB(16, 1) LNB(32, 1) LNB(64, 1) LNB(64, 2) LNB(64, 4)
@@ -298,7 +323,24 @@ int cmx_layernorm_bwd(const void* dy, const void* x, const float* gamma, const f
   CMX_REQUIRE(C % (dtype == 0 ? 4 : 8) == 0, CMX_ERR_SHAPE, "layernorm_bwd: C=%d", C);
   CMX_DISPATCH(dtype, T,
                return ln_bwd_launch<T>(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, workspace, R,
-                                       G, C, accumulate, s));
+                                       G, C, accumulate, nullptr, nullptr, nullptr, 1, nullptr, s));
+}
+
+// cmx_layernorm_bwd with dy + dy2 as the upstream gradient (two consumers of y), a residual
+// gradient dres added to dx and an optional DropPath-scaled copy
+// dxs = sscale[(g*R + row) / rows_per_sample] * dx (dy2 / dres / sscale / dxs may be NULL).
+int cmx_layernorm_bwd_res(const void* dy, const void* dy2, const void* x, const float* gamma, const float* mean,
+                          const float* rstd, const void* dres, const float* sscale, void* dxs, void* dx, float* dgamma,
+                          float* dbeta,
+                          float* workspace, long R, int G, int C, long rows_per_sample, int accumulate, int dtype,
+                          hipStream_t s) {
+  CMX_REQUIRE(R > 0 && G > 0 && C > 0 && C <= 1024, CMX_ERR_SHAPE, "layernorm_bwd_res: bad shape");
+  CMX_REQUIRE(C % (dtype == 0 ? 4 : 8) == 0, CMX_ERR_SHAPE, "layernorm_bwd_res: C=%d", C);
+  CMX_REQUIRE(!dxs || (sscale && rows_per_sample > 0), CMX_ERR_ARG, "layernorm_bwd_res: dxs needs sscale");
+  CMX_DISPATCH(dtype, T,
+               return ln_bwd_launch<T>(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, workspace, R,
+                                       G, C, accumulate, dres, sscale, dxs, rows_per_sample > 0 ? rows_per_sample : 1,
+                                       dy2, s));
 }
 
 }  // extern "C"

@@ -415,6 +415,14 @@ int bwd_qc(int N, int nchunk) {
 
 }  // namespace
 
+// sra_fast.hip: LDS-resident K/V path for bf16, D = 64, Nk <= 320
+bool sra_fast_ok(int D, int Nk, int dtype, const void* const* ptrs, int nptr, const long* strides, int nstr);
+void sra_fwd_fast_launch(const void* q, const void* k, const void* v, void* o, float* lse, int Bt, int N, int Nk,
+                         int heads, long qs, long kvs, long os, float sl2, hipStream_t s);
+void sra_dq_fast_launch(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                        const float* lse, float* Dws, void* dq, int Bt, int N, int Nk, int heads, long qs, long kvs,
+                        long os, long dos, long dqs, float sl2, float scale, hipStream_t s);
+
 #define SRA_D_DISPATCH(D, ...)                                              \
   do {                                                                      \
     if ((D) == 64) { constexpr int DD = 64; __VA_ARGS__; }                  \
@@ -431,6 +439,14 @@ int cmx_sra_attn_fwd(const void* q, const void* k, const void* v, void* o, float
   CMX_REQUIRE(Bt > 0 && N > 0 && Nk > 0 && heads > 0, CMX_ERR_SHAPE, "sra_fwd: bad shape");
   CMX_REQUIRE(qs % 8 == 0 && kvs % 8 == 0 && os % 8 == 0, CMX_ERR_SHAPE, "sra_fwd: strides %% 8");
   const float sl2 = scale * 1.4426950408889634f;
+  {
+    const void* ptrs[] = {q, k, v, o};
+    const long strides[] = {qs, kvs, os};
+    if (sra_fast_ok(D, Nk, dtype, ptrs, 4, strides, 3)) {
+      sra_fwd_fast_launch(q, k, v, o, lse, Bt, N, Nk, heads, qs, kvs, os, sl2, s);
+      return cmx_check_launch("sra_fwd");
+    }
+  }
   const dim3 grid(cdiv(N, BQ), heads, Bt);
   SRA_D_DISPATCH(D, CMX_DISPATCH(dtype, T, {
     hipLaunchKernelGGL((sra_fwd_kernel<T, DD>), grid, dim3(256), 0, s, (const T*)q, (const T*)k,
@@ -458,10 +474,16 @@ int cmx_sra_attn_bwd(const void* q, const void* k, const void* v, const void* o,
   float* Dws = workspace;
   float* ws_dk = Dws + (size_t)Bt * heads * N;
   float* ws_dv = ws_dk + (size_t)nc * Bt * heads * Nk * D;
+  const void* ptrs[] = {q, k, v, o, dout, dq};
+  const long strides[] = {qs, kvs, os, dos, dqs};
+  const bool fast = sra_fast_ok(D, Nk, dtype, ptrs, 6, strides, 5);
   SRA_D_DISPATCH(D, CMX_DISPATCH(dtype, T, {
-    hipLaunchKernelGGL((sra_bwd_dq_kernel<T, DD>), dim3(cdiv(N, BQ), heads, Bt), dim3(256), 0, s,
-                       (const T*)q, (const T*)k, (const T*)v, (const T*)o, (const T*)dout, lse, Dws,
-                       (T*)dq, N, Nk, heads, qs, kvs, os, dos, dqs, sl2, scale);
+    if (fast)
+      sra_dq_fast_launch(q, k, v, o, dout, lse, Dws, dq, Bt, N, Nk, heads, qs, kvs, os, dos, dqs, sl2, scale, s);
+    else
+      hipLaunchKernelGGL((sra_bwd_dq_kernel<T, DD>), dim3(cdiv(N, BQ), heads, Bt), dim3(256), 0, s,
+                         (const T*)q, (const T*)k, (const T*)v, (const T*)o, (const T*)dout, lse, Dws,
+                         (T*)dq, N, Nk, heads, qs, kvs, os, dos, dqs, sl2, scale);
     hipLaunchKernelGGL((sra_bwd_dkv_kernel<T, DD>), dim3(cdiv(Nk, BK), heads, Bt * nc), dim3(256), 0, s,
                        (const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse, Dws, ws_dk, ws_dv, Bt,
                        N, Nk, heads, qs, kvs, dos, qc, nc, sl2, scale);

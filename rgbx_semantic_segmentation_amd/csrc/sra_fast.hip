@@ -1,0 +1,344 @@
+// SRA attention, bf16 / head dim 64 fast path (every stage of CMX-B2/B4 at 480x640: Nk = 300).
+//
+// Same math as sra_attention.hip (dual_segformer.py:130-134: softmax(q k^T d^-1/2) v and its
+// backward), re-decomposed for gfx950 around one fact: a whole (b, head)'s keys fit in LDS.
+// K and V of one (b, head) are (Nk x 64) bf16 = 38 KB each at Nk = 300, so a workgroup
+// stages BOTH once, in its prologue, and its waves then sweep every key tile with no
+// barrier in the loop (the generic kernels restage a 32-key tile between two barriers per
+// step, which left the stage-1 forward at ~4 % of MFMA peak).  80 KB of LDS per workgroup
+// (Nk <= 320) keeps two workgroups per CU.
+//
+// Images: a key-row-major [nkp][64] bf16 image (128-B rows) per operand, 16-B chunks
+// XOR-swizzled by (row >> 1) & 7.  A wave reads it two ways without a second copy:
+//  * frag_k: 32 rows x 8 contiguous d per lane (ds_read_b128) -- K or V as the A operand of
+//    S^T = K Q^T and dP^T = V dO^T;
+//  * frag_t: the transposed view (d on the lane, 8 keys per lane) with gfx950's
+//    ds_read_b64_tr_b16, in the k-permuted order in which an accumulator tile is fed back as
+//    the B operand (accrow(8s + j, h), cmx_mfma.h) -- V^T of O^T = V^T P^T and K^T of
+//    dQ^T = K^T dS^T, straight from the accumulator with no LDS round trip.
+// Queries stay on the MFMA lane (S^T tiles), so the online softmax is per lane plus one
+// cross-half shuffle; each wave owns QW 32-query sub-tiles for MFMA/VALU overlap.
+#include "cmx_mfma.h"
+#include "cmx_dma.h"
+
+namespace {
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int HD = 64;          // head dim
+constexpr int ROWB = 128;       // bytes per key row of an image
+constexpr int NKP_MAX = 320;    // keys held in LDS (Nk <= 320)
+constexpr int KTILE = 64;       // keys per loop step
+constexpr int NWAVE = 8;        // waves per workgroup: two per SIMD share one K/V image
+
+__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
+
+// rows [0, nkp) of a (Nk x 64) bf16 matrix with row stride ld -> swizzled image, by LDS-DMA
+// (no register staging; rows >= Nk come back as zeros through the buffer range check).  One
+// wave instruction fills 8 rows (1 KB) in lane order: lane L lands on row 8j + L / 8, slot
+// L % 8, which must hold chunk (L % 8) ^ swz(row).  Completion: vm_wait<0>() + barrier.
+__device__ __forceinline__ void stage_rows(const bf16* __restrict__ g, long ld, int Nk, int nkp, char* img, int wave,
+                                           int lane, int nwaves) {
+  const i32x4 rs = make_rsrc(g);
+  for (int j = wave; j < nkp / 8; j += nwaves) {
+    const int row = j * 8 + (lane >> 3), c = (lane & 7) ^ swz(row);
+    const int off = row < Nk ? (int)(((long)row * ld + c * 8) * 2) : OOB;
+    dma16(rs, lds_addr(img + j * 1024), off);
+  }
+}
+
+// A operand, k = d contiguous: row rb + (lane & 31), d in [16 s + 8 h, +8)
+__device__ __forceinline__ bf16x8 frag_k(const char* img, int rb, int s, int lane) {
+  const int row = rb + (lane & 31), h = lane >> 5;
+  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(img + row * ROWB + (((2 * s + h) ^ swz(row)) << 4)));
+}
+
+// A operand from the transposed view: d = db + (lane & 31) on the lane, k = rows
+// kb + 16 s + 4 h + {0..3, 8..11} (the accumulator-as-B order of MF<bf16>::from_acc)
+__device__ __forceinline__ bf16x8 frag_t(const char* img, int kb, int db, int s, int lane) {
+  const int h = lane >> 5, g16 = (lane >> 4) & 1, i = lane & 15, q = i >> 2, pp = i & 3;
+  const int chunk = (db + 16 * g16 + 4 * pp) >> 3;
+  s16x4 v[2];
+#pragma unroll
+  for (int rd = 0; rd < 2; ++rd) {
+    const int kk = kb + 16 * s + 4 * h + 8 * rd + q;
+    const int off = kk * ROWB + ((chunk ^ swz(kk)) << 4) + ((pp & 1) << 3);
+    v[rd] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        reinterpret_cast<__attribute__((address_space(3))) s16x4*>(reinterpret_cast<uintptr_t>(img + off)));
+  }
+  const s16x8 c = __builtin_shufflevector(v[0], v[1], 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, c);
+}
+
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+__device__ __forceinline__ void store_rows(bf16* row_ptr, const f32x16& acc, int t, int h, float mul) {
+#pragma unroll
+  for (int k4 = 0; k4 < 4; ++k4) {
+    const uint32_t a = pack2_bf16(acc[4 * k4] * mul, acc[4 * k4 + 1] * mul);
+    const uint32_t b = pack2_bf16(acc[4 * k4 + 2] * mul, acc[4 * k4 + 3] * mul);
+    *reinterpret_cast<uint2*>(row_ptr + 32 * t + 8 * k4 + 4 * h) = make_uint2(a, b);
+  }
+}
+
+// ------------------------------------------------------------------------ forward
+template <int QW>
+__global__ __launch_bounds__(64 * NWAVE) void sra_fwd_fast(const bf16* __restrict__ q, const bf16* __restrict__ k,
+                                                       const bf16* __restrict__ v, bf16* __restrict__ o,
+                                                       float* __restrict__ lse, int N, int Nk, int nkp, int heads,
+                                                       long qs, long kvs, long os, float sl2) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * NKP_MAX * ROWB];
+  char* Ki = smem;
+  char* Vi = smem + NKP_MAX * ROWB;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int b = blockIdx.z, head = blockIdx.y;
+  stage_rows(k + (long)b * Nk * kvs + head * HD, kvs, Nk, nkp, Ki, wave, lane, NWAVE);
+  stage_rows(v + (long)b * Nk * kvs + head * HD, kvs, Nk, nkp, Vi, wave, lane, NWAVE);
+
+  const int q0 = (blockIdx.x * NWAVE + wave) * 32 * QW;
+  const bf16* qb = q + (long)b * N * qs + head * HD;
+  bf16x8 qf[QW][4];
+#pragma unroll
+  for (int u = 0; u < QW; ++u) {
+    const int qi = q0 + 32 * u + r;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      qf[u][s] = qi < N ? __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(qb + (long)qi * qs + 16 * s + 8 * h))
+                        : zfrag<bf16>();
+  }
+  f32x16 acc[QW][2];
+  float m[QW], l[QW];
+#pragma unroll
+  for (int u = 0; u < QW; ++u) {
+    acc[u][0] = acc[u][1] = zero16();
+    m[u] = -INFINITY;
+    l[u] = 0.f;
+  }
+  vm_wait<0>();
+  __syncthreads();
+
+  for (int t0 = 0; t0 < nkp; t0 += KTILE) {
+    f32x16 sa[QW][2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 kf[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) kf[s] = frag_k(Ki, t0 + 32 * ks, s, lane);
+#pragma unroll
+      for (int u = 0; u < QW; ++u) {
+        sa[u][ks] = zero16();
+#pragma unroll
+        for (int s = 0; s < 4; ++s) sa[u][ks] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[s], qf[u][s], sa[u][ks], 0, 0, 0);
+      }
+    }
+    const bool tail = t0 + KTILE > Nk;
+#pragma unroll
+    for (int u = 0; u < QW; ++u) {
+      float mt = -INFINITY;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float x = sa[u][ks][i];
+          if (tail && t0 + 32 * ks + accrow(i, h) >= Nk) x = -INFINITY;
+          sa[u][ks][i] = x;
+          mt = fmaxf(mt, x);
+        }
+      // max on the raw scores (the scale is positive), exponent as one FMA per score
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
+      const float mn = fmaxf(m[u], mt);
+      const float alpha = fexp2(m[u] - mn);
+      float rs = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = fexp2(fmaf(sa[u][ks][i], sl2, -mn));
+          sa[u][ks][i] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 32, 64);
+      l[u] = l[u] * alpha + rs;
+      m[u] = mn;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[u][t][i] *= alpha;
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 v0 = frag_t(Vi, t0 + 32 * ks, 0, s, lane);
+        const bf16x8 v1 = frag_t(Vi, t0 + 32 * ks, 32, s, lane);
+#pragma unroll
+        for (int u = 0; u < QW; ++u) {
+          const bf16x8 pf = MF<bf16>::from_acc(sa[u][ks], s);
+          acc[u][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v0, pf, acc[u][0], 0, 0, 0);
+          acc[u][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v1, pf, acc[u][1], 0, 0, 0);
+        }
+      }
+  }
+#pragma unroll
+  for (int u = 0; u < QW; ++u) {
+    const int qi = q0 + 32 * u + r;
+    if (qi >= N) continue;
+    const float inv = 1.f / l[u];
+    bf16* ob = o + ((long)b * N + qi) * os + head * HD;
+    store_rows(ob, acc[u][0], 0, h, inv);
+    store_rows(ob, acc[u][1], 1, h, inv);
+    if (h == 0 && lse) lse[((long)b * heads + head) * N + qi] = (m[u] + __log2f(l[u])) * 0.69314718055994531f;
+  }
+}
+
+// ------------------------------------------------------------------------ backward: dQ (+ Dq)
+// dS^T = P^T o (dP^T - Dq), P^T = exp(S^T - lse), dP^T = V dO^T; dQ^T = K^T dS^T * scale.
+template <int QW>
+__global__ __launch_bounds__(64 * NWAVE) void sra_dq_fast(const bf16* __restrict__ q, const bf16* __restrict__ k,
+                                                      const bf16* __restrict__ v, const bf16* __restrict__ o,
+                                                      const bf16* __restrict__ dout, const float* __restrict__ lse,
+                                                      float* __restrict__ Dws, bf16* __restrict__ dq, int N, int Nk,
+                                                      int nkp, int heads, long qs, long kvs, long os, long dos,
+                                                      long dqs, float sl2, float scale) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * NKP_MAX * ROWB];
+  char* Ki = smem;
+  char* Vi = smem + NKP_MAX * ROWB;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int b = blockIdx.z, head = blockIdx.y;
+  stage_rows(k + (long)b * Nk * kvs + head * HD, kvs, Nk, nkp, Ki, wave, lane, NWAVE);
+  stage_rows(v + (long)b * Nk * kvs + head * HD, kvs, Nk, nkp, Vi, wave, lane, NWAVE);
+
+  const int q0 = (blockIdx.x * NWAVE + wave) * 32 * QW;
+  bf16x8 qf[QW][4], df[QW][4];
+  float Dq[QW], lse2[QW];
+#pragma unroll
+  for (int u = 0; u < QW; ++u) {
+    const int qi = q0 + 32 * u + r;
+    const bool live = qi < N;
+    const bf16* qrow = q + ((long)b * N + qi) * qs + head * HD;
+    const bf16* orow = o + ((long)b * N + qi) * os + head * HD;
+    const bf16* drow = dout + ((long)b * N + qi) * dos + head * HD;
+    float dot = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (live) {
+        const uint4 qv = *reinterpret_cast<const uint4*>(qrow + 16 * s + 8 * h);
+        const uint4 dv = *reinterpret_cast<const uint4*>(drow + 16 * s + 8 * h);
+        qf[u][s] = __builtin_bit_cast(bf16x8, qv);
+        df[u][s] = __builtin_bit_cast(bf16x8, dv);
+        float x[8], y[8];
+        load_vec<bf16>(drow + 16 * s + 8 * h, x);
+        load_vec<bf16>(orow + 16 * s + 8 * h, y);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dot += x[j] * y[j];
+      } else {
+        qf[u][s] = df[u][s] = zfrag<bf16>();
+      }
+    }
+    dot += __shfl_xor(dot, 32, 64);
+    Dq[u] = dot;
+    const long sidx = ((long)b * heads + head) * N + qi;
+    lse2[u] = live ? lse[sidx] * 1.4426950408889634f : 0.f;
+    if (live && h == 0) Dws[sidx] = dot;
+  }
+  f32x16 acc[QW][2];
+#pragma unroll
+  for (int u = 0; u < QW; ++u) acc[u][0] = acc[u][1] = zero16();
+  vm_wait<0>();
+  __syncthreads();
+
+  for (int t0 = 0; t0 < nkp; t0 += KTILE) {
+    const bool tail = t0 + KTILE > Nk;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int kb = t0 + 32 * ks;
+      bf16x8 kf[4], vf[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        kf[s] = frag_k(Ki, kb, s, lane);
+        vf[s] = frag_k(Vi, kb, s, lane);
+      }
+      f32x16 ds[QW];
+#pragma unroll
+      for (int u = 0; u < QW; ++u) {
+        f32x16 sa = zero16(), dp = zero16();
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[s], qf[u][s], sa, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[s], df[u][s], dp, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float p = fexp2(sa[i] * sl2 - lse2[u]);
+          if (tail && kb + accrow(i, h) >= Nk) p = 0.f;
+          ds[u][i] = p * (dp[i] - Dq[u]);
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 k0 = frag_t(Ki, kb, 0, s, lane);
+        const bf16x8 k1 = frag_t(Ki, kb, 32, s, lane);
+#pragma unroll
+        for (int u = 0; u < QW; ++u) {
+          const bf16x8 sf = MF<bf16>::from_acc(ds[u], s);
+          acc[u][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, sf, acc[u][0], 0, 0, 0);
+          acc[u][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, sf, acc[u][1], 0, 0, 0);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < QW; ++u) {
+    const int qi = q0 + 32 * u + r;
+    if (qi >= N) continue;
+    bf16* out = dq + ((long)b * N + qi) * dqs + head * HD;
+    store_rows(out, acc[u][0], 0, h, scale);
+    store_rows(out, acc[u][1], 1, h, scale);
+  }
+}
+
+int pick_qw(int N, int heads, int Bt) {
+  const long wg2 = (long)cdiv(N, 64 * NWAVE) * heads * Bt;   // workgroups at 2 sub-tiles per wave
+  return wg2 >= 512 ? 2 : 1;
+}
+
+}  // namespace
+
+// bf16, D = 64, Nk <= 320, 16-B aligned rows: the LDS-resident path (sra_attention.hip calls these)
+bool sra_fast_ok(int D, int Nk, int dtype, const void* const* ptrs, int nptr, const long* strides, int nstr) {
+  if (dtype != 1 || D != HD || Nk > NKP_MAX || Nk <= 0) return false;
+  for (int i = 0; i < nptr; ++i)
+    if (ptrs[i] && ((uintptr_t)ptrs[i] & 15)) return false;
+  for (int i = 0; i < nstr; ++i)
+    if (strides[i] % 8) return false;
+  return true;
+}
+
+void sra_fwd_fast_launch(const void* q, const void* k, const void* v, void* o, float* lse, int Bt, int N, int Nk,
+                         int heads, long qs, long kvs, long os, float sl2, hipStream_t s) {
+  const int nkp = (Nk + KTILE - 1) / KTILE * KTILE;
+  const int qw = pick_qw(N, heads, Bt);
+  const dim3 grid(cdiv(N, 32 * NWAVE * qw), heads, Bt);
+  if (qw == 2)
+    hipLaunchKernelGGL(sra_fwd_fast<2>, grid, dim3(64 * NWAVE), 0, s, (const bf16*)q, (const bf16*)k, (const bf16*)v,
+                       (bf16*)o, lse, N, Nk, nkp, heads, qs, kvs, os, sl2);
+  else
+    hipLaunchKernelGGL(sra_fwd_fast<1>, grid, dim3(64 * NWAVE), 0, s, (const bf16*)q, (const bf16*)k, (const bf16*)v,
+                       (bf16*)o, lse, N, Nk, nkp, heads, qs, kvs, os, sl2);
+}
+
+void sra_dq_fast_launch(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                        const float* lse, float* Dws, void* dq, int Bt, int N, int Nk, int heads, long qs, long kvs,
+                        long os, long dos, long dqs, float sl2, float scale, hipStream_t s) {
+  const int nkp = (Nk + KTILE - 1) / KTILE * KTILE;
+  const int qw = pick_qw(N, heads, Bt);
+  const dim3 grid(cdiv(N, 32 * NWAVE * qw), heads, Bt);
+  if (qw == 2)
+    hipLaunchKernelGGL(sra_dq_fast<2>, grid, dim3(64 * NWAVE), 0, s, (const bf16*)q, (const bf16*)k, (const bf16*)v,
+                       (const bf16*)o, (const bf16*)dout, lse, Dws, (bf16*)dq, N, Nk, nkp, heads, qs, kvs, os, dos, dqs,
+                       sl2, scale);
+  else
+    hipLaunchKernelGGL(sra_dq_fast<1>, grid, dim3(64 * NWAVE), 0, s, (const bf16*)q, (const bf16*)k, (const bf16*)v,
+                       (const bf16*)o, (const bf16*)dout, lse, Dws, (bf16*)dq, N, Nk, nkp, heads, qs, kvs, os, dos, dqs,
+                       sl2, scale);
+}

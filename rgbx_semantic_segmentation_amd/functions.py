@@ -115,26 +115,30 @@ class GLinear(Function):
     x + drop_path(proj/fc2(...)), dual_segformer.py:168-169)."""
 
     @staticmethod
-    def forward(ctx, W, Wg, b, bg, anchor, act, res, rscale, rps, x1, x2):
+    def forward(ctx, W, Wg, b, bg, anchor, act, res, rscale, rps, x1, x2, tap=None):
         G, N, Ktot = W.shape
         M = x1.shape[1]
         assert x1.shape[-1] + (x2.shape[-1] if x2 is not None else 0) == Ktot, (x1.shape, W.shape)
         y = torch.empty(G, M, N, dtype=x1.dtype, device=x1.device)
         _fwd_gemm(x1, W, b, y, act=act, res=res, rscale=rscale, rps=rps, x2=x2)
         ctx.save_for_backward(W, x1, x2, y if act == "relu" else None)
-        ctx.meta = (Wg, bg, act, res is not None, rscale, rps)
+        ctx.meta = (Wg, bg, act, res is not None, rscale, rps, tap)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         W, x1, x2, y = ctx.saved_tensors
-        Wg, bg, act, has_res, rscale, rps = ctx.meta
+        Wg, bg, act, has_res, rscale, rps, tap = ctx.meta
         dy = _c(dy)
         G, M, N = dy.shape
         dres = dy if has_res else None
         dz = dy
         if rscale is not None:
-            dz = K.scale_samples(dz, rscale, rps * N)
+            # the DropPath-scaled gradient, written by the consumer norm's backward when it
+            # could (GradTap), else one scaling pass
+            dz = tap.take(dy) if tap is not None else None
+            if dz is None:
+                dz = K.scale_samples(dy, rscale, rps * N)
         if act == "relu":
             dz = K.act_bwd(dz, y, "relu")
         k1 = x1.shape[-1]
@@ -148,10 +152,10 @@ class GLinear(Function):
             if x2 is not None:
                 _wgrad_into(dz, x2, Wg[:, :, k1:])
         run_side(wgrads, dz, x1, x2)
-        return (None, None, None, None, None, None, dres, None, None, dx1, dx2)
+        return (None, None, None, None, None, None, dres, None, None, dx1, dx2, None)
 
 
-def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1):
+def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1, tap=None):
     """Grouped linear using parameter ``wp`` (and bias ``bp``) of the store; x2 = second
     input segment (cat-free), res/rscale/rps = fused DropPath residual (rps = rows per sample)."""
     W = store.w(wp)
@@ -163,10 +167,78 @@ def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1
     if bp is not None:
         b = store.w(bp, compute=False).view(G, -1)
         bg = store.g(bp).view(G, -1)
-    return GLinear.apply(W, Wg, b, bg, wp, act, res, rscale, rps, x1, x2)
+    return GLinear.apply(W, Wg, b, bg, wp, act, res, rscale, rps, x1, x2, tap)
 
 
 # ---------------------------------------------------------------------------- LayerNorm
+class GradTap:
+    """Side channel from a norm's backward to the backward of the residual-branch GEMM that
+    produced the norm's input (Block: x1 = x + drop_path(proj(o)) -> norm2(x1),
+    dual_segformer.py:168-169): the norm's backward kernel also writes the DropPath-scaled
+    gradient s[sample] * dx1, which the GEMM's backward uses as its dz (no scaling pass)."""
+    __slots__ = ("t",)
+
+    def __init__(self):
+        self.t = None
+
+    def put(self, t):
+        self.t = t
+
+    def take(self, like):
+        t, self.t = self.t, None
+        return t if (t is not None and t.shape == like.shape) else None
+
+
+class LayerNormResF(Function):
+    """y = LN(x), plus x passed through as a second output for a residual add downstream:
+    the backward then receives both gradients and sums them in the LN backward kernel
+    (cmx_layernorm_bwd_res) instead of autograd adding them.  ``scale``/``tap``: also emit
+    scale[sample] * dx for the producer of x (GradTap)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, gg, bg, eps, G, scale, rps, tap, anchor):
+        y, mean, rstd = K.layernorm_fwd(x, gamma, beta, eps, G=G)
+        ctx.save_for_backward(x, gamma, mean, rstd)
+        ctx.meta = (gg, bg, G, scale, rps, tap)
+        # y twice (a view for the second consumer, so its gradient arrives separately) and x
+        return y, y.view_as(y), x
+
+    @staticmethod
+    def backward(ctx, dy, dy2, dres):
+        x, gamma, mean, rstd = ctx.saved_tensors
+        gg, bg, G, scale, rps, tap = ctx.meta
+        C = x.shape[-1]
+        R = x.numel() // C // G
+        if dy is None:
+            dy, dy2 = dy2, None
+        dy = _c(dy) if dy is not None else torch.zeros_like(x)
+        dy2 = _c(dy2) if dy2 is not None else None
+        dres = _c(dres) if dres is not None else None
+        dx = torch.empty_like(x)
+        dxs = torch.empty_like(x) if (tap is not None and scale is not None) else None
+        nbytes = K.query("cmx_layernorm_bwd_workspace", R, G, C, K.dtype_code(x))
+        ws = K._ws(nbytes, x.device)
+        defer = deferred.ENABLED
+        K.call("cmx_layernorm_bwd_res", K.ptr(dy), K.ptr(dy2), K.ptr(x), K.ptr(gamma), K.ptr(mean), K.ptr(rstd), K.ptr(dres),
+               K.ptr(scale), K.ptr(dxs), K.ptr(dx), 0 if defer else K.ptr(gg), 0 if defer else K.ptr(bg),
+               K.ptr(ws), R, G, C, int(rps), 0, K.dtype_code(x), K.stream())
+        if defer:
+            nb = nbytes // (8 * G * C)
+            deferred.reduce(ws, gg, bg, G, nb, nb * 2 * C, 2 * C, 1, 2 * C, C, gg.stride(0), 0, bg.stride(0), 0)
+        if dxs is not None:
+            tap.put(dxs)
+        return dx, None, None, None, None, None, None, None, None, None, None
+
+
+def layernorm_res(store, mod, x, G, scale=None, rps=1, tap=None):
+    """(LN(x), LN(x) for a second consumer, x) with the fused backward (LayerNormResF)."""
+    gamma = store.w(mod.weight, compute=False).view(G, -1)
+    beta = store.w(mod.bias, compute=False).view(G, -1)
+    gg = store.g(mod.weight).view(G, -1)
+    bg = store.g(mod.bias).view(G, -1)
+    return LayerNormResF.apply(x, gamma, beta, gg, bg, mod.eps, G, scale, rps, tap, mod.weight)
+
+
 class LayerNormF(Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, gg, bg, eps, G, anchor):

@@ -121,27 +121,37 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
                 rows.append((1.0 - self.dp[s][0][i], 1.0 - self.dp[s][1][i]))
         return rows
 
-    def run_block(self, store, blk: Block, x, B, H, W, s_attn, s_mlp):
+    def run_block(self, store, blk: Block, x, B, H, W, s_attn, s_mlp, prev=(None, None)):
+        """One Block (dual_segformer.py:166-180) for both streams.  ``prev`` = (DropPath scale,
+        GradTap) of the residual branch that produced ``x`` (the previous block's fc2): norm1's
+        backward writes that branch's scaled gradient.  Returns (x_out, (s_mlp, tap)) for the
+        next consumer of x_out."""
         G, M, C = x.shape
         N = H * W
         a = blk.attn
-        h = F.layernorm(store, blk.norm1, x, G)
+        # norm1 also passes x through for the attention residual: its backward sums both gradients
+        # (q and the SR path read norm1's output through separate handles: the norm's backward
+        # sums their gradients on load)
+        h, h2, xr = F.layernorm_res(store, blk.norm1, x, G, scale=prev[0], rps=N, tap=prev[1])
         q = F.glinear(store, a.q.weight, a.q.bias, h)
         if a.sr_ratio > 1:
             R = a.sr_ratio
-            xs, Hk, Wk = F.conv(store, a.sr, h, G, G * B, H, W, C, R, 0)
+            xs, Hk, Wk = F.conv(store, a.sr, h2, G, G * B, H, W, C, R, 0)
             xs = F.layernorm(store, a.norm, xs, G)
             Nk = Hk * Wk
         else:
-            xs, Nk = h, N
+            xs, Nk = h2, N
         kv = F.glinear(store, a.kv.weight, a.kv.bias, xs)
         o = F.SRAttentionF.apply(q, kv, G * B, N, Nk, a.num_heads, C // a.num_heads)
         # x + drop_path(proj(o)): residual and DropPath scale fused into the proj GEMM epilogue
-        x = F.glinear(store, a.proj.weight, a.proj.bias, o, res=x, rscale=s_attn, rps=N)
-        h = F.layernorm(store, blk.norm2, x, G)
+        tap_a = F.GradTap() if s_attn is not None else None
+        x = F.glinear(store, a.proj.weight, a.proj.bias, o, res=xr, rscale=s_attn, rps=N, tap=tap_a)
+        h, _, xr = F.layernorm_res(store, blk.norm2, x, G, scale=s_attn, rps=N, tap=tap_a)
         f = F.glinear(store, blk.mlp.fc1.weight, blk.mlp.fc1.bias, h)
         f = F.dwconv(store, blk.mlp.dwconv.dwconv, f, G * B, B, H, W, "gelu")
-        return F.glinear(store, blk.mlp.fc2.weight, blk.mlp.fc2.bias, f, res=x, rscale=s_mlp, rps=N)
+        tap_m = F.GradTap() if s_mlp is not None else None
+        x = F.glinear(store, blk.mlp.fc2.weight, blk.mlp.fc2.bias, f, res=xr, rscale=s_mlp, rps=N, tap=tap_m)
+        return x, (s_mlp, tap_m)
 
     def run(self, store, images, B, H, W, training, dp_scales: Optional[torch.Tensor], bn_group=None):
         """images: (2*B, 3, H, W) fp32 NCHW (RGB batch then X batch).
@@ -157,13 +167,16 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
             x, Ho, Wo = F.conv(store, pe.proj, x, G, G * B, Hc, Wc, Cin, pe.stride, pe.pad, nchw=(s == 0))
             x = F.layernorm(store, pe.norm, x, G)
             Hc, Wc, Cin = Ho, Wo, self.embed_dims[s]
+            prev = (None, None)
             for i, blk in enumerate(getattr(self, f"block{s + 1}")):
                 sa = sm = None
                 if dp_scales is not None:
                     sa, sm = dp_scales[bi, 0], dp_scales[bi, 1]
-                x = self.run_block(store, blk, x, B, Hc, Wc, sa, sm)
+                x, prev = self.run_block(store, blk, x, B, Hc, Wc, sa, sm, prev)
                 bi += 1
-            x = F.layernorm(store, getattr(self, f"norm{s + 1}"), x, G)
+            # stage norm: its backward also writes the last block's DropPath-scaled gradient
+            x, _, _ = F.layernorm_res(store, getattr(self, f"norm{s + 1}"), x, G, scale=prev[0], rps=Hc * Wc,
+                                      tap=prev[1])
             C = self.embed_dims[s]
             r = F.frm(store, self.FRMs[s], x.view(G, B, Hc * Wc, C))
             outs.append(self.FFMs[s].run(store, r, B, Hc, Wc, training))
