@@ -40,6 +40,7 @@
 #include "cmx_mfma.h"
 #include "cmx_dma.h"
 #include <string.h>
+#include <stdlib.h>
 
 namespace {
 
@@ -758,13 +759,37 @@ bool fast_ok(const void* A, const void* A2, const void* B, int M, int N, int K, 
 
 int tile_dim(int n) { return n <= 64 ? 64 : 128; }
 
+// Tile policy of the bf16 path (CMX_GEMM_TILES=0 restores the 128-wide-first policy, for A/B
+// measurements).  Policy 1: when 128-wide tiles leave the chip under-filled (< 240 tiles),
+// take 64 x 64 tiles -- 4x the tiles, a lighter per-block k-loop and no split-K combine --
+// and split K only when even those leave it under-filled.
+int tile_policy() {
+  static const int p = [] {
+    const char* e = getenv("CMX_GEMM_TILES");
+    return e ? atoi(e) : 1;
+  }();
+  return p;
+}
+
+void plan_tiles(int G, int M, int nb, int* bm, int* bn) {
+  *bm = tile_dim(M);
+  *bn = tile_dim(nb);
+  if (tile_policy() == 1) {
+    const long t128 = (long)cdiv(M, *bm) * cdiv(nb, *bn) * G;
+    if (t128 < 240) *bm = *bn = 64;
+  }
+}
+
 // split factor for the bf16 path: one block per CU when the output has few tiles (each split
 // keeps >= 4 k-tiles of 64; the slabs cost 8 B of HBM traffic per output element and split)
 int auto_split(int G, int M, int N, int K, int ones_col) {
   const int nb = ones_col ? N - 1 : N;
-  const long tiles = (long)cdiv(M, tile_dim(M)) * cdiv(nb, tile_dim(nb)) * G;
+  int bm, bn;
+  plan_tiles(G, M, nb, &bm, &bn);
+  const long tiles = (long)cdiv(M, bm) * cdiv(nb, bn) * G;
   const int nk = (K + FBK - 1) / FBK;
-  if (tiles >= 200 || nk < 8) return 1;
+  const long full = tile_policy() == 1 ? 128 : 200;
+  if (tiles >= full || nk < 8) return 1;
   long s = (256 + tiles - 1) / tiles;
   s = s < nk / 4 ? s : nk / 4;
   if (s > 128) s = 128;
@@ -835,7 +860,8 @@ int cmx_gemm(const void* A, const void* A2, const void* B, void* C, const float*
   splitk = (nk + a.kt_per_split - 1) / a.kt_per_split;      // no empty splits
   a.nsplit = splitk;
   if (fast) {
-    const int bm = tile_dim(M), bn = tile_dim(nb);
+    int bm, bn;
+    plan_tiles(G, M, nb, &bm, &bn);
     a.tiles_m = cdiv(M, bm); a.tiles_n = cdiv(nb, bn);
     if (bm == 64 && bn == 64) launch_bf16_ns<64, 64>(a, G, splitk, transA, transB, s);
     else if (bm == 64) launch_bf16_ns<64, 128>(a, G, splitk, transA, transB, s);
