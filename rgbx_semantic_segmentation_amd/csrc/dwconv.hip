@@ -346,15 +346,26 @@ __device__ __forceinline__ Tile2 tile2_of(int CB, int ipg, int tiles_x, int tile
 
 // stage a (RY x RX)-pixel region with origin (y0, x0) of image `base` (channels cb0..cb0+CB)
 // into img[cg][px][8]; zeros outside the image
+// Two phases, unrolled: every global load of the thread is issued before the first LDS store,
+// so the region costs one memory latency instead of one per 256-item round (the stores would
+// otherwise order each round's load after the previous round's LDS write).
 template <typename T, int CB, int RY_, int RX_>
 __device__ __forceinline__ void stage_region(const T* __restrict__ base, T* img, int y0, int x0, int H, int W, int C) {
   constexpr int NCG = CB / 8, NPX = RY_ * RX_;
-  for (int it = threadIdx.x; it < NCG * NPX; it += 256) {
+  constexpr int ITER = (NCG * NPX + 255) / 256;
+  V8<T> v[ITER];
+#pragma unroll
+  for (int k = 0; k < ITER; ++k) {
+    const int it = threadIdx.x + k * 256;
     const int cg = it % NCG, px = it / NCG;
     const int y = y0 + px / RX_, x = x0 + px % RX_;
-    V8<T> v = v8_zero<T>();
-    if (y >= 0 && y < H && x >= 0 && x < W) v = v8_load<T>(base + ((long)y * W + x) * C + cg * 8);
-    v8_store<T>(img + (cg * NPX + px) * 8, v);
+    v[k] = v8_zero<T>();
+    if (it < NCG * NPX && y >= 0 && y < H && x >= 0 && x < W) v[k] = v8_load<T>(base + ((long)y * W + x) * C + cg * 8);
+  }
+#pragma unroll
+  for (int k = 0; k < ITER; ++k) {
+    const int it = threadIdx.x + k * 256;
+    if (it < NCG * NPX) v8_store<T>(img + ((it % NCG) * NPX + it / NCG) * 8, v[k]);
   }
 }
 

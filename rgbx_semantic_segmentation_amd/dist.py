@@ -17,13 +17,98 @@ class GradAllReduce:
     """Callable used by FusedAdamW.step(): all-reduce(SUM) the flat gradient buffer and
     return the scale (1/world) the optimizer applies."""
 
-    def __init__(self, store, group=None):
+    def __init__(self, store, group=None, overlap=None):
+        import os
         self.store = store
         self.group = group
-        self.world = dist.get_world_size(group)
+        self.world = self._world()
+        # CMX_DP_OVERLAP=0: one blocking all-reduce per segment at optimizer time (no overlap)
+        self.overlap = (os.environ.get("CMX_DP_OVERLAP", "1") == "1") if overlap is None else overlap
 
     def __call__(self, flat_grad: torch.Tensor) -> float:
         dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=self.group)
+        return 1.0 / self.world
+
+
+class BucketedGradSync:
+    """Gradient all-reduce overlapped with the backward pass (the DDP reducer's bucketed
+    overlap, train.py:145-146, restated for the flat ParamStore).
+
+    The store lays parameters out by backward-completion segment (models.builder.
+    backward_segment): decode head + stage 4, stage 3, stage 2, stage 1.  When the backward
+    has passed a stage's patch embed (a tensor hook on that stage's input), the segment's
+    queued weight gradients are flushed (deferred.flush) and its contiguous gradient range
+    is all-reduced asynchronously (RCCL on the process group's own stream) while the
+    backward of the earlier stages continues.  The last segment goes at the end of the
+    backward.  ``__call__`` (from FusedAdamW.step) makes the current stream wait for every
+    outstanding all-reduce and returns the 1/P scale the AdamW kernel applies."""
+
+    def __init__(self, store, group=None, overlap=None):
+        import os
+        self.store = store
+        self.group = group
+        self.world = self._world()
+        # CMX_DP_OVERLAP=0: one blocking all-reduce per segment at optimizer time (no overlap)
+        self.overlap = (os.environ.get("CMX_DP_OVERLAP", "1") == "1") if overlap is None else overlap
+        self.ranges = {sid: (a, b) for sid, a, b in store.segments}
+        self.works = []
+        self.launched = set()
+        self._armed = False
+        self.side = None
+
+    def _launch(self, sid):
+        """Flush the queued gradient work, then all-reduce segment ``sid`` on the side stream:
+        the side stream waits for the backward so far, the blocking all-reduce blocks only the
+        side stream, and the main stream runs on.  (A plain stream fork/join, so it is also
+        captured into the step's HIP graph; async_op works are not capture-safe here.)"""
+        from . import deferred
+        if sid in self.launched or sid not in self.ranges:
+            return
+        deferred.flush()
+        a, b = self.ranges[sid]
+        main = torch.cuda.current_stream() if self.store.grad.is_cuda else None
+        if main is None:                         # CPU tensors (gloo tests): blocking, in order
+            self._reduce(self.store.grad[a:b])
+        else:
+            if self.side is None:
+                self.side = torch.cuda.Stream(device=main.device)
+            self.side.wait_stream(main)
+            with torch.cuda.stream(self.side):
+                self._reduce(self.store.grad[a:b])
+            self.works.append(self.side)
+        self.launched.add(sid)
+
+    def _world(self) -> int:
+        return dist.get_world_size(self.group)
+
+    def _reduce(self, seg: torch.Tensor) -> None:
+        dist.all_reduce(seg, op=dist.ReduceOp.SUM, group=self.group)
+
+    def _finish_backward(self):
+        self._armed = False
+        for sid in sorted(self.ranges):
+            self._launch(sid)
+
+    def segment_hook(self, sid):
+        """Tensor hook: the backward is past segment ``sid`` (and every earlier segment)."""
+        def hook(grad):
+            if not self.overlap:
+                return None
+            if not self._armed:
+                self._armed = True
+                torch.autograd.Variable._execution_engine.queue_callback(self._finish_backward)
+            for s in sorted(self.ranges):
+                if s <= sid:
+                    self._launch(s)
+            return None
+        return hook
+
+    def __call__(self, flat_grad: torch.Tensor) -> float:
+        for sid in sorted(self.ranges):       # whatever the backward's hooks / callback did not launch
+            self._launch(sid)
+        if self.works:
+            torch.cuda.current_stream().wait_stream(self.side)
+        self.works, self.launched = [], set()
         return 1.0 / self.world
 
 

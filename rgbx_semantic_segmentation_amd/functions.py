@@ -200,6 +200,7 @@ class LayerNormResF(Function):
         y, mean, rstd = K.layernorm_fwd(x, gamma, beta, eps, G=G)
         ctx.save_for_backward(x, gamma, mean, rstd)
         ctx.meta = (gg, bg, G, scale, rps, tap)
+        ctx.set_materialize_grads(False)     # unused outputs arrive as None, not zero-filled tensors
         # y twice (a view for the second consumer, so its gradient arrives separately) and x
         return y, y.view_as(y), x
 

@@ -48,6 +48,22 @@ def _get(cfg, name, default):
     return getattr(cfg, name, default)
 
 
+def backward_segment(name: str) -> int:
+    """Backward-completion segment of a parameter: 0 = decode head + stage 4 (done first),
+    1 = stage 3, 2 = stage 2, 3 = stage 1.  A stage's patch embed, blocks, norm, FRM and FFM
+    all have their final gradients once the backward has passed that stage's patch embed."""
+    import re
+    if name.startswith("decode_head.") or name.startswith("aux_head."):
+        return 0
+    m = re.match(r"backbone\.(?:extra_)?(?:patch_embed|block|norm)(\d)\.", name)
+    if m:
+        return 4 - int(m.group(1))
+    m = re.match(r"backbone\.(?:FRMs|FFMs)\.(\d)\.", name)
+    if m:
+        return 3 - int(m.group(1))
+    return 0
+
+
 class EncoderDecoder(nn.Module):
     def __init__(self, cfg=None, criterion=None, norm_layer=nn.BatchNorm2d):
         super().__init__()
@@ -117,7 +133,8 @@ class EncoderDecoder(nn.Module):
         if self.store is None:
             self.store = ParamStore(self, device, self.compute_dtype,
                                     conv_pad={"backbone.patch_embed1.proj.weight": PE1_KPAD,
-                                              "backbone.extra_patch_embed1.proj.weight": PE1_KPAD})
+                                              "backbone.extra_patch_embed1.proj.weight": PE1_KPAD},
+                                    segment_of=backward_segment)
         from .. import deferred
         deferred.reserve()          # pinned launch-record tables for captured backward passes
         return self

@@ -162,8 +162,13 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
         outs, grids = [], []
         bi = 0
         Hc, Wc, Cin = H, W, 3
+        sync = getattr(self, "grad_sync", None)     # dist.BucketedGradSync (data parallel) or None
         for s in range(4):
             pe = getattr(self, f"patch_embed{s + 1}")
+            if sync is not None and s > 0 and x.requires_grad:
+                # the gradient of this stage's input exists once the backward has passed the
+                # stage (segment 3 - s): its gradients can be all-reduced while stages < s run
+                x.register_hook(sync.segment_hook(3 - s))
             x, Ho, Wo = F.conv(store, pe.proj, x, G, G * B, Hc, Wc, Cin, pe.stride, pe.pad, nchw=(s == 0))
             x = F.layernorm(store, pe.norm, x, G)
             Hc, Wc, Cin = Ho, Wo, self.embed_dims[s]

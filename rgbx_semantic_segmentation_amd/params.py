@@ -58,7 +58,11 @@ class Slot:
 
 class ParamStore:
     def __init__(self, model: nn.Module, device, compute_dtype=torch.float32,
-                 conv_pad: Dict[str, int] | None = None):
+                 conv_pad: Dict[str, int] | None = None, segment_of=None):
+        """segment_of(name) -> int: optional backward-completion segment of each parameter.
+        The flat buffers are laid out segment by segment (0 first), so each segment's
+        gradients form ONE contiguous range (``self.segments``) that the data-parallel
+        gradient exchange can all-reduce as soon as that part of the backward is done."""
         self.device = torch.device(device)
         self.compute_dtype = compute_dtype
         conv_pad = conv_pad or {}
@@ -78,9 +82,14 @@ class ParamStore:
         placed = set()
         off = 0
         order: List[Tuple[str, int]] = []
-        for name, p in named:
+        seg_of = segment_of or (lambda n: 0)
+        placement = sorted(named, key=lambda kv: seg_of(kv[0]))      # stable: module order within a segment
+        seg_bounds: Dict[int, List[int]] = {}
+        for name, p in placement:
             if name in placed:
                 continue
+            sid = seg_of(name)
+            seg_bounds.setdefault(sid, [off, off])
             pn = partner_name(name)
             group = [name] + ([pn] if pn and pn in by_name and pn not in placed else [])
             kind, sshape = self._storage(name, p, conv_pad)
@@ -97,7 +106,10 @@ class ParamStore:
                 self.slots[n] = Slot(n, off, stride, len(group), i, sshape, kind, id(by_name[n]) in decay_ids)
                 placed.add(n)
             off += _pad(stride * len(group))
+            seg_bounds[sid][1] = off
         self.numel = off
+        # [(segment id, start, end)] in element offsets, in layout order
+        self.segments = [(sid, b[0], b[1]) for sid, b in sorted(seg_bounds.items())]
         self.flat = torch.zeros(off, dtype=torch.float32, device=self.device)
         self.grad = torch.zeros(off, dtype=torch.float32, device=self.device)
         self.shadow = (torch.zeros(off, dtype=torch.bfloat16, device=self.device)

@@ -49,6 +49,18 @@ def _worker(rank, world, port, q):
         ok2 = count == world * 7 and torch.allclose(mean, feats.mean(0)) and torch.allclose(var, feats.var(0, unbiased=False))
         loss = all_reduce_tensor(torch.tensor([float(rank)]), world_size=world)
         ok3 = abs(loss.item() - (world - 1) / 2) < 1e-12
+        # segment-bucketed overlap: launching segments out of order / in pieces, then waiting,
+        # equals one all-reduce of the whole flat buffer
+        from rgbx_semantic_segmentation_amd.dist import BucketedGradSync
+        st2 = Store()
+        st2.grad = torch.arange(23, dtype=torch.float32) * (rank + 1)
+        st2.segments = [(0, 0, 9), (1, 9, 16), (2, 16, 23)]
+        bs = BucketedGradSync(st2, None)
+        bs._launch(1)
+        bs._launch(0)
+        sc = bs(st2.grad)          # launches the rest, waits
+        ok3 = ok3 and sc == 1.0 / world and torch.equal(st2.grad, torch.arange(23, dtype=torch.float32) * sum(
+            r + 1 for r in range(world))) and not bs.works
         q.put((rank, bool(ok1), bool(ok2), bool(ok3)))
     finally:
         dist.destroy_process_group()

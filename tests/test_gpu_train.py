@@ -28,3 +28,44 @@ def test_train_loop_and_resume(dev, tmp_path, monkeypatch):
     # (lr 1e-4: at 1e-3 AdamW overshoots on these random labels and epoch 2 rises even uninterrupted)
     l2 = train.main(base + ["--nepochs", "2", "-c", str(ck)])
     assert l2 < l1, (l1, l2)
+
+
+@pytest.mark.gpu
+def test_segment_allreduce_sees_final_gradients(dev):
+    """The overlapped gradient exchange (dist.BucketedGradSync) must reduce each segment only
+    after every gradient in it is final.  World-size-1 rehearsal: the "all-reduce" doubles its
+    segment on the side stream; any gradient written after its segment was launched stays
+    undoubled and shows up against 2x the gradients of a plain backward."""
+    from rgbx_semantic_segmentation_amd.dist import BucketedGradSync
+    from rgbx_semantic_segmentation_amd.models.builder import EncoderDecoder
+
+    class Doubling(BucketedGradSync):
+        def _world(self):
+            return 1
+
+        def _reduce(self, seg):
+            seg.mul_(2.0)
+
+    torch.manual_seed(0)
+    model = EncoderDecoder(dict(backbone="mit_b0", num_classes=9, compute_dtype="bfloat16",
+                                decoder_embed_dim=256)).to(dev)
+    model.eval()                        # deterministic (no DropPath / Dropout2d randomness)
+    g = torch.Generator().manual_seed(3)
+    rgb = torch.randn(2, 3, 64, 96, generator=g).to(dev)
+    x = torch.randn(2, 3, 64, 96, generator=g).to(dev)
+    lab = torch.randint(0, 9, (2, 64, 96), generator=g).to(dev)
+    assert len(model.store.segments) == 4, model.store.segments
+    model(rgb, x, lab).backward()
+    torch.cuda.synchronize()
+    ref = model.store.grad.clone()
+    sync = Doubling(model.store, None)
+    model.backbone.grad_sync = sync
+    try:
+        model(rgb, x, lab).backward()
+        assert sync.launched, "no segment was launched during the backward"
+        assert sync(model.store.grad) == 1.0
+    finally:
+        model.backbone.grad_sync = None
+    torch.cuda.synchronize()
+    bad = (model.store.grad - 2 * ref).abs() > 1e-6 * (1 + ref.abs())
+    assert not bad.any(), f"{int(bad.sum())} gradient elements were reduced before they were final"

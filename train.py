@@ -88,7 +88,8 @@ def main(argv=None):
             group = torch.distributed.group.WORLD
             model.process_group = group
             cdist.broadcast_parameters(model, group)
-            sync = cdist.GradAllReduce(model.store, group)
+            sync = cdist.BucketedGradSync(model.store, group)
+            model.backbone.grad_sync = sync    # segment all-reduces overlap the backward
         optimizer = FusedAdamW(model, lr=args.lr, betas=(0.9, 0.999), weight_decay=args.weight_decay,
                                grad_sync=sync)
         total_iteration = args.nepochs * args.niters_per_epoch
