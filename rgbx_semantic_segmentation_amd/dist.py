@@ -17,13 +17,10 @@ class GradAllReduce:
     """Callable used by FusedAdamW.step(): all-reduce(SUM) the flat gradient buffer and
     return the scale (1/world) the optimizer applies."""
 
-    def __init__(self, store, group=None, overlap=None):
-        import os
+    def __init__(self, store, group=None):
         self.store = store
         self.group = group
-        self.world = self._world()
-        # CMX_DP_OVERLAP=0: one blocking all-reduce per segment at optimizer time (no overlap)
-        self.overlap = (os.environ.get("CMX_DP_OVERLAP", "1") == "1") if overlap is None else overlap
+        self.world = dist.get_world_size(group)
 
     def __call__(self, flat_grad: torch.Tensor) -> float:
         dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=self.group)
@@ -38,10 +35,10 @@ class BucketedGradSync:
     backward_segment): decode head + stage 4, stage 3, stage 2, stage 1.  When the backward
     has passed a stage's patch embed (a tensor hook on that stage's input), the segment's
     queued weight gradients are flushed (deferred.flush) and its contiguous gradient range
-    is all-reduced asynchronously (RCCL on the process group's own stream) while the
-    backward of the earlier stages continues.  The last segment goes at the end of the
-    backward.  ``__call__`` (from FusedAdamW.step) makes the current stream wait for every
-    outstanding all-reduce and returns the 1/P scale the AdamW kernel applies."""
+    is all-reduced on a side stream (RCCL) while the backward of the earlier stages
+    continues.  The last segment goes at the end of the backward.  ``__call__`` (from
+    FusedAdamW.step) joins the side stream into the current one and returns the 1/P scale
+    the AdamW kernel applies."""
 
     def __init__(self, store, group=None, overlap=None):
         import os
