@@ -377,25 +377,46 @@ __global__ __launch_bounds__(256) void sra_bwd_dkv_kernel(
   }
 }
 
-// dk/dv[(b*Nk + key)*kvs + head*D + d] = sum_c slab[c][b][head][key][d]
+// dk/dv[(b*Nk + key)*kvs + head*D + d] = sum_c slab[c][b][head][key][d].  A thread owns 4
+// consecutive d (16-B loads) and every 4th chunk; the 4 chunk slices meet in LDS (a single
+// thread walking up to 64 chunks serially was latency-bound).
 template <typename T>
-__global__ void sra_dkv_reduce_kernel(const float* __restrict__ ws_dk, const float* __restrict__ ws_dv,
-                                      T* __restrict__ dk, T* __restrict__ dv, int Bt, int Nk, int heads,
-                                      int D, long kvs, int nchunk) {
+__global__ __launch_bounds__(256) void sra_dkv_reduce_kernel(const float* __restrict__ ws_dk,
+                                                             const float* __restrict__ ws_dv, T* __restrict__ dk,
+                                                             T* __restrict__ dv, int Bt, int Nk, int heads, int D,
+                                                             long kvs, int nchunk) {
+  __shared__ float4 red[3][64][2];
   const long total = (long)Bt * heads * Nk * D;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)total; i += gridDim.x * blockDim.x) {
-    const int d = i % D;
-    const int key = (i / D) % Nk;
-    const int head = (i / (D * Nk)) % heads;
-    const int b = i / (D * Nk * heads);
-    float sk = 0.f, sv = 0.f;
-    for (int c = 0; c < nchunk; ++c) {
-      sk += ws_dk[(long)c * total + i];
-      sv += ws_dv[(long)c * total + i];
+  const int gl = threadIdx.x & 63, zl = threadIdx.x >> 6;
+  const long i = ((long)blockIdx.x * 64 + gl) * 4;
+  float4 sk = make_float4(0.f, 0.f, 0.f, 0.f), sv = sk;
+  if (i < total) {
+    for (int c = zl; c < nchunk; c += 4) {
+      const float4 a = *reinterpret_cast<const float4*>(ws_dk + (long)c * total + i);
+      const float4 b = *reinterpret_cast<const float4*>(ws_dv + (long)c * total + i);
+      sk.x += a.x; sk.y += a.y; sk.z += a.z; sk.w += a.w;
+      sv.x += b.x; sv.y += b.y; sv.z += b.z; sv.w += b.w;
     }
-    const long oo = ((long)b * Nk + key) * kvs + head * D + d;
-    dk[oo] = from_f32<T>(sk);
-    dv[oo] = from_f32<T>(sv);
+  }
+  if (zl > 0) { red[zl - 1][gl][0] = sk; red[zl - 1][gl][1] = sv; }
+  __syncthreads();
+  if (zl > 0 || i >= total) return;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const float4 a = red[q][gl][0], b = red[q][gl][1];
+    sk.x += a.x; sk.y += a.y; sk.z += a.z; sk.w += a.w;
+    sv.x += b.x; sv.y += b.y; sv.z += b.z; sv.w += b.w;
+  }
+  const int d = (int)(i % D);
+  const int key = (int)((i / D) % Nk);
+  const int head = (int)((i / ((long)D * Nk)) % heads);
+  const int b = (int)(i / ((long)D * Nk * heads));
+  const long oo = ((long)b * Nk + key) * kvs + head * D + d;
+  const float kk[4] = {sk.x, sk.y, sk.z, sk.w}, vv[4] = {sv.x, sv.y, sv.z, sv.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    dk[oo + e] = from_f32<T>(kk[e]);
+    dv[oo + e] = from_f32<T>(vv[e]);
   }
 }
 
@@ -422,6 +443,10 @@ void sra_fwd_fast_launch(const void* q, const void* k, const void* v, void* o, f
 void sra_dq_fast_launch(const void* q, const void* k, const void* v, const void* o, const void* dout,
                         const float* lse, float* Dws, void* dq, int Bt, int N, int Nk, int heads, long qs, long kvs,
                         long os, long dos, long dqs, float sl2, float scale, hipStream_t s);
+int sra_dkv_fast_chunks(int Bt, int N, int heads);
+void sra_dkv_fast_launch(const void* q, const void* k, const void* v, const void* dout, const float* lse,
+                         const float* Dws, float* ws_dk, float* ws_dv, int Bt, int N, int Nk, int heads, long qs,
+                         long kvs, long dos, int nchunk, float sl2, float scale, hipStream_t s);
 
 #define SRA_D_DISPATCH(D, ...)                                              \
   do {                                                                      \
@@ -456,7 +481,9 @@ int cmx_sra_attn_fwd(const void* q, const void* k, const void* v, void* o, float
 }
 
 size_t cmx_sra_attn_bwd_workspace(int Bt, int N, int Nk, int heads, int D) {
-  const int nc = bwd_nchunk(Bt, N, Nk, heads);
+  int nc = bwd_nchunk(Bt, N, Nk, heads);
+  const int ncf = sra_dkv_fast_chunks(Bt, N, heads);   // the bf16 fast path may take either
+  if (ncf > nc) nc = ncf;
   const size_t slab = (size_t)nc * Bt * heads * Nk * D;
   return ((size_t)Bt * heads * N + 2 * slab) * sizeof(float);
 }
@@ -469,14 +496,14 @@ int cmx_sra_attn_bwd(const void* q, const void* k, const void* v, const void* o,
   CMX_REQUIRE(qs % 8 == 0 && kvs % 8 == 0 && os % 8 == 0 && dos % 8 == 0 && dqs % 8 == 0 && dkvs % 8 == 0,
               CMX_ERR_SHAPE, "sra_bwd: strides %% 8");
   const float sl2 = scale * 1.4426950408889634f;
-  const int nc = bwd_nchunk(Bt, N, Nk, heads);
+  const void* ptrs[] = {q, k, v, o, dout, dq};
+  const long strides[] = {qs, kvs, os, dos, dqs};
+  const bool fast = sra_fast_ok(D, Nk, dtype, ptrs, 6, strides, 5);
+  const int nc = fast ? sra_dkv_fast_chunks(Bt, N, heads) : bwd_nchunk(Bt, N, Nk, heads);
   const int qc = bwd_qc(N, nc);
   float* Dws = workspace;
   float* ws_dk = Dws + (size_t)Bt * heads * N;
   float* ws_dv = ws_dk + (size_t)nc * Bt * heads * Nk * D;
-  const void* ptrs[] = {q, k, v, o, dout, dq};
-  const long strides[] = {qs, kvs, os, dos, dqs};
-  const bool fast = sra_fast_ok(D, Nk, dtype, ptrs, 6, strides, 5);
   SRA_D_DISPATCH(D, CMX_DISPATCH(dtype, T, {
     if (fast)
       sra_dq_fast_launch(q, k, v, o, dout, lse, Dws, dq, Bt, N, Nk, heads, qs, kvs, os, dos, dqs, sl2, scale, s);
@@ -484,12 +511,15 @@ int cmx_sra_attn_bwd(const void* q, const void* k, const void* v, const void* o,
       hipLaunchKernelGGL((sra_bwd_dq_kernel<T, DD>), dim3(cdiv(N, BQ), heads, Bt), dim3(256), 0, s,
                          (const T*)q, (const T*)k, (const T*)v, (const T*)o, (const T*)dout, lse, Dws,
                          (T*)dq, N, Nk, heads, qs, kvs, os, dos, dqs, sl2, scale);
-    hipLaunchKernelGGL((sra_bwd_dkv_kernel<T, DD>), dim3(cdiv(Nk, BK), heads, Bt * nc), dim3(256), 0, s,
-                       (const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse, Dws, ws_dk, ws_dv, Bt,
-                       N, Nk, heads, qs, kvs, dos, qc, nc, sl2, scale);
-    const long total = (long)Bt * heads * Nk * D;
-    hipLaunchKernelGGL((sra_dkv_reduce_kernel<T>), dim3(cdiv(total, 256) < 4096 ? cdiv(total, 256) : 4096),
-                       dim3(256), 0, s, ws_dk, ws_dv, (T*)dk, (T*)dv, Bt, Nk, heads, D, dkvs, nc);
+    if (fast)
+      sra_dkv_fast_launch(q, k, v, dout, lse, Dws, ws_dk, ws_dv, Bt, N, Nk, heads, qs, kvs, dos, nc, sl2, scale, s);
+    else
+      hipLaunchKernelGGL((sra_bwd_dkv_kernel<T, DD>), dim3(cdiv(Nk, BK), heads, Bt * nc), dim3(256), 0, s,
+                         (const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse, Dws, ws_dk, ws_dv, Bt,
+                         N, Nk, heads, qs, kvs, dos, qc, nc, sl2, scale);
+    const long total = (long)Bt * heads * Nk * D;     // D % 4 == 0: 4-wide groups never straddle a row
+    hipLaunchKernelGGL((sra_dkv_reduce_kernel<T>), dim3(cdiv(total / 4, 64)), dim3(256), 0, s, ws_dk, ws_dv, (T*)dk,
+                       (T*)dv, Bt, Nk, heads, D, dkvs, nc);
   }));
   return cmx_check_launch("sra_bwd");
 }

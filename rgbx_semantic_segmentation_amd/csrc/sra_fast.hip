@@ -297,6 +297,137 @@ __global__ __launch_bounds__(64 * NWAVE) void sra_dq_fast(const bf16* __restrict
   }
 }
 
+
+// ------------------------------------------------------------------------ backward: dK, dV
+// Key on the lane: a workgroup owns ALL keys of one (b, head) (wave w: keys 64w .. 64w + 63,
+// their K and V fragments in registers) and sweeps a chunk of queries in 64-query tiles.  The
+// Q / dO tiles (+ lse, Dq) are staged ONCE per workgroup by LDS-DMA into a double buffer and
+// shared by every wave (the generic kernel re-staged them per 128-key workgroup).  Per tile
+// and key sub-tile: S and dP (8 MFMA), P and dS on the VALU, dV^T += dO^T P and
+// dK^T += Q^T dS (8 MFMA, the accumulators fed back as B operands).  Partial dK / dV of the
+// chunk go to the fp32 slab sra_dkv_reduce_kernel folds (same layout as the generic path).
+__device__ __forceinline__ void dma4(const i32x4 rsrc, uint32_t lds, int voffset) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds"
+               :: "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voffset), "s"(rsrc) : "memory");
+}
+
+constexpr int QT = 64;                          // queries per tile
+constexpr int DKV_TILE_BYTES = 2 * QT * ROWB + 2 * QT * 4;   // Q, dO images + lse, Dq
+
+__global__ __launch_bounds__(64 * (NKP_MAX / 32)) void sra_dkv_fast(
+    const bf16* __restrict__ q, const bf16* __restrict__ k, const bf16* __restrict__ v, const bf16* __restrict__ dout,
+    const float* __restrict__ lse, const float* __restrict__ Dws, float* __restrict__ ws_dk, float* __restrict__ ws_dv,
+    int Bt, int N, int Nk, int heads, long qs, long kvs, long dos, int QC, int nchunk, float sl2, float scale) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * DKV_TILE_BYTES];
+  const int nw = blockDim.x >> 6;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int head = blockIdx.y, b = blockIdx.z, c = blockIdx.x;
+  const int qbeg = c * QC, qend = min(N, qbeg + QC);
+  const long sbase = ((long)b * heads + head) * N;
+  const i32x4 rq = make_rsrc(q + (long)b * N * qs + head * HD);
+  const i32x4 rd = make_rsrc(dout + (long)b * N * dos + head * HD);
+  const i32x4 rl = make_rsrc(lse + sbase);
+  const i32x4 rD = make_rsrc(Dws + sbase);
+
+  // DMA of query tile [q0, q0 + 64): 8 Q + 8 dO row-groups (1 KB each) + lse + Dq, round-robin
+  auto issue = [&](int q0, char* buf) {
+    for (int j = wave; j < 18; j += nw) {
+      if (j < 16) {
+        const int row = (j & 7) * 8 + (lane >> 3), cc = (lane & 7) ^ swz(row);
+        const int gq = q0 + row;
+        if (j < 8) {
+          const int off = gq < qend ? (int)(((long)gq * qs + cc * 8) * 2) : OOB;
+          dma16(rq, lds_addr(buf + j * 1024), off);
+        } else {
+          const int off = gq < qend ? (int)(((long)gq * dos + cc * 8) * 2) : OOB;
+          dma16(rd, lds_addr(buf + QT * ROWB + (j - 8) * 1024), off);
+        }
+      } else {
+        const int gq = q0 + lane;
+        const int off = gq < qend ? gq * 4 : OOB;
+        if (j == 16) dma4(rl, lds_addr(buf + 2 * QT * ROWB), off);
+        else dma4(rD, lds_addr(buf + 2 * QT * ROWB + QT * 4), off);
+      }
+    }
+  };
+
+  // this wave's 32 keys: K, V fragments as B operands (k = d), lane = key
+  const int key = 32 * wave + r;
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (key < Nk) {
+      kf[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(k + ((long)b * Nk + key) * kvs + head * HD + 16 * s + 8 * h));
+      vf[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(v + ((long)b * Nk + key) * kvs + head * HD + 16 * s + 8 * h));
+    } else {
+      kf[s] = vf[s] = zfrag<bf16>();
+    }
+  }
+  f32x16 ak[2], av[2];
+  ak[0] = ak[1] = av[0] = av[1] = zero16();
+
+  if (qbeg < qend) issue(qbeg, smem);
+  vm_wait<0>();
+  __syncthreads();
+  int cur = 0;
+  for (int q0 = qbeg; q0 < qend; q0 += QT) {
+    if (q0 + QT < qend) issue(q0 + QT, smem + (cur ^ 1) * DKV_TILE_BYTES);
+    const char* Qi = smem + cur * DKV_TILE_BYTES;
+    const char* Di = Qi + QT * ROWB;
+    const float* ls = reinterpret_cast<const float*>(Qi + 2 * QT * ROWB);
+    const float* Ds = ls + QT;
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const int qb = 32 * qt;
+      f32x16 sa = zero16(), dp = zero16();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_k(Qi, qb, s, lane), kf[s], sa, 0, 0, 0);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_k(Di, qb, s, lane), vf[s], dp, 0, 0, 0);
+      const bool tail = q0 + qb + 32 > qend;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 l4 = *reinterpret_cast<const float4*>(ls + qb + 8 * g4 + 4 * h);
+        const float4 d4 = *reinterpret_cast<const float4*>(Ds + qb + 8 * g4 + 4 * h);
+        const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * g4 + e;
+          float p = fexp2(fmaf(sa[i], sl2, -lv[e] * 1.4426950408889634f));
+          if (tail && q0 + qb + accrow(i, h) >= qend) p = 0.f;
+          sa[i] = p;
+          dp[i] = p * (dp[i] - dv[e]);
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pf = MF<bf16>::from_acc(sa, s);
+        const bf16x8 sf = MF<bf16>::from_acc(dp, s);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          av[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_t(Di, qb, 32 * t, s, lane), pf, av[t], 0, 0, 0);
+          ak[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_t(Qi, qb, 32 * t, s, lane), sf, ak[t], 0, 0, 0);
+        }
+      }
+    }
+    vm_wait<0>();
+    __syncthreads();
+    cur ^= 1;
+  }
+  if (key >= Nk) return;
+  const long o = ((((long)c * Bt + b) * heads + head) * Nk + key) * HD;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = 32 * t + 8 * g4 + 4 * h;
+      *reinterpret_cast<float4*>(ws_dk + o + d) = make_float4(ak[t][4 * g4] * scale, ak[t][4 * g4 + 1] * scale,
+                                                              ak[t][4 * g4 + 2] * scale, ak[t][4 * g4 + 3] * scale);
+      *reinterpret_cast<float4*>(ws_dv + o + d) = make_float4(av[t][4 * g4], av[t][4 * g4 + 1], av[t][4 * g4 + 2],
+                                                              av[t][4 * g4 + 3]);
+    }
+}
+
 int pick_qw(int N, int heads, int Bt) {
   const long wg2 = (long)cdiv(N, 64 * NWAVE) * heads * Bt;   // workgroups at 2 sub-tiles per wave
   return wg2 >= 512 ? 2 : 1;
@@ -341,4 +472,25 @@ void sra_dq_fast_launch(const void* q, const void* k, const void* v, const void*
     hipLaunchKernelGGL(sra_dq_fast<1>, grid, dim3(64 * NWAVE), 0, s, (const bf16*)q, (const bf16*)k, (const bf16*)v,
                        (const bf16*)o, (const bf16*)dout, lse, Dws, (bf16*)dq, N, Nk, nkp, heads, qs, kvs, os, dos, dqs,
                        sl2, scale);
+}
+
+// partial dK / dV slabs of the query chunks (layout of sra_attention.hip's generic path)
+int sra_dkv_fast_chunks(int Bt, int N, int heads) {
+  const long base = (long)Bt * heads;
+  long nc = (256 + base - 1) / base;              // ~one workgroup per CU
+  const long maxc = (N + QT - 1) / QT;
+  if (nc > maxc) nc = maxc;
+  if (nc > 64) nc = 64;
+  return (int)(nc < 1 ? 1 : nc);
+}
+
+void sra_dkv_fast_launch(const void* q, const void* k, const void* v, const void* dout, const float* lse,
+                         const float* Dws, float* ws_dk, float* ws_dv, int Bt, int N, int Nk, int heads, long qs,
+                         long kvs, long dos, int nchunk, float sl2, float scale, hipStream_t s) {
+  const int nkw = (Nk + 31) / 32 * 32;           // one 32-key sub-tile per wave
+  int qc = (N + nchunk - 1) / nchunk;
+  qc = (qc + QT - 1) / QT * QT;
+  hipLaunchKernelGGL(sra_dkv_fast, dim3(nchunk, heads, Bt), dim3(2 * nkw), 0, s, (const bf16*)q, (const bf16*)k,
+                     (const bf16*)v, (const bf16*)dout, lse, Dws, ws_dk, ws_dv, Bt, N, Nk, heads, qs, kvs, dos, qc,
+                     nchunk, sl2, scale);
 }
