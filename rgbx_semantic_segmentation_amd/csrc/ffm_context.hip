@@ -73,9 +73,13 @@ __global__ __launch_bounds__(256) void ctx_reduce_kernel(const T* __restrict__ X
 
 // one block per BH; thread per column j (D threads) for the softmax modes
 template <int D>
-__global__ void ctx_finalize_kernel(const float* __restrict__ slab, const float* __restrict__ ctx,
-                                    float* __restrict__ out, int nchunk, int BH, int mode, float alpha,
-                                    int swapB, int heads) {
+__global__ __launch_bounds__(256) void ctx_finalize_kernel(const float* __restrict__ slab, const float* __restrict__ ctx,
+                                                           float* __restrict__ out, int nchunk, int BH, int mode,
+                                                           float alpha, int swapB, int heads) {
+  // 256 threads: column j = tid % D, row slice rg = tid / D (256 / D slices); per-column max /
+  // sum / dot over the slices meet in LDS (one thread per column walking D rows serially, with
+  // three exp passes, took ~30 us per launch)
+  constexpr int NS = 256 / D;
   const int bh = blockIdx.x;
   int obh = bh;
   if (swapB > 0) {  // (g, b, head) -> (1 - g, b, head)
@@ -83,32 +87,50 @@ __global__ void ctx_finalize_kernel(const float* __restrict__ slab, const float*
     obh = (1 - g) * swapB * heads + rest;
   }
   __shared__ float S[D][D + 1];
-  for (int e = threadIdx.x; e < D * D; e += blockDim.x) {
-    float s = 0.f;
-    for (int c = 0; c < nchunk; ++c) s += slab[((long)c * BH + bh) * D * D + e];
-    S[e / D][e % D] = s;
+  __shared__ float red[NS][D];
+  for (int e = threadIdx.x; e < D * D; e += 256) {
+    float sm = 0.f;
+    for (int c = 0; c < nchunk; ++c) sm += slab[((long)c * BH + bh) * D * D + e];
+    S[e / D][e % D] = sm;
   }
   __syncthreads();
   float* o = out + (long)obh * D * D;
   if (mode == 0) {
-    for (int e = threadIdx.x; e < D * D; e += blockDim.x) o[e] = alpha * S[e / D][e % D];
+    for (int e = threadIdx.x; e < D * D; e += 256) o[e] = alpha * S[e / D][e % D];
     return;
   }
-  const int j = threadIdx.x;
-  if (j >= D) return;
-  if (mode == 1) {
+  const int j = threadIdx.x % D, rg = threadIdx.x / D;
+  constexpr int RPS = D / NS;                    // rows per slice
+  const int i0 = rg * RPS;
+  if (mode == 1) {                               // softmax over rows i (dim -2) of column j
     float m = -INFINITY;
-    for (int i = 0; i < D; ++i) m = fmaxf(m, alpha * S[i][j]);
+    for (int i = i0; i < i0 + RPS; ++i) m = fmaxf(m, alpha * S[i][j]);
+    red[rg][j] = m;
+    __syncthreads();
+    m = red[0][j];
+#pragma unroll
+    for (int q = 1; q < NS; ++q) m = fmaxf(m, red[q][j]);
+    __syncthreads();
     float l = 0.f;
-    for (int i = 0; i < D; ++i) l += __expf(alpha * S[i][j] - m);
+    for (int i = i0; i < i0 + RPS; ++i) l += __expf(alpha * S[i][j] - m);
+    red[rg][j] = l;
+    __syncthreads();
+    l = 0.f;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) l += red[q][j];
     const float inv = 1.f / l;
-    for (int i = 0; i < D; ++i) o[i * D + j] = __expf(alpha * S[i][j] - m) * inv;
+    for (int i = i0; i < i0 + RPS; ++i) o[i * D + j] = __expf(alpha * S[i][j] - m) * inv;
   } else {
     // S holds dctx for context obh; ctx (BH, D, D)
     const float* cx = ctx + (long)obh * D * D;
     float dot = 0.f;
-    for (int i = 0; i < D; ++i) dot += cx[i * D + j] * S[i][j];
-    for (int i = 0; i < D; ++i) o[i * D + j] = alpha * cx[i * D + j] * (S[i][j] - dot);
+    for (int i = i0; i < i0 + RPS; ++i) dot += cx[i * D + j] * S[i][j];
+    red[rg][j] = dot;
+    __syncthreads();
+    dot = 0.f;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) dot += red[q][j];
+    for (int i = i0; i < i0 + RPS; ++i) o[i * D + j] = alpha * cx[i * D + j] * (S[i][j] - dot);
   }
 }
 
@@ -216,7 +238,7 @@ int cmx_ffm_ctx_reduce(const void* X, const void* Y, const float* ctx, float* ou
                        workspace, N, heads, (long)xs, (long)ys, chunk, nc, BH);
     const int st = cmx_reduce_partials(workspace, sum, 1, nc, BH * DD * DD, 0, 1.f, s);
     if (st) return st;
-    hipLaunchKernelGGL((ctx_finalize_kernel<DD>), dim3(BH), dim3(64), 0, s, sum, ctx, out, 1, BH, mode,
+    hipLaunchKernelGGL((ctx_finalize_kernel<DD>), dim3(BH), dim3(256), 0, s, sum, ctx, out, 1, BH, mode,
                        alpha, swapB, heads);
   }));
   return cmx_check_launch("ffm_ctx_reduce");

@@ -34,25 +34,41 @@ __global__ void pool_partial_kernel(const T* __restrict__ x, float* __restrict__
   }
 }
 
-__global__ void pool_final_kernel(const float* __restrict__ psum, const float* __restrict__ pmax,
-                                  const int* __restrict__ pidx, float* __restrict__ pooled, int* __restrict__ argmax,
-                                  int B, int N, int C, int nchunk) {
-  const long total = 2L * B * C;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)total; i += gridDim.x * blockDim.x) {
-    const int c = i % C;
-    const int gb = i / C;
-    const int g = gb / B, b = gb % B;
-    float s = 0.f, m = -INFINITY;
-    int mi = 0;
-    for (int k = 0; k < nchunk; ++k) {
+// block = 64 channels x 4 chunk slices of one (group, image); the slices meet in LDS.  Max ties
+// resolve to the lowest token index, as the sequential scan over chunks would.
+__global__ __launch_bounds__(256) void pool_final_kernel(const float* __restrict__ psum, const float* __restrict__ pmax,
+                                                         const int* __restrict__ pidx, float* __restrict__ pooled,
+                                                         int* __restrict__ argmax, int B, int N, int C, int nchunk) {
+  __shared__ float rs[3][64], rm[3][64];
+  __shared__ int ri[3][64];
+  const int gb = blockIdx.y, cl = threadIdx.x & 63, zl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float sm = 0.f, m = -INFINITY;
+  int mi = 0x7fffffff;
+  if (c < C) {
+#pragma unroll 4
+    for (int k = zl; k < nchunk; k += 4) {
       const long o = ((long)gb * nchunk + k) * C + c;
-      s += psum[o];
-      if (pmax[o] > m) { m = pmax[o]; mi = pidx[o]; }
+      sm += psum[o];
+      const float v = pmax[o];
+      const int ix = pidx[o];
+      if (v > m || (v == m && ix < mi)) { m = v; mi = ix; }
     }
-    pooled[(long)b * 4 * C + g * C + c] = s / N;
-    pooled[(long)b * 4 * C + 2 * C + g * C + c] = m;
-    argmax[(long)b * 2 * C + g * C + c] = mi;
   }
+  if (zl > 0) { rs[zl - 1][cl] = sm; rm[zl - 1][cl] = m; ri[zl - 1][cl] = mi; }
+  __syncthreads();
+  if (zl > 0 || c >= C) return;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    sm += rs[q][cl];
+    const float v = rm[q][cl];
+    const int ix = ri[q][cl];
+    if (v > m || (v == m && ix < mi)) { m = v; mi = ix; }
+  }
+  const int g = gb / B, b = gb % B;
+  pooled[(long)b * 4 * C + g * C + c] = sm / N;
+  pooled[(long)b * 4 * C + 2 * C + g * C + c] = m;
+  argmax[(long)b * 2 * C + g * C + c] = mi;
 }
 
 // one wave per output feature n; M rows
@@ -328,9 +344,9 @@ unsigned gridcap(long total) {
   const unsigned g = cdiv(total, 256);
   return g < 8192 ? (g ? g : 1) : 8192;
 }
-int combine_nblk(int N, int rpb) {
+int combine_nblk(int N, int rpb) {              // <= 256 blocks per image (partials reduced after)
   int nb = (N + rpb - 1) / rpb;
-  return nb < 64 ? nb : 64;
+  return nb < 256 ? nb : 256;
 }
 int spatial_nblk(long rows) {
   long nb = (rows + 15) / 16;
@@ -362,7 +378,7 @@ int cmx_frm_pool_fwd(const void* x, float* pooled, int* argmax, float* workspace
     hipLaunchKernelGGL(pool_partial_kernel<T>, dim3(nc, 2 * B), dim3(C < 256 ? 64 * ((C + 63) / 64) : 256), 0, s,
                        (const T*)x, psum, pmax, pidx, B, N, C, chunk);
   });
-  hipLaunchKernelGGL(pool_final_kernel, dim3(gridcap(2L * B * C)), dim3(256), 0, s, psum, pmax, pidx, pooled, argmax,
+  hipLaunchKernelGGL(pool_final_kernel, dim3(cdiv(C, 64), 2 * B), dim3(256), 0, s, psum, pmax, pidx, pooled, argmax,
                      B, N, C, nc);
   return cmx_check_launch("frm_pool_fwd");
 }
@@ -442,7 +458,7 @@ int cmx_frm_combine_fwd(const void* x, const float* cw, const float* sw, void* o
 }
 
 size_t cmx_frm_combine_bwd_workspace(int B, int N, int C) {
-  return (size_t)B * combine_nblk(N, 4) * 2 * C * sizeof(float);
+  return (size_t)B * combine_nblk(N, 16) * 2 * C * sizeof(float);
 }
 
 // dx (2,B,N,C) direct path; dsw (B,N,2); dcw (B, 2C) = [dcw0 | dcw1] (overwritten)
@@ -450,11 +466,22 @@ int cmx_frm_combine_bwd(const void* dout, const void* x, const float* cw, const 
                         float* dcw, float* workspace, int B, int N, int C, int dtype, hipStream_t s) {
   const int V = dtype == 0 ? 4 : 8;
   CMX_REQUIRE(C % V == 0 && C / V <= 4 * 64, CMX_ERR_SHAPE, "frm_combine_bwd: C=%d", C);
-  const int nb = combine_nblk(N, 4);   // grid fixed to the TPR=64 row-slot count (4 rows/block)
+  const int nb = combine_nblk(N, 16);
+  // lanes per row = the row's 16-B chunks rounded up to a power of two (C = 64 bf16: 8 lanes,
+  // 32 rows per block in flight), capped at a wave
+  const int chunks = C / V;
+  int tpr = 4;
+  while (tpr < chunks && tpr < 64) tpr <<= 1;
+#define CMB(TPR) hipLaunchKernelGGL((combine_bwd_kernel<T, TPR>), dim3(nb, B), dim3(256), 0, s, (const T*)dout, \
+                                    (const T*)x, cw, sw, (T*)dx, dsw, workspace, B, N, C)
   CMX_DISPATCH(dtype, T, {
-    hipLaunchKernelGGL((combine_bwd_kernel<T, 64>), dim3(nb, B), dim3(256), 0, s, (const T*)dout, (const T*)x, cw, sw,
-                       (T*)dx, dsw, workspace, B, N, C);
+    if (tpr == 4) CMB(4);
+    else if (tpr == 8) CMB(8);
+    else if (tpr == 16) CMB(16);
+    else if (tpr == 32) CMB(32);
+    else CMB(64);
   });
+#undef CMB
   int st = cmx_check_launch("frm_combine_bwd");
   if (st) return st;
   return cmx_reduce_partials(workspace, dcw, B, nb, 2 * C, 0, 1.f, s);
