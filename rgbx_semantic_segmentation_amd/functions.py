@@ -280,6 +280,37 @@ def layernorm(store, mod, x, G):
     return LayerNormF.apply(x, gamma, beta, gg, bg, mod.eps, G, mod.weight)
 
 
+# ---------------------------------------------------------------------------- split
+class SplitF(Function):
+    """(t[..., :k] along ``dim``, the rest) as views (CrossPath's chunk(2, dim=-1),
+    net_utils.py:275-276; the modality pair o[0], o[1]); the backward concatenates the two
+    gradients in one pass instead of autograd's zero-fill + slice-copy per view."""
+
+    @staticmethod
+    def forward(ctx, t, k, dim):
+        ctx.k, ctx.dim, ctx.n = k, dim, t.shape[dim]
+        ctx.set_materialize_grads(False)
+        return t.narrow(dim, 0, k), t.narrow(dim, k, t.shape[dim] - k)
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        if g1 is None and g2 is None:
+            return None, None, None
+        ref = g1 if g1 is not None else g2
+        shp = list(ref.shape)
+        if g1 is None:
+            shp[ctx.dim] = ctx.k
+            g1 = torch.zeros(shp, dtype=ref.dtype, device=ref.device)
+        if g2 is None:
+            shp[ctx.dim] = ctx.n - ctx.k
+            g2 = torch.zeros(shp, dtype=ref.dtype, device=ref.device)
+        return torch.cat([g1, g2], ctx.dim), None, None
+
+
+def split(t, k, dim=-1):
+    return SplitF.apply(t, k, dim % t.dim())
+
+
 # ---------------------------------------------------------------------------- residual
 class ResidualF(Function):
     """x + drop_path(y): timm DropPath as a per-sample scale (0 or 1/keep) fused in the add."""
