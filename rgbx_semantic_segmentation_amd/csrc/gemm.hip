@@ -724,8 +724,8 @@ void launch_bf16(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream
 template <int BM, int BN>
 void launch_bf16_ns(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream_t s) {
   const long blocks = (long)a.tiles_m * a.tiles_n * G * nsplit;
-  // a 64 x 64 stage is only 16 KB: a 4-deep ring (64 KB) still leaves two blocks per CU, and
-  // measured: no gain (2.82 vs 2.95 ms of GEMM per step), so off by default (CMX_GEMM_NS64=4)
+  // a 64 x 64 stage is only 16 KB, so a 4-deep ring (64 KB) would still leave two blocks per
+  // CU; measured: no gain (2.82 vs 2.95 ms of GEMM per step), so off by default (CMX_GEMM_NS64=4)
   static const int ns64 = [] { const char* e = getenv("CMX_GEMM_NS64"); return e ? atoi(e) : 2; }();
   if (blocks <= 256 || (BM == 64 && BN == 64 && ns64 == 4)) launch_bf16<BM, BN, 4>(a, G, nsplit, tA, tB, s);
   else launch_bf16<BM, BN, 2>(a, G, nsplit, tA, tB, s);
