@@ -121,7 +121,11 @@ int cmx_bilinear_adjoint_1d(const void* in, void* out, int64_t P, int Lo, int Li
 
 /* ---- fused final upsample + CrossEntropyLoss(mean, ignore_index=255) (builder.py:233,249). */
 size_t cmx_upsample_ce_workspace(int B, int H, int W);
+/* grad = NULL: loss only (H = 4h, W = 4w, K <= 40), the backward then recomputes the gradient tile by tile:
+ * cmx_upsample_ce_bwd writes dlogits (B, h, w, K) = bilinear adjoint of (softmax - onehot) * dloss[0] * stats[1]
+ * (stats = the forward's out) without materialising any full-resolution tensor. */
 int cmx_upsample_ce_fwd(const void* logits, const int64_t* label, void* grad, float* out, float* workspace, int B, int h, int w, int H, int W, int K, int ignore_index, int dtype, hipStream_t stream);
+int cmx_upsample_ce_bwd(const void* logits, const int64_t* label, const float* dloss, const float* stats, void* dlogits, int B, int h, int w, int H, int W, int K, int ignore_index, int dtype, hipStream_t stream);
 
 /* ---- dense layers: batched MFMA GEMM with fused epilogues -----------------------------
  * Replaces every nn.Linear and 1x1 Conv2d of the path (dual_segformer.py:42-43, 87-96, 110;

@@ -108,15 +108,32 @@ int ce_nblk(long total) {
 }
 }  // namespace
 
+// ce_fused.hip: LDS-tiled loss-only forward (grad == NULL)
+int ce_fwd_tiled_nblk(int B, int H, int W);
+bool ce_tiled_ok(int h, int w, int H, int W, int K);
+int ce_fwd_tiled_launch(const void* logits, const int64_t* label, float* part, int B, int h, int w, int H, int W,
+                        int K, int ignore, int dtype, hipStream_t s);
+
 extern "C" {
 
-size_t cmx_upsample_ce_workspace(int B, int H, int W) { return (size_t)ce_nblk((long)B * H * W) * 2 * sizeof(float); }
+size_t cmx_upsample_ce_workspace(int B, int H, int W) {
+  const long a = ce_nblk((long)B * H * W), b = ce_fwd_tiled_nblk(B, H, W);
+  return (size_t)(a > b ? a : b) * 2 * sizeof(float);
+}
 
 // logits (B, h, w, K) dtype; label (B, H, W) int64; grad (B, H, W, K) dtype (softmax - onehot);
 // out (3) fp32 = [loss, 1/n_valid, n_valid]
 int cmx_upsample_ce_fwd(const void* logits, const int64_t* label, void* grad, float* out, float* workspace, int B,
                         int h, int w, int H, int W, int K, int ignore_index, int dtype, hipStream_t s) {
   CMX_REQUIRE(K > 0 && K <= KMAX, CMX_ERR_SHAPE, "upsample_ce: K=%d > %d", K, KMAX);
+  if (!grad) {                 // loss only (the backward recomputes the gradient: cmx_upsample_ce_bwd)
+    CMX_REQUIRE(ce_tiled_ok(h, w, H, W, K), CMX_ERR_SHAPE, "upsample_ce: loss-only mode needs H = 4h, W = 4w, K <= 40");
+    const int nbt = ce_fwd_tiled_nblk(B, H, W);
+    const int st = ce_fwd_tiled_launch(logits, label, workspace, B, h, w, H, W, K, ignore_index, dtype, s);
+    if (st) return st;
+    hipLaunchKernelGGL(ce_finalize_kernel, dim3(1), dim3(256), 0, s, workspace, nbt, out);
+    return cmx_check_launch("upsample_ce_fwd");
+  }
   const int nb = ce_nblk((long)B * H * W);
   CMX_DISPATCH(dtype, T, {
     hipLaunchKernelGGL(upsample_ce_kernel<T>, dim3(nb), dim3(256), 0, s, (const T*)logits, label, (T*)grad, workspace,

@@ -720,12 +720,17 @@ class UpsampleCEF(Function):
     @staticmethod
     def forward(ctx, logits, label, dims, ignore):
         B, h, w, H, W, Kc = dims
-        grad = torch.empty(B, H, W, Kc, dtype=logits.dtype, device=logits.device)
+        # exact x4 (every CMX config), K <= 40: loss only here, the gradient is recomputed tile
+        # by tile in the backward (cmx_upsample_ce_bwd); else the materialised-gradient path
+        fused = H == 4 * h and W == 4 * w and Kc <= 40
+        logits = _c(logits)
+        grad = None if fused else torch.empty(B, H, W, Kc, dtype=logits.dtype, device=logits.device)
         out = torch.empty(3, dtype=torch.float32, device=logits.device)
         ws = K._ws(K.query("cmx_upsample_ce_workspace", B, H, W), logits.device)
-        K.call("cmx_upsample_ce_fwd", K.ptr(_c(logits)), K.ptr(label), K.ptr(grad), K.ptr(out), K.ptr(ws), B, h, w, H,
+        K.call("cmx_upsample_ce_fwd", K.ptr(logits), K.ptr(label), K.ptr(grad), K.ptr(out), K.ptr(ws), B, h, w, H,
                W, Kc, ignore, K.dtype_code(logits), K.stream())
-        ctx.save_for_backward(grad, out)
+        ctx.save_for_backward(logits if fused else grad, out, label)
+        ctx.fused, ctx.ignore = fused, ignore
         ctx.dims = dims
         ctx.ldtype = logits.dtype
         ctx.lshape = logits.shape
@@ -733,9 +738,15 @@ class UpsampleCEF(Function):
 
     @staticmethod
     def backward(ctx, dloss):
-        grad, out = ctx.saved_tensors
+        grad, out, label = ctx.saved_tensors
         B, h, w, H, W, Kc = ctx.dims
         dloss = _c(dloss.reshape(1).to(torch.float32))
+        if ctx.fused:
+            logits = grad
+            dl = torch.empty(B, h * w, Kc, dtype=ctx.ldtype, device=logits.device)
+            K.call("cmx_upsample_ce_bwd", K.ptr(logits), K.ptr(label), K.ptr(dloss), K.ptr(out), K.ptr(dl), B, h, w,
+                   H, W, Kc, ctx.ignore, K.dtype_code(logits), K.stream())
+            return dl.view(ctx.lshape), None, None, None
         tmp = torch.empty(B * H, w, Kc, dtype=torch.float32, device=grad.device)
         K.call("cmx_bilinear_adjoint_1d", K.ptr(grad), K.ptr(tmp), B * H, W, w, Kc, W * Kc, Kc, 0, 0, 1.0,
                K.dtype_code(grad), 0, K.stream())

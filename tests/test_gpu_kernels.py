@@ -75,3 +75,30 @@ def test_sra_attention(dev, dtype, Bt, N, Nk, heads, D):
     assert relerr(dq, qr.grad) < TOL[dtype] * 2, relerr(dq, qr.grad)
     assert relerr(dkv[..., :C], kvr.grad[..., :C]) < TOL[dtype] * 2, relerr(dkv[..., :C], kvr.grad[..., :C])
     assert relerr(dkv[..., C:], kvr.grad[..., C:]) < TOL[dtype] * 2, relerr(dkv[..., C:], kvr.grad[..., C:])
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("B,h,w,K", [(2, 120, 160, 40), (1, 15, 20, 9), (2, 16, 24, 19)])
+@pytest.mark.parametrize("fused", [True, False])
+def test_upsample_ce(dev, dtype, B, h, w, K, fused):
+    """Final x4 bilinear upsample + CrossEntropyLoss(mean, ignore_index=255) (builder.py:233,249;
+    train.py:72-73): loss and d logits against torch fp64 autograd.  fused=True: loss-only
+    forward + tile-recomputing backward (ce_fused.hip); False: the materialised-gradient path
+    (forced by a non-x4 output size)."""
+    import torch.nn.functional as Fn
+    from rgbx_semantic_segmentation_amd.functions import UpsampleCEF
+    torch.manual_seed(7)
+    H, W = (4 * h, 4 * w) if fused else (4 * h - 2, 4 * w + 3)
+    lg = torch.randn(B, h, w, K, dtype=torch.float64) * 3
+    lab = torch.randint(0, K, (B, H, W))
+    lab[:, 5:30, 7:40] = 255
+    ref = lg.clone().requires_grad_(True)
+    up = Fn.interpolate(ref.permute(0, 3, 1, 2), size=(H, W), mode="bilinear", align_corners=False)
+    loss_ref = Fn.cross_entropy(up, lab, reduction="mean", ignore_index=255)
+    (loss_ref * 0.7).backward()
+    x = lg.to(dev, dtype).requires_grad_(True)
+    loss = UpsampleCEF.apply(x, lab.to(dev), (B, h, w, H, W, K), 255)
+    (loss * 0.7).backward()
+    torch.cuda.synchronize()
+    assert abs(loss.item() - loss_ref.item()) / loss_ref.item() < (1e-5 if dtype == torch.float32 else 1e-2)
+    assert relerr(x.grad, ref.grad) < TOL[dtype] * 2, relerr(x.grad, ref.grad)
