@@ -38,6 +38,8 @@ def parse():
     p.add_argument("--classes", type=int, default=40)
     p.add_argument("--dtype", default="bfloat16")
     p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--loss-scaling", action="store_true",
+                   help="config 5's AMP step: dynamic loss scaling (GradScaler) inside the captured step")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-steps", type=int, default=1)
     p.add_argument("--cpu-threads", type=int, default=16)
@@ -98,10 +100,20 @@ def main():
     policy = WarmUpPolyLR(6e-5, 0.9, 200 * niters, niters * 10)
     rgb, x, lab = make_batch(args.batch, args.height, args.width, args.classes, seed=12345 + rank, device=dev)
 
+    scaler = None
+    if args.loss_scaling:
+        from rgbx_semantic_segmentation_amd.optim import GradScaler
+        scaler = GradScaler(device=dev)
+
     def step():
         loss = model(rgb, x, lab)
-        loss.backward()
-        opt.step()
+        if scaler is not None:
+            scaler.scale(loss).backward()
+            scaler.step(opt)
+            scaler.update()
+        else:
+            loss.backward()
+            opt.step()
         return loss
 
     it = 0
@@ -191,7 +203,8 @@ def main():
                                    f"{args.height}x{args.width}", "model": f"CMX-{args.backbone}",
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "image": [args.height, args.width], "classes": args.classes,
-                       "parallelism": f"dp{world}", "hip_graph": graph is not None},
+                       "parallelism": f"dp{world}", "hip_graph": graph is not None,
+                       "loss_scaling": bool(args.loss_scaling)},
             "step_mfma_roofline": {"train_gflop_per_image": round(fl_img / 1e9, 3),
                                    "achieved_tflops": round((ips / world) * fl_img / 1e12, 2),
                                    "peak_tflops": PEAK_BF16_TFLOPS, "frac": round(step_frac, 5)},

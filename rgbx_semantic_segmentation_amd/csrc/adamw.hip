@@ -16,7 +16,11 @@
 __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                              float* __restrict__ v, bf16* __restrict__ shadow, const uint8_t* __restrict__ decay64,
                              long n, const float* __restrict__ lr_ptr, const float* __restrict__ step_ptr, float b1,
-                             float b2, float eps, float wd, float gscale) {
+                             float b2, float eps, float wd, float gscale, const float* __restrict__ loss_scale,
+                             const float* __restrict__ found_inf) {
+  // GradScaler semantics (train.py:185-198): a step whose gradients held inf / nan is skipped
+  if (found_inf && *found_inf != 0.f) return;
+  if (loss_scale) gscale /= *loss_scale;                       // unscale
   const float lr = *lr_ptr;
   const float t = *step_ptr;
   const float bc1 = 1.f - powf(b1, t);
@@ -52,7 +56,34 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
   }
 }
 
-__global__ void step_incr_kernel(float* step) { *step += 1.f; }
+__global__ void step_incr_kernel(float* step, const float* found_inf) {
+  if (!(found_inf && *found_inf != 0.f)) *step += 1.f;
+}
+
+// found_inf[0] = 1 if any of g[0, n) is inf / nan (left untouched otherwise; reset by the
+// loss-scale update).  Benign race: every writer stores the same 1.
+__global__ __launch_bounds__(256) void nonfinite_kernel(const float* __restrict__ g, long n, float* __restrict__ found) {
+  int bad = 0;
+  const long nv = n / 4;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (long)gridDim.x * blockDim.x) {
+    const float4 x = reinterpret_cast<const float4*>(g)[i];
+    bad |= !isfinite(x.x) | !isfinite(x.y) | !isfinite(x.z) | !isfinite(x.w);
+  }
+  if (__syncthreads_or(bad) && threadIdx.x == 0) *found = 1.f;
+}
+
+// torch.cuda.amp.GradScaler.update(): backoff on overflow, grow after `interval` clean steps
+__global__ void loss_scale_update_kernel(float* scale, int* tracker, float* found, float growth, float backoff,
+                                         int interval) {
+  if (*found != 0.f) {
+    *scale *= backoff;
+    *tracker = 0;
+  } else if (++*tracker >= interval) {
+    *scale *= growth;
+    *tracker = 0;
+  }
+  *found = 0.f;
+}
 
 extern "C" {
 
@@ -60,13 +91,36 @@ extern "C" {
 int cmx_adamw_step(float* p, const float* g, float* m, float* v, void* shadow_bf16, const uint8_t* decay64, int64_t n,
                    const float* lr_ptr, float* step_ptr, float beta1, float beta2, float eps, float weight_decay,
                    float grad_scale, hipStream_t s) {
+  return cmx_adamw_step_scaled(p, g, m, v, shadow_bf16, decay64, n, lr_ptr, step_ptr, beta1, beta2, eps, weight_decay,
+                               grad_scale, nullptr, nullptr, s);
+}
+
+int cmx_adamw_step_scaled(float* p, const float* g, float* m, float* v, void* shadow_bf16, const uint8_t* decay64,
+                          int64_t n, const float* lr_ptr, float* step_ptr, float beta1, float beta2, float eps,
+                          float weight_decay, float grad_scale, const float* loss_scale, const float* found_inf,
+                          hipStream_t s) {
   CMX_REQUIRE(n % 64 == 0, CMX_ERR_SHAPE, "adamw: n must be a multiple of 64");
-  hipLaunchKernelGGL(step_incr_kernel, dim3(1), dim3(1), 0, s, step_ptr);
+  hipLaunchKernelGGL(step_incr_kernel, dim3(1), dim3(1), 0, s, step_ptr, found_inf);
   long blocks = (n / 4 + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, g, m, v, (bf16*)shadow_bf16, decay64,
-                     (long)n, lr_ptr, step_ptr, beta1, beta2, eps, weight_decay, grad_scale);
+                     (long)n, lr_ptr, step_ptr, beta1, beta2, eps, weight_decay, grad_scale, loss_scale, found_inf);
   return cmx_check_launch("adamw_step");
+}
+
+int cmx_grad_nonfinite(const float* g, int64_t n, float* found_inf, hipStream_t s) {
+  CMX_REQUIRE(n % 4 == 0 && found_inf, CMX_ERR_SHAPE, "grad_nonfinite: n %% 4");
+  long blocks = (n / 4 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(nonfinite_kernel, dim3((unsigned)blocks), dim3(256), 0, s, g, (long)n, found_inf);
+  return cmx_check_launch("grad_nonfinite");
+}
+
+int cmx_loss_scale_update(float* scale, int* growth_tracker, float* found_inf, float growth_factor,
+                          float backoff_factor, int growth_interval, hipStream_t s) {
+  hipLaunchKernelGGL(loss_scale_update_kernel, dim3(1), dim3(1), 0, s, scale, growth_tracker, found_inf, growth_factor,
+                     backoff_factor, growth_interval);
+  return cmx_check_launch("loss_scale_update");
 }
 
 }  // extern "C"

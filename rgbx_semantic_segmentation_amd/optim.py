@@ -74,11 +74,19 @@ class FusedAdamW:
         """No-op: gradients are overwritten by every backward (see module docstring)."""
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, scaler: "GradScaler | None" = None):
         s = self.store
         gscale = 1.0
         if self.grad_sync is not None:
             gscale = float(self.grad_sync(s.grad))
+        if scaler is not None and scaler.enabled:
+            # GradScaler.step: skip the update if any (scaled) gradient is inf / nan, else unscale
+            call("cmx_grad_nonfinite", ptr(s.grad), s.numel, ptr(scaler.found_inf), stream())
+            call("cmx_adamw_step_scaled", ptr(s.flat), ptr(s.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq),
+                 ptr(s.shadow), ptr(s.decay64), s.numel, ptr(self.lr_t), ptr(self.step_t), self.betas[0],
+                 self.betas[1], self.eps, self.weight_decay, gscale, ptr(scaler.scale_t), ptr(scaler.found_inf),
+                 stream())
+            return None
         call("cmx_adamw_step", ptr(s.flat), ptr(s.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq), ptr(s.shadow),
              ptr(s.decay64), s.numel, ptr(self.lr_t), ptr(self.step_t), self.betas[0], self.betas[1], self.eps,
              self.weight_decay, gscale, stream())
@@ -115,3 +123,59 @@ class FusedAdamW:
             self.step_t.fill_(float(st["step"]))
         for g, gs in zip(self.param_groups, sd["param_groups"]):
             g["lr"] = gs["lr"]
+
+
+class GradScaler:
+    """Dynamic loss scaling with the API of ``torch.cuda.amp.GradScaler`` as the reference's
+    AMP path uses it (train.py:13,56,185-198: ``scaler.scale(loss).backward();
+    scaler.step(optimizer); scaler.update()``), defaults init_scale 2**16, growth x2 every
+    2000 clean steps, backoff x0.5 on inf / nan.
+
+    The scale, growth tracker and found-inf flag are device tensors updated by kernels
+    (csrc/adamw.hip), so a scaled training step never syncs the host and can be replayed
+    from a HIP graph.  ``scale(loss)`` multiplies the loss by the device scale (its backward
+    carries the scale into every gradient); ``step`` checks the gradients for inf / nan and
+    runs the fused AdamW unscaled by 1 / scale, skipping the update on overflow; ``update``
+    applies backoff / growth.  The compute dtype stays the model's (bf16 here; fp16 storage
+    is not built)."""
+
+    def __init__(self, init_scale=2.0 ** 16, growth_factor=2.0, backoff_factor=0.5, growth_interval=2000,
+                 enabled=True, device="cuda"):
+        self.enabled = bool(enabled)
+        self.growth_factor, self.backoff_factor = float(growth_factor), float(backoff_factor)
+        self.growth_interval = int(growth_interval)
+        self.scale_t = torch.full((1,), float(init_scale), dtype=torch.float32, device=device)
+        self.tracker = torch.zeros(1, dtype=torch.int32, device=device)
+        self.found_inf = torch.zeros(1, dtype=torch.float32, device=device)
+
+    def scale(self, loss: torch.Tensor) -> torch.Tensor:
+        return loss * self.scale_t[0] if self.enabled else loss
+
+    def step(self, optimizer, *args, **kwargs):
+        return optimizer.step(scaler=self)
+
+    def update(self, new_scale=None):
+        if not self.enabled:
+            return
+        if new_scale is not None:
+            self.scale_t.fill_(float(new_scale))
+            return
+        call("cmx_loss_scale_update", ptr(self.scale_t), ptr(self.tracker), ptr(self.found_inf), self.growth_factor,
+             self.backoff_factor, self.growth_interval, stream())
+
+    def get_scale(self) -> float:
+        return float(self.scale_t.item()) if self.enabled else 1.0
+
+    def is_enabled(self) -> bool:
+        return self.enabled
+
+    def state_dict(self):
+        return {"scale": self.get_scale(), "growth_factor": self.growth_factor, "backoff_factor": self.backoff_factor,
+                "growth_interval": self.growth_interval, "_growth_tracker": int(self.tracker.item())}
+
+    def load_state_dict(self, sd):
+        self.scale_t.fill_(float(sd["scale"]))
+        self.tracker.fill_(int(sd.get("_growth_tracker", 0)))
+        self.growth_factor = float(sd.get("growth_factor", self.growth_factor))
+        self.backoff_factor = float(sd.get("backoff_factor", self.backoff_factor))
+        self.growth_interval = int(sd.get("growth_interval", self.growth_interval))

@@ -69,3 +69,49 @@ def test_segment_allreduce_sees_final_gradients(dev):
     torch.cuda.synchronize()
     bad = (model.store.grad - 2 * ref).abs() > 1e-6 * (1 + ref.abs())
     assert not bad.any(), f"{int(bad.sum())} gradient elements were reduced before they were final"
+
+
+@pytest.mark.gpu
+def test_grad_scaler_protocol(dev):
+    """GradScaler (train.py:185-198 AMP path, config 5): a scaled step updates the parameters
+    like an unscaled one (the power-of-two scale is exact in fp32); an inf gradient skips
+    the update and the step count and halves the scale; growth after growth_interval clean
+    steps.  All on device, no host sync inside the step."""
+    from rgbx_semantic_segmentation_amd.models.builder import EncoderDecoder
+    from rgbx_semantic_segmentation_amd.optim import FusedAdamW, GradScaler
+    torch.manual_seed(0)
+    g = torch.Generator().manual_seed(5)
+    rgb = torch.randn(2, 3, 64, 96, generator=g).to(dev)
+    x = torch.randn(2, 3, 64, 96, generator=g).to(dev)
+    lab = torch.randint(0, 9, (2, 64, 96), generator=g).to(dev)
+    cfg = dict(backbone="mit_b0", num_classes=9, compute_dtype="float32", decoder_embed_dim=256)
+    ref = EncoderDecoder(cfg).to(dev)
+    ref.eval()
+    mod = EncoderDecoder(cfg).to(dev)
+    mod.load_state_dict(ref.state_dict())
+    mod.eval()
+    o_ref, o = FusedAdamW(ref), FusedAdamW(mod)
+    sc = GradScaler(init_scale=2.0 ** 10, growth_interval=2, device=dev)
+    ref(rgb, x, lab).backward()
+    o_ref.step()
+    sc.scale(mod(rgb, x, lab)).backward()
+    sc.step(o)
+    sc.update()
+    torch.cuda.synchronize()
+    d = (mod.store.flat - ref.store.flat).abs().max().item()
+    assert d < 1e-6 * (1 + ref.store.flat.abs().max().item()), d
+    # overflow: the step is skipped, the scale halves
+    before = mod.store.flat.clone()
+    sc.scale(mod(rgb, x, lab)).backward()
+    mod.store.grad[123] = float("inf")
+    sc.step(o)
+    sc.update()
+    torch.cuda.synchronize()
+    assert torch.equal(before, mod.store.flat)
+    assert sc.get_scale() == 2.0 ** 9 and float(o.step_t.item()) == 1.0
+    # two clean steps: growth back to 2**10
+    for _ in range(2):
+        sc.scale(mod(rgb, x, lab)).backward()
+        sc.step(o)
+        sc.update()
+    assert sc.get_scale() == 2.0 ** 10 and float(o.step_t.item()) == 3.0
