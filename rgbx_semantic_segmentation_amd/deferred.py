@@ -47,7 +47,13 @@ class _Queue:
         self.gemms = []        # argument tuples of cmx_gemm_group_pack (minus rec / ws / splitk / blk0)
         self.reds = []         # argument tuples of cmx_reduce_pack (minus rec / blk0)
         self.keep = []         # tensors the queued work reads or writes
+        self.streams = {}      # streams the queued operands were produced on (FFM's side stream)
         self.armed = False
+
+
+def _note_stream():
+    st = torch.cuda.current_stream()
+    _q.streams[st.cuda_stream] = st
 
 
 _q = _Queue()
@@ -108,6 +114,7 @@ def wgrad(dz: torch.Tensor, x: torch.Tensor, Wg: torch.Tensor, bg: torch.Tensor 
         return False
     _q.gemms.append(args)
     _q.keep.extend((dz, x))
+    _note_stream()
     arm()
     return True
 
@@ -121,6 +128,7 @@ def reduce(src: torch.Tensor, dst: torch.Tensor, dst2: torch.Tensor | None, G: i
     _q.reds.append((src.data_ptr(), dst.data_ptr(), ptr(dst2), G, nblk, sg, sb, rows, cols, csplit, dg, ldd, dg2,
                     ldd2, int(accumulate)))
     _q.keep.append(src)
+    _note_stream()
     arm()
 
 
@@ -179,8 +187,15 @@ def flush() -> None:
     if not (q.gemms or q.reds):
         return
     gemms, reds, keep = q.gemms, list(q.reds), q.keep
-    q.gemms, q.reds, q.keep = [], [], []
+    producers = q.streams
+    q.gemms, q.reds, q.keep, q.streams = [], [], [], {}
     device = keep[0].device
+    cur = torch.cuda.current_stream()
+    for sid, st in producers.items():      # operands made on another stream: order after them
+        if sid != cur.cuda_stream:
+            cur.wait_stream(st)
+            for t in keep:
+                t.record_stream(cur)
     if gemms:
         splits = [query("cmx_gemm_grouped_splitk", a[4], a[5], a[6], a[7], int(a[3] is not None)) for a in gemms]
         sizes = [query("cmx_gemm_workspace", a[4], a[5], a[6], s) if s > 1 else 0 for a, s in zip(gemms, splits)]

@@ -17,6 +17,7 @@ import torch
 import torch.nn as nn
 
 from ... import functions as F
+from ... import streams
 from ..net_utils import FeatureRectifyModule, FeatureFusionModule, init_segformer
 
 MIT_SPECS = {
@@ -163,6 +164,8 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
         bi = 0
         Hc, Wc, Cin = H, W, 3
         sync = getattr(self, "grad_sync", None)     # dist.BucketedGradSync (data parallel) or None
+        main = torch.cuda.current_stream() if images.is_cuda else None
+        side = streams.ffm_stream(main.device) if (main is not None and streams.FFM_SIDE) else None
         for s in range(4):
             pe = getattr(self, f"patch_embed{s + 1}")
             if sync is not None and s > 0 and x.requires_grad:
@@ -184,9 +187,21 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
                                       tap=prev[1])
             C = self.embed_dims[s]
             r = F.frm(store, self.FRMs[s], x.view(G, B, Hc * Wc, C))
-            outs.append(self.FFMs[s].run(store, r, B, Hc, Wc, training))
+            if side is not None:
+                # FFM_s only feeds the decoder: run it beside stage s + 1 on the side stream
+                # (its backward then runs there too, beside the encoder's backward)
+                side.wait_stream(main)
+                r.record_stream(side)
+                with torch.cuda.stream(side):
+                    outs.append(self.FFMs[s].run(store, r, B, Hc, Wc, training))
+            else:
+                outs.append(self.FFMs[s].run(store, r, B, Hc, Wc, training))
             grids.append((Hc, Wc))
             x = r.view(G, B * Hc * Wc, C)
+        if side is not None:
+            main.wait_stream(side)
+            for o in outs:
+                o.record_stream(main)
         return outs, grids
 
 

@@ -20,6 +20,16 @@ import os
 import torch
 
 ENABLED = os.environ.get("CMX_SIDE_STREAM", "0") == "1"
+# FFM (the fusion branch feeding only the decoder) on its own stream beside the encoder
+FFM_SIDE = os.environ.get("CMX_FFM_STREAM", "1") == "1"
+_ffm: dict = {}
+
+
+def ffm_stream(device) -> torch.cuda.Stream:
+    idx = torch.device(device).index
+    if idx not in _ffm:
+        _ffm[idx] = torch.cuda.Stream(device=device)
+    return _ffm[idx]
 _side: dict = {}
 _pending: set = set()
 
