@@ -372,7 +372,8 @@ __device__ __forceinline__ void stage_region(const T* __restrict__ base, T* img,
 template <typename T, int CB, int ACT, bool FLIP>
 __global__ __launch_bounds__(256) void dw2_fwd_kernel(const T* __restrict__ h, const float* __restrict__ w,
                                                       const float* __restrict__ b, T* __restrict__ out, int ipg, int H,
-                                                      int W, int C, int tiles_x, int tiles_y, int ncb) {
+                                                      int W, int C, int tiles_x, int tiles_y, int ncb,
+                                                      T* __restrict__ gprime) {
   constexpr int NCG = CB / 8, TPC = 256 / NCG;
   __shared__ __attribute__((aligned(16))) T hs[NCG * EY * EX * 8];
   const Tile2 t = tile2_of(CB, ipg, tiles_x, tiles_y, ncb);
@@ -408,6 +409,12 @@ __global__ __launch_bounds__(256) void dw2_fwd_kernel(const T* __restrict__ h, c
 #pragma unroll
         for (int u = 0; u < 4; ++u) acc[u] = pk_fma(wr[u][tap], v[u], acc[u]);
       }
+    if (gprime) {              // act'(z), saved so the backward needs no conv recompute
+      cmx_f2 gd[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) gd[u] = act2_grad<ACT>(acc[u]);
+      v8_store<T>(gprime + ibase + ((long)y * W + x) * C + cg * 8, v8_pack<T>(gd));
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc[u] = act2_fwd<ACT>(acc[u]);
     v8_store<T>(out + ibase + ((long)y * W + x) * C + cg * 8, v8_pack<T>(acc));
@@ -425,6 +432,107 @@ __device__ __forceinline__ void rs_step(const float (&v)[N], float (&o)[N / 2], 
     o[k] = keep + __shfl_xor(send, off, 64);
   }
 }
+
+// Backward from a saved act'(z) (cmx_dwconv3x3_fwd_save): dz = da * act'(z) on the tile + 1-pixel
+// halo is one multiply per element (no 3x3 recompute of z, no erf / exp), then dh = conv^T(dz)
+// and the dW / db partials exactly as dw2_bwd_kernel.  h is staged with a 1-pixel halo only.
+template <typename T, int CB>
+__global__ __launch_bounds__(256, 2) void dw2_bwdg_kernel(const T* __restrict__ da, const T* __restrict__ h,
+                                                       const T* __restrict__ gprime, const float* __restrict__ w,
+                                                       T* __restrict__ dh, float* __restrict__ part, int ipg, int H,
+                                                       int W, int C, int tiles_x, int tiles_y, int ncb, int nsp) {
+  constexpr int NCG = CB / 8, TPC = 256 / NCG;
+  __shared__ __attribute__((aligned(16))) T hs[NCG * EY * EX * 8];
+  __shared__ __attribute__((aligned(16))) T dzs[NCG * EY * EX * 8];
+  __shared__ __attribute__((aligned(16))) T gs[NCG * EY * EX * 8];
+  const Tile2 t = tile2_of(CB, ipg, tiles_x, tiles_y, ncb);
+  const long ibase = ((long)t.g * ipg + t.img) * H * W * C + t.cb0;
+  stage_region<T, CB, EY, EX>(h + ibase, hs, t.ty0 - 1, t.tx0 - 1, H, W, C);
+  stage_region<T, CB, EY, EX>(da + ibase, dzs, t.ty0 - 1, t.tx0 - 1, H, W, C);
+  stage_region<T, CB, EY, EX>(gprime + ibase, gs, t.ty0 - 1, t.tx0 - 1, H, W, C);
+  const int cg = threadIdx.x / TPC, pl = threadIdx.x % TPC;
+  const int c0 = t.cb0 + cg * 8;
+  cmx_f2 wr[4][9];
+  load_w72(w + ((long)t.g * C + c0) * 9, wr);
+  __syncthreads();
+  const T* hc = hs + cg * EY * EX * 8;
+  T* dzc = dzs + cg * EY * EX * 8;
+  const T* gc = gs + cg * EY * EX * 8;
+  // dz = da * act'(z) in place (outside the image both staged tiles are zero: dz = 0 there)
+  for (int it = pl; it < EY * EX; it += TPC) {
+    cmx_f2 d[4], gd[4];
+    v8_unpack<T>(v8_load<T>(dzc + it * 8), d);
+    v8_unpack<T>(v8_load<T>(gc + it * 8), gd);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) d[u] = d[u] * gd[u];
+    v8_store<T>(dzc + it * 8, v8_pack<T>(d));
+  }
+  __syncthreads();
+  if (dh) {
+    for (int it = pl; it < TY2 * TX2; it += TPC) {
+      const int r = it / TX2, c = it % TX2;
+      const int y = t.ty0 + r, x = t.tx0 + c;
+      if (y >= H || x >= W) continue;
+      cmx_f2 g[4] = {pk_splat(0.f), pk_splat(0.f), pk_splat(0.f), pk_splat(0.f)};
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          cmx_f2 dv[4];           // dh[y][x] += w[i][j] dz[y-i+1][x-j+1]
+          v8_unpack<T>(v8_load<T>(dzc + ((r + 2 - i) * EX + c + 2 - j) * 8), dv);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) g[u] = pk_fma(wr[u][i * 3 + j], dv[u], g[u]);
+        }
+      v8_store<T>(dh + ibase + ((long)y * W + x) * C + cg * 8, v8_pack<T>(g));
+    }
+  }
+  cmx_f2 acc[4][10];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) acc[u][k] = pk_splat(0.f);
+  for (int it = pl; it < TY2 * TX2; it += TPC) {
+    const int r = it / TX2, c = it % TX2;
+    if (t.ty0 + r >= H || t.tx0 + c >= W) continue;
+    cmx_f2 dz0[4];
+    v8_unpack<T>(v8_load<T>(dzc + ((r + 1) * EX + c + 1) * 8), dz0);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        cmx_f2 hv[4];             // dW[i][j] += dz[y][x] h[y+i-1][x+j-1]
+        v8_unpack<T>(v8_load<T>(hc + ((r + i) * EX + c + j) * 8), hv);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[u][i * 3 + j] = pk_fma(dz0[u], hv[u], acc[u][i * 3 + j]);
+      }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u][9] += dz0[u];
+  }
+  const int lane = threadIdx.x & 63;
+  float flat[80], r40[40], r20[20], r10[10], r5[5];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      flat[(2 * u) * 10 + k] = acc[u][k].x;
+      flat[(2 * u + 1) * 10 + k] = acc[u][k].y;
+    }
+  int seg = 0, s_off = TPC >> 1;
+  rs_step<80>(flat, r40, s_off, (lane & s_off) != 0); seg = seg * 2 + ((lane & s_off) != 0); s_off >>= 1;
+  rs_step<40>(r40, r20, s_off, (lane & s_off) != 0); seg = seg * 2 + ((lane & s_off) != 0); s_off >>= 1;
+  rs_step<20>(r20, r10, s_off, (lane & s_off) != 0); seg = seg * 2 + ((lane & s_off) != 0); s_off >>= 1;
+  rs_step<10>(r10, r5, s_off, (lane & s_off) != 0); seg = seg * 2 + ((lane & s_off) != 0); s_off >>= 1;
+  for (; s_off > 0; s_off >>= 1) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) r5[k] += __shfl_xor(r5[k], s_off, 64);
+  }
+  if ((lane & (TPC / 16 - 1)) == 0) {
+    float* o = part + ((long)t.g * nsp + t.sp) * C * 10 + (long)c0 * 10 + seg * 5;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) o[k] = r5[k];
+  }
+}
+
 
 template <typename T, int CB, int ACT>
 __global__ __launch_bounds__(256, 2) void dw2_bwd_kernel(const T* __restrict__ da, const T* __restrict__ h,
@@ -566,7 +674,13 @@ extern "C" {
 
 int cmx_dwconv3x3_fwd(const void* h, const float* w, const float* b, void* out, int NI, int imgs_per_group, int H,
                       int W, int C, int act, int dtype, hipStream_t s) {
+  return cmx_dwconv3x3_fwd_save(h, w, b, out, nullptr, NI, imgs_per_group, H, W, C, act, dtype, s);
+}
+
+int cmx_dwconv3x3_fwd_save(const void* h, const float* w, const float* b, void* out, void* gprime, int NI,
+                           int imgs_per_group, int H, int W, int C, int act, int dtype, hipStream_t s) {
   CMX_REQUIRE(C % 4 == 0 && NI % imgs_per_group == 0, CMX_ERR_SHAPE, "dwconv_fwd: C=%d", C);
+  CMX_REQUIRE(!gprime || tile_cb(C, dtype), CMX_ERR_SHAPE, "dwconv_fwd_save: C=%d has no LDS-tiled path", C);
   CMX_REQUIRE((long)NI * H * W * C < (1L << 31), CMX_ERR_SHAPE, "dwconv_fwd: tensor too large for 32-bit indexing");
   const int G = NI / imgs_per_group;
   const int CB = tile_cb(C, dtype);
@@ -577,10 +691,10 @@ int cmx_dwconv3x3_fwd(const void* h, const float* w, const float* b, void* out, 
       CMX_ACT_DISPATCH(act, A, {
         if (CB == 32) {
           hipLaunchKernelGGL((dw2_fwd_kernel<T, 32, A, false>), grid, dim3(256), 0, s, (const T*)h, w, b, (T*)out,
-                             imgs_per_group, H, W, C, tx, ty, ncb);
+                             imgs_per_group, H, W, C, tx, ty, ncb, (T*)gprime);
         } else if constexpr (sizeof(T) == 2) {
           hipLaunchKernelGGL((dw2_fwd_kernel<T, 64, A, false>), grid, dim3(256), 0, s, (const T*)h, w, b, (T*)out,
-                             imgs_per_group, H, W, C, tx, ty, ncb);
+                             imgs_per_group, H, W, C, tx, ty, ncb, (T*)gprime);
         }
       });
     });
@@ -595,6 +709,35 @@ int cmx_dwconv3x3_fwd(const void* h, const float* w, const float* b, void* out, 
     });
   });
   return cmx_check_launch("dwconv_fwd");
+}
+
+int cmx_dwconv3x3_bwd_saved(const void* da, const void* h, const void* gprime, const float* w, void* dh, float* dw,
+                            float* db, float* workspace, int NI, int imgs_per_group, int H, int W, int C, int accumulate,
+                            int dtype, hipStream_t s) {
+  const int CB = tile_cb(C, dtype);
+  CMX_REQUIRE(CB && NI % imgs_per_group == 0 && gprime, CMX_ERR_SHAPE, "dwconv_bwd_saved: C=%d", C);
+  CMX_REQUIRE((long)NI * H * W * C < (1L << 31), CMX_ERR_SHAPE, "dwconv_bwd_saved: tensor too large");
+  const int G = NI / imgs_per_group;
+  const int tx = cdiv(W, TX2), ty = cdiv(H, TY2), ncb = C / CB;
+  const int P = imgs_per_group * ty * tx;
+  const dim3 grid((unsigned)P * ncb, G);
+  CMX_DISPATCH(dtype, T, {
+    if (CB == 32) {
+      hipLaunchKernelGGL((dw2_bwdg_kernel<T, 32>), grid, dim3(256), 0, s, (const T*)da, (const T*)h,
+                         (const T*)gprime, w, (T*)dh, workspace, imgs_per_group, H, W, C, tx, ty, ncb, P);
+    } else if constexpr (sizeof(T) == 2) {
+      hipLaunchKernelGGL((dw2_bwdg_kernel<T, 64>), grid, dim3(256), 0, s, (const T*)da, (const T*)h,
+                         (const T*)gprime, w, (T*)dh, workspace, imgs_per_group, H, W, C, tx, ty, ncb, P);
+    }
+  });
+  if (!dw && !db) return cmx_check_launch("dwconv_bwd_saved");
+  float* tmp = workspace + (size_t)G * P * C * 10;
+  int st = cmx_reduce_partials(workspace, tmp, G, P, C * 10, 0, 1.f, s);
+  if (st) return st;
+  const long tot = (long)G * C * 10;
+  hipLaunchKernelGGL(dw_scatter_kernel, dim3(cdiv(tot, 256) < 4096 ? cdiv(tot, 256) : 4096), dim3(256), 0, s, tmp, dw,
+                     db, G, C, accumulate);
+  return cmx_check_launch("dwconv_bwd_saved");
 }
 
 size_t cmx_dwconv3x3_bwd_workspace(int NI, int imgs_per_group, int H, int W, int C) {

@@ -370,18 +370,34 @@ class DWConvF(Function):
     def forward(ctx, h, w, b, wg, bg, NI, ipg, H, W, act, anchor):
         C = h.shape[-1]
         out = torch.empty_like(h)
-        K.call("cmx_dwconv3x3_fwd", K.ptr(h), K.ptr(w), K.ptr(b), K.ptr(out), NI, ipg, H, W, C, K.ACT[act],
-               K.dtype_code(h), K.stream())
-        ctx.save_for_backward(h, w, b)
+        # LDS-tiled channel counts: also save act'(z) so the backward skips the 3x3 recompute
+        tiled = C % (64 if h.dtype == torch.bfloat16 else 32) == 0
+        gprime = torch.empty_like(h) if tiled else None
+        K.call("cmx_dwconv3x3_fwd_save", K.ptr(h), K.ptr(w), K.ptr(b), K.ptr(out), K.ptr(gprime), NI, ipg, H, W, C,
+               K.ACT[act], K.dtype_code(h), K.stream())
+        ctx.save_for_backward(h, w, b, gprime)
         ctx.meta = (wg, bg, NI, ipg, H, W, act)
         return out
 
     @staticmethod
     def backward(ctx, da):
-        h, w, b = ctx.saved_tensors
+        h, w, b, gprime = ctx.saved_tensors
         wg, bg, NI, ipg, H, W, act = ctx.meta
         C = h.shape[-1]
         da = _c(da)
+        if gprime is not None:
+            dh = torch.empty_like(h) if ctx.needs_input_grad[0] else None
+            nbytes = K.query("cmx_dwconv3x3_bwd_workspace", NI, ipg, H, W, C)
+            ws = K._ws(nbytes, h.device)
+            defer = deferred.ENABLED
+            K.call("cmx_dwconv3x3_bwd_saved", K.ptr(da), K.ptr(h), K.ptr(gprime), K.ptr(w), K.ptr(dh),
+                   0 if defer else K.ptr(wg), 0 if defer else K.ptr(bg), K.ptr(ws), NI, ipg, H, W, C, 0,
+                   K.dtype_code(h), K.stream())
+            if defer:
+                G = NI // ipg
+                P = nbytes // (40 * G * C) - 1
+                deferred.reduce(ws, wg, bg, G, P, P * C * 10, C * 10, C, 10, 9, wg.stride(0), 9, bg.stride(0), 1)
+            return dh, None, None, None, None, None, None, None, None, None, None
         # the LDS-tiled backward (C % 32 == 0) keeps dz on chip; the strip path writes it
         dz = torch.empty_like(h) if C % 32 else None
         dh = torch.empty_like(h) if ctx.needs_input_grad[0] else None
