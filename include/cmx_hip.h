@@ -156,6 +156,12 @@ size_t cmx_gemm_group_record_size(void);
 int cmx_gemm_grouped_splitk(int G, int M, int N, int K, int ones_col);
 int cmx_gemm_group_pack(void* rec, const void* A, const void* B, void* C, float* dbias, float* workspace, int G, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t sA, int64_t sB, int64_t sC, int64_t sdb, int transA, int transB, int out_mode, int ones_col, int splitk, int blk0);
 int cmx_gemm_grouped(const void* recs, int nrec, int total_blocks, hipStream_t stream);
+/* ---- im2col-free convolution on the same GEMM (bf16, NHWC, C % 64 == 0 for the forward): OverlapPatchEmbed.proj
+ *      (k3 s2 p1, dual_segformer.py:196-197) and Attention.sr (kR sR, :95-96).  The forward's A operand is DMA'd
+ *      tap by tap straight from x (padding = zeros from the buffer range check); the weight gradient is one
+ *      grouped-GEMM record per tap whose B operand gathers x at that tap (dW row pitch KH*KW*C). */
+int cmx_conv_implicit_fwd(const void* x, const void* Wt, void* y, const float* bias, float* workspace, int G, int NIg, int H, int Wd, int C, int KH, int KW, int stride, int pad, int Ho, int Wo, int N, int64_t sx, int64_t sW, int64_t sy, int64_t sbias, int splitk, int dtype, hipStream_t stream);
+int cmx_gemm_group_pack_conv_wgrad(void* rec, const void* dy, const void* x, float* dW, float* dbias, float* workspace, int G, int NIg, int H, int Wd, int C, int KH, int KW, int stride, int pad, int Ho, int Wo, int N, int tap, int64_t sdy, int64_t sx, int64_t sdW, int64_t sdb, int splitk, int blk0);
 size_t cmx_reduce_record_size(void);
 int cmx_reduce_pack(void* rec, const float* src, float* dst, float* dst2, int G, int nblk, int64_t sg, int64_t sb, int rows, int cols, int csplit, int64_t dg, int ldd, int64_t dg2, int ldd2, int accumulate, int blk0);
 int cmx_reduce_grouped(const void* recs, int nrec, int total_blocks, hipStream_t stream);

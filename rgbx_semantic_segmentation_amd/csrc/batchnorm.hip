@@ -14,16 +14,23 @@
 #include "cmx_common.h"
 
 namespace {
-constexpr int TPR = 32;           // lanes across channel chunks
-constexpr int RS = 256 / TPR;     // row slots
+// lanes across a row's 16-B channel chunks: TPR = min(32, chunks) rounded up to a power of two,
+// so narrow layers (C = 64 bf16: 8 chunks) do not leave 3 of 4 lanes idle; RS = 256 / TPR rows
+// in flight per block
+int bn_tpr(int chunks) {
+  int t = 4;
+  while (t < chunks && t < 32) t <<= 1;
+  return t;
+}
 
 int bn_nblk(long M) {
-  long nb = (M + RS * 16 - 1) / (RS * 16);
+  long nb = (M + 8 * 16 - 1) / (8 * 16);
   return (int)(nb < 256 ? (nb > 0 ? nb : 1) : 256);
 }
 
-template <typename T>
+template <typename T, int TPR>
 __global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, double* __restrict__ ws, long M, int C) {
+  constexpr int RS = 256 / TPR;
   constexpr int V = VecT<T>::N;
   __shared__ double red[RS][TPR * V * 2];
   const int lane = threadIdx.x % TPR, slot = threadIdx.x / TPR;
@@ -131,12 +138,13 @@ __global__ void bn_apply_kernel(const T* __restrict__ x, const float* __restrict
 }
 
 // partials (nblk, 2, C) doubles of sum g and sum g*xhat
-template <typename T>
+template <typename T, int TPR>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                             const float* __restrict__ mean, const float* __restrict__ invstd,
                                                             const float* __restrict__ gamma, const float* __restrict__ beta,
                                                             const T* __restrict__ res, const float* __restrict__ dscale,
                                                             double* __restrict__ ws, long M, int C, long rps, int act) {
+  constexpr int RS = 256 / TPR;
   constexpr int V = VecT<T>::N;
   __shared__ double red[RS][TPR * V * 2];
   const int lane = threadIdx.x % TPR, slot = threadIdx.x / TPR;
@@ -231,10 +239,16 @@ int cmx_bn_stats(const void* x, double* sums, double* workspace, int64_t M, int 
   const int V = dtype == 0 ? 4 : 8;
   CMX_REQUIRE(C % V == 0 && M > 0, CMX_ERR_SHAPE, "bn_stats: C=%d", C);
   const int nb = bn_nblk(M);
+  const int tpr = bn_tpr(C / V);
+#define BNS(TP) hipLaunchKernelGGL((bn_stats_kernel<T, TP>), dim3(nb, cdiv(C / V, TP)), dim3(256), 0, s, \
+                                   (const T*)x, workspace, (long)M, C)
   CMX_DISPATCH(dtype, T, {
-    hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(nb, cdiv(C / V, TPR)), dim3(256), 0, s, (const T*)x, workspace,
-                       (long)M, C);
+    if (tpr == 4) BNS(4);
+    else if (tpr == 8) BNS(8);
+    else if (tpr == 16) BNS(16);
+    else BNS(32);
   });
+#undef BNS
   hipLaunchKernelGGL(bn_sum_blocks_kernel, dim3(cdiv(2 * C, 64)), dim3(256), 0, s, workspace, sums, nb, C);
   return cmx_check_launch("bn_stats");
 }
@@ -273,11 +287,17 @@ int cmx_bn_bwd_reduce(const void* dy, const void* x, const float* mean, const fl
   const int V = dtype == 0 ? 4 : 8;
   CMX_REQUIRE(C % V == 0 && M > 0, CMX_ERR_SHAPE, "bn_bwd_reduce: C=%d", C);
   const int nb = bn_nblk(M);
+  const int tpr = bn_tpr(C / V);
+#define BNR(TP) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, TP>), dim3(nb, cdiv(C / V, TP)), dim3(256), 0, s, \
+                                   (const T*)dy, (const T*)x, mean, invstd, gamma, beta, (const T*)res, dscale, \
+                                   workspace, (long)M, C, (long)rows_per_sample, act)
   CMX_DISPATCH(dtype, T, {
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(nb, cdiv(C / V, TPR)), dim3(256), 0, s, (const T*)dy,
-                       (const T*)x, mean, invstd, gamma, beta, (const T*)res, dscale, workspace, (long)M, C,
-                       (long)rows_per_sample, act);
+    if (tpr == 4) BNR(4);
+    else if (tpr == 8) BNR(8);
+    else if (tpr == 16) BNR(16);
+    else BNR(32);
   });
+#undef BNR
   hipLaunchKernelGGL(bn_sum_blocks_kernel, dim3(cdiv(2 * C, 64)), dim3(256), 0, s, workspace, sums, nb, C);
   hipLaunchKernelGGL(bn_param_grad_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, sums, dgamma, dbeta, C, accumulate);
   return cmx_check_launch("bn_bwd_reduce");

@@ -49,6 +49,10 @@ struct GemmArgs {
   float* dbias; float* ws;
   int G, M, N, K, K1, kt_per_split, rows_per_sample, act, out_mode, tiles_m, tiles_n, ones_col, nsplit, vec, cvec;
   long lda, lda2, ldb, ldc, sA, sA2, sB, sC, sbias, sdb;
+  // implicit convolution (NHWC input x of H x W x C per image, KH x KW taps, stride, pad -> Ho x Wo):
+  //   conv = 1: A(i = output pixel, k = (kh, kw, c)) gathered from x (forward, no im2col);
+  //   conv = 2: B(j = c, k = output pixel) = x at tap `ctap` of pixel k (weight gradient of one tap)
+  int conv, cH, cW, cC, cKW, cst, cpad, cHo, cWo, ctap;
 };
 
 // block id -> tile id, giving each of the 8 XCDs (hardware deals block b to XCD b % 8) a
@@ -241,16 +245,72 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
   const int kt0 = z * p.kt_per_split;
   const int kt1 = min(nk, kt0 + p.kt_per_split);
 
+  // conv = 1: this lane's output pixels (one per A-staging instruction), decoded once
+  constexpr int NIA = BM / 32;
+  int cv_y[NIA], cv_x[NIA], cv_base[NIA];
+  if constexpr (!TA) {
+    if (p.conv == 1) {
+      const int hw = p.cHo * p.cWo;
+#pragma unroll
+      for (int n = 0; n < NIA; ++n) {
+        const int gr = i0 + (w * NIA + n) * 8 + (lane >> 3);
+        const int b = gr / hw, r2 = gr - b * hw, oy = r2 / p.cWo, ox = r2 - oy * p.cWo;
+        cv_y[n] = gr < p.M ? oy * p.cst - p.cpad : -(1 << 28);   // out-of-range rows: never in bounds
+        cv_x[n] = ox * p.cst - p.cpad;
+        cv_base[n] = (b * p.cH + cv_y[n]) * p.cW + cv_x[n];
+      }
+    }
+  }
+
   auto stage = [&](int kt, char* buf) {
     const int k0 = kt * FBK;
     if constexpr (TA) {
       stage_r<BM>(rA, buf, p.lda, i0, p.M, k0, p.K, w, lane);
     } else {
-      if (k0 < p.K1) stage_k<BM>(rA, buf, p.lda, i0, p.M, k0, p.K1, w, lane);
-      else stage_k<BM>(rA2, buf, p.lda2, i0, p.M, k0 - p.K1, p.K - p.K1, w, lane);
+      if (p.conv == 1) {
+        // a 64-wide k-tile lies inside one tap (C % 64 == 0): tap uniform, 8 channels per chunk
+        const int tap = k0 / p.cC, cb = k0 - tap * p.cC;
+        const int kh = tap / p.cKW, kw = tap - kh * p.cKW;
+#pragma unroll
+        for (int n = 0; n < NIA; ++n) {
+          const int row = (w * NIA + n) * 8 + (lane >> 3);
+          const int c = (lane & 7) ^ ((row >> 1) & 7);
+          const int iy = cv_y[n] + kh, ix = cv_x[n] + kw;
+          const bool ok = k0 < p.K && iy >= 0 && iy < p.cH && ix >= 0 && ix < p.cW;
+          const int off = ok ? ((cv_base[n] + kh * p.cW + kw) * p.cC + cb + c * 8) * 2 : OOB;
+          dma16(rA, lds_addr(buf + (w * NIA + n) * 1024), off);
+        }
+      } else if (k0 < p.K1) {
+        stage_k<BM>(rA, buf, p.lda, i0, p.M, k0, p.K1, w, lane);
+      } else {
+        stage_k<BM>(rA2, buf, p.lda2, i0, p.M, k0 - p.K1, p.K - p.K1, w, lane);
+      }
     }
-    if constexpr (TB) stage_r<BN>(rB, buf + A_BYTES, p.ldb, j0, nreal, k0, p.K, w, lane);
-    else stage_k<BN>(rB, buf + A_BYTES, p.ldb, j0, nreal, k0, p.K, w, lane);
+    if constexpr (TB) {
+      if (p.conv == 2) {
+        // B(j = channel, k = output pixel m) = x[pixel(m) at tap ctap][j]: rows of 8 channels
+        constexpr int NI = BN / 32, CPR = BN / 8, KPI = 64 / CPR;
+        const int hw = p.cHo * p.cWo;
+        const int kh = p.ctap / p.cKW, kw = p.ctap - kh * p.cKW;
+#pragma unroll
+        for (int n = 0; n < NI; ++n) {
+          const int kk = (w * NI + n) * KPI + lane / CPR;
+          const int c = (lane % CPR) ^ tr_swz<BN>(kk);
+          const int m = k0 + kk, gr = j0 + c * 8;
+          int off = OOB;
+          if (m < p.K && gr < nreal) {
+            const int b = m / hw, r2 = m - b * hw, oy = r2 / p.cWo, ox = r2 - oy * p.cWo;
+            const int iy = oy * p.cst - p.cpad + kh, ix = ox * p.cst - p.cpad + kw;
+            if (iy >= 0 && iy < p.cH && ix >= 0 && ix < p.cW) off = (((b * p.cH + iy) * p.cW + ix) * p.cC + gr) * 2;
+          }
+          dma16(rB, lds_addr(buf + A_BYTES + (w * NI + n) * 1024), off);
+        }
+      } else {
+        stage_r<BN>(rB, buf + A_BYTES, p.ldb, j0, nreal, k0, p.K, w, lane);
+      }
+    } else {
+      stage_k<BN>(rB, buf + A_BYTES, p.ldb, j0, nreal, k0, p.K, w, lane);
+    }
   };
 
   auto compute = [&](const char* buf) {
@@ -938,6 +998,82 @@ int cmx_gemm_group_pack(void* rec, const void* A, const void* B, void* C, float*
   r.nblk = a.tiles_m * a.tiles_n * G * a.nsplit;
   memcpy(rec, &r, sizeof(r));
   return r.nblk;
+}
+
+// weight gradient of ONE tap of an NHWC convolution as a grouped-GEMM record:
+// dW[g][n][tap*C + c] (row pitch K = KH*KW*C) = sum_m dy[g][m][n] * x[g][pixel(m) at tap][c]
+int cmx_gemm_group_pack_conv_wgrad(void* rec, const void* dy, const void* x, float* dW, float* dbias, float* workspace,
+                                   int G, int NIg, int H, int Wd, int C, int KH, int KW, int stride, int pad, int Ho,
+                                   int Wo, int N, int tap, int64_t sdy, int64_t sx, int64_t sdW, int64_t sdb,
+                                   int splitk, int blk0) {
+  const int M = NIg * Ho * Wo;                  // reduction length (output pixels)
+  CMX_REQUIRE(rec && G > 0 && N > 0 && C % 8 == 0 && N % 8 == 0 && M % 8 == 0 && tap >= 0 && tap < KH * KW,
+              CMX_ERR_SHAPE, "gemm_group_pack_conv_wgrad: bad problem");
+  CMX_REQUIRE(((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0 && sdy % 8 == 0 && sx % 8 == 0, CMX_ERR_ARG,
+              "gemm_group_pack_conv_wgrad: alignment");
+  CMX_REQUIRE((long)NIg * H * Wd * C < (1L << 30) && (long)M * N < (1L << 30), CMX_ERR_SHAPE,
+              "gemm_group_pack_conv_wgrad: too large for 31-bit offsets");
+  const int ones = dbias ? 1 : 0;
+  const int Nk = C + ones;                      // output columns (+ bias-gradient column)
+  if (splitk <= 0) splitk = cmx_gemm_grouped_splitk(G, N, Nk, M, ones);
+  CMX_REQUIRE(splitk == 1 || workspace, CMX_ERR_ARG, "gemm_group_pack_conv_wgrad: split-K needs a workspace");
+  GroupRec r{};
+  GemmArgs& a = r.a;
+  a.A = dy; a.B = x; a.C = dW + (long)tap * C; a.dbias = dbias; a.ws = workspace;
+  a.G = G; a.M = N; a.N = Nk; a.K = M; a.K1 = M; a.rows_per_sample = 1;
+  a.out_mode = 1; a.ones_col = ones; a.vec = 1;
+  a.lda = N; a.sA = sdy; a.ldb = 0; a.sB = sx; a.ldc = (long)KH * KW * C; a.sC = sdW; a.sdb = sdb;
+  a.cvec = (((uintptr_t)a.C % 16) == 0) && (a.ldc * 4) % 16 == 0 && (sdW * 4) % 16 == 0;
+  a.conv = 2; a.cH = H; a.cW = Wd; a.cC = C; a.cKW = KW; a.cst = stride; a.cpad = pad; a.cHo = Ho; a.cWo = Wo;
+  a.ctap = tap;
+  const int nk = (M + FBK - 1) / FBK;
+  a.kt_per_split = (nk + splitk - 1) / splitk;
+  a.nsplit = (nk + a.kt_per_split - 1) / a.kt_per_split;
+  r.bm = tile_dim(N); r.bn = tile_dim(C);
+  a.tiles_m = cdiv(N, r.bm); a.tiles_n = cdiv(C, r.bn);
+  r.blk0 = blk0;
+  r.nblk = a.tiles_m * a.tiles_n * G * a.nsplit;
+  memcpy(rec, &r, sizeof(r));
+  return r.nblk;
+}
+
+// y[g] (NIg*Ho*Wo, N) = conv(x[g]) + bias[g] with the im2col done by the GEMM's operand DMA
+// (OverlapPatchEmbed.proj k3 s2 p1, dual_segformer.py:196-197; Attention.sr kR sR, :95-96).
+// bf16, NHWC x with C % 64 == 0, weights (N, KH, KW, C).
+int cmx_conv_implicit_fwd(const void* x, const void* Wt, void* y, const float* bias, float* workspace, int G, int NIg,
+                          int H, int Wd, int C, int KH, int KW, int stride, int pad, int Ho, int Wo, int N, int64_t sx,
+                          int64_t sW, int64_t sy, int64_t sbias, int splitk, int dtype, hipStream_t s) {
+  CMX_REQUIRE(dtype == 1 && C % 64 == 0 && N % 8 == 0 && G > 0 && NIg > 0, CMX_ERR_SHAPE,
+              "conv_implicit_fwd: bf16 with C %% 64 == 0 only (C=%d, N=%d)", C, N);
+  CMX_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)Wt & 15) == 0 && ((uintptr_t)y & 15) == 0 && sx % 8 == 0 &&
+              sW % 8 == 0 && sy % 8 == 0, CMX_ERR_ARG, "conv_implicit_fwd: alignment");
+  const long M = (long)NIg * Ho * Wo, K = (long)KH * KW * C;
+  CMX_REQUIRE((long)NIg * H * Wd * C < (1L << 30) && M * N < (1L << 31) && (long)N * K < (1L << 30), CMX_ERR_SHAPE,
+              "conv_implicit_fwd: too large for 31-bit offsets");
+  GemmArgs a{};
+  a.A = x; a.B = Wt; a.C = y; a.bias = bias;
+  a.G = G; a.M = (int)M; a.N = N; a.K = (int)K; a.K1 = (int)K; a.rows_per_sample = 1; a.vec = 1;
+  a.lda = 0; a.sA = sx; a.ldb = K; a.sB = sW; a.ldc = N; a.sC = sy; a.sbias = sbias;
+  a.cvec = (N * 2) % 16 == 0 && (sy * 2) % 16 == 0;
+  a.conv = 1; a.cH = H; a.cW = Wd; a.cC = C; a.cKW = KW; a.cst = stride; a.cpad = pad; a.cHo = Ho; a.cWo = Wo;
+  // the SR conv has few output pixels and a long K (stage 1: 600 x 64 x 4096): split K like a
+  // plain GEMM (splitk <= 0: the library's choice, cmx_gemm_splitk(G, M, N, K, 0, 1))
+  if (splitk <= 0) splitk = auto_split(G, (int)M, N, (int)K, 0);
+  CMX_REQUIRE(splitk == 1 || workspace, CMX_ERR_ARG, "conv_implicit_fwd: split-K needs a workspace");
+  a.ws = workspace;
+  const int nk = (int)((K + FBK - 1) / FBK);
+  a.kt_per_split = (nk + splitk - 1) / splitk;
+  splitk = (nk + a.kt_per_split - 1) / a.kt_per_split;
+  a.nsplit = splitk;
+  int bm, bn;
+  plan_tiles(G, (int)M, N, &bm, &bn);
+  a.tiles_m = cdiv(M, bm); a.tiles_n = cdiv(N, bn);
+  if (bm == 64 && bn == 64) launch_bf16_ns<64, 64>(a, G, splitk, 0, 0, s);
+  else if (bm == 64) launch_bf16_ns<64, 128>(a, G, splitk, 0, 0, s);
+  else if (bn == 64) launch_bf16_ns<128, 64>(a, G, splitk, 0, 0, s);
+  else launch_bf16_ns<128, 128>(a, G, splitk, 0, 0, s);
+  if (splitk > 1) launch_reduce<bf16>(a, G, (long)M * ((N + 7) / 8), s);
+  return cmx_check_launch("conv_implicit_fwd");
 }
 
 int cmx_gemm_grouped(const void* recs, int nrec, int total_blocks, hipStream_t s) {

@@ -45,6 +45,7 @@ _RREC = query("cmx_reduce_record_size")
 class _Queue:
     def __init__(self):
         self.gemms = []        # argument tuples of cmx_gemm_group_pack (minus rec / ws / splitk / blk0)
+        self.convs = []        # argument tuples of cmx_gemm_group_pack_conv_wgrad (one per tap)
         self.reds = []         # argument tuples of cmx_reduce_pack (minus rec / blk0)
         self.keep = []         # tensors the queued work reads or writes
         self.streams = {}      # streams the queued operands were produced on (FFM's side stream)
@@ -65,7 +66,7 @@ _inflight = collections.deque()   # (event, pinned table) of eager uploads
 
 
 def pending() -> bool:
-    return bool(_q.gemms or _q.reds)
+    return bool(_q.gemms or _q.convs or _q.reds)
 
 
 def arm() -> None:
@@ -114,6 +115,33 @@ def wgrad(dz: torch.Tensor, x: torch.Tensor, Wg: torch.Tensor, bg: torch.Tensor 
         return False
     _q.gemms.append(args)
     _q.keep.extend((dz, x))
+    _note_stream()
+    arm()
+    return True
+
+
+def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, Wg: torch.Tensor, bg, geom) -> bool:
+    """Queue the weight gradient of an NHWC convolution without im2col: one grouped-GEMM
+    record per tap, its B operand gathered from x at that tap (cmx_gemm_group_pack_conv_wgrad).
+    dy (G, NIg*Ho*Wo, N) bf16, x (G*NIg, H, W, C) bf16, Wg fp32 (G, N, KH*KW*C), bg (G, N) or None;
+    geom = (G, NIg, H, W, C, KH, KW, stride, pad, Ho, Wo).  False: not eligible, run the
+    im2col path instead."""
+    if not ENABLED or dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16:
+        return False
+    G, NIg, H, W, C, KH, KW, st, pad, Ho, Wo = geom
+    N = dy.shape[-1]
+    if not (dy.is_contiguous() and x.is_contiguous() and Wg.stride(2) == 1 and Wg.shape[-1] == KH * KW * C):
+        return False
+    if C % 8 or N % 8 or (NIg * Ho * Wo) % 8:
+        return False
+    if not _free:
+        reserve()
+    sdy, sx = dy.stride(0), NIg * H * W * C
+    sdb = (bg.stride(0) if bg.dim() == 2 else 0) if bg is not None else 0
+    for tap in range(KH * KW):
+        b = bg if tap == 0 else None
+        _q.convs.append((dy, x, Wg, b, G, NIg, H, W, C, KH, KW, st, pad, Ho, Wo, N, tap, sdy, sx, Wg.stride(0), sdb))
+    _q.keep.extend((dy, x))
     _note_stream()
     arm()
     return True
@@ -184,11 +212,11 @@ def flush() -> None:
     """Issue the queued weight-gradient GEMMs (one launch) and reductions (one launch)."""
     q = _q
     q.armed = False
-    if not (q.gemms or q.reds):
+    if not (q.gemms or q.convs or q.reds):
         return
-    gemms, reds, keep = q.gemms, list(q.reds), q.keep
+    gemms, convs, reds, keep = q.gemms, q.convs, list(q.reds), q.keep
     producers = q.streams
-    q.gemms, q.reds, q.keep, q.streams = [], [], [], {}
+    q.gemms, q.convs, q.reds, q.keep, q.streams = [], [], [], [], {}
     device = keep[0].device
     cur = torch.cuda.current_stream()
     for sid, st in producers.items():      # operands made on another stream: order after them
@@ -196,33 +224,52 @@ def flush() -> None:
             cur.wait_stream(st)
             for t in keep:
                 t.record_stream(cur)
-    if gemms:
-        splits = [query("cmx_gemm_grouped_splitk", a[4], a[5], a[6], a[7], int(a[3] is not None)) for a in gemms]
-        sizes = [query("cmx_gemm_workspace", a[4], a[5], a[6], s) if s > 1 else 0 for a, s in zip(gemms, splits)]
+    if gemms or convs:
+        # one record per problem: (G, M, N incl. bias column, K, has_bias) drives split and slabs
+        dims = [(a[4], a[5], a[6], a[7], a[3] is not None) for a in gemms]
+        for c in convs:
+            G, NIg, H, W, C, KH, KW, st, pad, Ho, Wo, N = c[4:16]
+            dims.append((G, N, C + (1 if c[3] is not None else 0), NIg * Ho * Wo, c[3] is not None))
+        splits = [query("cmx_gemm_grouped_splitk", G, M, N, K, int(hb)) for (G, M, N, K, hb) in dims]
+        sizes = [query("cmx_gemm_workspace", G, M, N, s) if s > 1 else 0 for (G, M, N, K, hb), s in zip(dims, splits)]
         arena = torch.empty(max(1, sum((z + 255) // 256 * 64 for z in sizes)), dtype=torch.float32, device=device)
-        table = _table(len(gemms) * _GREC)
+        nrec = len(dims)
+        table = _table(nrec * _GREC)
         base = table.data_ptr()
         blk, off = 0, 0
-        for i, (a, s, sz) in enumerate(zip(gemms, splits, sizes)):
-            A, B, Wg, bg, G, M, N, K, lda, ldb, ldc, sA, sB, sC, sdb = a
+        for i in range(nrec):
+            s, sz = splits[i], sizes[i]
             ws = arena.data_ptr() + off if s > 1 else 0
-            nb = LIB.cmx_gemm_group_pack(base + i * _GREC, ptr(A), ptr(B), ptr(Wg), ptr(bg), ws, G, M, N, K, lda, ldb,
-                                         ldc, sA, sB, sC, sdb, 1, 1, 1, int(bg is not None), s, blk)
+            if i < len(gemms):
+                A, B, Wg, bg, G, M, N, K, lda, ldb, ldc, sA, sB, sC, sdb = gemms[i]
+                nb = LIB.cmx_gemm_group_pack(base + i * _GREC, ptr(A), ptr(B), ptr(Wg), ptr(bg), ws, G, M, N, K, lda,
+                                             ldb, ldc, sA, sB, sC, sdb, 1, 1, 1, int(bg is not None), s, blk)
+                dst = Wg.data_ptr()
+            else:
+                (dy, x, Wg, bg, G, NIg, H, W, C, KH, KW, st, pad, Ho, Wo, Nout, tap, sdy, sx, sC, sdb) = \
+                    convs[i - len(gemms)]
+                nb = LIB.cmx_gemm_group_pack_conv_wgrad(base + i * _GREC, ptr(dy), ptr(x), ptr(Wg), ptr(bg), ws, G, NIg,
+                                                        H, W, C, KH, KW, st, pad, Ho, Wo, Nout, tap, sdy, sx, sC, sdb, s,
+                                                        blk)
+                M, N, ldc = Nout, C + (1 if bg is not None else 0), KH * KW * C
+                dst = Wg.data_ptr() + 4 * tap * C
             if nb <= 0:
-                raise _lib.CMXError(f"cmx_gemm_group_pack failed ({nb}): {_lib.last_error()}")
+                raise _lib.CMXError(f"grouped-GEMM record pack failed ({nb}): {_lib.last_error()}")
             blk += nb
             if s > 1:
                 # slabs: (G, s, M, Nr) fp32, Nr = real columns; then the bias-gradient column (G, s, M)
                 Nr = N - 1 if bg is not None else N
-                reds.append((ws, Wg.data_ptr(), 0, G, s, s * M * Nr, M * Nr, M, Nr, Nr, sC, ldc, 0, 0, 0))
+                reds.append((ws, dst, 0, G, s, s * M * Nr, M * Nr, M, Nr, Nr, sC, ldc, 0, 0, 0))
                 if bg is not None:
                     reds.append((ws + 4 * G * s * M * Nr, bg.data_ptr(), 0, G, s, s * M, M, 1, M, M, sdb, M, 0, 0, 0))
                 off += (sz + 255) // 256 * 256
-        dev = _upload(table, len(gemms) * _GREC, device)
-        call("cmx_gemm_grouped", dev.data_ptr(), len(gemms), blk, stream())
+        dev = _upload(table, nrec * _GREC, device)
+        call("cmx_gemm_grouped", dev.data_ptr(), nrec, blk, stream())
         keep.append(arena)
         if observer is not None:
-            observer(dev, len(gemms), blk, gemms, keep)
+            # algorithmic work per problem: (G, M, real N, K) and operand / result bytes
+            work = [(G, M, N - (1 if hb else 0), K) for (G, M, N, K, hb) in dims]
+            observer(dev, nrec, blk, work, keep)
     if reds:
         table = _table(len(reds) * _RREC)
         base = table.data_ptr()

@@ -423,7 +423,9 @@ def dwconv(store, conv, h, NI, ipg, H, W, act):
     return DWConvF.apply(h, w, b, wg, bg, NI, ipg, H, W, act, conv.weight)
 
 
-# ---------------------------------------------------------------------------- conv (im2col + GEMM)
+# ---------------------------------------------------------------------------- conv (implicit GEMM / im2col + GEMM)
+# CMX_IMPLICIT_CONV=0 restores the materialised-im2col forward (A/B switch for measurements)
+IMPLICIT_CONV = os.environ.get("CMX_IMPLICIT_CONV", "1") != "0"
 class ConvF(Function):
     """Conv2d as im2col + grouped GEMM on NHWC (OverlapPatchEmbed.proj, Attention.sr)."""
 
@@ -432,6 +434,23 @@ class ConvF(Function):
         # geom: (G, NI, H, Wd, C, KH, KW, stride, pad, Ho, Wo, nchw)
         G, NI, H, Wd, C, KH, KW, st, pad, Ho, Wo, nchw = geom
         Kp = W.shape[-1]
+        if IMPLICIT_CONV and not nchw and x.dtype == torch.bfloat16 and C % 64 == 0 and x.is_contiguous():
+            # im2col-free: the GEMM's A operand is DMA'd tap by tap straight from x
+            N = W.shape[1]
+            NIg = NI // G
+            y = torch.empty(G, NIg * Ho * Wo, N, dtype=x.dtype, device=x.device)
+            M = NIg * Ho * Wo
+            sk = K.query("cmx_gemm_splitk", G, M, N, Kp, 0, 1)
+            ws = K._ws(K.query("cmx_gemm_workspace", G, M, N, sk), x.device) if sk > 1 else None
+            K.call("cmx_conv_implicit_fwd", K.ptr(x), K.ptr(W), K.ptr(y), K.ptr(b), K.ptr(ws), G, NIg, H, Wd, C, KH, KW,
+                   st, pad, Ho, Wo, N, NIg * H * Wd * C, W.stride(0), y.stride(0), b.stride(0) if b is not None else 0,
+                   sk, 1, K.stream())
+            ctx.save_for_backward(x, W)
+            ctx.meta = (Wg, bg, geom)
+            ctx.xshape = x.shape
+            ctx.implicit = True
+            return y
+        ctx.implicit = False
         cols = torch.empty(G, NI // G * Ho * Wo, Kp, dtype=W.dtype, device=W.device)
         if nchw:
             K.call("cmx_im2col_nchw_f32", K.ptr(x), K.ptr(cols), NI, C, H, Wd, KH, KW, st, pad, Ho, Wo, Kp,
@@ -451,10 +470,18 @@ class ConvF(Function):
         Wg, bg, geom = ctx.meta
         G, NI, H, Wd, C, KH, KW, st, pad, Ho, Wo, nchw = geom
         dy = _c(dy)
-        run_side(lambda: _wgrad_into(dy, cols, Wg, bg), dy, cols)
+        if ctx.implicit:
+            x = cols                 # the conv input (no cols were materialised)
+            if not deferred.conv_wgrad(dy, x, Wg, bg, (G, NI // G, H, Wd, C, KH, KW, st, pad, Ho, Wo)):
+                cols = torch.empty(G, NI // G * Ho * Wo, W.shape[-1], dtype=x.dtype, device=x.device)
+                K.call("cmx_im2col_nhwc", K.ptr(x), K.ptr(cols), NI, H, Wd, C, KH, KW, st, pad, Ho, Wo, W.shape[-1],
+                       K.dtype_code(cols), K.stream())
+                _wgrad_into(dy, cols, Wg, bg)
+        else:
+            run_side(lambda: _wgrad_into(dy, cols, Wg, bg), dy, cols)
         dx = None
         if ctx.needs_input_grad[0] and not nchw:
-            dcols = _dgrad(dy, W, torch.empty_like(cols))
+            dcols = _dgrad(dy, W, torch.empty(G, NI // G * Ho * Wo, W.shape[-1], dtype=dy.dtype, device=dy.device))
             dx = torch.empty(NI, H, Wd, C, dtype=dy.dtype, device=dy.device)
             K.call("cmx_col2im_nhwc", K.ptr(dcols), K.ptr(dx), NI, H, Wd, C, KH, KW, st, pad, Ho, Wo, W.shape[-1],
                    K.dtype_code(dx), K.stream())
@@ -682,7 +709,7 @@ def batchnorm(store, bn, x, training, res=None, act="none", dscale=None, rps=1, 
     prm = (store.w(bn.weight, stacked=False, compute=False), store.w(bn.bias, stacked=False, compute=False),
            store.g(bn.weight, stacked=False), store.g(bn.bias, stacked=False), bn.running_mean, bn.running_var,
            float(bn.eps), float(bn.momentum))
-    if training:
+    if training and not getattr(bn, "_nbt_shared", False):
         bn.num_batches_tracked.add_(1)
     return BatchNormF.apply(x, res, prm, training, act, dscale, rps, group, bn.weight)
 

@@ -137,6 +137,16 @@ class EncoderDecoder(nn.Module):
                                     segment_of=backward_segment)
         from .. import deferred
         deferred.reserve()          # pinned launch-record tables for captured backward passes
+        # every BatchNorm's num_batches_tracked is a view into one counter: one increment per
+        # training forward instead of one launch per BN
+        bns = [m for m in self.modules() if isinstance(m, nn.modules.batchnorm._BatchNorm)
+               and m.num_batches_tracked is not None]
+        if bns and getattr(self, "_nbt", None) is None:
+            cnt = torch.stack([m.num_batches_tracked.to(device) for m in bns]).contiguous()
+            for i, m in enumerate(bns):
+                m._buffers["num_batches_tracked"] = cnt[i]
+                m._nbt_shared = True
+            self._nbt = cnt
         return self
 
     def cuda(self, device=None):
@@ -192,6 +202,8 @@ class EncoderDecoder(nn.Module):
         images = torch.cat([rgb, modal_x], 0).to(device=dev, dtype=torch.float32).contiguous()
         dp, d2 = self._stochastic(B, dev)
         group = self.process_group if (self.sync_bn and self.training) else None
+        if self.training and getattr(self, "_nbt", None) is not None:
+            self._nbt.add_(1)
         feats, grids = self.backbone.run(self.store, images, B, H, W, self.training, dp)
         logits = self.decode_head.run(self.store, feats, grids, B, self.training, dscale=d2, group=group)
         return logits, grids[0]

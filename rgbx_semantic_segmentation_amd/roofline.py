@@ -44,8 +44,8 @@ def measure_dominant(model, batch, iters: int = 20):
     rgb, x, lab = batch
     seen = []
 
-    def obs(dev, nrec, blk, gemms, keep):
-        seen.append((dev, nrec, blk, list(gemms), list(keep)))
+    def obs(dev, nrec, blk, work, keep):
+        seen.append((dev, nrec, blk, list(work), list(keep)))
 
     deferred.observer = obs
     try:
@@ -56,11 +56,10 @@ def measure_dominant(model, batch, iters: int = 20):
     torch.cuda.synchronize()
     if not seen:
         return None
-    dev, nrec, blk, gemms, keep = max(seen, key=lambda s: s[2])
+    dev, nrec, blk, work, keep = max(seen, key=lambda s: s[2])
     flops = 0.0
     nbytes = 0.0
-    for (A, B, Wg, bg, G, M, N, K, *_rest) in gemms:
-        Nr = N - 1 if bg is not None else N
+    for (G, M, Nr, K) in work:
         flops += 2.0 * G * M * Nr * K
         nbytes += 2.0 * G * (M + Nr) * K + 4.0 * G * M * Nr
     launch = lambda: _lib.call("cmx_gemm_grouped", dev.data_ptr(), nrec, blk, _lib.stream())
@@ -75,7 +74,7 @@ def measure_dominant(model, batch, iters: int = 20):
     torch.cuda.synchronize()
     t = s.elapsed_time(e) / iters * 1e-3
     traffic, src = _pmc_traffic("gemm_grouped_kernel")
-    out = {"kernel": f"gemm_grouped_kernel (all {nrec} weight-gradient GEMMs of the backward, one launch, "
+    out = {"kernel": f"gemm_grouped_kernel (all {nrec} weight-gradient GEMM problems of the backward, one launch, "
                      f"{blk} workgroups)",
            "bound": "mfma", "achieved": round(flops / t / 1e12, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
            "frac": round(flops / t / 1e12 / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
@@ -83,5 +82,5 @@ def measure_dominant(model, batch, iters: int = 20):
            "algorithmic_bytes_per_launch": nbytes, "achieved_hbm_gbs": round(nbytes / t / 1e9, 1)}
     if src:
         out["traffic_source"] = src
-    del seen, keep, gemms
+    del seen, keep, work
     return out

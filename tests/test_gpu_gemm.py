@@ -6,6 +6,8 @@ N = 40 the NYUv2 classifier), every epilogue (bias, GELU / ReLU, DropPath-scaled
 fp32 store / accumulate) and both storage dtypes.  Tolerances: fp32 mode 1e-5 relative
 (exact fp32 MFMA, summation order differs); bf16 mode 1e-2 relative (bf16 output
 rounding, fp32 accumulation)."""
+import math
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -157,3 +159,45 @@ def test_gemm_step_shapes_bf16(dev, G, M, N, K, tA, tB):
     Kn.gemm(Av, Bv, C, out_mode=1)
     ref = torch.bmm(A.float(), B.float().transpose(1, 2))
     assert rel(C, ref) < 1e-5
+
+
+@pytest.mark.parametrize("Cin,Cout,k,st,pad,H,W", [(64, 128, 3, 2, 1, 30, 40), (128, 320, 3, 2, 1, 15, 20),
+                                                   (64, 64, 8, 8, 0, 120, 160), (320, 320, 2, 2, 0, 30, 40)])
+def test_implicit_conv(dev, Cin, Cout, k, st, pad, H, W):
+    """im2col-free conv (cmx_conv_implicit_fwd) and its per-tap grouped weight gradient
+    (deferred.conv_wgrad) against torch fp32 conv2d: OverlapPatchEmbed k3 s2 p1 and the SRA
+    spatial-reduction conv kR sR (dual_segformer.py:95-96, 196-197).  bf16 tolerance 1e-2."""
+    from rgbx_semantic_segmentation_amd import deferred
+    from rgbx_semantic_segmentation_amd import kernels as K
+    torch.manual_seed(3)
+    G, NIg = 2, 2
+    Ho, Wo = (H + 2 * pad - k) // st + 1, (W + 2 * pad - k) // st + 1
+    x = torch.randn(G * NIg, H, W, Cin, device=dev).bfloat16()
+    Wt = (torch.randn(G, Cout, k, k, Cin, device=dev) / math.sqrt(k * k * Cin)).bfloat16()
+    b = torch.randn(G, Cout, device=dev)
+    y = torch.empty(G, NIg * Ho * Wo, Cout, device=dev, dtype=torch.bfloat16)
+    M = NIg * Ho * Wo
+    sk = K.query("cmx_gemm_splitk", G, M, Cout, k * k * Cin, 0, 1)
+    ws = K._ws(K.query("cmx_gemm_workspace", G, M, Cout, sk), dev) if sk > 1 else None
+    K.call("cmx_conv_implicit_fwd", K.ptr(x), K.ptr(Wt), K.ptr(y), K.ptr(b), K.ptr(ws), G, NIg, H, W, Cin, k, k, st,
+           pad, Ho, Wo, Cout, NIg * H * W * Cin, Wt[0].numel(), y.stride(0), Cout, sk, 1, K.stream())
+    xr = x.float().view(G, NIg, H, W, Cin).permute(0, 1, 4, 2, 3)
+    for g in range(G):
+        ref = F.conv2d(xr[g], Wt[g].float().permute(0, 3, 1, 2), b[g], stride=st, padding=pad)   # (NIg, Cout, Ho, Wo)
+        got = y[g].view(NIg, Ho, Wo, Cout).permute(0, 3, 1, 2)
+        assert rel(got, ref) < 1e-2, rel(got, ref)
+    # weight gradient of every tap in one grouped launch
+    dy = torch.randn(G, NIg * Ho * Wo, Cout, device=dev).bfloat16()
+    Wg = torch.full((G, Cout, k * k * Cin), float("nan"), device=dev)
+    bg = torch.full((G, Cout), float("nan"), device=dev)
+    assert deferred.conv_wgrad(dy, x, Wg, bg, (G, NIg, H, W, Cin, k, k, st, pad, Ho, Wo))
+    deferred.flush()
+    torch.cuda.synchronize()
+    for g in range(G):
+        wr = Wt[g].float().permute(0, 3, 1, 2).clone().requires_grad_(True)
+        xg = xr[g].clone()
+        out = F.conv2d(xg, wr, None, stride=st, padding=pad)
+        out.backward(dy[g].float().view(NIg, Ho, Wo, Cout).permute(0, 3, 1, 2))
+        ref_w = wr.grad.permute(0, 2, 3, 1).reshape(Cout, -1)
+        assert rel(Wg[g], ref_w) < 1e-2, rel(Wg[g], ref_w)
+        assert rel(bg[g], dy[g].float().sum(0)) < 1e-2
