@@ -112,6 +112,7 @@ int cmx_frm_combine_bwd(const void* dout, const void* x, const float* cw, const 
  *      fp64 channel sums -> (all-reduce for SyncBN) -> finalize; fused residual / act / Dropout2d. */
 size_t cmx_bn_workspace(int64_t M, int C);
 int cmx_bn_stats(const void* x, double* sums, double* workspace, int64_t M, int C, int dtype, hipStream_t stream);
+int cmx_bn_stats_finalize(const void* x, double* sums, double* workspace, int64_t M, int C, float eps, float momentum, float* running_mean, float* running_var, float* mean, float* invstd, int dtype, hipStream_t stream);
 int cmx_bn_finalize(const double* sums, double count, float eps, float momentum, float* running_mean, float* running_var, float* mean, float* invstd, int C, int training, hipStream_t stream);
 int cmx_bn_apply(const void* x, const float* mean, const float* invstd, const float* gamma, const float* beta, const void* res, const float* dscale, void* y, int64_t M, int C, int64_t rows_per_sample, int act, int dtype, hipStream_t stream);
 int cmx_bn_bwd_reduce(const void* dy, const void* x, const float* mean, const float* invstd, const float* gamma, const float* beta, const void* res, const float* dscale, double* sums, float* dgamma, float* dbeta, double* workspace, int64_t M, int C, int64_t rows_per_sample, int act, int accumulate, int dtype, hipStream_t stream);

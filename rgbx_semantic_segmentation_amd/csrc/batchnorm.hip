@@ -11,6 +11,12 @@
 // backward: g = dy * dscale * act'(pre);  local sums (sum g, sum g*xhat) give dgamma/dbeta
 //        (per-rank, averaged by the gradient all-reduce like PyTorch SyncBN); the sums
 //        (all-reduced for SyncBN) give dx = gamma*invstd*(g - sum_g/n - xhat*sum_gx/n).
+//
+// Launch shape: the row reductions keep 4 rows' loads in flight per lane (a 2-4 us HBM latency
+// per dependent load otherwise bounds them); the per-block partials are folded by one
+// 1024-lane kernel that also finalizes (mean / invstd / running stats) or writes the
+// parameter gradients; the elementwise passes stage per-channel coefficients in LDS once
+// per block (no per-element fp64 divide or scalar parameter loads).
 #include "cmx_common.h"
 
 namespace {
@@ -28,6 +34,9 @@ int bn_nblk(long M) {
   return (int)(nb < 256 ? (nb > 0 ? nb : 1) : 256);
 }
 
+constexpr int UNR = 4;            // rows per lane with loads in flight together
+constexpr int BN_MAXC = 2048;     // LDS coefficient staging limit of the elementwise passes
+
 template <typename T, int TPR>
 __global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, double* __restrict__ ws, long M, int C) {
   constexpr int RS = 256 / TPR;
@@ -40,11 +49,22 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, 
 #pragma unroll
   for (int j = 0; j < V; ++j) s[j] = q[j] = 0.0;
   if (live) {
-    for (long m = (long)blockIdx.x * RS + slot; m < M; m += (long)gridDim.x * RS) {
-      float v[V];
-      load_vec<T>(x + m * C + ch * V, v);
+    const long stride = (long)gridDim.x * RS;
+    for (long m = (long)blockIdx.x * RS + slot; m < M; m += UNR * stride) {
+      float v[UNR][V];
 #pragma unroll
-      for (int j = 0; j < V; ++j) { s[j] += v[j]; q[j] += (double)v[j] * v[j]; }
+      for (int u = 0; u < UNR; ++u) {
+        const long mu = m + u * stride;
+        if (mu < M) load_vec<T>(x + mu * C + ch * V, v[u]);
+        else {
+#pragma unroll
+          for (int j = 0; j < V; ++j) v[u][j] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)
+#pragma unroll
+        for (int j = 0; j < V; ++j) { s[j] += v[u][j]; q[j] += (double)v[u][j] * v[u][j]; }
     }
   }
 #pragma unroll
@@ -58,21 +78,66 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, 
   }
 }
 
-// sums (2, C) = sum over blocks of ws (nblk, 2, C); 64 columns x 4 row slices per block
-__global__ __launch_bounds__(256) void bn_sum_blocks_kernel(const double* __restrict__ ws, double* __restrict__ sums,
-                                                            int nblk, int C) {
-  __shared__ double red[4][64];
+// what the block-partials fold does with the (2, C) sums besides storing them
+struct BnFold {
+  int mode;                        // 0: sums only; 1: + finalize (forward); 2: + dgamma / dbeta (backward)
+  double count;
+  float eps, momentum;
+  float *running_mean, *running_var, *mean, *invstd;
+  float *dgamma, *dbeta;
+  int accumulate;
+};
+
+// sums (2, C) = sum over blocks of ws (nblk, 2, C).  A block owns 32 channels (both halves:
+// lanes tx < 32 sum column c, lanes tx >= 32 column C + c) and 16 row slices of the partials,
+// 4 independent loads in flight per lane; then the channel's epilogue per BnFold.
+__global__ __launch_bounds__(1024) void bn_fold_kernel(const double* __restrict__ ws, double* __restrict__ sums,
+                                                      int nblk, int C, BnFold f) {
+  __shared__ double red[16][65];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int e = blockIdx.x * 64 + tx;
-  double a0 = 0.0, a1 = 0.0;
-  if (e < 2 * C) {
+  const int c = blockIdx.x * 32 + (tx & 31);
+  const int e = (tx < 32 ? 0 : C) + c;
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
+  if (c < C) {
     int b = ty;
-    for (; b + 4 < nblk; b += 8) { a0 += ws[(long)b * 2 * C + e]; a1 += ws[(long)(b + 4) * 2 * C + e]; }
-    for (; b < nblk; b += 4) a0 += ws[(long)b * 2 * C + e];
+    for (; b + 48 < nblk; b += 64) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] += ws[(long)(b + 16 * u) * 2 * C + e];
+    }
+    for (; b < nblk; b += 16) a[0] += ws[(long)b * 2 * C + e];
   }
-  red[ty][tx] = a0 + a1;
+  red[ty][tx] = (a[0] + a[1]) + (a[2] + a[3]);
   __syncthreads();
-  if (ty == 0 && e < 2 * C) sums[e] = ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx];
+  if (ty != 0) return;
+  double t = 0.0;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) t += red[r][tx];
+  const double t2 = __shfl(t, (tx + 32) & 63);      // lane tx < 32: the sum of column C + c
+  if (c >= C) return;
+  sums[e] = t;
+  if (tx >= 32) return;
+  const double s1 = t, s2 = t2;
+  if (f.mode == 1) {
+    const double mu = s1 / f.count;
+    double var = s2 / f.count - mu * mu;
+    if (var < 0) var = 0;
+    f.mean[c] = (float)mu;
+    f.invstd[c] = (float)(1.0 / sqrt(var + (double)f.eps));
+    if (f.running_mean) {
+      const double unb = f.count > 1 ? var * f.count / (f.count - 1) : var;
+      f.running_mean[c] = (float)((1.0 - f.momentum) * f.running_mean[c] + f.momentum * mu);
+      f.running_var[c] = (float)((1.0 - f.momentum) * f.running_var[c] + f.momentum * unb);
+    }
+  } else if (f.mode == 2) {
+    const float gb = (float)s1, gg = (float)s2;
+    if (f.dbeta) f.dbeta[c] = f.accumulate ? f.dbeta[c] + gb : gb;
+    if (f.dgamma) f.dgamma[c] = f.accumulate ? f.dgamma[c] + gg : gg;
+  }
+}
+
+int launch_fold(const double* ws, double* sums, int nblk, int C, const BnFold& f, hipStream_t s) {
+  hipLaunchKernelGGL(bn_fold_kernel, dim3(cdiv(C, 32)), dim3(1024), 0, s, ws, sums, nblk, C, f);
+  return 0;
 }
 
 __global__ void bn_finalize_kernel(const double* __restrict__ sums, double count, float eps, float momentum,
@@ -100,38 +165,48 @@ __global__ void bn_eval_stats_kernel(const float* __restrict__ rm, const float* 
   invstd[c] = 1.f / sqrtf(rv[c] + eps);
 }
 
-template <typename T>
-__device__ __forceinline__ void bn_pre(const T* x, const T* res, const float* mean, const float* invstd,
-                                       const float* gamma, const float* beta, long e, int c0, float* xh, float* pre) {
-  constexpr int V = VecT<T>::N;
-  float v[V], r[V];
-  load_vec<T>(x + e, v);
-  if (res) load_vec<T>(res + e, r);
+// 8 (bf16) / 4 (fp32) consecutive floats of an LDS or global array
+template <int V>
+__device__ __forceinline__ void ld_coef(const float* p, float* o) {
 #pragma unroll
-  for (int j = 0; j < V; ++j) {
-    const int c = c0 + j;
-    xh[j] = (v[j] - mean[c]) * invstd[c];
-    pre[j] = xh[j] * gamma[c] + beta[c] + (res ? r[j] : 0.f);
+  for (int j = 0; j < V; j += 4) {
+    const float4 t = *reinterpret_cast<const float4*>(p + j);
+    o[j] = t.x; o[j + 1] = t.y; o[j + 2] = t.z; o[j + 3] = t.w;
   }
 }
 
+// y = act(x*sc + sh + res) * dscale, sc = gamma*invstd, sh = beta - mean*sc (LDS per block)
 template <typename T>
-__global__ void bn_apply_kernel(const T* __restrict__ x, const float* __restrict__ mean, const float* __restrict__ invstd,
-                                const float* __restrict__ gamma, const float* __restrict__ beta, const T* __restrict__ res,
-                                const float* __restrict__ dscale, T* __restrict__ y, long M, int C, long rps, int act) {
+__global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x, const float* __restrict__ mean,
+                                                       const float* __restrict__ invstd, const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, const T* __restrict__ res,
+                                                       const float* __restrict__ dscale, T* __restrict__ y, long M,
+                                                       int C, long rps, int act) {
   constexpr int V = VecT<T>::N;
+  extern __shared__ float sp[];
+  float* ssc = sp;
+  float* ssh = sp + C;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const float sc = gamma[c] * invstd[c];
+    ssc[c] = sc;
+    ssh[c] = beta[c] - mean[c] * sc;
+  }
+  __syncthreads();
   const long nvec = M * C / V;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)nvec; i += gridDim.x * blockDim.x) {
     const int e = i * V;
     const int c0 = e % C;
-    float xh[V], pre[V];
-    bn_pre<T>(x, res, mean, invstd, gamma, beta, e, c0, xh, pre);
+    float v[V], sc[V], sh[V], r[V], ds[V];
+    load_vec<T>(x + e, v);
+    if (res) load_vec<T>(res + e, r);
+    ld_coef<V>(ssc + c0, sc);
+    ld_coef<V>(ssh + c0, sh);
+    if (dscale) ld_coef<V>(dscale + (long)((e / C) / (int)rps) * C + c0, ds);
     float o[V];
-    const int b = (e / C) / (int)rps;
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      o[j] = act_fwd(pre[j], act);
-      if (dscale) o[j] *= dscale[b * C + c0 + j];
+      o[j] = act_fwd(v[j] * sc[j] + sh[j] + (res ? r[j] : 0.f), act);
+      if (dscale) o[j] *= ds[j];
     }
     store_vec<T>(y + e, o);
   }
@@ -155,19 +230,41 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
   for (int j = 0; j < V; ++j) s[j] = q[j] = 0.0;
   if (live) {
     const int c0 = ch * V;
-    for (long m = (long)blockIdx.x * RS + slot; m < M; m += (long)gridDim.x * RS) {
-      const long e = m * C + c0;
-      float xh[V], pre[V], d[V];
-      bn_pre<T>(x, res, mean, invstd, gamma, beta, e, c0, xh, pre);
-      load_vec<T>(dy + e, d);
-      const long b = m / rps;
+    float mu[V], is[V], sc[V], sh[V];
 #pragma unroll
-      for (int j = 0; j < V; ++j) {
-        float g = d[j] * act_grad(pre[j], act);
-        if (dscale) g *= dscale[b * C + c0 + j];
-        s[j] += g;
-        q[j] += (double)g * xh[j];
+    for (int j = 0; j < V; ++j) {
+      mu[j] = mean[c0 + j];
+      is[j] = invstd[c0 + j];
+      sc[j] = gamma[c0 + j] * is[j];
+      sh[j] = beta[c0 + j] - mu[j] * sc[j];
+    }
+    const long stride = (long)gridDim.x * RS;
+    for (long m = (long)blockIdx.x * RS + slot; m < M; m += UNR * stride) {
+      float xv[UNR][V], d[UNR][V], r[UNR][V], ds[UNR][V];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const long mu_ = m + u * stride;
+        if (mu_ < M) {
+          const long e = mu_ * C + c0;
+          load_vec<T>(x + e, xv[u]);
+          load_vec<T>(dy + e, d[u]);
+          if (res) load_vec<T>(res + e, r[u]);
+          if (dscale) ld_coef<V>(dscale + (mu_ / rps) * C + c0, ds[u]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < V; ++j) { xv[u][j] = 0.f; d[u][j] = 0.f; r[u][j] = 0.f; ds[u][j] = 0.f; }
+        }
       }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const float pre = xv[u][j] * sc[j] + sh[j] + (res ? r[u][j] : 0.f);
+          float g = d[u][j] * act_grad(pre, act);
+          if (dscale) g *= ds[u][j];
+          s[j] += g;
+          q[j] += (double)g * ((xv[u][j] - mu[j]) * is[j]);
+        }
     }
   }
 #pragma unroll
@@ -181,43 +278,52 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
   }
 }
 
-__global__ void bn_param_grad_kernel(const double* __restrict__ sums, float* __restrict__ dgamma,
-                                     float* __restrict__ dbeta, int C, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  const float gb = (float)sums[c], gg = (float)sums[C + c];
-  if (dbeta) dbeta[c] = accumulate ? dbeta[c] + gb : gb;
-  if (dgamma) dgamma[c] = accumulate ? dgamma[c] + gg : gg;
-}
-
+// dx = sc*(g - mg - xhat*mgx) (training) or sc*g (eval); per-channel mean, invstd, sc, sh,
+// mg = sum_g/n and mgx = sum_gx/n staged in LDS once per block
 template <typename T>
-__global__ void bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x, const float* __restrict__ mean,
-                                    const float* __restrict__ invstd, const float* __restrict__ gamma,
-                                    const float* __restrict__ beta, const T* __restrict__ res,
-                                    const float* __restrict__ dscale, const double* __restrict__ sums, double count,
-                                    T* __restrict__ dx, T* __restrict__ dres, long M, int C, long rps, int act,
-                                    int training) {
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                           const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                           const T* __restrict__ res, const float* __restrict__ dscale,
+                                                           const double* __restrict__ sums, double rcount,
+                                                           T* __restrict__ dx, T* __restrict__ dres, long M, int C,
+                                                           long rps, int act, int training) {
   constexpr int V = VecT<T>::N;
+  extern __shared__ float sp[];
+  float *smu = sp, *sis = sp + C, *ssc = sp + 2 * C, *ssh = sp + 3 * C, *smg = sp + 4 * C, *smx = sp + 5 * C;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const float is = invstd[c], sc = gamma[c] * is;
+    smu[c] = mean[c];
+    sis[c] = is;
+    ssc[c] = sc;
+    ssh[c] = beta[c] - mean[c] * sc;
+    smg[c] = training ? (float)(sums[c] * rcount) : 0.f;
+    smx[c] = training ? (float)(sums[C + c] * rcount) : 0.f;
+  }
+  __syncthreads();
   const long nvec = M * C / V;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)nvec; i += gridDim.x * blockDim.x) {
     const int e = i * V;
     const int c0 = e % C;
-    float xh[V], pre[V], d[V], o[V], gr[V];
-    bn_pre<T>(x, res, mean, invstd, gamma, beta, e, c0, xh, pre);
+    float xv[V], d[V], r[V], ds[V], mu[V], is[V], sc[V], sh[V], mg[V], mx[V];
+    load_vec<T>(x + e, xv);
     load_vec<T>(dy + e, d);
-    const int b = (e / C) / (int)rps;
+    if (res) load_vec<T>(res + e, r);
+    if (dscale) ld_coef<V>(dscale + (long)((e / C) / (int)rps) * C + c0, ds);
+    ld_coef<V>(smu + c0, mu);
+    ld_coef<V>(sis + c0, is);
+    ld_coef<V>(ssc + c0, sc);
+    ld_coef<V>(ssh + c0, sh);
+    ld_coef<V>(smg + c0, mg);
+    ld_coef<V>(smx + c0, mx);
+    float o[V], gr[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      const int c = c0 + j;
-      float g = d[j] * act_grad(pre[j], act);
-      if (dscale) g *= dscale[b * C + c];
+      const float pre = xv[j] * sc[j] + sh[j] + (res ? r[j] : 0.f);
+      float g = d[j] * act_grad(pre, act);
+      if (dscale) g *= ds[j];
       gr[j] = g;
-      if (training) {
-        const float mg = (float)(sums[c] / count), mgx = (float)(sums[C + c] / count);
-        o[j] = gamma[c] * invstd[c] * (g - mg - xh[j] * mgx);
-      } else {
-        o[j] = gamma[c] * invstd[c] * g;
-      }
+      o[j] = sc[j] * (g - mg[j] - (xv[j] - mu[j]) * is[j] * mx[j]);
     }
     store_vec<T>(dx + e, o);
     if (dres) store_vec<T>(dres + e, gr);
@@ -226,7 +332,21 @@ __global__ void bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restric
 
 unsigned ew_grid(long nvec) {
   const unsigned g = cdiv(nvec, 256);
-  return g < 8192 ? (g ? g : 1) : 8192;
+  return g < 2048 ? (g ? g : 1) : 2048;
+}
+
+template <typename T>
+int launch_stats(const void* x, double* workspace, long M, int C, int nb, hipStream_t s) {
+  constexpr int V = VecT<T>::N;
+  const int tpr = bn_tpr(C / V);
+#define BNS(TP) hipLaunchKernelGGL((bn_stats_kernel<T, TP>), dim3(nb, cdiv(C / V, TP)), dim3(256), 0, s, \
+                                   (const T*)x, workspace, M, C)
+  if (tpr == 4) BNS(4);
+  else if (tpr == 8) BNS(8);
+  else if (tpr == 16) BNS(16);
+  else BNS(32);
+#undef BNS
+  return 0;
 }
 }  // namespace
 
@@ -239,18 +359,27 @@ int cmx_bn_stats(const void* x, double* sums, double* workspace, int64_t M, int 
   const int V = dtype == 0 ? 4 : 8;
   CMX_REQUIRE(C % V == 0 && M > 0, CMX_ERR_SHAPE, "bn_stats: C=%d", C);
   const int nb = bn_nblk(M);
-  const int tpr = bn_tpr(C / V);
-#define BNS(TP) hipLaunchKernelGGL((bn_stats_kernel<T, TP>), dim3(nb, cdiv(C / V, TP)), dim3(256), 0, s, \
-                                   (const T*)x, workspace, (long)M, C)
-  CMX_DISPATCH(dtype, T, {
-    if (tpr == 4) BNS(4);
-    else if (tpr == 8) BNS(8);
-    else if (tpr == 16) BNS(16);
-    else BNS(32);
-  });
-#undef BNS
-  hipLaunchKernelGGL(bn_sum_blocks_kernel, dim3(cdiv(2 * C, 64)), dim3(256), 0, s, workspace, sums, nb, C);
+  CMX_DISPATCH(dtype, T, { launch_stats<T>(x, workspace, (long)M, C, nb, s); });
+  BnFold f{};
+  launch_fold(workspace, sums, nb, C, f, s);
   return cmx_check_launch("bn_stats");
+}
+
+// local statistics in two launches: the row reduction, then the fold that also finalizes
+// (mean / invstd, running stats with momentum and the unbiased variance) -- BatchNorm2d
+// training forward without a SyncBN exchange between the sums and the finalize
+int cmx_bn_stats_finalize(const void* x, double* sums, double* workspace, int64_t M, int C, float eps, float momentum,
+                          float* running_mean, float* running_var, float* mean, float* invstd, int dtype,
+                          hipStream_t s) {
+  const int V = dtype == 0 ? 4 : 8;
+  CMX_REQUIRE(C % V == 0 && M > 0, CMX_ERR_SHAPE, "bn_stats_finalize: C=%d", C);
+  const int nb = bn_nblk(M);
+  CMX_DISPATCH(dtype, T, { launch_stats<T>(x, workspace, (long)M, C, nb, s); });
+  BnFold f{};
+  f.mode = 1; f.count = (double)M; f.eps = eps; f.momentum = momentum;
+  f.running_mean = running_mean; f.running_var = running_var; f.mean = mean; f.invstd = invstd;
+  launch_fold(workspace, sums, nb, C, f, s);
+  return cmx_check_launch("bn_stats_finalize");
 }
 
 // training: mean/invstd from (possibly all-reduced) sums over `count` rows, running stats
@@ -271,10 +400,12 @@ int cmx_bn_apply(const void* x, const float* mean, const float* invstd, const fl
                  const void* res, const float* dscale, void* y, int64_t M, int C, int64_t rows_per_sample, int act,
                  int dtype, hipStream_t s) {
   const int V = dtype == 0 ? 4 : 8;
-  CMX_REQUIRE(C % V == 0, CMX_ERR_SHAPE, "bn_apply: C=%d", C);
+  CMX_REQUIRE(C % V == 0 && C <= BN_MAXC, CMX_ERR_SHAPE, "bn_apply: C=%d", C);
+  CMX_REQUIRE(!dscale || ((uintptr_t)dscale & 15) == 0, CMX_ERR_ARG, "bn_apply: dscale alignment");
   CMX_DISPATCH(dtype, T, {
-    hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(ew_grid(M * C / V)), dim3(256), 0, s, (const T*)x, mean, invstd,
-                       gamma, beta, (const T*)res, dscale, (T*)y, (long)M, C, (long)rows_per_sample, act);
+    hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(ew_grid(M * C / V)), dim3(256), 2 * C * sizeof(float), s,
+                       (const T*)x, mean, invstd, gamma, beta, (const T*)res, dscale, (T*)y, (long)M, C,
+                       (long)rows_per_sample, act);
   });
   return cmx_check_launch("bn_apply");
 }
@@ -286,6 +417,7 @@ int cmx_bn_bwd_reduce(const void* dy, const void* x, const float* mean, const fl
                       int accumulate, int dtype, hipStream_t s) {
   const int V = dtype == 0 ? 4 : 8;
   CMX_REQUIRE(C % V == 0 && M > 0, CMX_ERR_SHAPE, "bn_bwd_reduce: C=%d", C);
+  CMX_REQUIRE(!dscale || ((uintptr_t)dscale & 15) == 0, CMX_ERR_ARG, "bn_bwd_reduce: dscale alignment");
   const int nb = bn_nblk(M);
   const int tpr = bn_tpr(C / V);
 #define BNR(TP) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, TP>), dim3(nb, cdiv(C / V, TP)), dim3(256), 0, s, \
@@ -298,8 +430,9 @@ int cmx_bn_bwd_reduce(const void* dy, const void* x, const float* mean, const fl
     else BNR(32);
   });
 #undef BNR
-  hipLaunchKernelGGL(bn_sum_blocks_kernel, dim3(cdiv(2 * C, 64)), dim3(256), 0, s, workspace, sums, nb, C);
-  hipLaunchKernelGGL(bn_param_grad_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, sums, dgamma, dbeta, C, accumulate);
+  BnFold f{};
+  f.mode = 2; f.dgamma = dgamma; f.dbeta = dbeta; f.accumulate = accumulate;
+  launch_fold(workspace, sums, nb, C, f, s);
   return cmx_check_launch("bn_bwd_reduce");
 }
 
@@ -309,11 +442,14 @@ int cmx_bn_bwd_apply(const void* dy, const void* x, const float* mean, const flo
                      void* dx, void* dres, int64_t M, int C, int64_t rows_per_sample, int act, int training, int dtype,
                      hipStream_t s) {
   const int V = dtype == 0 ? 4 : 8;
-  CMX_REQUIRE(C % V == 0, CMX_ERR_SHAPE, "bn_bwd_apply: C=%d", C);
+  CMX_REQUIRE(C % V == 0 && C <= BN_MAXC, CMX_ERR_SHAPE, "bn_bwd_apply: C=%d", C);
+  CMX_REQUIRE(!dscale || ((uintptr_t)dscale & 15) == 0, CMX_ERR_ARG, "bn_bwd_apply: dscale alignment");
+  CMX_REQUIRE(!training || count > 0, CMX_ERR_ARG, "bn_bwd_apply: count");
+  const double rcount = training ? 1.0 / count : 0.0;
   CMX_DISPATCH(dtype, T, {
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(ew_grid(M * C / V)), dim3(256), 0, s, (const T*)dy, (const T*)x,
-                       mean, invstd, gamma, beta, (const T*)res, dscale, sums, count, (T*)dx, (T*)dres, (long)M, C,
-                       (long)rows_per_sample, act, training);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(ew_grid(M * C / V)), dim3(256), 6 * C * sizeof(float), s,
+                       (const T*)dy, (const T*)x, mean, invstd, gamma, beta, (const T*)res, dscale, sums, rcount,
+                       (T*)dx, (T*)dres, (long)M, C, (long)rows_per_sample, act, training);
   });
   return cmx_check_launch("bn_bwd_apply");
 }

@@ -667,10 +667,14 @@ class BatchNormF(Function):
         if training:
             sums = torch.empty(2, C, dtype=torch.float64, device=x.device)
             ws = torch.empty(max(1, K.query("cmx_bn_workspace", M, C) // 8), dtype=torch.float64, device=x.device)
-            K.call("cmx_bn_stats", K.ptr(x), K.ptr(sums), K.ptr(ws), M, C, dt, K.stream())
-            count = sync_bn_sums(sums, count, group)
-            K.call("cmx_bn_finalize", K.ptr(sums), count, eps, momentum, K.ptr(rm), K.ptr(rv), K.ptr(mean),
-                   K.ptr(invstd), C, 1, K.stream())
+            if group is None:       # local statistics: the fold finalizes (no exchange in between)
+                K.call("cmx_bn_stats_finalize", K.ptr(x), K.ptr(sums), K.ptr(ws), M, C, eps, momentum, K.ptr(rm),
+                       K.ptr(rv), K.ptr(mean), K.ptr(invstd), dt, K.stream())
+            else:
+                K.call("cmx_bn_stats", K.ptr(x), K.ptr(sums), K.ptr(ws), M, C, dt, K.stream())
+                count = sync_bn_sums(sums, count, group)
+                K.call("cmx_bn_finalize", K.ptr(sums), count, eps, momentum, K.ptr(rm), K.ptr(rv), K.ptr(mean),
+                       K.ptr(invstd), C, 1, K.stream())
         else:
             K.call("cmx_bn_finalize", 0, 1.0, eps, momentum, K.ptr(rm), K.ptr(rv), K.ptr(mean), K.ptr(invstd), C, 0,
                    K.stream())

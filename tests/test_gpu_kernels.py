@@ -102,3 +102,76 @@ def test_upsample_ce(dev, dtype, B, h, w, K, fused):
     torch.cuda.synchronize()
     assert abs(loss.item() - loss_ref.item()) / loss_ref.item() < (1e-5 if dtype == torch.float32 else 1e-2)
     assert relerr(x.grad, ref.grad) < TOL[dtype] * 2, relerr(x.grad, ref.grad)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("M,C,rps,act,use_res,use_ds,training", [
+    (19200 * 2, 512, 19200, "relu", False, True, True),     # decoder linear_fuse BN + ReLU + Dropout2d
+    (4800, 64, 2400, "none", True, False, True),             # ChannelEmbed norm(residual + BN(...))
+    (1200, 320, 600, "relu", False, False, True),            # ChannelEmbed channel_embed.4 BN
+    (333, 136, 333, "relu", True, True, True),               # ragged rows / channel count
+    (4800, 128, 2400, "none", True, False, False),           # eval: running statistics
+])
+def test_batchnorm(dev, dtype, M, C, rps, act, use_res, use_ds, training):
+    """BatchNorm2d train / eval forward and backward through the C-ABI (cmx_bn_stats_finalize /
+    cmx_bn_apply / cmx_bn_bwd_reduce / cmx_bn_bwd_apply; ChannelEmbed net_utils.py:319-329 and
+    the decoder's linear_fuse BN + ReLU + Dropout2d, MLPDecoder.py:51-55) against fp64 torch
+    autograd on token-major (M, C) rows."""
+    from rgbx_semantic_segmentation_amd import kernels as K
+    torch.manual_seed(5)
+    eps, mom = 1e-5, 0.1
+    x = (torch.randn(M, C, device=dev) * 2 + 0.5).to(dtype)
+    res = torch.randn(M, C, device=dev).to(dtype) if use_res else None
+    nb = M // rps
+    ds = ((torch.rand(nb, C, device=dev) > 0.1).float() / 0.9) if use_ds else None
+    gamma = torch.rand(C, device=dev) + 0.5
+    beta = torch.randn(C, device=dev)
+    rm0, rv0 = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5
+    rm, rv = rm0.clone(), rv0.clone()
+    mean = torch.empty(C, device=dev)
+    invstd = torch.empty(C, device=dev)
+    sums = torch.empty(2, C, dtype=torch.float64, device=dev)
+    ws = torch.empty(max(1, K.query("cmx_bn_workspace", M, C) // 8), dtype=torch.float64, device=dev)
+    dt = K.dtype_code(x)
+    if training:
+        K.call("cmx_bn_stats_finalize", K.ptr(x), K.ptr(sums), K.ptr(ws), M, C, eps, mom, K.ptr(rm), K.ptr(rv),
+               K.ptr(mean), K.ptr(invstd), dt, K.stream())
+    else:
+        K.call("cmx_bn_finalize", 0, 1.0, eps, mom, K.ptr(rm), K.ptr(rv), K.ptr(mean), K.ptr(invstd), C, 0, K.stream())
+    y = torch.empty_like(x)
+    K.call("cmx_bn_apply", K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(gamma), K.ptr(beta), K.ptr(res), K.ptr(ds),
+           K.ptr(y), M, C, rps, K.ACT[act], dt, K.stream())
+    dy = torch.randn(M, C, device=dev).to(dtype)
+    gg = torch.full((C,), float("nan"), device=dev)
+    gb = torch.full((C,), float("nan"), device=dev)
+    K.call("cmx_bn_bwd_reduce", K.ptr(dy), K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(gamma), K.ptr(beta),
+           K.ptr(res), K.ptr(ds), K.ptr(sums), K.ptr(gg), K.ptr(gb), K.ptr(ws), M, C, rps, K.ACT[act], 0, dt,
+           K.stream())
+    dx = torch.empty_like(x)
+    dres = torch.empty_like(x) if use_res else None
+    K.call("cmx_bn_bwd_apply", K.ptr(dy), K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(gamma), K.ptr(beta),
+           K.ptr(res), K.ptr(ds), K.ptr(sums), float(M), K.ptr(dx), K.ptr(dres), M, C, rps, K.ACT[act],
+           int(training), dt, K.stream())
+    torch.cuda.synchronize()
+    # fp64 reference
+    xr = x.double().cpu().requires_grad_(True)
+    g_ = gamma.double().cpu().requires_grad_(True)
+    b_ = beta.double().cpu().requires_grad_(True)
+    rr = res.double().cpu().requires_grad_(True) if use_res else None
+    rmr, rvr = rm0.double().cpu(), rv0.double().cpu()
+    z = torch.nn.functional.batch_norm(xr, rmr, rvr, g_, b_, training, mom, eps)
+    if use_res:
+        z = z + rr
+    if act == "relu":
+        z = torch.relu(z)
+    if use_ds:
+        z = (z.view(nb, rps, C) * ds.double().cpu()[:, None, :]).view(M, C)
+    z.backward(dy.double().cpu())
+    tol = TOL[dtype]
+    assert relerr(y, z) < tol
+    assert relerr(dx, xr.grad) < tol * 2
+    assert relerr(gg, g_.grad) < tol and relerr(gb, b_.grad) < tol
+    if use_res:
+        assert relerr(dres, rr.grad) < tol
+    if training:
+        assert relerr(rm, rmr) < 1e-4 and relerr(rv, rvr) < 1e-4
