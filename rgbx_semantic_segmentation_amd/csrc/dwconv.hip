@@ -369,55 +369,103 @@ __device__ __forceinline__ void stage_region(const T* __restrict__ base, T* img,
   }
 }
 
+// Channel-fast thread mapping (forward and saved-act backward): thread t owns the 4 channels
+// cq = t % (CB / 4) of pixels p = t / (CB / 4), + 256 / (CB / 4), ... of the tile.  LDS images are
+// pixel-major [px][CB] (a straight copy of the NHWC rows), so the 16 (CB = 64) lanes of one
+// pixel read 128 contiguous bytes (conflict-free) and every global store is a coalesced
+// 128-B (bf16, CB = 64) row segment -- not one 8-B / 16-B piece per lane at a C-element stride.
+template <typename T> struct V4;                  // 4 channels as stored
+template <> struct V4<bf16> { uint2 a; };
+template <> struct V4<float> { float4 a; };
+template <typename T>
+__device__ __forceinline__ V4<T> v4_load(const T* p) {
+  V4<T> v;
+  if constexpr (sizeof(T) == 2) v.a = *reinterpret_cast<const uint2*>(p);
+  else v.a = *reinterpret_cast<const float4*>(p);
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ void v4_unpack(const V4<T>& v, cmx_f2 (&o)[2]) {
+  if constexpr (sizeof(T) == 2) {
+    o[0] = (cmx_f2){__uint_as_float(v.a.x << 16), __uint_as_float(v.a.x & 0xffff0000u)};
+    o[1] = (cmx_f2){__uint_as_float(v.a.y << 16), __uint_as_float(v.a.y & 0xffff0000u)};
+  } else {
+    o[0] = (cmx_f2){v.a.x, v.a.y}; o[1] = (cmx_f2){v.a.z, v.a.w};
+  }
+}
+template <typename T>
+__device__ __forceinline__ void v4_store(T* p, const cmx_f2 (&o)[2]) {
+  if constexpr (sizeof(T) == 2) *reinterpret_cast<uint2*>(p) = make_uint2(pack2_bf16(o[0].x, o[0].y), pack2_bf16(o[1].x, o[1].y));
+  else *reinterpret_cast<float4*>(p) = make_float4(o[0].x, o[0].y, o[1].x, o[1].y);
+}
+// stage a (RY x RX)-pixel region into a pixel-major image img[px][CB]; zeros outside the image
+template <typename T, int CB, int RY_, int RX_>
+__device__ __forceinline__ void stage_region_pm(const T* __restrict__ base, T* img, int y0, int x0, int H, int W, int C) {
+  constexpr int NCG = CB / 8, NPX = RY_ * RX_;
+  constexpr int ITER = (NCG * NPX + 255) / 256;
+  V8<T> v[ITER];
+#pragma unroll
+  for (int k = 0; k < ITER; ++k) {
+    const int it = threadIdx.x + k * 256;
+    const int cg = it % NCG, px = it / NCG;
+    const int y = y0 + px / RX_, x = x0 + px % RX_;
+    v[k] = v8_zero<T>();
+    if (it < NCG * NPX && y >= 0 && y < H && x >= 0 && x < W) v[k] = v8_load<T>(base + ((long)y * W + x) * C + cg * 8);
+  }
+#pragma unroll
+  for (int k = 0; k < ITER; ++k) {
+    const int it = threadIdx.x + k * 256;
+    if (it < NCG * NPX) v8_store<T>(img + it * 8, v[k]);
+  }
+}
+
 template <typename T, int CB, int ACT, bool FLIP>
 __global__ __launch_bounds__(256) void dw2_fwd_kernel(const T* __restrict__ h, const float* __restrict__ w,
                                                       const float* __restrict__ b, T* __restrict__ out, int ipg, int H,
                                                       int W, int C, int tiles_x, int tiles_y, int ncb,
                                                       T* __restrict__ gprime) {
-  constexpr int NCG = CB / 8, TPC = 256 / NCG;
-  __shared__ __attribute__((aligned(16))) T hs[NCG * EY * EX * 8];
+  constexpr int NCQ = CB / 4, PPI = 256 / NCQ;     // channel quads; pixels per block-wide step
+  __shared__ __attribute__((aligned(16))) T hs[EY * EX * CB];
   const Tile2 t = tile2_of(CB, ipg, tiles_x, tiles_y, ncb);
   const long ibase = ((long)t.g * ipg + t.img) * H * W * C + t.cb0;
-  stage_region<T, CB, EY, EX>(h + ibase, hs, t.ty0 - 1, t.tx0 - 1, H, W, C);
-  const int cg = threadIdx.x / TPC, pl = threadIdx.x % TPC;
-  const int c0 = t.cb0 + cg * 8;
-  cmx_f2 wr[4][9], bias[4];
-  load_w72(w + ((long)t.g * C + c0) * 9, wr);
+  stage_region_pm<T, CB, EY, EX>(h + ibase, hs, t.ty0 - 1, t.tx0 - 1, H, W, C);
+  const int cq = threadIdx.x % NCQ, pl = threadIdx.x / NCQ;
+  const int c0 = t.cb0 + cq * 4;
+  __syncthreads();
+  cmx_f2 wr[2][9], bias[2];
+  load_w36(w + ((long)t.g * C + c0) * 9, wr);
   if (b) {
     const float4 b0 = *reinterpret_cast<const float4*>(b + (long)t.g * C + c0);
-    const float4 b1 = *reinterpret_cast<const float4*>(b + (long)t.g * C + c0 + 4);
     bias[0] = (cmx_f2){b0.x, b0.y}; bias[1] = (cmx_f2){b0.z, b0.w};
-    bias[2] = (cmx_f2){b1.x, b1.y}; bias[3] = (cmx_f2){b1.z, b1.w};
   } else {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) bias[u] = pk_splat(0.f);
+    bias[0] = bias[1] = pk_splat(0.f);
   }
-  __syncthreads();
-  const T* hc = hs + cg * EY * EX * 8;
-  for (int it = pl; it < TY2 * TX2; it += TPC) {
+  const T* hc = hs + cq * 4;
+  for (int it = pl; it < TY2 * TX2; it += PPI) {
     const int r = it / TX2, c = it % TX2;
     const int y = t.ty0 + r, x = t.tx0 + c;
     if (y >= H || x >= W) continue;
-    cmx_f2 acc[4] = {bias[0], bias[1], bias[2], bias[3]};
+    cmx_f2 acc[2] = {bias[0], bias[1]};
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        cmx_f2 v[4];
-        v8_unpack<T>(v8_load<T>(hc + ((r + i) * EX + c + j) * 8), v);
+        cmx_f2 v[2];
+        v4_unpack<T>(v4_load<T>(hc + ((r + i) * EX + c + j) * CB), v);
         const int tap = FLIP ? 8 - (i * 3 + j) : i * 3 + j;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) acc[u] = pk_fma(wr[u][tap], v[u], acc[u]);
+        for (int u = 0; u < 2; ++u) acc[u] = pk_fma(wr[u][tap], v[u], acc[u]);
       }
+    const long o = ibase + ((long)y * W + x) * C + cq * 4;
     if (gprime) {              // act'(z), saved so the backward needs no conv recompute
-      cmx_f2 gd[4];
+      cmx_f2 gd[2];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) gd[u] = act2_grad<ACT>(acc[u]);
-      v8_store<T>(gprime + ibase + ((long)y * W + x) * C + cg * 8, v8_pack<T>(gd));
+      for (int u = 0; u < 2; ++u) gd[u] = act2_grad<ACT>(acc[u]);
+      v4_store<T>(gprime + o, gd);
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc[u] = act2_fwd<ACT>(acc[u]);
-    v8_store<T>(out + ibase + ((long)y * W + x) * C + cg * 8, v8_pack<T>(acc));
+    for (int u = 0; u < 2; ++u) acc[u] = act2_fwd<ACT>(acc[u]);
+    v4_store<T>(out + o, acc);
   }
 }
 
@@ -433,103 +481,152 @@ __device__ __forceinline__ void rs_step(const float (&v)[N], float (&o)[N / 2], 
   }
 }
 
-// Backward from a saved act'(z) (cmx_dwconv3x3_fwd_save): dz = da * act'(z) on the tile + 1-pixel
-// halo is one multiply per element (no 3x3 recompute of z, no erf / exp), then dh = conv^T(dz)
-// and the dW / db partials exactly as dw2_bwd_kernel.  h is staged with a 1-pixel halo only.
+// Backward from a saved act'(z) (cmx_dwconv3x3_fwd_save).  Staging: da and act'(z) of the tile
+// + 1-pixel halo are loaded together (16-B loads, all issued before the first LDS store) and
+// multiplied in registers, so ONE LDS image holds dz = da * act'(z) (zero outside the image);
+// h is staged for the inner tile only.  Then ONE pass over the inner pixels reads each
+// pixel's 3 x 3 dz neighbourhood once and uses it twice:
+//   dh[y][x]  = sum_ij w[i][j] dz[y-i+1][x-j+1]     (transposed conv)
+//   dW[i][j] += h[y][x] dz[y-i+1][x-j+1]            (each in-image h pixel owned by one tile)
+// and db += dz[y][x] (the centre tap).  Channel-fast mapping (see dw2_fwd_kernel): 4 channels
+// per thread, pixel-major LDS images, coalesced dh rows.  The 40 dW / db partials of a thread
+// are reduce-scattered over the lanes of its quad inside the wave, then summed over the 4
+// waves through LDS (reusing the dz image) into the block's (group, tile) slab.
 template <typename T, int CB>
-__global__ __launch_bounds__(256, 2) void dw2_bwdg_kernel(const T* __restrict__ da, const T* __restrict__ h,
+__device__ __forceinline__ void stage_dz_h(const T* __restrict__ da, const T* __restrict__ gp,
+                                           const T* __restrict__ h, T* dzs, T* hs, int ty0, int tx0, int H, int W,
+                                           int C) {
+  constexpr int NCG = CB / 8, NE = EY * EX, NIN = TY2 * TX2;
+  constexpr int ITE = (NCG * NE + 255) / 256, ITI = (NCG * NIN + 255) / 256;
+  V8<T> a[ITE], g[ITE], hv[ITI];
+#pragma unroll
+  for (int k = 0; k < ITE; ++k) {
+    const int it = threadIdx.x + k * 256;
+    const int cg = it % NCG, px = it / NCG;
+    const int y = ty0 - 1 + px / EX, x = tx0 - 1 + px % EX;
+    a[k] = v8_zero<T>();
+    g[k] = v8_zero<T>();
+    if (it < NCG * NE && y >= 0 && y < H && x >= 0 && x < W) {
+      const long o = ((long)y * W + x) * C + cg * 8;
+      a[k] = v8_load<T>(da + o);
+      g[k] = v8_load<T>(gp + o);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < ITI; ++k) {
+    const int it = threadIdx.x + k * 256;
+    const int cg = it % NCG, px = it / NCG;
+    const int y = ty0 + px / TX2, x = tx0 + px % TX2;
+    hv[k] = v8_zero<T>();
+    if (it < NCG * NIN && y < H && x < W) hv[k] = v8_load<T>(h + ((long)y * W + x) * C + cg * 8);
+  }
+#pragma unroll
+  for (int k = 0; k < ITE; ++k) {
+    const int it = threadIdx.x + k * 256;
+    if (it < NCG * NE) {
+      cmx_f2 d[4], gd[4];
+      v8_unpack<T>(a[k], d);
+      v8_unpack<T>(g[k], gd);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) d[u] = d[u] * gd[u];
+      v8_store<T>(dzs + it * 8, v8_pack<T>(d));
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < ITI; ++k) {
+    const int it = threadIdx.x + k * 256;
+    if (it < NCG * NIN) v8_store<T>(hs + it * 8, hv[k]);
+  }
+}
+
+template <typename T, int CB>
+__global__ __launch_bounds__(256, 4) void dw2_bwdg_kernel(const T* __restrict__ da, const T* __restrict__ h,
                                                        const T* __restrict__ gprime, const float* __restrict__ w,
                                                        T* __restrict__ dh, float* __restrict__ part, int ipg, int H,
                                                        int W, int C, int tiles_x, int tiles_y, int ncb, int nsp) {
-  constexpr int NCG = CB / 8, TPC = 256 / NCG;
-  __shared__ __attribute__((aligned(16))) T hs[NCG * EY * EX * 8];
-  __shared__ __attribute__((aligned(16))) T dzs[NCG * EY * EX * 8];
-  __shared__ __attribute__((aligned(16))) T gs[NCG * EY * EX * 8];
+  constexpr int NCQ = CB / 4, PPI = 256 / NCQ;
+  constexpr int NE = EY * EX, NIN = TY2 * TX2;
+  constexpr int LPQ = 64 / NCQ;                     // lanes of one quad in a wave (4 or 8)
+  constexpr int NV = LPQ == 4 ? 10 : 5;             // partials per lane after the in-wave reduce-scatter
+  __shared__ __attribute__((aligned(16))) T dzs[NE * CB];
+  __shared__ __attribute__((aligned(16))) T hs[NIN * CB];
+  static_assert(sizeof(dzs) >= 4 * 64 * NV * sizeof(float), "cross-wave reduce buffer");
   const Tile2 t = tile2_of(CB, ipg, tiles_x, tiles_y, ncb);
   const long ibase = ((long)t.g * ipg + t.img) * H * W * C + t.cb0;
-  stage_region<T, CB, EY, EX>(h + ibase, hs, t.ty0 - 1, t.tx0 - 1, H, W, C);
-  stage_region<T, CB, EY, EX>(da + ibase, dzs, t.ty0 - 1, t.tx0 - 1, H, W, C);
-  stage_region<T, CB, EY, EX>(gprime + ibase, gs, t.ty0 - 1, t.tx0 - 1, H, W, C);
-  const int cg = threadIdx.x / TPC, pl = threadIdx.x % TPC;
-  const int c0 = t.cb0 + cg * 8;
-  cmx_f2 wr[4][9];
-  load_w72(w + ((long)t.g * C + c0) * 9, wr);
+  stage_dz_h<T, CB>(da + ibase, gprime + ibase, h + ibase, dzs, hs, t.ty0, t.tx0, H, W, C);
+  const int cq = threadIdx.x % NCQ, pl = threadIdx.x / NCQ;
+  const int c0 = t.cb0 + cq * 4;
   __syncthreads();
-  const T* hc = hs + cg * EY * EX * 8;
-  T* dzc = dzs + cg * EY * EX * 8;
-  const T* gc = gs + cg * EY * EX * 8;
-  // dz = da * act'(z) in place (outside the image both staged tiles are zero: dz = 0 there)
-  for (int it = pl; it < EY * EX; it += TPC) {
-    cmx_f2 d[4], gd[4];
-    v8_unpack<T>(v8_load<T>(dzc + it * 8), d);
-    v8_unpack<T>(v8_load<T>(gc + it * 8), gd);
+  cmx_f2 wr[2][9];
+  load_w36(w + ((long)t.g * C + c0) * 9, wr);
+  const T* hc = hs + cq * 4;
+  const T* dzc = dzs + cq * 4;
+  cmx_f2 acc[2][10];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) d[u] = d[u] * gd[u];
-    v8_store<T>(dzc + it * 8, v8_pack<T>(d));
-  }
-  __syncthreads();
-  if (dh) {
-    for (int it = pl; it < TY2 * TX2; it += TPC) {
-      const int r = it / TX2, c = it % TX2;
-      const int y = t.ty0 + r, x = t.tx0 + c;
-      if (y >= H || x >= W) continue;
-      cmx_f2 g[4] = {pk_splat(0.f), pk_splat(0.f), pk_splat(0.f), pk_splat(0.f)};
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          cmx_f2 dv[4];           // dh[y][x] += w[i][j] dz[y-i+1][x-j+1]
-          v8_unpack<T>(v8_load<T>(dzc + ((r + 2 - i) * EX + c + 2 - j) * 8), dv);
-#pragma unroll
-          for (int u = 0; u < 4; ++u) g[u] = pk_fma(wr[u][i * 3 + j], dv[u], g[u]);
-        }
-      v8_store<T>(dh + ibase + ((long)y * W + x) * C + cg * 8, v8_pack<T>(g));
-    }
-  }
-  cmx_f2 acc[4][10];
-#pragma unroll
-  for (int u = 0; u < 4; ++u)
+  for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int k = 0; k < 10; ++k) acc[u][k] = pk_splat(0.f);
-  for (int it = pl; it < TY2 * TX2; it += TPC) {
+  for (int it = pl; it < NIN; it += PPI) {
     const int r = it / TX2, c = it % TX2;
-    if (t.ty0 + r >= H || t.tx0 + c >= W) continue;
-    cmx_f2 dz0[4];
-    v8_unpack<T>(v8_load<T>(dzc + ((r + 1) * EX + c + 1) * 8), dz0);
+    const int y = t.ty0 + r, x = t.tx0 + c;
+    if (y >= H || x >= W) continue;
+    cmx_f2 hv[2];
+    v4_unpack<T>(v4_load<T>(hc + it * CB), hv);
+    cmx_f2 g[2] = {pk_splat(0.f), pk_splat(0.f)};
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        cmx_f2 hv[4];             // dW[i][j] += dz[y][x] h[y+i-1][x+j-1]
-        v8_unpack<T>(v8_load<T>(hc + ((r + i) * EX + c + j) * 8), hv);
+        cmx_f2 dv[2];
+        v4_unpack<T>(v4_load<T>(dzc + ((r + 2 - i) * EX + c + 2 - j) * CB), dv);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) acc[u][i * 3 + j] = pk_fma(dz0[u], hv[u], acc[u][i * 3 + j]);
+        for (int u = 0; u < 2; ++u) {
+          g[u] = pk_fma(wr[u][i * 3 + j], dv[u], g[u]);
+          acc[u][i * 3 + j] = pk_fma(hv[u], dv[u], acc[u][i * 3 + j]);
+        }
+        if (i == 1 && j == 1) {
+#pragma unroll
+          for (int u = 0; u < 2; ++u) acc[u][9] += dv[u];
+        }
       }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) acc[u][9] += dz0[u];
+    if (dh) v4_store<T>(dh + ibase + ((long)y * W + x) * C + cq * 4, g);
   }
-  const int lane = threadIdx.x & 63;
-  float flat[80], r40[40], r20[20], r10[10], r5[5];
+  // in-wave reduce-scatter over the LPQ lanes of the quad (xor NCQ, 2 NCQ, ...): 40 -> NV
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float flat[40], r20[20], r10[10];
 #pragma unroll
-  for (int u = 0; u < 4; ++u)
+  for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int k = 0; k < 10; ++k) {
       flat[(2 * u) * 10 + k] = acc[u][k].x;
       flat[(2 * u + 1) * 10 + k] = acc[u][k].y;
     }
-  int seg = 0, s_off = TPC >> 1;
-  rs_step<80>(flat, r40, s_off, (lane & s_off) != 0); seg = seg * 2 + ((lane & s_off) != 0); s_off >>= 1;
-  rs_step<40>(r40, r20, s_off, (lane & s_off) != 0); seg = seg * 2 + ((lane & s_off) != 0); s_off >>= 1;
-  rs_step<20>(r20, r10, s_off, (lane & s_off) != 0); seg = seg * 2 + ((lane & s_off) != 0); s_off >>= 1;
-  rs_step<10>(r10, r5, s_off, (lane & s_off) != 0); seg = seg * 2 + ((lane & s_off) != 0); s_off >>= 1;
-  for (; s_off > 0; s_off >>= 1) {
+  int seg = 0;
+  rs_step<40>(flat, r20, NCQ, (lane & NCQ) != 0); seg = seg * 2 + ((lane & NCQ) != 0);
+  rs_step<20>(r20, r10, 2 * NCQ, (lane & (2 * NCQ)) != 0); seg = seg * 2 + ((lane & (2 * NCQ)) != 0);
+  float rv[NV];
+  if constexpr (NV == 5) {
+    rs_step<10>(r10, rv, 4 * NCQ, (lane & (4 * NCQ)) != 0); seg = seg * 2 + ((lane & (4 * NCQ)) != 0);
+  } else {
 #pragma unroll
-    for (int k = 0; k < 5; ++k) r5[k] += __shfl_xor(r5[k], s_off, 64);
+    for (int k = 0; k < 10; ++k) rv[k] = r10[k];
   }
-  if ((lane & (TPC / 16 - 1)) == 0) {
-    float* o = part + ((long)t.g * nsp + t.sp) * C * 10 + (long)c0 * 10 + seg * 5;
+  // lane holds values [seg * NV, seg * NV + NV) of its quad's 40 (4 channels x 10)
+  __syncthreads();                                  // every wave is done reading dzs
+  float* red = reinterpret_cast<float*>(dzs);
 #pragma unroll
-    for (int k = 0; k < 5; ++k) o[k] = r5[k];
+  for (int k = 0; k < NV; ++k) red[(wv * 64 + lane) * NV + k] = rv[k];
+  __syncthreads();
+  float* o = part + ((long)t.g * nsp + t.sp) * C * 10 + (long)t.cb0 * 10;
+  for (int e = threadIdx.x; e < 64 * NV; e += 256) {
+    const float v = red[e] + red[64 * NV + e] + red[128 * NV + e] + red[192 * NV + e];
+    const int l = e / NV, k = e % NV;
+    const int q = l % NCQ, sg = (l / NCQ);          // lane l's quad and its segment bits (xor order)
+    // seg was accumulated high bit first from (lane & NCQ), (lane & 2NCQ)[, (lane & 4NCQ)]
+    int sgi = 0;
+#pragma unroll
+    for (int bit = 0; bit < (NV == 5 ? 3 : 2); ++bit) sgi = sgi * 2 + ((sg >> bit) & 1);
+    o[q * 40 + sgi * NV + k] = v;
   }
 }
 

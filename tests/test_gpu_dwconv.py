@@ -63,3 +63,45 @@ def test_dwconv_fwd_bwd(dev, dtype, C, H, W, act):
     assert rel(dh, hr.grad) < tol
     assert rel(dw, wr.grad) < (tol if dtype == torch.float32 else 1e-2)
     assert rel(db, br.grad) < (tol if dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dtype,C,H,W", [(torch.bfloat16, 64, 30, 44), (torch.bfloat16, 256, 17, 16),
+                                         (torch.bfloat16, 320, 9, 33), (torch.bfloat16, 512, 15, 20),
+                                         (torch.float32, 32, 8, 10), (torch.float32, 160, 9, 33),
+                                         (torch.float32, 64, 30, 44)])
+@pytest.mark.parametrize("act", ["gelu", "relu"])
+def test_dwconv_fwd_save_bwd_saved(dev, dtype, C, H, W, act):
+    """The training path: forward saves act'(z); the backward forms dz = da * act'(z) and the
+    transposed conv and dW / db from one LDS image (tiles ragged in H and W)."""
+    from rgbx_semantic_segmentation_amd import kernels as Kn
+    torch.manual_seed(1)
+    G, B = 2, 2
+    NI = G * B
+    h = torch.randn(NI, H * W, C, device="cuda")
+    w = torch.randn(G, C, 9, device="cuda") * 0.3
+    b = torch.randn(G, C, device="cuda") * 0.1
+    da = torch.randn(NI, H * W, C, device="cuda")
+    hq, daq = h.to(dtype), da.to(dtype)
+    hr = hq.float().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    out_ref = ref_dw(hr, wr, br, act, G, B, H, W)
+    out_ref.backward(daq.float())
+    out = torch.empty_like(hq)
+    gp = torch.empty_like(hq)
+    Kn.call("cmx_dwconv3x3_fwd_save", Kn.ptr(hq), Kn.ptr(w), Kn.ptr(b), Kn.ptr(out), Kn.ptr(gp), NI, B, H, W, C,
+            Kn.ACT[act], Kn.dtype_code(hq), Kn.stream())
+    dh = torch.empty_like(hq)
+    dw = torch.empty(G, C, 9, device="cuda")
+    db = torch.empty(G, C, device="cuda")
+    ws = Kn._ws(Kn.query("cmx_dwconv3x3_bwd_workspace", NI, B, H, W, C), h.device)
+    Kn.call("cmx_dwconv3x3_bwd_saved", Kn.ptr(daq), Kn.ptr(hq), Kn.ptr(gp), Kn.ptr(w), Kn.ptr(dh), Kn.ptr(dw),
+            Kn.ptr(db), Kn.ptr(ws), NI, B, H, W, C, 0, Kn.dtype_code(hq), Kn.stream())
+    torch.cuda.synchronize()
+    # dz = da * act'(z) is rounded to the storage dtype once (as the reference's autograd
+    # under autocast stores it): bf16 2e-2 relative, fp32 1e-5
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert rel(out, out_ref) < tol
+    assert rel(dh, hr.grad) < tol
+    assert rel(dw, wr.grad) < (tol if dtype == torch.float32 else 1e-2)
+    assert rel(db, br.grad) < (tol if dtype == torch.float32 else 1e-2)
