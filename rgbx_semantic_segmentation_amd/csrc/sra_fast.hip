@@ -82,8 +82,8 @@ __device__ __forceinline__ void store_rows(bf16* row_ptr, const f32x16& acc, int
 }
 
 // ------------------------------------------------------------------------ forward
-template <int QW>
-__global__ __launch_bounds__(64 * NWAVE) void sra_fwd_fast(const bf16* __restrict__ q, const bf16* __restrict__ k,
+template <int QW, int NW>
+__global__ __launch_bounds__(64 * NW) void sra_fwd_fast(const bf16* __restrict__ q, const bf16* __restrict__ k,
                                                        const bf16* __restrict__ v, bf16* __restrict__ o,
                                                        float* __restrict__ lse, int N, int Nk, int nkp, int heads,
                                                        long qs, long kvs, long os, float sl2) {
@@ -92,10 +92,10 @@ __global__ __launch_bounds__(64 * NWAVE) void sra_fwd_fast(const bf16* __restric
   char* Vi = smem + NKP_MAX * ROWB;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int b = blockIdx.z, head = blockIdx.y;
-  stage_rows(k + (long)b * Nk * kvs + head * HD, kvs, Nk, nkp, Ki, wave, lane, NWAVE);
-  stage_rows(v + (long)b * Nk * kvs + head * HD, kvs, Nk, nkp, Vi, wave, lane, NWAVE);
+  stage_rows(k + (long)b * Nk * kvs + head * HD, kvs, Nk, nkp, Ki, wave, lane, NW);
+  stage_rows(v + (long)b * Nk * kvs + head * HD, kvs, Nk, nkp, Vi, wave, lane, NW);
 
-  const int q0 = (blockIdx.x * NWAVE + wave) * 32 * QW;
+  const int q0 = (blockIdx.x * NW + wave) * 32 * QW;
   const bf16* qb = q + (long)b * N * qs + head * HD;
   bf16x8 qf[QW][4];
 #pragma unroll
@@ -193,8 +193,8 @@ __global__ __launch_bounds__(64 * NWAVE) void sra_fwd_fast(const bf16* __restric
 
 // ------------------------------------------------------------------------ backward: dQ (+ Dq)
 // dS^T = P^T o (dP^T - Dq), P^T = exp(S^T - lse), dP^T = V dO^T; dQ^T = K^T dS^T * scale.
-template <int QW>
-__global__ __launch_bounds__(64 * NWAVE) void sra_dq_fast(const bf16* __restrict__ q, const bf16* __restrict__ k,
+template <int QW, int NW>
+__global__ __launch_bounds__(64 * NW) void sra_dq_fast(const bf16* __restrict__ q, const bf16* __restrict__ k,
                                                       const bf16* __restrict__ v, const bf16* __restrict__ o,
                                                       const bf16* __restrict__ dout, const float* __restrict__ lse,
                                                       float* __restrict__ Dws, bf16* __restrict__ dq, int N, int Nk,
@@ -205,10 +205,10 @@ __global__ __launch_bounds__(64 * NWAVE) void sra_dq_fast(const bf16* __restrict
   char* Vi = smem + NKP_MAX * ROWB;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int b = blockIdx.z, head = blockIdx.y;
-  stage_rows(k + (long)b * Nk * kvs + head * HD, kvs, Nk, nkp, Ki, wave, lane, NWAVE);
-  stage_rows(v + (long)b * Nk * kvs + head * HD, kvs, Nk, nkp, Vi, wave, lane, NWAVE);
+  stage_rows(k + (long)b * Nk * kvs + head * HD, kvs, Nk, nkp, Ki, wave, lane, NW);
+  stage_rows(v + (long)b * Nk * kvs + head * HD, kvs, Nk, nkp, Vi, wave, lane, NW);
 
-  const int q0 = (blockIdx.x * NWAVE + wave) * 32 * QW;
+  const int q0 = (blockIdx.x * NW + wave) * 32 * QW;
   bf16x8 qf[QW][4], df[QW][4];
   float Dq[QW], lse2[QW];
 #pragma unroll
@@ -433,6 +433,17 @@ int pick_qw(int N, int heads, int Bt) {
   return wg2 >= 512 ? 2 : 1;
 }
 
+
+// waves per workgroup: 8 (two per SIMD share one K/V image) unless that leaves fewer than
+// 128 workgroups (stage 3: 100, stage 4: 64 at B2 480x640), where 2-wave workgroups spread
+// the work over 2.5-4x more CUs (measured: dQ 17.7 -> 14.8 us at stages 3 and 4; 4-wave
+// workgroups at stage 2 (152 -> 304) were slower, 13.8 -> 16.4 us forward).  Every workgroup
+// stages the (b, head)'s K / V (L2-resident after the first): only L2 -> LDS traffic.
+int pick_nw(int N, int heads, int Bt, int qw) {
+  if (qw == 2 || (long)cdiv(N, 32 * NWAVE) * heads * Bt >= 128) return NWAVE;
+  return 2;
+}
+
 }  // namespace
 
 // bf16, D = 64, Nk <= 320, 16-B aligned rows: the LDS-resident path (sra_attention.hip calls these)
@@ -449,13 +460,17 @@ void sra_fwd_fast_launch(const void* q, const void* k, const void* v, void* o, f
                          int heads, long qs, long kvs, long os, float sl2, hipStream_t s) {
   const int nkp = (Nk + KTILE - 1) / KTILE * KTILE;
   const int qw = pick_qw(N, heads, Bt);
-  const dim3 grid(cdiv(N, 32 * NWAVE * qw), heads, Bt);
-  if (qw == 2)
-    hipLaunchKernelGGL(sra_fwd_fast<2>, grid, dim3(64 * NWAVE), 0, s, (const bf16*)q, (const bf16*)k, (const bf16*)v,
-                       (bf16*)o, lse, N, Nk, nkp, heads, qs, kvs, os, sl2);
-  else
-    hipLaunchKernelGGL(sra_fwd_fast<1>, grid, dim3(64 * NWAVE), 0, s, (const bf16*)q, (const bf16*)k, (const bf16*)v,
-                       (bf16*)o, lse, N, Nk, nkp, heads, qs, kvs, os, sl2);
+  const int nw = pick_nw(N, heads, Bt, qw);
+  const dim3 grid(cdiv(N, 32 * nw * qw), heads, Bt);
+#define CMX_SRA_FWD(QW_, NW_)                                                                                       \
+  hipLaunchKernelGGL((sra_fwd_fast<QW_, NW_>), grid, dim3(64 * NW_), 0, s, (const bf16*)q, (const bf16*)k,         \
+                     (const bf16*)v, (bf16*)o, lse, N, Nk, nkp, heads, qs, kvs, os, sl2)
+  if (qw == 2) CMX_SRA_FWD(2, 8);
+  else if (nw == 8) CMX_SRA_FWD(1, 8);
+  else if (nw == 4) CMX_SRA_FWD(1, 4);
+  else if (nw == 2) CMX_SRA_FWD(1, 2);
+  else CMX_SRA_FWD(1, 1);
+#undef CMX_SRA_FWD
 }
 
 void sra_dq_fast_launch(const void* q, const void* k, const void* v, const void* o, const void* dout,
@@ -463,15 +478,18 @@ void sra_dq_fast_launch(const void* q, const void* k, const void* v, const void*
                         long os, long dos, long dqs, float sl2, float scale, hipStream_t s) {
   const int nkp = (Nk + KTILE - 1) / KTILE * KTILE;
   const int qw = pick_qw(N, heads, Bt);
-  const dim3 grid(cdiv(N, 32 * NWAVE * qw), heads, Bt);
-  if (qw == 2)
-    hipLaunchKernelGGL(sra_dq_fast<2>, grid, dim3(64 * NWAVE), 0, s, (const bf16*)q, (const bf16*)k, (const bf16*)v,
-                       (const bf16*)o, (const bf16*)dout, lse, Dws, (bf16*)dq, N, Nk, nkp, heads, qs, kvs, os, dos, dqs,
-                       sl2, scale);
-  else
-    hipLaunchKernelGGL(sra_dq_fast<1>, grid, dim3(64 * NWAVE), 0, s, (const bf16*)q, (const bf16*)k, (const bf16*)v,
-                       (const bf16*)o, (const bf16*)dout, lse, Dws, (bf16*)dq, N, Nk, nkp, heads, qs, kvs, os, dos, dqs,
-                       sl2, scale);
+  const int nw = pick_nw(N, heads, Bt, qw);
+  const dim3 grid(cdiv(N, 32 * nw * qw), heads, Bt);
+#define CMX_SRA_DQ(QW_, NW_)                                                                                        \
+  hipLaunchKernelGGL((sra_dq_fast<QW_, NW_>), grid, dim3(64 * NW_), 0, s, (const bf16*)q, (const bf16*)k,          \
+                     (const bf16*)v, (const bf16*)o, (const bf16*)dout, lse, Dws, (bf16*)dq, N, Nk, nkp, heads, qs,  \
+                     kvs, os, dos, dqs, sl2, scale)
+  if (qw == 2) CMX_SRA_DQ(2, 8);
+  else if (nw == 8) CMX_SRA_DQ(1, 8);
+  else if (nw == 4) CMX_SRA_DQ(1, 4);
+  else if (nw == 2) CMX_SRA_DQ(1, 2);
+  else CMX_SRA_DQ(1, 1);
+#undef CMX_SRA_DQ
 }
 
 // partial dK / dV slabs of the query chunks (layout of sra_attention.hip's generic path)
