@@ -178,6 +178,17 @@ int cmx_adamw_step_scaled(float* p, const float* g, float* m, float* v, void* sh
 int cmx_grad_nonfinite(const float* g, int64_t n, float* found_inf, hipStream_t stream);
 int cmx_loss_scale_update(float* scale, int* growth_tracker, float* found_inf, float growth_factor, float backoff_factor, int growth_interval, hipStream_t stream);
 
+/* ---- evaluation (engine/evaluator.py:306-396, utils/metric.py:8-15, eval.py:23-36).
+ *      seg_window_accumulate: one sliding-window crop -- acc[k, sy+i, sx+j] += exp(s1[k, m0+i, m2+j]
+ *      (+ s2[k, m0+i, cw-1-(m2+j)] when s2, the is_flip pass)), s1/s2 (K, ch, cw) fp32 logits of the crop,
+ *      margins m0..m3 = top/bottom/left/right padding of the crop (pad_image_to_shape), acc (K, PH, PW) fp32.
+ *      seg_argmax_confusion: pred = first argmax over K of score (K, HW) fp32; for labels in [0, n_cl):
+ *      hist[n_cl*gt + pred] += 1, counts[0] (labeled) += 1, counts[1] (correct) += pred == gt.  hist (n_cl*n_cl)
+ *      and counts (2) are int64 and ACCUMULATE; pred (int32, HW) may be NULL; label_dtype 0 = int64, 1 = uint8.
+ *      score == NULL: pred is an INPUT class map (hist_info(n_cl, pred, gt)). */
+int cmx_seg_window_accumulate(const float* s1, const float* s2, float* acc, int K, int ch, int cw, int m0, int m1, int m2, int m3, int PH, int PW, int sy, int sx, hipStream_t stream);
+int cmx_seg_argmax_confusion(const float* score, int K, int64_t HW, const void* label, int label_dtype, int n_cl, int* pred, int64_t* hist, int64_t* counts, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

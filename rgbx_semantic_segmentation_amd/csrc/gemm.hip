@@ -834,13 +834,25 @@ int tile_policy() {
   return p;
 }
 
-void plan_tiles(int G, int M, int nb, int* bm, int* bn) {
+// Small-K policy (CMX_GEMM_SMALLK=k): problems with K <= k take 64 x 64 tiles whatever their
+// tile count -- a one- or two-k-tile block is a latency chain (DMA, MFMA, epilogue), and the
+// 128 x 128 tile's 67 KB epilogue image allows only two such chains per CU.
+int smallk_policy() {
+  static const int p = [] {
+    const char* e = getenv("CMX_GEMM_SMALLK");
+    return e ? atoi(e) : 0;
+  }();
+  return p;
+}
+
+void plan_tiles(int G, int M, int nb, int K, int* bm, int* bn) {
   *bm = tile_dim(M);
   *bn = tile_dim(nb);
   if (tile_policy() == 1) {
     const long t128 = (long)cdiv(M, *bm) * cdiv(nb, *bn) * G;
     if (t128 < 240) *bm = *bn = 64;
   }
+  if (K <= smallk_policy()) *bm = *bn = 64;
 }
 
 // split factor for the bf16 path: one block per CU when the output has few tiles (each split
@@ -848,7 +860,7 @@ void plan_tiles(int G, int M, int nb, int* bm, int* bn) {
 int auto_split(int G, int M, int N, int K, int ones_col) {
   const int nb = ones_col ? N - 1 : N;
   int bm, bn;
-  plan_tiles(G, M, nb, &bm, &bn);
+  plan_tiles(G, M, nb, K, &bm, &bn);
   const long tiles = (long)cdiv(M, bm) * cdiv(nb, bn) * G;
   const int nk = (K + FBK - 1) / FBK;
   const long full = tile_policy() == 1 ? 128 : 200;
@@ -924,7 +936,7 @@ int cmx_gemm(const void* A, const void* A2, const void* B, void* C, const float*
   a.nsplit = splitk;
   if (fast) {
     int bm, bn;
-    plan_tiles(G, M, nb, &bm, &bn);
+    plan_tiles(G, M, nb, K, &bm, &bn);
     a.tiles_m = cdiv(M, bm); a.tiles_n = cdiv(nb, bn);
     if (bm == 64 && bn == 64) launch_bf16_ns<64, 64>(a, G, splitk, transA, transB, s);
     else if (bm == 64) launch_bf16_ns<64, 128>(a, G, splitk, transA, transB, s);
@@ -1066,7 +1078,7 @@ int cmx_conv_implicit_fwd(const void* x, const void* Wt, void* y, const float* b
   splitk = (nk + a.kt_per_split - 1) / a.kt_per_split;
   a.nsplit = splitk;
   int bm, bn;
-  plan_tiles(G, (int)M, N, &bm, &bn);
+  plan_tiles(G, (int)M, N, (int)K, &bm, &bn);
   a.tiles_m = cdiv(M, bm); a.tiles_n = cdiv(N, bn);
   if (bm == 64 && bn == 64) launch_bf16_ns<64, 64>(a, G, splitk, 0, 0, s);
   else if (bm == 64) launch_bf16_ns<64, 128>(a, G, splitk, 0, 0, s);

@@ -1,0 +1,207 @@
+"""Drop-in mirror of the reference's sliding-window evaluator (engine/evaluator.py:18-431) on
+the device.
+
+Same class, constructor and method names as the reference; the network runs through the HIP
+forward (``EncoderDecoder.forward(rgb, x)`` in eval mode), and the two per-pixel passes the
+reference runs on the host or as eager torch ops are HIP kernels (csrc/metric.hip):
+  * ``cmx_seg_window_accumulate`` -- exp(score (+ mirrored flip score)) of one crop, minus its
+    padding margin, added into the scale accumulator (evaluator.py:345-368, 374-396);
+  * ``cmx_seg_argmax_confusion``  -- argmax over classes + hist_info (evaluator.py:322,
+    eval.py:35, utils/metric.py:8-15), accumulating on the device.
+Resizes (cv2.resize INTER_LINEAR, evaluator.py:311-316, 371) use the bilinear kernel of the
+decoder (csrc/bilinear.hip, the same half-pixel rule); padding and the per-channel normalise
+are torch elementwise plumbing.
+
+Kept from the reference, deliberately: the window origin / end index quirk (stride[0] and
+crop_size[0] on x, evaluator.py:352-357; negative starts are Python slices from the end), the
+second normalisation inside ``process_image_rgbX`` (:408-412).  Differences: scores of the
+scales are summed in fp32 on the device (the reference sums float64 on the host), and a
+scale's image size is round(s * size) with the in/out resize rule (cv2 uses 1/fx; identical
+when s * size is an integer, as for 0.75 / 1.25 of 480 x 640).  One process per GPU (the
+reference's spawn pool of per-device workers is replaced by the Engine's one-process-per-GPU
+launch); ``run`` evaluates a dataset and returns the metric line.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as TF
+
+from .. import _lib
+from ..utils.metric import ConfusionCounter, compute_score
+
+
+def _pad_margin(h, w, crop):
+    """utils/transforms.py:61-70 margins (top, bottom, left, right) padding (h, w) up to crop."""
+    ph, pw = max(crop[0] - h, 0), max(crop[1] - w, 0)
+    return ph // 2, ph // 2 + ph % 2, pw // 2, pw // 2 + pw % 2
+
+
+def _resize_chw(x: torch.Tensor, oh: int, ow: int) -> torch.Tensor:
+    """(C, H, W) fp32 -> (C, oh, ow) fp32, bilinear align_corners=False (cv2 INTER_LINEAR)."""
+    C, H, W = x.shape
+    if (H, W) == (oh, ow):
+        return x
+    src = x.permute(1, 2, 0).contiguous()                    # NHWC input of the kernel
+    out = torch.empty(C, oh, ow, device=x.device, dtype=torch.float32)
+    _lib.call("cmx_bilinear_fwd_nchw_f32", _lib.ptr(src), _lib.ptr(out), 1, H, W, oh, ow, C, 0, _lib.stream())
+    return out
+
+
+class Evaluator(object):
+    def __init__(self, dataset, class_num, norm_mean, norm_std, network, multi_scales, is_flip, devices,
+                 verbose=False, save_path=None, show_image=False):
+        self.eval_time = 0
+        self.dataset = dataset
+        self.ndata = dataset.get_length() if dataset is not None and hasattr(dataset, "get_length") else 0
+        self.class_num = class_num
+        self.norm_mean = np.asarray(norm_mean, dtype=np.float64)
+        self.norm_std = np.asarray(norm_std, dtype=np.float64)
+        self.multi_scales = multi_scales
+        self.is_flip = is_flip
+        self.network = network
+        self.devices = devices
+        self.val_func = network
+        self.verbose = verbose
+        self.save_path = save_path
+        self.show_image = show_image
+
+    # ------------------------------------------------------------------ per-sample API
+    def func_per_iteration(self, data, device):
+        raise NotImplementedError           # subclass (eval.py:22-66)
+
+    def compute_metric(self, results):
+        raise NotImplementedError           # subclass (eval.py:69-83)
+
+    def _device(self, device):
+        if device is None:
+            return torch.device("cuda", torch.cuda.current_device())
+        return torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+
+    def _chw(self, a, dev):
+        """HWC (numpy or tensor, any numeric dtype) -> (C, H, W) float32 on the device."""
+        t = a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(a))
+        t = t.to(device=dev, dtype=torch.float32)
+        if t.dim() == 2:
+            t = t[..., None]
+        return t.permute(2, 0, 1).contiguous()
+
+    def sliding_scores_rgbX(self, img, modal_x, crop_size, stride_rate, device=None) -> torch.Tensor:
+        """Sum over scales of the per-scale score maps, (K, H, W) fp32 on the device."""
+        dev = self._device(device)
+        crop = (int(crop_size[0]), int(crop_size[1])) if not isinstance(crop_size, int) else (crop_size, crop_size)
+        img_c, x_c = self._chw(img, dev), self._chw(modal_x, dev)
+        _, ori_rows, ori_cols = img_c.shape
+        processed = torch.zeros(self.class_num, ori_rows, ori_cols, device=dev, dtype=torch.float32)
+        for s in self.multi_scales:
+            nh, nw = int(round(ori_rows * s)), int(round(ori_cols * s))
+            processed += self.scale_process_rgbX(_resize_chw(img_c, nh, nw), _resize_chw(x_c, nh, nw),
+                                                 (ori_rows, ori_cols), crop, stride_rate, dev)
+        return processed
+
+    def sliding_eval_rgbX(self, img, modal_x, crop_size, stride_rate, device=None):
+        """evaluator.py:306-324: the (H, W) class map (numpy int64, as the reference returns)."""
+        score = self.sliding_scores_rgbX(img, modal_x, crop_size, stride_rate, device)
+        pred = torch.empty(score.shape[1:], dtype=torch.int32, device=score.device)
+        cc = ConfusionCounter(self.class_num, score.device)
+        dummy = torch.full(score.shape[1:], 255, dtype=torch.uint8, device=score.device)
+        cc.add_score(score, dummy, pred_out=pred)            # argmax only (every label ignored)
+        return pred.cpu().numpy().astype(np.int64)
+
+    def scale_process_rgbX(self, img, modal_x, ori_shape, crop_size, stride_rate, device=None):
+        """evaluator.py:326-372 on (C, h, w) device images; returns (K, H, W) at ori_shape."""
+        dev = img.device
+        _, new_rows, new_cols = img.shape
+        K = self.class_num
+        if new_cols <= crop_size[1] or new_rows <= crop_size[0]:
+            m = _pad_margin(new_rows, new_cols, crop_size)
+            ph, pw = new_rows + m[0] + m[1], new_cols + m[2] + m[3]
+            score = torch.zeros(K, new_rows, new_cols, device=dev, dtype=torch.float32)
+            self._crop_into(img, modal_x, crop_size, score, 0, 0, m, (ph, pw))
+        else:
+            stride = (int(math.ceil(crop_size[0] * stride_rate)), int(math.ceil(crop_size[1] * stride_rate)))
+            m = _pad_margin(new_rows, new_cols, crop_size)
+            img_pad = TF.pad(img, (m[2], m[3], m[0], m[1]))
+            x_pad = TF.pad(modal_x, (m[2], m[3], m[0], m[1]))
+            pad_rows, pad_cols = img_pad.shape[1], img_pad.shape[2]
+            r_grid = int(np.ceil((pad_rows - crop_size[0]) / stride[0])) + 1
+            c_grid = int(np.ceil((pad_cols - crop_size[1]) / stride[1])) + 1
+            data_scale = torch.zeros(K, pad_rows, pad_cols, device=dev, dtype=torch.float32)
+            for gy in range(r_grid):
+                for gx in range(c_grid):
+                    s_x = gx * stride[0]                      # (sic) evaluator.py:352-357
+                    s_y = gy * stride[1]
+                    e_x = min(s_x + crop_size[0], pad_cols)
+                    e_y = min(s_y + crop_size[1], pad_rows)
+                    s_x = e_x - crop_size[0]
+                    s_y = e_y - crop_size[1]
+                    # Python slice semantics of a negative start (numpy / torch in the reference)
+                    sy0 = s_y if s_y >= 0 else max(pad_rows + s_y, 0)
+                    sx0 = s_x if s_x >= 0 else max(pad_cols + s_x, 0)
+                    if e_y <= sy0 or e_x <= sx0:
+                        continue
+                    sub_i = img_pad[:, sy0:e_y, sx0:e_x]
+                    sub_x = x_pad[:, sy0:e_y, sx0:e_x]
+                    tm = _pad_margin(e_y - sy0, e_x - sx0, crop_size)
+                    self._crop_into(sub_i, sub_x, crop_size, data_scale, sy0, sx0, tm,
+                                    (e_y - sy0 + tm[0] + tm[1], e_x - sx0 + tm[2] + tm[3]))
+            score = data_scale[:, m[0]:pad_rows - m[1], m[2]:pad_cols - m[3]]
+        return _resize_chw(score.contiguous(), ori_shape[0], ori_shape[1])
+
+    def _crop_into(self, img, modal_x, crop_size, acc, sy, sx, margin, padded):
+        """process_image_rgbX + val_func_process_rgbX + margin crop + window add (one kernel)."""
+        d, x = self.process_image_rgbX(img, modal_x, crop_size)
+        s1, s2 = self.val_func_process_rgbX(d, x)
+        K, ch, cw = s1.shape
+        _lib.call("cmx_seg_window_accumulate", _lib.ptr(s1), _lib.ptr(s2), _lib.ptr(acc), K, ch, cw,
+                  margin[0], margin[1], margin[2], margin[3], acc.shape[1], acc.shape[2], sy, sx, _lib.stream())
+
+    def val_func_process_rgbX(self, input_data, input_modal_x, device=None):
+        """evaluator.py:374-396 up to the exp: the logits of the crop and (is_flip) of its mirror,
+        (K, h, w) fp32 each; the sum, mirror and exp are fused into cmx_seg_window_accumulate."""
+        net = self.val_func
+        was_training = net.training
+        net.eval()
+        with torch.no_grad():
+            score = net(input_data[None].contiguous(), input_modal_x[None].contiguous())[0].float().contiguous()
+            flip = None
+            if self.is_flip:
+                flip = net(input_data.flip(-1)[None].contiguous(),
+                           input_modal_x.flip(-1)[None].contiguous())[0].float().contiguous()
+        if was_training:
+            net.train()
+        return score, flip
+
+    def process_image_rgbX(self, img, modal_x, crop_size=None):
+        """evaluator.py:398-431 on (3, h, w) device images: normalise (utils/transforms.py:182-187,
+        applied to whatever the dataset produced, as the reference does) and pad to crop_size."""
+        mean = torch.as_tensor(self.norm_mean, dtype=torch.float32, device=img.device).view(-1, 1, 1)
+        std = torch.as_tensor(self.norm_std, dtype=torch.float32, device=img.device).view(-1, 1, 1)
+        p_img = (img / 255.0 - mean) / std
+        if modal_x.shape[0] == 1:                   # a 2-D modal map: normalize(x, 0, 1) (:404-406)
+            p_x = modal_x / 255.0
+        else:
+            p_x = (modal_x / 255.0 - mean) / std
+        if crop_size is not None:
+            m = _pad_margin(p_img.shape[1], p_img.shape[2], crop_size)
+            p_img = TF.pad(p_img, (m[2], m[3], m[0], m[1]))
+            p_x = TF.pad(p_x, (m[2], m[3], m[0], m[1]))
+        return p_img.contiguous(), p_x.contiguous()
+
+    # ------------------------------------------------------------------ dataset pass
+    def run(self, dataset=None, crop_size=None, stride_rate=2 / 3, device=None):
+        """Evaluate every sample (dict with data / modal_x / label, HWC / HW) and return
+        (iou, mean_IoU, mean_IoU_no_back, freq_IoU, mean_pixel_acc, pixel_acc)."""
+        dataset = dataset if dataset is not None else self.dataset
+        dev = self._device(device)
+        cc = ConfusionCounter(self.class_num, dev)
+        n = dataset.get_length() if hasattr(dataset, "get_length") else len(dataset)
+        for i in range(n):
+            d = dataset[i]
+            img = d["data"].transpose(1, 2, 0) if d["data"].ndim == 3 and d["data"].shape[0] == 3 else d["data"]
+            score = self.sliding_scores_rgbX(img, d["modal_x"], crop_size, stride_rate, dev)
+            cc.add_score(score, torch.as_tensor(np.ascontiguousarray(d["label"])))
+        hist, labeled, correct = cc.result()
+        return compute_score(hist, correct, labeled)
