@@ -26,17 +26,21 @@
 
 namespace {
 
+// one (class, crop row) per blockIdx.y row-chunk; lanes along the row (coalesced, no 64-bit
+// index division per element)
 __global__ void window_acc_kernel(const float* __restrict__ s1, const float* __restrict__ s2, float* __restrict__ acc,
                                   int K, int ch, int cw, int m0, int m2, int h, int w, int PH, int PW, int sy, int sx) {
-  const long n = (long)K * h * w;
-  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
-    const int j = (int)(e % w);
-    const long r = e / w;
-    const int i = (int)(r % h), k = (int)(r / h);
-    const long srow = ((long)k * ch + m0 + i) * cw;
-    float v = s1[srow + m2 + j];
-    if (s2) v += s2[srow + cw - 1 - (m2 + j)];
-    acc[((long)k * PH + sy + i) * PW + sx + j] += expf(v);
+  const int rows = K * h;
+  for (int r = blockIdx.x; r < rows; r += gridDim.x) {
+    const int k = r / h, i = r - k * h;
+    const float* a = s1 + ((long)k * ch + m0 + i) * cw;
+    const float* b = s2 ? s2 + ((long)k * ch + m0 + i) * cw : nullptr;
+    float* o = acc + ((long)k * PH + sy + i) * PW + sx;
+    for (int j = threadIdx.x; j < w; j += blockDim.x) {
+      float v = a[m2 + j];
+      if (b) v += b[cw - 1 - (m2 + j)];
+      o[j] += expf(v);
+    }
   }
 }
 
@@ -57,15 +61,21 @@ __global__ __launch_bounds__(CONF_THREADS) void argmax_conf_kernel(const float* 
     int bi;
     if (score) {
       // first maximum over classes (consecutive threads: consecutive pixels of one class row)
+      // 8 class rows in flight per step (loads first, then the ordered comparisons)
       float best = score[p];
       bi = 0;
       bool bnan = best != best;
-      for (int k = 1; k < K; ++k) {
-        const float v = score[(long)k * HW + p];
-        if (!bnan && (v > best || v != v)) {
-          best = v;
-          bi = k;
-          bnan = v != v;
+      for (int k0 = 1; k0 < K; k0 += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = k0 + u < K ? score[(long)(k0 + u) * HW + p] : -INFINITY;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (k0 + u < K && !bnan && (v[u] > best || v[u] != v[u])) {
+            best = v[u];
+            bi = k0 + u;
+            bnan = v[u] != v[u];
+          }
         }
       }
       if (pred) pred[p] = bi;
@@ -102,11 +112,10 @@ int cmx_seg_window_accumulate(const float* s1, const float* s2, float* acc, int 
               "seg_window_accumulate: K=%d crop %dx%d margins %d %d %d %d", K, ch, cw, m0, m1, m2, m3);
   CMX_REQUIRE(sy >= 0 && sx >= 0 && sy + h <= PH && sx + w <= PW, CMX_ERR_SHAPE,
               "seg_window_accumulate: window (%d, %d) + %dx%d outside %dx%d", sy, sx, h, w, PH, PW);
-  const long n = (long)K * h * w;
-  long blocks = (n + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(window_acc_kernel, dim3((unsigned)blocks), dim3(256), 0, s, s1, s2, acc, K, ch, cw, m0, m2, h, w,
-                     PH, PW, sy, sx);
+  const long rows = (long)K * h;
+  const unsigned blocks = (unsigned)(rows < 65536 ? rows : 65536);
+  hipLaunchKernelGGL(window_acc_kernel, dim3(blocks), dim3(w >= 256 ? 256 : 64 * ((w + 63) / 64)), 0, s, s1, s2, acc,
+                     K, ch, cw, m0, m2, h, w, PH, PW, sy, sx);
   return cmx_check_launch("seg_window_accumulate");
 }
 
