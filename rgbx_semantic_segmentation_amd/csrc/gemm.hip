@@ -450,9 +450,20 @@ struct GroupRec {
   int bm, bn, blk0, nblk;
 };
 
-__global__ __launch_bounds__(256, 2) void gemm_grouped_kernel(const GroupRec* __restrict__ recs, int nrec) {
+// chunked round-robin block -> tile map: runs of `ch` consecutive tiles (neighbours sharing
+// operand panels in one L2) are dealt to the 8 XCDs in turn, so problems whose tiles cost very
+// different k-loop lengths spread over every XCD instead of loading the one whose contiguous
+// range they fall in (xcd_tile).  Tiles past the last whole round keep the identity map.
+__device__ __forceinline__ int xcd_chunk_tile(int b, int nt, int ch) {
+  const int full = nt / (8 * ch) * (8 * ch);
+  if (b >= full) return b;
+  const int x = b & 7, j = b >> 3;
+  return ((j / ch) * 8 + x) * ch + j % ch;
+}
+
+__global__ __launch_bounds__(256, 2) void gemm_grouped_kernel(const GroupRec* __restrict__ recs, int nrec, int chunk) {
   __shared__ __attribute__((aligned(1024))) char smem[gemm_smem_bytes<128, 128, 2>()];
-  const int lin = xcd_tile(blockIdx.x, gridDim.x);
+  const int lin = chunk > 0 ? xcd_chunk_tile(blockIdx.x, gridDim.x, chunk) : xcd_tile(blockIdx.x, gridDim.x);
   int lo = 0, hi = nrec - 1;                    // last record with blk0 <= lin
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -1090,7 +1101,14 @@ int cmx_conv_implicit_fwd(const void* x, const void* Wt, void* y, const float* b
 
 int cmx_gemm_grouped(const void* recs, int nrec, int total_blocks, hipStream_t s) {
   CMX_REQUIRE(recs && nrec > 0 && total_blocks > 0, CMX_ERR_ARG, "gemm_grouped: empty launch");
-  hipLaunchKernelGGL(gemm_grouped_kernel, dim3(total_blocks), dim3(256), 0, s, (const GroupRec*)recs, nrec);
+  // XCD map of the grouped grid: chunked round-robin with 16-tile runs (CMX_GROUPED_CHUNK=n to
+  // change the run, 0 = the contiguous xcd_tile map).  Measured on the B2 step's 8174-block
+  // launch: 695-702 us contiguous, 624-633 us for runs of 4..128 tiles (scripts/grouped_chunk_sweep.sh)
+  static const int chunk = [] {
+    const char* e = getenv("CMX_GROUPED_CHUNK");
+    return e ? atoi(e) : 16;
+  }();
+  hipLaunchKernelGGL(gemm_grouped_kernel, dim3(total_blocks), dim3(256), 0, s, (const GroupRec*)recs, nrec, chunk);
   return cmx_check_launch("gemm_grouped");
 }
 
