@@ -1101,12 +1101,14 @@ int cmx_conv_implicit_fwd(const void* x, const void* Wt, void* y, const float* b
 
 int cmx_gemm_grouped(const void* recs, int nrec, int total_blocks, hipStream_t s) {
   CMX_REQUIRE(recs && nrec > 0 && total_blocks > 0, CMX_ERR_ARG, "gemm_grouped: empty launch");
-  // XCD map of the grouped grid: chunked round-robin with 16-tile runs (CMX_GROUPED_CHUNK=n to
+  // XCD map of the grouped grid: chunked round-robin with 64-tile runs (CMX_GROUPED_CHUNK=n to
   // change the run, 0 = the contiguous xcd_tile map).  Measured on the B2 step's 8174-block
-  // launch: 695-702 us contiguous, 624-633 us for runs of 4..128 tiles (scripts/grouped_chunk_sweep.sh)
+  // launch: 695-702 us contiguous, 624-633 us for runs of 4..128 tiles
+  // (scripts/grouped_chunk_sweep.sh); PMC HBM bytes per launch 3.13 GB at 16-tile runs,
+  // 2.48 GB at 64 (contiguous: 2.43 GB), so 64 keeps the L2 reuse of neighbouring tiles
   static const int chunk = [] {
     const char* e = getenv("CMX_GROUPED_CHUNK");
-    return e ? atoi(e) : 16;
+    return e ? atoi(e) : 64;
   }();
   hipLaunchKernelGGL(gemm_grouped_kernel, dim3(total_blocks), dim3(256), 0, s, (const GroupRec*)recs, nrec, chunk);
   return cmx_check_launch("gemm_grouped");
