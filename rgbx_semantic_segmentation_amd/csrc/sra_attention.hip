@@ -438,6 +438,7 @@ int bwd_qc(int N, int nchunk) {
 
 // sra_fast.hip: LDS-resident K/V path for bf16, D = 64, Nk <= 320
 bool sra_fast_ok(int D, int Nk, int dtype, const void* const* ptrs, int nptr, const long* strides, int nstr);
+bool sra_fast_fwd_ok(int D, int Nk, int dtype, const void* const* ptrs, int nptr, const long* strides, int nstr);
 void sra_fwd_fast_launch(const void* q, const void* k, const void* v, void* o, float* lse, int Bt, int N, int Nk,
                          int heads, long qs, long kvs, long os, float sl2, hipStream_t s);
 void sra_dq_fast_launch(const void* q, const void* k, const void* v, const void* o, const void* dout,
@@ -467,7 +468,7 @@ int cmx_sra_attn_fwd(const void* q, const void* k, const void* v, void* o, float
   {
     const void* ptrs[] = {q, k, v, o};
     const long strides[] = {qs, kvs, os};
-    if (sra_fast_ok(D, Nk, dtype, ptrs, 4, strides, 3)) {
+    if (sra_fast_fwd_ok(D, Nk, dtype, ptrs, 4, strides, 3)) {
       sra_fwd_fast_launch(q, k, v, o, lse, Bt, N, Nk, heads, qs, kvs, os, sl2, s);
       return cmx_check_launch("sra_fwd");
     }

@@ -92,8 +92,6 @@ __global__ __launch_bounds__(64 * NW) void sra_fwd_fast(const bf16* __restrict__
   char* Vi = smem + NKP_MAX * ROWB;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int b = blockIdx.z, head = blockIdx.y;
-  stage_rows(k + (long)b * Nk * kvs + head * HD, kvs, Nk, nkp, Ki, wave, lane, NW);
-  stage_rows(v + (long)b * Nk * kvs + head * HD, kvs, Nk, nkp, Vi, wave, lane, NW);
 
   const int q0 = (blockIdx.x * NW + wave) * 32 * QW;
   const bf16* qb = q + (long)b * N * qs + head * HD;
@@ -114,10 +112,18 @@ __global__ __launch_bounds__(64 * NW) void sra_fwd_fast(const bf16* __restrict__
     m[u] = -INFINITY;
     l[u] = 0.f;
   }
+  // keys in LDS-sized chunks (one chunk when Nk <= NKP_MAX, every B2 / B4 stage; B5 at
+  // 1024 x 1024 has Nk = 1024 at every stage): the online softmax state carries across chunks
+  for (int c0 = 0; c0 < Nk; c0 += NKP_MAX) {
+  const int nc = min(NKP_MAX, Nk - c0);
+  const int nkc = (nc + KTILE - 1) / KTILE * KTILE;
+  if (c0 > 0) __syncthreads();                  // every wave is done with the previous chunk
+  stage_rows(k + ((long)b * Nk + c0) * kvs + head * HD, kvs, nc, nkc, Ki, wave, lane, NW);
+  stage_rows(v + ((long)b * Nk + c0) * kvs + head * HD, kvs, nc, nkc, Vi, wave, lane, NW);
   vm_wait<0>();
   __syncthreads();
 
-  for (int t0 = 0; t0 < nkp; t0 += KTILE) {
+  for (int t0 = 0; t0 < nkc; t0 += KTILE) {
     f32x16 sa[QW][2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -131,7 +137,7 @@ __global__ __launch_bounds__(64 * NW) void sra_fwd_fast(const bf16* __restrict__
         for (int s = 0; s < 4; ++s) sa[u][ks] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[s], qf[u][s], sa[u][ks], 0, 0, 0);
       }
     }
-    const bool tail = t0 + KTILE > Nk;
+    const bool tail = t0 + KTILE > nc;
 #pragma unroll
     for (int u = 0; u < QW; ++u) {
       float mt = -INFINITY;
@@ -140,7 +146,7 @@ __global__ __launch_bounds__(64 * NW) void sra_fwd_fast(const bf16* __restrict__
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           float x = sa[u][ks][i];
-          if (tail && t0 + 32 * ks + accrow(i, h) >= Nk) x = -INFINITY;
+          if (tail && t0 + 32 * ks + accrow(i, h) >= nc) x = -INFINITY;
           sa[u][ks][i] = x;
           mt = fmaxf(mt, x);
         }
@@ -179,6 +185,7 @@ __global__ __launch_bounds__(64 * NW) void sra_fwd_fast(const bf16* __restrict__
         }
       }
   }
+  }                                             // key chunks
 #pragma unroll
   for (int u = 0; u < QW; ++u) {
     const int qi = q0 + 32 * u + r;
@@ -445,6 +452,16 @@ int pick_nw(int N, int heads, int Bt, int qw) {
 }
 
 }  // namespace
+
+// the forward streams keys through LDS in NKP_MAX-key chunks: any Nk (bf16, D = 64, 16-B rows)
+bool sra_fast_fwd_ok(int D, int Nk, int dtype, const void* const* ptrs, int nptr, const long* strides, int nstr) {
+  if (dtype != 1 || D != HD || Nk <= 0) return false;
+  for (int i = 0; i < nptr; ++i)
+    if (ptrs[i] && ((uintptr_t)ptrs[i] & 15)) return false;
+  for (int i = 0; i < nstr; ++i)
+    if (strides[i] % 8) return false;
+  return true;
+}
 
 // bf16, D = 64, Nk <= 320, 16-B aligned rows: the LDS-resident path (sra_attention.hip calls these)
 bool sra_fast_ok(int D, int Nk, int dtype, const void* const* ptrs, int nptr, const long* strides, int nstr) {

@@ -54,7 +54,10 @@ def sra_ref(q, kv, heads, D):
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("Bt,N,Nk,heads,D", [(4, 19200 // 16, 300, 1, 64), (2, 333, 70, 2, 32),
                                               (4, 300, 300, 8, 64), (2, 1200, 300, 5, 64),
-                                              (1, 65, 80, 8, 32)])
+                                              (1, 65, 80, 8, 32),
+                                              # Nk > 320: the fast forward streams keys in
+                                              # LDS-sized chunks (B5 1024 x 1024: Nk = 1024)
+                                              (2, 700, 1024, 2, 64), (1, 333, 650, 1, 64)])
 def test_sra_attention(dev, dtype, Bt, N, Nk, heads, D):
     from rgbx_semantic_segmentation_amd import kernels as K
     torch.manual_seed(1)
