@@ -499,14 +499,15 @@ int cmx_sra_attn_bwd(const void* q, const void* k, const void* v, const void* o,
   const float sl2 = scale * 1.4426950408889634f;
   const void* ptrs[] = {q, k, v, o, dout, dq};
   const long strides[] = {qs, kvs, os, dos, dqs};
-  const bool fast = sra_fast_ok(D, Nk, dtype, ptrs, 6, strides, 5);
+  const bool fast = sra_fast_ok(D, Nk, dtype, ptrs, 6, strides, 5);          // dK / dV: Nk <= 320
+  const bool fast_dq = sra_fast_fwd_ok(D, Nk, dtype, ptrs, 6, strides, 5);    // dQ: K / V chunked
   const int nc = fast ? sra_dkv_fast_chunks(Bt, N, heads) : bwd_nchunk(Bt, N, Nk, heads);
   const int qc = bwd_qc(N, nc);
   float* Dws = workspace;
   float* ws_dk = Dws + (size_t)Bt * heads * N;
   float* ws_dv = ws_dk + (size_t)nc * Bt * heads * Nk * D;
   SRA_D_DISPATCH(D, CMX_DISPATCH(dtype, T, {
-    if (fast)
+    if (fast_dq)
       sra_dq_fast_launch(q, k, v, o, dout, lse, Dws, dq, Bt, N, Nk, heads, qs, kvs, os, dos, dqs, sl2, scale, s);
     else
       hipLaunchKernelGGL((sra_bwd_dq_kernel<T, DD>), dim3(cdiv(N, BQ), heads, Bt), dim3(256), 0, s,

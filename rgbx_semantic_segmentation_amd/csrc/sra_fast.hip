@@ -212,8 +212,6 @@ __global__ __launch_bounds__(64 * NW) void sra_dq_fast(const bf16* __restrict__ 
   char* Vi = smem + NKP_MAX * ROWB;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int b = blockIdx.z, head = blockIdx.y;
-  stage_rows(k + (long)b * Nk * kvs + head * HD, kvs, Nk, nkp, Ki, wave, lane, NW);
-  stage_rows(v + (long)b * Nk * kvs + head * HD, kvs, Nk, nkp, Vi, wave, lane, NW);
 
   const int q0 = (blockIdx.x * NW + wave) * 32 * QW;
   bf16x8 qf[QW][4], df[QW][4];
@@ -251,11 +249,18 @@ __global__ __launch_bounds__(64 * NW) void sra_dq_fast(const bf16* __restrict__ 
   f32x16 acc[QW][2];
 #pragma unroll
   for (int u = 0; u < QW; ++u) acc[u][0] = acc[u][1] = zero16();
+  // keys in LDS-sized chunks, as the forward (dQ sums over every key: nothing to carry but acc)
+  for (int c0 = 0; c0 < Nk; c0 += NKP_MAX) {
+  const int nc = min(NKP_MAX, Nk - c0);
+  const int nkc = (nc + KTILE - 1) / KTILE * KTILE;
+  if (c0 > 0) __syncthreads();                  // every wave is done with the previous chunk
+  stage_rows(k + ((long)b * Nk + c0) * kvs + head * HD, kvs, nc, nkc, Ki, wave, lane, NW);
+  stage_rows(v + ((long)b * Nk + c0) * kvs + head * HD, kvs, nc, nkc, Vi, wave, lane, NW);
   vm_wait<0>();
   __syncthreads();
 
-  for (int t0 = 0; t0 < nkp; t0 += KTILE) {
-    const bool tail = t0 + KTILE > Nk;
+  for (int t0 = 0; t0 < nkc; t0 += KTILE) {
+    const bool tail = t0 + KTILE > nc;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int kb = t0 + 32 * ks;
@@ -277,7 +282,7 @@ __global__ __launch_bounds__(64 * NW) void sra_dq_fast(const bf16* __restrict__ 
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           float p = fexp2(sa[i] * sl2 - lse2[u]);
-          if (tail && kb + accrow(i, h) >= Nk) p = 0.f;
+          if (tail && kb + accrow(i, h) >= nc) p = 0.f;
           ds[u][i] = p * (dp[i] - Dq[u]);
         }
       }
@@ -294,6 +299,7 @@ __global__ __launch_bounds__(64 * NW) void sra_dq_fast(const bf16* __restrict__ 
       }
     }
   }
+  }                                             // key chunks
 #pragma unroll
   for (int u = 0; u < QW; ++u) {
     const int qi = q0 + 32 * u + r;
