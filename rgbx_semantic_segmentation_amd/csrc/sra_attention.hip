@@ -499,8 +499,9 @@ int cmx_sra_attn_bwd(const void* q, const void* k, const void* v, const void* o,
   const float sl2 = scale * 1.4426950408889634f;
   const void* ptrs[] = {q, k, v, o, dout, dq};
   const long strides[] = {qs, kvs, os, dos, dqs};
-  const bool fast = sra_fast_ok(D, Nk, dtype, ptrs, 6, strides, 5);          // dK / dV: Nk <= 320
-  const bool fast_dq = sra_fast_fwd_ok(D, Nk, dtype, ptrs, 6, strides, 5);    // dQ: K / V chunked
+  // fast path for any Nk: dQ streams K / V in LDS-sized chunks, dK / dV splits keys over workgroups
+  const bool fast = sra_fast_fwd_ok(D, Nk, dtype, ptrs, 6, strides, 5);
+  const bool fast_dq = fast;
   const int nc = fast ? sra_dkv_fast_chunks(Bt, N, heads) : bwd_nchunk(Bt, N, Nk, heads);
   const int qc = bwd_qc(N, nc);
   float* Dws = workspace;

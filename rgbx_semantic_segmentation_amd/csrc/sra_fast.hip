@@ -334,7 +334,8 @@ __global__ __launch_bounds__(64 * (NKP_MAX / 32)) void sra_dkv_fast(
   __shared__ __attribute__((aligned(1024))) char smem[2 * DKV_TILE_BYTES];
   const int nw = blockDim.x >> 6;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  const int head = blockIdx.y, b = blockIdx.z, c = blockIdx.x;
+  // blockIdx.x = (key chunk, query chunk): a workgroup holds at most NKP_MAX keys on its lanes
+  const int head = blockIdx.y, b = blockIdx.z, c = blockIdx.x % nchunk, kc0 = blockIdx.x / nchunk * NKP_MAX;
   const int qbeg = c * QC, qend = min(N, qbeg + QC);
   const long sbase = ((long)b * heads + head) * N;
   const i32x4 rq = make_rsrc(q + (long)b * N * qs + head * HD);
@@ -365,7 +366,7 @@ __global__ __launch_bounds__(64 * (NKP_MAX / 32)) void sra_dkv_fast(
   };
 
   // this wave's 32 keys: K, V fragments as B operands (k = d), lane = key
-  const int key = 32 * wave + r;
+  const int key = kc0 + 32 * wave + r;
   bf16x8 kf[4], vf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
@@ -528,10 +529,11 @@ int sra_dkv_fast_chunks(int Bt, int N, int heads) {
 void sra_dkv_fast_launch(const void* q, const void* k, const void* v, const void* dout, const float* lse,
                          const float* Dws, float* ws_dk, float* ws_dv, int Bt, int N, int Nk, int heads, long qs,
                          long kvs, long dos, int nchunk, float sl2, float scale, hipStream_t s) {
-  const int nkw = (Nk + 31) / 32 * 32;           // one 32-key sub-tile per wave
+  const int nkw = ((Nk < NKP_MAX ? Nk : NKP_MAX) + 31) / 32 * 32;   // one 32-key sub-tile per wave
+  const int nkc = (Nk + NKP_MAX - 1) / NKP_MAX;                       // key chunks (Nk > NKP_MAX)
   int qc = (N + nchunk - 1) / nchunk;
   qc = (qc + QT - 1) / QT * QT;
-  hipLaunchKernelGGL(sra_dkv_fast, dim3(nchunk, heads, Bt), dim3(2 * nkw), 0, s, (const bf16*)q, (const bf16*)k,
+  hipLaunchKernelGGL(sra_dkv_fast, dim3(nchunk * nkc, heads, Bt), dim3(2 * nkw), 0, s, (const bf16*)q, (const bf16*)k,
                      (const bf16*)v, (const bf16*)dout, lse, Dws, ws_dk, ws_dv, Bt, N, Nk, heads, qs, kvs, dos, qc,
                      nchunk, sl2, scale);
 }
