@@ -75,6 +75,7 @@ int cmx_dwconv3x3_fwd(const void* h, const float* w, const float* b, void* out, 
 /* fwd_save also writes gprime = act'(z) (z = the conv + bias pre-activation); bwd_saved then forms dz = da * gprime
  * with no 3x3 recompute (LDS-tiled channel counts only; dw = db = NULL leaves the partials as cmx_dwconv3x3_bwd). */
 int cmx_dwconv3x3_fwd_save(const void* h, const float* w, const float* b, void* out, void* gprime, int NI, int imgs_per_group, int H, int W, int C, int act, int dtype, hipStream_t stream);
+int cmx_dwconv3x3_bwd_saved_tiles(int imgs_per_group, int H, int W);
 int cmx_dwconv3x3_bwd_saved(const void* da, const void* h, const void* gprime, const float* w, void* dh, float* dw, float* db, float* workspace, int NI, int imgs_per_group, int H, int W, int C, int accumulate, int dtype, hipStream_t stream);
 size_t cmx_dwconv3x3_bwd_workspace(int NI, int imgs_per_group, int H, int W, int C);
 int cmx_dwconv3x3_bwd(const void* da, const void* h, const float* w, const float* b, void* dz, void* dh, float* dw, float* db, float* workspace, int NI, int imgs_per_group, int H, int W, int C, int act, int accumulate, int dtype, hipStream_t stream);

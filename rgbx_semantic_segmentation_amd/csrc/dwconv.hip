@@ -271,6 +271,9 @@ __global__ void dw_scatter_kernel(const float* __restrict__ tmp, float* __restri
 constexpr int TY2 = 8, TX2 = 16;                 // inner tile
 constexpr int EY = TY2 + 2, EX = TX2 + 2;         // + 1-pixel halo
 constexpr int HY = TY2 + 4, HX = TX2 + 4;         // + 2-pixel halo (backward h tile)
+// saved-act backward tile: 16 x 16 (halo 1.27x instead of 1.41x; measured stage 1 70.6 -> 52.3 us,
+// while the forward is faster at 8 x 16: 34.2 vs 37.0 us, scripts/bench_dw.py)
+constexpr int TYB = 16, TXB = 16, EYB = TYB + 2, EXB = TXB + 2;
 
 template <typename T> struct V8;                  // 8 channels as stored
 template <> struct V8<bf16> { uint4 a; };
@@ -331,6 +334,7 @@ __device__ __forceinline__ void load_w72(const float* wg, cmx_f2 (&w2)[4][9]) {
 struct Tile2 {
   int g, img, ty0, tx0, cb0, sp;
 };
+template <int TY_ = TY2, int TX_ = TX2>
 __device__ __forceinline__ Tile2 tile2_of(int CB, int ipg, int tiles_x, int tiles_y, int ncb) {
   Tile2 t;
   int b = blockIdx.x;
@@ -340,7 +344,7 @@ __device__ __forceinline__ Tile2 tile2_of(int CB, int ipg, int tiles_x, int tile
   const int ty = b % tiles_y; b /= tiles_y;
   t.img = b;
   t.g = blockIdx.y;
-  t.ty0 = ty * TY2; t.tx0 = tx * TX2; t.cb0 = cb * CB;
+  t.ty0 = ty * TY_; t.tx0 = tx * TX_; t.cb0 = cb * CB;
   return t;
 }
 
@@ -496,14 +500,14 @@ template <typename T, int CB>
 __device__ __forceinline__ void stage_dz_h(const T* __restrict__ da, const T* __restrict__ gp,
                                            const T* __restrict__ h, T* dzs, T* hs, int ty0, int tx0, int H, int W,
                                            int C) {
-  constexpr int NCG = CB / 8, NE = EY * EX, NIN = TY2 * TX2;
+  constexpr int NCG = CB / 8, NE = EYB * EXB, NIN = TYB * TXB;
   constexpr int ITE = (NCG * NE + 255) / 256, ITI = (NCG * NIN + 255) / 256;
   V8<T> a[ITE], g[ITE], hv[ITI];
 #pragma unroll
   for (int k = 0; k < ITE; ++k) {
     const int it = threadIdx.x + k * 256;
     const int cg = it % NCG, px = it / NCG;
-    const int y = ty0 - 1 + px / EX, x = tx0 - 1 + px % EX;
+    const int y = ty0 - 1 + px / EXB, x = tx0 - 1 + px % EXB;
     a[k] = v8_zero<T>();
     g[k] = v8_zero<T>();
     if (it < NCG * NE && y >= 0 && y < H && x >= 0 && x < W) {
@@ -516,7 +520,7 @@ __device__ __forceinline__ void stage_dz_h(const T* __restrict__ da, const T* __
   for (int k = 0; k < ITI; ++k) {
     const int it = threadIdx.x + k * 256;
     const int cg = it % NCG, px = it / NCG;
-    const int y = ty0 + px / TX2, x = tx0 + px % TX2;
+    const int y = ty0 + px / TXB, x = tx0 + px % TXB;
     hv[k] = v8_zero<T>();
     if (it < NCG * NIN && y < H && x < W) hv[k] = v8_load<T>(h + ((long)y * W + x) * C + cg * 8);
   }
@@ -540,18 +544,18 @@ __device__ __forceinline__ void stage_dz_h(const T* __restrict__ da, const T* __
 }
 
 template <typename T, int CB>
-__global__ __launch_bounds__(256, 4) void dw2_bwdg_kernel(const T* __restrict__ da, const T* __restrict__ h,
+__global__ __launch_bounds__(256, 2) void dw2_bwdg_kernel(const T* __restrict__ da, const T* __restrict__ h,
                                                        const T* __restrict__ gprime, const float* __restrict__ w,
                                                        T* __restrict__ dh, float* __restrict__ part, int ipg, int H,
                                                        int W, int C, int tiles_x, int tiles_y, int ncb, int nsp) {
   constexpr int NCQ = CB / 4, PPI = 256 / NCQ;
-  constexpr int NE = EY * EX, NIN = TY2 * TX2;
+  constexpr int NE = EYB * EXB, NIN = TYB * TXB;
   constexpr int LPQ = 64 / NCQ;                     // lanes of one quad in a wave (4 or 8)
   constexpr int NV = LPQ == 4 ? 10 : 5;             // partials per lane after the in-wave reduce-scatter
   __shared__ __attribute__((aligned(16))) T dzs[NE * CB];
   __shared__ __attribute__((aligned(16))) T hs[NIN * CB];
   static_assert(sizeof(dzs) >= 4 * 64 * NV * sizeof(float), "cross-wave reduce buffer");
-  const Tile2 t = tile2_of(CB, ipg, tiles_x, tiles_y, ncb);
+  const Tile2 t = tile2_of<TYB, TXB>(CB, ipg, tiles_x, tiles_y, ncb);
   const long ibase = ((long)t.g * ipg + t.img) * H * W * C + t.cb0;
   stage_dz_h<T, CB>(da + ibase, gprime + ibase, h + ibase, dzs, hs, t.ty0, t.tx0, H, W, C);
   const int cq = threadIdx.x % NCQ, pl = threadIdx.x / NCQ;
@@ -567,7 +571,7 @@ __global__ __launch_bounds__(256, 4) void dw2_bwdg_kernel(const T* __restrict__ 
 #pragma unroll
     for (int k = 0; k < 10; ++k) acc[u][k] = pk_splat(0.f);
   for (int it = pl; it < NIN; it += PPI) {
-    const int r = it / TX2, c = it % TX2;
+    const int r = it / TXB, c = it % TXB;
     const int y = t.ty0 + r, x = t.tx0 + c;
     if (y >= H || x >= W) continue;
     cmx_f2 hv[2];
@@ -578,7 +582,7 @@ __global__ __launch_bounds__(256, 4) void dw2_bwdg_kernel(const T* __restrict__ 
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         cmx_f2 dv[2];
-        v4_unpack<T>(v4_load<T>(dzc + ((r + 2 - i) * EX + c + 2 - j) * CB), dv);
+        v4_unpack<T>(v4_load<T>(dzc + ((r + 2 - i) * EXB + c + 2 - j) * CB), dv);
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           g[u] = pk_fma(wr[u][i * 3 + j], dv[u], g[u]);
@@ -815,7 +819,7 @@ int cmx_dwconv3x3_bwd_saved(const void* da, const void* h, const void* gprime, c
   CMX_REQUIRE(CB && NI % imgs_per_group == 0 && gprime, CMX_ERR_SHAPE, "dwconv_bwd_saved: C=%d", C);
   CMX_REQUIRE((long)NI * H * W * C < (1L << 31), CMX_ERR_SHAPE, "dwconv_bwd_saved: tensor too large");
   const int G = NI / imgs_per_group;
-  const int tx = cdiv(W, TX2), ty = cdiv(H, TY2), ncb = C / CB;
+  const int tx = cdiv(W, TXB), ty = cdiv(H, TYB), ncb = C / CB;
   const int P = imgs_per_group * ty * tx;
   const dim3 grid((unsigned)P * ncb, G);
   CMX_DISPATCH(dtype, T, {
@@ -835,6 +839,12 @@ int cmx_dwconv3x3_bwd_saved(const void* da, const void* h, const void* gprime, c
   hipLaunchKernelGGL(dw_scatter_kernel, dim3(cdiv(tot, 256) < 4096 ? cdiv(tot, 256) : 4096), dim3(256), 0, s, tmp, dw,
                      db, G, C, accumulate);
   return cmx_check_launch("dwconv_bwd_saved");
+}
+
+// partial-slab count (tiles per group) of cmx_dwconv3x3_bwd_saved: its dW / db partials occupy
+// the first G * P * C * 10 floats of the (larger) cmx_dwconv3x3_bwd_workspace
+int cmx_dwconv3x3_bwd_saved_tiles(int imgs_per_group, int H, int W) {
+  return imgs_per_group * cdiv(H, TYB) * cdiv(W, TXB);
 }
 
 size_t cmx_dwconv3x3_bwd_workspace(int NI, int imgs_per_group, int H, int W, int C) {

@@ -395,7 +395,7 @@ class DWConvF(Function):
                    K.dtype_code(h), K.stream())
             if defer:
                 G = NI // ipg
-                P = nbytes // (40 * G * C) - 1
+                P = K.query("cmx_dwconv3x3_bwd_saved_tiles", ipg, H, W)
                 deferred.reduce(ws, wg, bg, G, P, P * C * 10, C * 10, C, 10, 9, wg.stride(0), 9, bg.stride(0), 1)
             return dh, None, None, None, None, None, None, None, None, None, None
         # the LDS-tiled backward (C % 32 == 0) keeps dz on chip; the strip path writes it
