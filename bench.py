@@ -41,25 +41,57 @@ def parse():
     p.add_argument("--loss-scaling", action="store_true",
                    help="config 5's AMP step: dynamic loss scaling (GradScaler) inside the captured step")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-steps", type=int, default=1)
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-steps", type=int, default=3)
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="0: every CPU this process may use (affinity, capped by the cgroup CPU quota)")
     return p.parse_args()
 
 
+def host_cpus():
+    """(threads to use, nproc, CPU model).  ``nproc`` is the machine's count; the usable share
+    is the affinity mask capped by the cgroup v2 CPU quota (the GPU box grants a share of a
+    much larger host: oversubscribing it would understate the CPU baseline)."""
+    nproc = os.cpu_count() or 1
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            usable = min(usable, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return usable, nproc, model
+
+
 def cpu_baseline(args):
-    """The oracle's restatement of the reference train step on the host cores (fp32),
-    bounded sample: 1 untimed + args.cpu_steps timed steps of the SAME workload."""
+    """The oracle's restatement of the reference train step on the host cores (fp32), on
+    bounded samples: the SAME workload as the GPU line (1 untimed + args.cpu_steps timed
+    steps) and config 1 of BASELINE.json (CMX-B0 240x320 bs=1 K=9: 2 untimed + 10 timed)."""
     from oracle.cmx_ref import CMXConfig
     from oracle.train_ref import time_cpu_steps
     from rgbx_semantic_segmentation_amd.data import make_batch
-    threads = min(args.cpu_threads, os.cpu_count() or 1)
+    usable, nproc, model = host_cpus()
+    threads = args.cpu_threads or usable
     batch = make_batch(args.batch, args.height, args.width, args.classes, seed=12345)
     cfg = CMXConfig(backbone=args.backbone, num_classes=args.classes)
     sec = time_cpu_steps(cfg, batch, warmup=1, steps=args.cpu_steps, threads=threads)
+    b0 = make_batch(1, 240, 320, 9, seed=12345)
+    sec0 = time_cpu_steps(CMXConfig(backbone="mit_b0", num_classes=9), b0, warmup=2, steps=10, threads=threads)
     return {"value": round(args.batch / sec, 4), "unit": "images/s", "cores": threads, "kind": "port",
             "sample": f"oracle/train_ref.py (fp32 PyTorch-CPU restatement of train.py) {args.backbone} "
-                      f"{args.height}x{args.width} bs={args.batch}: 1 warm-up + {args.cpu_steps} timed step(s), "
-                      f"{sec:.2f} s/step"}
+                      f"{args.height}x{args.width} bs={args.batch} K={args.classes}: 1 warm-up + {args.cpu_steps} "
+                      f"timed steps, {sec:.2f} s/step",
+            "host": {"nproc": nproc, "threads_used": threads, "cpu_model": model},
+            "config1": {"workload": "CMX-B0 train step 240x320 bs=1 K=9 (BASELINE.json configs[0])",
+                        "value": round(1.0 / sec0, 4), "unit": "images/s", "sample": f"2 warm-up + 10 timed steps, "
+                                                                                     f"{sec0 * 1e3:.1f} ms/step"}}
 
 
 def main():
@@ -178,7 +210,9 @@ def main():
     # No optimizer step follows it, so the gradient all-reduce hooks are detached first.
     from rgbx_semantic_segmentation_amd.roofline import measure_dominant
     model.backbone.grad_sync = None
-    roof = measure_dominant(model, (rgb, x, lab))
+    workload = f"CMX-{args.backbone.replace('mit_', '').upper()} train step {args.height}x{args.width} " \
+               f"bs={args.batch} K={args.classes}"
+    roof = measure_dominant(model, (rgb, x, lab), workload)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -199,8 +233,7 @@ def main():
             "dtype": "bf16" if args.dtype in ("bfloat16", "bf16") else "fp32",
             "data": "synthetic (seeded uint8 RGB + replicated X plane, ImageNet-normalised; uniform labels "
                     "with one 25x25 ignore block per image; random-init weights)",
-            "config": {"workload": f"CMX-{args.backbone.replace('mit_', '').upper()} train step "
-                                   f"{args.height}x{args.width}", "model": f"CMX-{args.backbone}",
+            "config": {"workload": workload, "model": f"CMX-{args.backbone}",
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "image": [args.height, args.width], "classes": args.classes,
                        "parallelism": f"dp{world}", "hip_graph": graph is not None,

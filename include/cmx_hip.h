@@ -56,6 +56,11 @@ int cmx_act_fwd(const void* x, void* y, int64_t n, int act, int dtype, hipStream
 int cmx_act_bwd(const void* dy, const void* z, void* dx, int64_t n, int act, int dtype, hipStream_t stream);
 int cmx_partials_sum(const float* ws, float* out, int G, int nblk, int W, int accumulate, float alpha, hipStream_t stream);
 int cmx_cast_f32_bf16(const float* src, void* dst, int64_t n, hipStream_t stream);
+/* bf16 gradient payload of the DP exchange (replaces DDP's fp32 bucket all-reduce,
+   train.py:145-146 / engine.py:56): out = bf16(sum over P chunks of in, fp32 accumulate);
+   and the bf16 -> fp32 copy of the gathered sums. */
+int cmx_shard_sum_bf16(const void* in, void* out, int P, int64_t n, hipStream_t stream);
+int cmx_cast_bf16_f32(const void* src, float* dst, int64_t n, hipStream_t stream);
 size_t cmx_colsum_workspace(int64_t M, int G, int N);
 int cmx_colsum(const void* x, float* out, float* workspace, int64_t M, int G, int N, int64_t ld, int accumulate, float alpha, int dtype, hipStream_t stream);
 

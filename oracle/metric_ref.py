@@ -69,7 +69,9 @@ def pad_image_to_shape(img, shape, value=0):
 
 
 def resize_linear(img, out_h, out_w):
-    """cv2.resize INTER_LINEAR of a float (H, W[, C]) array (align_corners=False rule)."""
+    """cv2.resize INTER_LINEAR of an (H, W[, C]) array (align_corners=False rule).  cv2 returns
+    the input's dtype: a uint8 image comes back rounded to uint8 values (cv2's own 11-bit
+    fixed-point interpolation is not restated: opencv is absent, parity unpinned)."""
     H, W = img.shape[:2]
 
     def idx(n_out, n_in):
@@ -87,7 +89,10 @@ def resize_linear(img, out_h, out_w):
     ly, lx = ly.reshape(sh), lx.reshape(sw)
     top = img[y0][:, x0] * (1 - lx) + img[y0][:, x1] * lx
     bot = img[y1][:, x0] * (1 - lx) + img[y1][:, x1] * lx
-    return top * (1 - ly) + bot * ly
+    out = top * (1 - ly) + bot * ly
+    if img.dtype == np.uint8:
+        out = np.clip(np.rint(out), 0, 255)
+    return out
 
 
 class SlidingEvaluatorRef:

@@ -59,7 +59,7 @@ def train_steps(model, optimizer, lr_policy, batches, start_iter=0):
         lr = lr_policy.get_lr(start_iter + i)
         for g in optimizer.param_groups:
             g["lr"] = lr
-        losses.append(float(loss))
+        losses.append(float(loss.detach()))
     return losses
 
 

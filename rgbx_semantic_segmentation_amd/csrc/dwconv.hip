@@ -849,8 +849,17 @@ int cmx_dwconv3x3_bwd_saved_tiles(int imgs_per_group, int H, int W) {
 
 size_t cmx_dwconv3x3_bwd_workspace(int NI, int imgs_per_group, int H, int W, int C) {
   const int G = NI / imgs_per_group;
-  const int P = tile_cb(C, 0) ? imgs_per_group * cdiv(H, TY2) * cdiv(W, TX2)
-                           : bwd_slots(C / 4, cdiv(W, RXB) * cdiv(H, RY) * imgs_per_group);
+  // one workspace serves both LDS-tiled backwards: the recompute path's TY2 x TX2 tiles and
+  // the saved-act path's TYB x TXB tiles (cmx_dwconv3x3_bwd_saved_tiles); partial slabs are
+  // sized for whichever has more tiles, and the reduce's tmp sits after them
+  int P;
+  if (tile_cb(C, 0)) {
+    const int p8 = imgs_per_group * cdiv(H, TY2) * cdiv(W, TX2);
+    const int p16 = cmx_dwconv3x3_bwd_saved_tiles(imgs_per_group, H, W);
+    P = p8 > p16 ? p8 : p16;
+  } else {
+    P = bwd_slots(C / 4, cdiv(W, RXB) * cdiv(H, RY) * imgs_per_group);
+  }
   return ((size_t)G * P * C * 10 + (size_t)G * C * 10) * sizeof(float);
 }
 

@@ -117,6 +117,32 @@ __global__ void colsum_scalar_kernel(const T* __restrict__ x, float* __restrict_
   }
 }
 
+// bf16 gradient payload of the data-parallel exchange (dist.BucketedGradSync, payload "bf16"):
+// after an all-to-all, rank r holds P bf16 chunks of its shard, one per rank; they are summed
+// in fp32 and the shard is re-emitted in bf16 for the all-gather (fp32 accumulation, half the
+// bytes of an fp32 all-reduce on the wire).  8 elements per thread, 16-B accesses.
+__global__ void shard_sum_bf16_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, int P, long n8) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < P; ++p) {
+      float v[8];
+      load_vec<bf16>(in + ((long)p * n8 + i) * 8, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+    }
+    store_vec<bf16>(out + i * 8, acc);
+  }
+}
+
+__global__ void cast_bf16_f32_kernel(const bf16* __restrict__ src, float* __restrict__ dst, long n8) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float v[8];
+    load_vec<bf16>(src + i * 8, v);
+    reinterpret_cast<float4*>(dst + i * 8)[0] = make_float4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<float4*>(dst + i * 8)[1] = make_float4(v[4], v[5], v[6], v[7]);
+  }
+}
+
 static unsigned ew_grid(long nvec) {
   long b = (nvec + 255) / 256;
   return (unsigned)(b < 8192 ? (b > 0 ? b : 1) : 8192);
@@ -180,6 +206,24 @@ int cmx_cast_f32_bf16(const float* src, void* dst, long n, hipStream_t s) {
   if (n == 0) return CMX_OK;
   hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(ew_grid(n)), dim3(256), 0, s, src, (bf16*)dst, n);
   return cmx_check_launch("cast_f32_bf16");
+}
+
+// out[i] = bf16(sum_p in[p * n + i]) in fp32, p < P; n % 8 == 0
+int cmx_shard_sum_bf16(const void* in, void* out, int P, long n, hipStream_t s) {
+  CMX_REQUIRE(P > 0 && n % 8 == 0 && ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0, CMX_ERR_SHAPE,
+              "shard_sum_bf16: P=%d n=%ld (n %% 8, 16-B aligned)", P, n);
+  if (n == 0) return CMX_OK;
+  hipLaunchKernelGGL(shard_sum_bf16_kernel, dim3(ew_grid(n / 8)), dim3(256), 0, s, (const bf16*)in, (bf16*)out, P,
+                     n / 8);
+  return cmx_check_launch("shard_sum_bf16");
+}
+
+int cmx_cast_bf16_f32(const void* src, float* dst, long n, hipStream_t s) {
+  CMX_REQUIRE(n % 8 == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0, CMX_ERR_SHAPE,
+              "cast_bf16_f32: n=%ld (n %% 8, 16-B aligned)", n);
+  if (n == 0) return CMX_OK;
+  hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3(ew_grid(n / 8)), dim3(256), 0, s, (const bf16*)src, dst, n / 8);
+  return cmx_check_launch("cast_bf16_f32");
 }
 
 size_t cmx_colsum_workspace(long M, int G, int N) {

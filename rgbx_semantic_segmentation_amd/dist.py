@@ -40,13 +40,23 @@ class BucketedGradSync:
     FusedAdamW.step) joins the side stream into the current one and returns the 1/P scale
     the AdamW kernel applies."""
 
-    def __init__(self, store, group=None, overlap=None):
+    def __init__(self, store, group=None, overlap=None, payload=None, chunk_mb=None):
         import os
         self.store = store
         self.group = group
         self.world = self._world()
         # CMX_DP_OVERLAP=0: one blocking all-reduce per segment at optimizer time (no overlap)
         self.overlap = (os.environ.get("CMX_DP_OVERLAP", "1") == "1") if overlap is None else overlap
+        # gradient payload on the wire: "fp32" (SUM all-reduce of the fp32 gradients, DDP's
+        # semantics) or "bf16" (all-to-all of bf16 shards, fp32 accumulation, all-gather of the
+        # bf16 sums: half the bytes over xGMI; the summed gradient is rounded to bf16 once)
+        self.payload = (payload or os.environ.get("CMX_DP_PAYLOAD", "fp32")).lower()
+        if self.payload not in ("fp32", "bf16"):
+            raise ValueError(f"gradient payload {self.payload!r}: fp32 or bf16")
+        # collectives of at most ~chunk_mb of payload each (DDP's 25 MB bucket cap): a long
+        # segment is exchanged as a sequence of bounded messages
+        mb = float(chunk_mb if chunk_mb is not None else os.environ.get("CMX_DP_CHUNK_MB", "25"))
+        self.chunk = max(1024, int(mb * 2 ** 20) // (2 if self.payload == "bf16" else 4))
         self.ranges = {sid: (a, b) for sid, a, b in store.segments}
         self.works = []
         self.launched = set()
@@ -79,7 +89,46 @@ class BucketedGradSync:
         return dist.get_world_size(self.group)
 
     def _reduce(self, seg: torch.Tensor) -> None:
-        dist.all_reduce(seg, op=dist.ReduceOp.SUM, group=self.group)
+        for a in range(0, seg.numel(), self.chunk):
+            part = seg[a:a + self.chunk]
+            if self.payload == "fp32" or self.world == 1:
+                dist.all_reduce(part, op=dist.ReduceOp.SUM, group=self.group)
+            else:
+                self._reduce_bf16(part)
+
+    def _reduce_bf16(self, t: torch.Tensor) -> None:
+        """SUM over ranks of fp32 ``t`` in place with a bf16 payload and fp32 accumulation:
+        all-to-all of bf16 shards, each rank sums its P received chunks in fp32, all-gather of
+        the bf16 shard sums (2 + 2 bytes per element on the wire vs 8 for a ring fp32
+        all-reduce).  On the GPU the casts and the shard sum are HIP kernels
+        (cmx_cast_f32_bf16 / cmx_shard_sum_bf16 / cmx_cast_bf16_f32); the CPU branch is the
+        gloo rehearsal of the same protocol."""
+        P = self.world
+        n = t.numel()
+        shard = -(-n // (8 * P)) * 8                 # per-rank shard, a multiple of 8 elements
+        send = torch.zeros(P * shard, dtype=torch.bfloat16, device=t.device)
+        recv = torch.empty_like(send)
+        mine = torch.empty(shard, dtype=torch.bfloat16, device=t.device)
+        out = torch.empty_like(send)
+        if t.is_cuda:
+            from . import _lib
+            if n % 8 == 0:
+                _lib.call("cmx_cast_f32_bf16", _lib.ptr(t), _lib.ptr(send), n, _lib.stream())
+            else:
+                send[:n].copy_(t)
+            dist.all_to_all_single(recv, send, group=self.group)
+            _lib.call("cmx_shard_sum_bf16", _lib.ptr(recv), _lib.ptr(mine), P, shard, _lib.stream())
+            dist.all_gather_into_tensor(out, mine, group=self.group)
+            if n % 8 == 0:
+                _lib.call("cmx_cast_bf16_f32", _lib.ptr(out), _lib.ptr(t), n, _lib.stream())
+            else:
+                t.copy_(out[:n])
+        else:
+            send[:n].copy_(t)
+            dist.all_to_all_single(recv, send, group=self.group)
+            mine.copy_(recv.view(P, shard).float().sum(0))
+            dist.all_gather_into_tensor(out, mine, group=self.group)
+            t.copy_(out[:n])
 
     def _finish_backward(self):
         self._armed = False

@@ -39,15 +39,25 @@ def _pad_margin(h, w, crop):
     return ph // 2, ph // 2 + ph % 2, pw // 2, pw // 2 + pw % 2
 
 
-def _resize_chw(x: torch.Tensor, oh: int, ow: int) -> torch.Tensor:
-    """(C, H, W) fp32 -> (C, oh, ow) fp32, bilinear align_corners=False (cv2 INTER_LINEAR)."""
+def _resize_chw(x: torch.Tensor, oh: int, ow: int, as_uint8: bool = False) -> torch.Tensor:
+    """(C, H, W) fp32 -> (C, oh, ow) fp32, bilinear align_corners=False (cv2 INTER_LINEAR).
+    ``as_uint8``: the source image was uint8, and cv2.resize returns the input's dtype, so
+    the result is rounded and clamped to uint8 values.  cv2 interpolates uint8 images in
+    11-bit fixed point; this kernel interpolates in fp32, so a value on a .5 rounding boundary
+    can land one level apart (no cv2 here to pin it: parity unpinned)."""
     C, H, W = x.shape
     if (H, W) == (oh, ow):
         return x
     src = x.permute(1, 2, 0).contiguous()                    # NHWC input of the kernel
     out = torch.empty(C, oh, ow, device=x.device, dtype=torch.float32)
     _lib.call("cmx_bilinear_fwd_nchw_f32", _lib.ptr(src), _lib.ptr(out), 1, H, W, oh, ow, C, 0, _lib.stream())
+    if as_uint8:
+        out = out.round_().clamp_(0, 255)
     return out
+
+
+def _is_uint8(a) -> bool:
+    return (a.dtype == torch.uint8) if isinstance(a, torch.Tensor) else (np.asarray(a).dtype == np.uint8)
 
 
 class Evaluator(object):
@@ -93,11 +103,12 @@ class Evaluator(object):
         dev = self._device(device)
         crop = (int(crop_size[0]), int(crop_size[1])) if not isinstance(crop_size, int) else (crop_size, crop_size)
         img_c, x_c = self._chw(img, dev), self._chw(modal_x, dev)
+        u8_img, u8_x = _is_uint8(img), _is_uint8(modal_x)
         _, ori_rows, ori_cols = img_c.shape
         processed = torch.zeros(self.class_num, ori_rows, ori_cols, device=dev, dtype=torch.float32)
         for s in self.multi_scales:
             nh, nw = int(round(ori_rows * s)), int(round(ori_cols * s))
-            processed += self.scale_process_rgbX(_resize_chw(img_c, nh, nw), _resize_chw(x_c, nh, nw),
+            processed += self.scale_process_rgbX(_resize_chw(img_c, nh, nw, u8_img), _resize_chw(x_c, nh, nw, u8_x),
                                                  (ori_rows, ori_cols), crop, stride_rate, dev)
         return processed
 

@@ -7,9 +7,10 @@ Conventions
    pair, compute dtype); their gradients are written directly into the fp32 gradient
    buffer views passed alongside (``Wg``/``bg``).  Functions return ``None`` for those
    and take an ``anchor`` Parameter only so autograd records the node.
- * Plain dense GEMMs (Linear / 1x1 conv / im2col conv) are library GEMMs (hipBLASLt via
-   torch.bmm) in the compute dtype with fp32 weight gradients; everything else is a
-   hand-written gfx950 kernel (see include/cmx_hip.h).
+ * Every dense GEMM (Linear / 1x1 conv / implicit or im2col conv; fwd, dgrad, wgrad) runs
+   on cmx_gemm / cmx_conv_implicit_fwd / the deferred grouped launch (csrc/gemm.hip, MFMA
+   bf16 or fp32), with fp32 weight gradients; every other op is a hand-written gfx950
+   kernel too (see include/cmx_hip.h).  No library GEMM is on the path.
 """
 from __future__ import annotations
 
@@ -20,90 +21,28 @@ from torch.autograd import Function
 
 from . import deferred
 from . import kernels as K
-from .streams import run_side
 
 
 def _c(t):
     return t if t.is_contiguous() else t.contiguous()
 
 
-def _split_k(M: int) -> int:
-    """Chunks for the weight-gradient reduction over M tokens: hipBLASLt handles the skinny
-    (N x M) @ (M x K) product poorly at M ~ 1e4-1e5 (75 us for 2.5 GFLOP at stage 1), so
-    large M is cut into S chunks of >= 1200 rows, one batched GEMM over the chunks, and
-    the fp32 partial slabs are summed by cmx_partials_sum (20 us)."""
-    if M < 4800:
-        return 1
-    s = min(32, M // 1200)
-    while s > 1 and M % s:
-        s -= 1
-    return s
-
-
-def _wgrad(dy, x, out):
-    """out (fp32 view, (G, N, k)) = dy^T @ x with fp32 accumulation/output."""
-    G, M, N = dy.shape
-    S = _split_k(M) if (dy.is_contiguous() and x.is_contiguous() and out.is_contiguous()) else 1
-    if S > 1:
-        k = x.shape[-1]
-        Mc = M // S
-        part = torch.bmm(dy.view(G * S, Mc, N).transpose(1, 2), x.view(G * S, Mc, k),
-                         **({} if dy.dtype == torch.float32 else {"out_dtype": torch.float32}))
-        K.call("cmx_partials_sum", K.ptr(part), K.ptr(out), G, S, N * k, 0, 1.0, K.stream())
-        return
-    dyt = dy.transpose(1, 2)
-    if dy.dtype == torch.float32:
-        if out.is_contiguous():
-            torch.bmm(dyt, x, out=out)
-        else:
-            out.copy_(torch.bmm(dyt, x))
-    else:
-        out.copy_(torch.bmm(dyt, x, out_dtype=torch.float32))
-
-
-# ---------------------------------------------------------------------------- Linear
-# Dense layers run on cmx_gemm (csrc/gemm.hip).  CMX_GEMM=0 routes them through hipBLASLt
-# (torch.bmm) instead -- an A/B switch for measurements only.
-USE_CMX_GEMM = os.environ.get("CMX_GEMM", "1") != "0"
-
-
 def _dgrad(dz, W_slice, out):
     """out (G, M, k) = dz (G, M, N) @ W_slice (G, N, k)."""
-    if USE_CMX_GEMM:
-        K.gemm(dz, W_slice.transpose(1, 2), out)
-    else:
-        torch.bmm(dz, W_slice, out=out)
+    K.gemm(dz, W_slice.transpose(1, 2), out)
     return out
 
 
 def _wgrad_into(dz, x, Wg_slice, bg=None):
     """Wg_slice (fp32 view (G, N, k)) = dz^T x;  bg (G, N) = column sums of dz.  bf16: queued
     for the segment's grouped weight-gradient launch (deferred.py); otherwise run now."""
-    if USE_CMX_GEMM and deferred.wgrad(dz, x, Wg_slice, bg):
+    if deferred.wgrad(dz, x, Wg_slice, bg):
         return
-    if USE_CMX_GEMM:
-        K.gemm(dz.transpose(1, 2), x.transpose(1, 2), Wg_slice, out_mode=1, dbias=bg, splitk=0)
-        return
-    _wgrad(dz, x, Wg_slice)
-    if bg is not None:
-        K.colsum(dz, bg, G=dz.shape[0])
+    K.gemm(dz.transpose(1, 2), x.transpose(1, 2), Wg_slice, out_mode=1, dbias=bg, splitk=0)
 
 
 def _fwd_gemm(x, W, b, y, act="none", res=None, rscale=None, rps=1, x2=None):
-    if USE_CMX_GEMM:
-        K.gemm(x, W, y, bias=b, residual=res, rscale=rscale, rows_per_sample=rps, act=act, A2=x2)
-        return y
-    k1 = x.shape[-1]
-    if b is not None:
-        torch.baddbmm(b[:, None, :].to(y.dtype), x, W[:, :, :k1].transpose(1, 2), out=y)
-    else:
-        torch.bmm(x, W[:, :, :k1].transpose(1, 2), out=y)
-    if x2 is not None:
-        y.baddbmm_(x2, W[:, :, k1:].transpose(1, 2))
-    if act != "none":
-        y.copy_(K.act_fwd(y, act))
-    if res is not None:
-        y.copy_(K.residual_add(res, y, rscale, n_per_sample=rps * y.shape[-1]))
+    K.gemm(x, W, y, bias=b, residual=res, rscale=rscale, rows_per_sample=rps, act=act, A2=x2)
     return y
 
 
@@ -147,11 +86,9 @@ class GLinear(Function):
             dx1 = _dgrad(dz, W[:, :, :k1], torch.empty_like(x1))
         if x2 is not None and ctx.needs_input_grad[10]:
             dx2 = _dgrad(dz, W[:, :, k1:], torch.empty_like(x2))
-        def wgrads():
-            _wgrad_into(dz, x1, Wg[:, :, :k1], bg)
-            if x2 is not None:
-                _wgrad_into(dz, x2, Wg[:, :, k1:])
-        run_side(wgrads, dz, x1, x2)
+        _wgrad_into(dz, x1, Wg[:, :, :k1], bg)
+        if x2 is not None:
+            _wgrad_into(dz, x2, Wg[:, :, k1:])
         return (None, None, None, None, None, None, dres, None, None, dx1, dx2, None)
 
 
@@ -478,7 +415,7 @@ class ConvF(Function):
                        K.dtype_code(cols), K.stream())
                 _wgrad_into(dy, cols, Wg, bg)
         else:
-            run_side(lambda: _wgrad_into(dy, cols, Wg, bg), dy, cols)
+            _wgrad_into(dy, cols, Wg, bg)
         dx = None
         if ctx.needs_input_grad[0] and not nchw:
             dcols = _dgrad(dy, W, torch.empty(G, NI // G * Ho * Wo, W.shape[-1], dtype=dy.dtype, device=dy.device))
@@ -570,11 +507,7 @@ class FRMF(Function):
         K.call("cmx_small_linear_fwd", K.ptr(y1), K.ptr(W2), K.ptr(b2), K.ptr(cw), B, 4 * C, 2 * C, 3, K.stream())
         # h = cat(x1, x2) W0^T + b0 (SpatialWeights' first 1x1 conv, net_utils.py:72-73), cat-free
         h = torch.empty(1, B * N, C, dtype=x.dtype, device=x.device)
-        if USE_CMX_GEMM:
-            K.gemm(x[0].view(1, B * N, C), W0[None], h, bias=b0[None], A2=x[1].view(1, B * N, C))
-        else:
-            torch.addmm(b0.to(x.dtype), x[0].reshape(B * N, C), W0[:, :C].t(), out=h[0])
-            h[0].addmm_(x[1].reshape(B * N, C), W0[:, C:].t())
+        K.gemm(x[0].view(1, B * N, C), W0[None], h, bias=b0[None], A2=x[1].view(1, B * N, C))
         h = h[0]
         sw = torch.empty(B * N, 2, dtype=torch.float32, device=x.device)
         K.call("cmx_frm_spatial_fwd", K.ptr(h), K.ptr(w2s), K.ptr(b2s), K.ptr(sw), B * N, C, dt, K.stream())
@@ -605,14 +538,9 @@ class FRMF(Function):
                K.ptr(gb2s), K.ptr(ws2), B * N, C, 0, dt, K.stream())
         for i in range(2):          # dx_i += dh @ W0[:, iC:(i+1)C] (residual epilogue, in place)
             dxi = dx[i].view(1, B * N, C)
-            if USE_CMX_GEMM:
-                K.gemm(dh[None], W0[None, :, i * C:(i + 1) * C].transpose(1, 2), dxi, residual=dxi)
-            else:
-                dxi[0].addmm_(dh, W0[:, i * C:(i + 1) * C])
-        def wgrads():
-            _wgrad_into(dh[None], x[0].view(1, B * N, C), gW0[None, :, :C], gb0.view(1, C))
-            _wgrad_into(dh[None], x[1].view(1, B * N, C), gW0[None, :, C:])
-        run_side(wgrads, dh, x)
+            K.gemm(dh[None], W0[None, :, i * C:(i + 1) * C].transpose(1, 2), dxi, residual=dxi)
+        _wgrad_into(dh[None], x[0].view(1, B * N, C), gW0[None, :, :C], gb0.view(1, C))
+        _wgrad_into(dh[None], x[1].view(1, B * N, C), gW0[None, :, C:])
         # channel MLP backward (sigmoid then relu), then pooling backward
         dz = K._ws(K.query("cmx_small_linear_bwd_workspace", B, 4 * C, 4 * C), x.device)
         dy1 = torch.empty(B, 4 * C, dtype=torch.float32, device=x.device)

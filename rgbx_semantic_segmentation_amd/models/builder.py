@@ -74,6 +74,11 @@ class EncoderDecoder(nn.Module):
         decoder = _get(cfg, "decoder", "MLPDecoder")
         if decoder != "MLPDecoder":
             raise NotImplementedError(f"decoder {decoder!r}: only MLPDecoder is on the CMX hot path")
+        # config.py:57-58 selects the rectify / fusion blocks (dual_segformer.py:316-329)
+        for key, supported in (("feature_rectify_module", "FRM"), ("feature_fusion_module", "FFM")):
+            sel = _get(cfg, key, supported)
+            if sel != supported:
+                raise NotImplementedError(f"{key} {sel!r}: only {supported!r} is on the CMX hot path")
         if criterion is None:
             criterion = nn.CrossEntropyLoss(reduction="mean", ignore_index=int(_get(cfg, "background", 255)))
         if not isinstance(criterion, nn.CrossEntropyLoss) or criterion.reduction != "mean" or \

@@ -6,12 +6,14 @@ im2col-conv weight gradient of the backward pass in one launch.  ``measure_domin
 one eager training step, keeps the record table and operands of that launch, and re-launches
 it standalone on the same stream (inputs resident in HBM), bracketed by torch.cuda.Event.
 
-achieved = algorithmic FLOPs of one launch (SURVEY.md §8(d) counting: 2 * M * N * K per weight
-gradient; the bias-gradient column is not counted) / average launch duration.  The
-algorithmic bytes (each operand read once in bf16, each fp32 gradient written once) are
-reported beside it, and ``traffic`` is the PMC-measured HBM bytes per launch from the
-committed profile (profiles/*pmc*.json, FETCH_SIZE x 2 + WRITE_SIZE per the gfx950
-correction in MI355X_MICROARCH.md), or None when no such profile is present."""
+Algorithmic work of one launch (SURVEY.md §8(d) counting): FLOP = sum of 2 * M * N * K per
+weight gradient (the bias-gradient column is not counted); bytes = each bf16 operand read once
+plus each fp32 gradient written once.  Their ratio against the bf16 ridge point (314.6 FLOP/B)
+picks the roof: the grouped launch sits below it (~120 FLOP/B), so ``bound`` is "hbm" and
+``achieved`` = algorithmic bytes / average launch duration in GB/s; the MFMA figure is
+reported beside it.  ``traffic`` is the PMC-measured HBM bytes per launch from a committed
+profile of the SAME workload and grid (profiles/*pmc*.json, FETCH_SIZE x 2 + WRITE_SIZE per
+the gfx950 correction in MI355X_MICROARCH.md), or None when no such profile exists."""
 from __future__ import annotations
 
 import glob
@@ -27,20 +29,31 @@ PEAK_HBM_GBS = 8000.0
 _ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _pmc_traffic(kernel: str):
-    for path in sorted(glob.glob(os.path.join(_ROOT, "profiles", "*pmc*.json"))):
+RIDGE_FLOP_PER_BYTE = PEAK_BF16_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)      # 314.6
+
+
+def _pmc_traffic(kernel: str, workload: str, blocks: int):
+    """PMC HBM bytes per launch of ``kernel`` measured on THIS workload: a profile counts only
+    when its ``workload`` tag and the launch's workgroup count match (a B5 line must never
+    reuse B2 bytes).  Newest profile first."""
+    for path in sorted(glob.glob(os.path.join(_ROOT, "profiles", "*pmc*.json")), reverse=True):
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
             continue
+        if d.get("workload") != workload:
+            continue
         k = d.get("kernels", {}).get(kernel)
-        if k and k.get("hbm_bytes_per_launch"):
+        if k and k.get("hbm_bytes_per_launch") and k.get("blocks") in (None, blocks):
             return k["hbm_bytes_per_launch"], os.path.relpath(path, _ROOT)
     return None, None
 
 
-def measure_dominant(model, batch, iters: int = 20):
-    """Time the grouped weight-gradient GEMM of one eager step of ``model`` on ``batch``."""
+def measure_dominant(model, batch, workload: str, iters: int = 20):
+    """Time the grouped weight-gradient GEMM of one eager step of ``model`` on ``batch``.
+    ``bound`` follows the launch's arithmetic intensity against the bf16 ridge point
+    (algorithmic FLOP / algorithmic bytes vs 314.6 FLOP/B): below it the HBM roof binds and
+    ``achieved`` / ``peak`` are GB/s, else TFLOP/s; both fractions are reported."""
     rgb, x, lab = batch
     seen = []
 
@@ -73,13 +86,23 @@ def measure_dominant(model, batch, iters: int = 20):
     e.record()
     torch.cuda.synchronize()
     t = s.elapsed_time(e) / iters * 1e-3
-    traffic, src = _pmc_traffic("gemm_grouped_kernel")
+    traffic, src = _pmc_traffic("gemm_grouped_kernel", workload, blk)
+    tflops, gbs = flops / t / 1e12, nbytes / t / 1e9
+    ai = flops / nbytes
+    hbm = ai < RIDGE_FLOP_PER_BYTE
     out = {"kernel": f"gemm_grouped_kernel (all {nrec} weight-gradient GEMM problems of the backward, one launch, "
                      f"{blk} workgroups)",
-           "bound": "mfma", "achieved": round(flops / t / 1e12, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-           "frac": round(flops / t / 1e12 / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
-           "avg_launch_us": round(t * 1e6, 2), "algorithmic_per_launch": flops,
-           "algorithmic_bytes_per_launch": nbytes, "achieved_hbm_gbs": round(nbytes / t / 1e9, 1)}
+           "bound": "hbm" if hbm else "mfma",
+           "achieved": round(gbs, 1) if hbm else round(tflops, 2),
+           "peak": PEAK_HBM_GBS if hbm else PEAK_BF16_TFLOPS,
+           "unit": "GB/s" if hbm else "TFLOP/s",
+           "frac": round(gbs / PEAK_HBM_GBS if hbm else tflops / PEAK_BF16_TFLOPS, 4),
+           "traffic": traffic,
+           "arithmetic_intensity_flop_per_byte": round(ai, 1), "ridge_flop_per_byte": round(RIDGE_FLOP_PER_BYTE, 1),
+           "achieved_tflops": round(tflops, 2), "mfma_frac": round(tflops / PEAK_BF16_TFLOPS, 4),
+           "achieved_hbm_gbs": round(gbs, 1), "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
+           "avg_launch_us": round(t * 1e6, 2), "algorithmic_flop_per_launch": flops,
+           "algorithmic_bytes_per_launch": nbytes, "workload": workload}
     if src:
         out["traffic_source"] = src
     del seen, keep, work

@@ -2,8 +2,10 @@
 correction of MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB) reports half the bytes of wide
 coalesced streaming reads (double it); WRITE_SIZE (KB) is exact for 16-B stores.
 
-Usage: python scripts/pmc_summary.py out.json fetch_run.db write_run.db [kernel-substring ...]
-Writes {"kernels": {name: {"launches", "FETCH_SIZE_kb", "WRITE_SIZE_kb", "hbm_bytes_per_launch"}}}."""
+Usage: python scripts/pmc_summary.py out.json fetch_run.db write_run.db WORKLOAD [kernel-substring ...]
+Writes {"workload": WORKLOAD, "kernels": {name: {"launches", "FETCH_SIZE_kb", "WRITE_SIZE_kb",
+"hbm_bytes_per_launch"}}}; roofline.py only reuses the bytes for the same workload tag
+(bench.py's config.workload, e.g. "CMX-B2 train step 480x640 bs=2 K=40")."""
 import json
 import sqlite3
 import sys
@@ -21,8 +23,8 @@ def per_kernel(db, counter):
 
 
 def main():
-    out_path, fdb, wdb = sys.argv[1:4]
-    wanted = sys.argv[4:]
+    out_path, fdb, wdb, workload = sys.argv[1:5]
+    wanted = sys.argv[5:]
     f, cols = per_kernel(fdb, "FETCH_SIZE")
     w, _ = per_kernel(wdb, "WRITE_SIZE")
     agg = {}
@@ -42,7 +44,7 @@ def main():
         res[k] = {"launches": a["launches_fetch"], "FETCH_SIZE_kb_per_launch": fetch / 1024.0,
                   "WRITE_SIZE_kb_per_launch": write / 1024.0,
                   "hbm_bytes_per_launch": 2.0 * fetch + write}
-    json.dump({"correction": "hbm_bytes = 2 * FETCH_SIZE + WRITE_SIZE (gfx950, MI355X_MICROARCH.md HBM)",
+    json.dump({"workload": workload, "correction": "hbm_bytes = 2 * FETCH_SIZE + WRITE_SIZE (gfx950, MI355X_MICROARCH.md HBM)",
                "kernels": res}, open(out_path, "w"), indent=1)
     print(json.dumps(res, indent=1))
 

@@ -1,0 +1,162 @@
+"""Model-level parity of the BENCHMARKED bf16 training step at the BASELINE.json configs.
+
+The HIP EncoderDecoder in bf16 (the compute dtype of bench.py) runs one train-mode step with
+injected DropPath / Dropout2d masks at the configs' full shapes; the CPU oracle
+(oracle/cmx_ref.py) runs the same weights, inputs and masks in fp64.  Compared: train-mode
+logits (encode_decode), the loss, EVERY parameter gradient and the BN running statistics.
+
+This is the only end-to-end check of the bf16-only kernels inside a whole step: the
+deferred grouped weight-gradient GEMM, the implicit-GEMM patch-embed / SR convolutions, the
+LDS-resident SRA attention kernels (Nk = 300 at 480 x 640, the key-chunked ones at
+Nk = 1024 for B5) and the DWConv saved-activation backward.
+
+Tolerance (derived, not picked): the same oracle run in fp32 with bf16 STORAGE emulated
+(oracle/bf16_emul.py: bf16 GEMM weights, every Linear / Conv / norm input and output and the
+gradients crossing them rounded to bf16) gives, per compared tensor, the error e_emu that bf16
+storage alone causes against fp64.  The GPU error e_gpu must satisfy e_gpu <= RATIO * e_emu
+(RATIO = 4: the emulation rounds at fewer points than the fused kernels, e.g. not the GELU
+output or the attention probabilities), with a bounded number of outliers up to
+OUTLIER_RATIO * e_emu (ReLU / max-pool decisions flipped by rounding move the few gradients
+that sum over such a decision).  e = max|x - x64| / max|x64|.
+
+Reference: models/builder.py:212-253, models/encoders/dual_segformer.py:366-442,
+models/net_utils.py, models/decoders/MLPDecoder.py (train.py:185-200 step)."""
+import copy
+import time
+
+import pytest
+import torch
+
+from oracle.cmx_ref import EncoderDecoder as RefModel, CMXConfig, DropPath
+from oracle.bf16_emul import emulate_bf16
+
+pytestmark = pytest.mark.gpu
+
+RATIO = 4.0
+OUTLIER_RATIO = 12.0
+
+CONFIGS = {
+    # name: (backbone, H, W, batch, classes)      BASELINE.json configs[1..4]
+    "config2_b2_480x640_bs2": ("mit_b2", 480, 640, 2, 40),
+    "config4_b4_480x640_bs4": ("mit_b4", 480, 640, 4, 9),
+    "config5_b5_1024x1024_bs1": ("mit_b5", 1024, 1024, 1, 19),
+}
+
+
+def err(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+def _masks(model_gpu, refs, B, n_calls, seed=11):
+    """The same DropPath (per block, per branch, per sample) and Dropout2d (per sample,
+    channel) keep masks for the GPU model and every oracle model, for ``n_calls`` forwards."""
+    g = torch.Generator().manual_seed(seed)
+    bb = model_gpu.backbone
+    flags = torch.ones(sum(bb.depths), 2, 2 * B)
+    bi = 0
+    per_ref = []
+    for s in range(4):
+        for i in range(bb.depths[s]):
+            for stream, pre in enumerate(("", "extra_")):
+                rblk = getattr(refs[0].backbone, f"{pre}block{s + 1}")[i]
+                if isinstance(rblk.drop_path, DropPath):
+                    mk = [(torch.rand(B, generator=g) > 0.3).double() for _ in range(2)]
+                    per_ref.append((f"{pre}block{s + 1}", i, mk))
+                    for br in range(2):
+                        flags[bi, br, stream * B:(stream + 1) * B] = mk[br].float()
+            bi += 1
+    d2 = (torch.rand(B, model_gpu.decode_head.embed_dim, generator=g) > 0.1).double()
+    for ref in refs:
+        for name, i, mk in per_ref:
+            getattr(ref.backbone, name)[i].drop_path.masks = [m.clone() for _ in range(n_calls) for m in mk]
+        ref.decode_head.dropout.mask = d2
+    model_gpu.forced_masks = {"droppath": flags, "dropout2d": d2.float()}
+
+
+def _inputs(B, H, W, K, seed=3):
+    from rgbx_semantic_segmentation_amd.data import make_batch
+    return make_batch(B, H, W, K, seed=seed)
+
+
+def _check(name, e_gpu, e_emu, bad, ratio=RATIO):
+    ok = e_gpu <= ratio * e_emu
+    if not ok:
+        bad.append((round(e_gpu / max(e_emu, 1e-30), 2), e_gpu, e_emu, name))
+    return ok
+
+
+@pytest.mark.timeout(1800)
+@pytest.mark.parametrize("case", list(CONFIGS))
+def test_bf16_train_step_vs_fp64_oracle(dev, case):
+    from rgbx_semantic_segmentation_amd.models.builder import EncoderDecoder
+    backbone, H, W, B, K = CONFIGS[case]
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    torch.manual_seed(0)
+    ref = RefModel(CMXConfig(backbone=backbone, num_classes=K))
+    g = torch.Generator().manual_seed(1)
+    for n, b in ref.named_buffers():             # non-trivial BN running statistics
+        if n.endswith("running_mean"):
+            b.copy_(torch.rand(b.shape, generator=g) * 0.2 - 0.1)
+        elif n.endswith("running_var"):
+            b.copy_(torch.rand(b.shape, generator=g) + 0.5)
+    model = EncoderDecoder(dict(backbone=backbone, num_classes=K, compute_dtype="bfloat16",
+                                decoder_embed_dim=512)).to(dev)
+    model.load_state_dict(ref.state_dict(), strict=True)
+    emu = emulate_bf16(copy.deepcopy(ref))
+    ref64 = ref.double()
+    for m in (ref64, emu, model):
+        m.train()
+    _masks(model, [ref64, emu], B, n_calls=2)
+    rgb, x, lab = _inputs(B, H, W, K)
+
+    t0 = time.time()
+    with torch.no_grad():
+        lo64 = ref64.encode_decode(rgb.double(), x.double())
+        lo_emu = emu.encode_decode(rgb, x)
+        lo = model.encode_decode(rgb.to(dev), x.to(dev))
+    loss64 = ref64(rgb.double(), x.double(), lab)
+    loss64.backward()
+    loss_emu = emu(rgb, x, lab)
+    loss_emu.backward()
+    t_cpu = time.time() - t0
+    loss = model(rgb.to(dev), x.to(dev), lab.to(dev))
+    loss.backward()
+    torch.cuda.synchronize()
+
+    bad, rows = [], []
+    e_l, e_le = err(lo, lo64), err(lo_emu, lo64)
+    rows.append(("logits", e_l, e_le))
+    _check("logits", e_l, e_le, bad)
+    el = abs(loss.item() - loss64.item()) / abs(loss64.item())
+    ele = abs(loss_emu.item() - loss64.item()) / abs(loss64.item())
+    rows.append(("loss", el, ele))
+    _check("loss", el, max(ele, 1e-6), bad)
+
+    p64 = dict(ref64.named_parameters())
+    pem = dict(emu.named_parameters())
+    gmax = max(p.grad.abs().max().item() for p in ref64.parameters())
+    grad_bad = []
+    for n, p in model.named_parameters():
+        g64 = p64[n].grad
+        assert g64 is not None and p.grad is not None, n
+        den = max(g64.abs().max().item(), 1e-6 * gmax)
+        eg = (p.grad.detach().double().cpu() - g64).abs().max().item() / den
+        ee = (pem[n].grad.double() - g64).abs().max().item() / den
+        rows.append((n, eg, ee))
+        _check(n, eg, ee, grad_bad)
+    for n, b in model.named_buffers():
+        if "running" in n:
+            b64 = dict(ref64.named_buffers())[n]
+            eb, ebe = err(b, b64), err(dict(emu.named_buffers())[n], b64)
+            rows.append((n, eb, ebe))
+            _check(n, eb, max(ebe, 1e-7), bad)
+    ratios = sorted((e / max(ee, 1e-30), n) for n, e, ee in rows)
+    print(f"\n{case}: cpu oracle {t_cpu:.1f} s; loss gpu {loss.item():.6f} fp64 {loss64.item():.6f}; "
+          f"logits e_gpu {e_l:.3e} e_emu {e_le:.3e}; {len(rows)} tensors, gpu/emu error ratio "
+          f"median {ratios[len(ratios) // 2][0]:.2f}, max {ratios[-1][0]:.2f} ({ratios[-1][1]})")
+    print("worst ratios:", [(round(r, 2), n) for r, n in ratios[-8:]])
+    n_allowed = max(2, len(rows) // 100)
+    assert not bad, bad
+    assert len(grad_bad) <= n_allowed and all(b[0] <= OUTLIER_RATIO for b in grad_bad), grad_bad[:10]

@@ -77,3 +77,70 @@ def test_dp_semantics_gloo_world2():
     for p in procs:
         p.join(timeout=60)
     assert all(r[1] and r[2] and r[3] for r in res), res
+
+
+def _worker_store(rank, world, port, payload, q):
+    """BucketedGradSync over the real ParamStore layout of CMX-B0 (4 backward segments),
+    gradients from the oracle on each rank's slice of one global batch whose slices have
+    DIFFERENT numbers of valid (non-ignored) pixels."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle.cmx_ref import EncoderDecoder as RefModel, CMXConfig
+        from rgbx_semantic_segmentation_amd.models.builder import EncoderDecoder, backward_segment
+        from rgbx_semantic_segmentation_amd.params import ParamStore
+        from rgbx_semantic_segmentation_amd.dist import BucketedGradSync
+        torch.manual_seed(0)
+        ref = RefModel(CMXConfig(backbone="mit_b0", num_classes=5))
+        ref.eval()
+        prod = EncoderDecoder(dict(backbone="mit_b0", num_classes=5, decoder_embed_dim=512))
+        store = ParamStore(prod, "cpu", torch.float32, segment_of=backward_segment)
+        assert len(store.segments) == 4
+        g = torch.Generator().manual_seed(1)
+        H, W = 32, 48
+        rgb = torch.randn(world, 3, H, W, generator=g)
+        x = torch.randn(world, 3, H, W, generator=g)
+        lab = torch.randint(0, 5, (world, H, W), generator=g)
+        for r in range(world):                     # rank r: 40 * (r + 1) rows ignored
+            lab[r, :10 * (r + 1)] = 255
+
+        def grads(r):
+            ref.zero_grad()
+            ref(rgb[r:r + 1], x[r:r + 1], lab[r:r + 1]).backward()
+            return {n: p.grad.clone() for n, p in ref.named_parameters()}
+
+        mine = grads(rank)
+        for n, p in prod.named_parameters():        # the store's gradient views <- this rank's grads
+            p.grad.copy_(mine[n])
+        sync = BucketedGradSync(store, None, payload=payload, chunk_mb=0.05)   # many small chunks
+        for sid in (2, 0, 3, 1):                     # segments may complete in any order
+            sync._launch(sid)
+        scale = sync(store.grad)
+        per = [grads(r) for r in range(world)]
+        ddp = {n: sum(pr[n] for pr in per) / world for n in mine}     # DDP: mean of per-rank means
+        ref.zero_grad()
+        ref(rgb, x, lab).backward()                  # the global-pixel-mean gradient differs
+        worst, worst_glob = 0.0, 0.0
+        for n, p in prod.named_parameters():
+            got = p.grad * scale
+            den = ddp[n].abs().max().clamp_min(1e-12)
+            worst = max(worst, ((got - ddp[n]).abs().max() / den).item())
+            worst_glob = max(worst_glob, ((ref.get_parameter(n).grad - ddp[n]).abs().max() / den).item())
+        tol = 1e-6 if payload == "fp32" else 8e-3           # bf16: one rounding of the summed gradient
+        q.put((rank, worst <= tol, worst_glob > 1e-3, worst, worst_glob))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("payload", ["fp32", "bf16"])
+def test_bucketed_grad_sync_paramstore_unequal_pixels_gloo_world2(payload):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29700 + (os.getpid() % 500) + (0 if payload == "fp32" else 1)
+    procs = [ctx.Process(target=_worker_store, args=(r, 2, port, payload, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[1] and r[2] for r in res), res

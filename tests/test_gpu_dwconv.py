@@ -105,3 +105,38 @@ def test_dwconv_fwd_save_bwd_saved(dev, dtype, C, H, W, act):
     assert rel(dh, hr.grad) < tol
     assert rel(dw, wr.grad) < (tol if dtype == torch.float32 else 1e-2)
     assert rel(db, br.grad) < (tol if dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("C,H,W", [(64, 30, 44), (256, 17, 16), (512, 15, 20)])
+def test_dwconvf_deferred_reduce_matches_immediate(dev, C, H, W):
+    """functions.DWConvF backward with the deferred grouped reduce (deferred.py, the step's
+    path) against the immediate reduce, on tiles ragged in H and W: the grouped reduce reads
+    P = cmx_dwconv3x3_bwd_saved_tiles partial slabs of the shared workspace."""
+    from rgbx_semantic_segmentation_amd import deferred
+    from rgbx_semantic_segmentation_amd import functions as Fn
+    torch.manual_seed(2)
+    G, B = 2, 2
+    NI = G * B
+    h = torch.randn(NI, H * W, C, device="cuda").to(torch.bfloat16)
+    w = torch.randn(G, C, 9, device="cuda") * 0.3
+    b = torch.randn(G, C, device="cuda") * 0.1
+    da = torch.randn(NI, H * W, C, device="cuda").to(torch.bfloat16)
+    anchor = torch.nn.Parameter(torch.zeros(1, device="cuda"))
+    res = {}
+    saved = deferred.ENABLED
+    try:
+        for mode in (False, True):
+            deferred.ENABLED = mode
+            wg = torch.full((G, C, 9), float("nan"), device="cuda")
+            bg = torch.full((G, C), float("nan"), device="cuda")
+            hx = h.clone().requires_grad_(True)
+            out = Fn.DWConvF.apply(hx, w, b, wg, bg, NI, B, H, W, "gelu", anchor)
+            out.backward(da)
+            deferred.flush()
+            torch.cuda.synchronize()
+            res[mode] = (hx.grad.float(), wg.clone(), bg.clone())
+    finally:
+        deferred.ENABLED = saved
+    for a, c in zip(res[False], res[True]):
+        assert torch.isfinite(c).all()
+        assert rel(c, a) < 1e-6, rel(c, a)

@@ -140,8 +140,11 @@ def main(argv=None):
             if engine.local_rank == 0:
                 dt = time.time() - t0
                 logger.info(f"epoch {epoch}: {args.niters_per_epoch * args.batch_size / dt:.2f} images/s (eager)")
-            if args.checkpoint_dir and engine.local_rank == 0 and epoch >= args.checkpoint_start_epoch and \
-                    (epoch - args.checkpoint_start_epoch) % args.checkpoint_step == 0:
+            # the reference's schedule (train.py:310): from the start epoch on every step-th
+            # epoch, and always the last epoch
+            save = (epoch >= args.checkpoint_start_epoch and epoch % args.checkpoint_step == 0) or \
+                epoch == args.nepochs
+            if args.checkpoint_dir and engine.local_rank == 0 and save:
                 engine.save_and_link_checkpoint(args.checkpoint_dir, args.checkpoint_dir,
                                                 os.path.join(args.checkpoint_dir, "log_last"))
         return sum_loss / max(1, args.niters_per_epoch)
