@@ -174,13 +174,13 @@ int cmx_reduce_pack(void* rec, const float* src, float* dst, float* dst2, int G,
 int cmx_reduce_grouped(const void* recs, int nrec, int total_blocks, hipStream_t stream);
 
 /* ---- fused AdamW over the flat parameter buffer (train.py:128-129, init_func.py:33-57). */
-int cmx_adamw_step(float* p, const float* g, float* m, float* v, void* shadow_bf16, const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, float beta1, float beta2, float eps, float weight_decay, float grad_scale, hipStream_t stream);
+int cmx_adamw_step(float* p, const float* g, float* m, float* v, void* shadow_bf16, const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1, double beta2, float eps, double weight_decay, float grad_scale, hipStream_t stream);
 /* ---- dynamic loss scaling: torch.cuda.amp.GradScaler of the reference's AMP path (train.py:13,56,185-198, config 5).
  *      The scale, growth tracker and found-inf flag live on the device, so a scaled step replays from a HIP graph:
  *      grad_nonfinite sets found_inf if any gradient is inf/nan; adamw_step_scaled unscales by 1/loss_scale[0] and
  *      skips the whole update (and the step count) when found_inf[0] != 0; loss_scale_update applies backoff /
  *      growth (after growth_interval clean steps) and clears found_inf. */
-int cmx_adamw_step_scaled(float* p, const float* g, float* m, float* v, void* shadow_bf16, const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, float beta1, float beta2, float eps, float weight_decay, float grad_scale, const float* loss_scale, const float* found_inf, hipStream_t stream);
+int cmx_adamw_step_scaled(float* p, const float* g, float* m, float* v, void* shadow_bf16, const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1, double beta2, float eps, double weight_decay, float grad_scale, const float* loss_scale, const float* found_inf, hipStream_t stream);
 int cmx_grad_nonfinite(const float* g, int64_t n, float* found_inf, hipStream_t stream);
 int cmx_loss_scale_update(float* scale, int* growth_tracker, float* found_inf, float growth_factor, float backoff_factor, int growth_interval, hipStream_t stream);
 

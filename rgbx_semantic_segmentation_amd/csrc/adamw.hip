@@ -6,6 +6,9 @@
 // single-tensor update order of torch.optim.AdamW:
 //   p *= 1 - lr*wd ; m = lerp(m, g, 1-b1) ; v = b2*v + (1-b2)*g*g
 //   p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps)
+// with torch's scalar precision: the betas arrive as doubles, and 1 - b1, 1 - b2, 1 - lr*wd and
+// the bias corrections are formed in double and rounded to fp32 once (as torch rounds its
+// Python-float scalars), so 1 - 0.999 is 0.001f and not 1.f - 0.999f (1.3e-5 apart).
 // lr and t are read from device memory so the step can be replayed from a HIP graph while
 // WarmUpPolyLR changes lr.  The per-64-element decay flag follows the flat layout (every
 // parameter starts on a 64-element boundary).  Optionally emits the bf16 weight shadow for
@@ -15,17 +18,18 @@
 
 __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                              float* __restrict__ v, bf16* __restrict__ shadow, const uint8_t* __restrict__ decay64,
-                             long n, const float* __restrict__ lr_ptr, const float* __restrict__ step_ptr, float b1,
-                             float b2, float eps, float wd, float gscale, const float* __restrict__ loss_scale,
+                             long n, const float* __restrict__ lr_ptr, const float* __restrict__ step_ptr, double b1d,
+                             double b2d, float eps, double wd, float gscale, const float* __restrict__ loss_scale,
                              const float* __restrict__ found_inf) {
   // GradScaler semantics (train.py:185-198): a step whose gradients held inf / nan is skipped
   if (found_inf && *found_inf != 0.f) return;
   if (loss_scale) gscale /= *loss_scale;                       // unscale
-  const float lr = *lr_ptr;
-  const float t = *step_ptr;
-  const float bc1 = 1.f - powf(b1, t);
-  const float bc2s = sqrtf(1.f - powf(b2, t));
-  const float step_size = lr / bc1;
+  const double lr = *lr_ptr;
+  const double t = *step_ptr;
+  const float step_size = (float)(lr / (1.0 - pow(b1d, t)));
+  const float bc2s = (float)sqrt(1.0 - pow(b2d, t));
+  const float omb1 = (float)(1.0 - b1d), b2 = (float)b2d, omb2 = (float)(1.0 - b2d);
+  const float decf = (float)(1.0 - lr * wd);
   const long nv = n / 4;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)nv; i += gridDim.x * blockDim.x) {
     const long e = i * 4;
@@ -33,15 +37,15 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
     float4 gg = *reinterpret_cast<const float4*>(g + e);
     float4 mm = *reinterpret_cast<float4*>(m + e);
     float4 vv = *reinterpret_cast<float4*>(v + e);
-    const float dec = decay64[e >> 6] ? 1.f - lr * wd : 1.f;
+    const float dec = decay64[e >> 6] ? decf : 1.f;
     float pa[4] = {pp.x, pp.y, pp.z, pp.w}, ga[4] = {gg.x, gg.y, gg.z, gg.w};
     float ma[4] = {mm.x, mm.y, mm.z, mm.w}, va[4] = {vv.x, vv.y, vv.z, vv.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float gj = ga[j] * gscale;
       pa[j] *= dec;
-      ma[j] = ma[j] + (1.f - b1) * (gj - ma[j]);
-      va[j] = va[j] * b2 + (1.f - b2) * gj * gj;
+      ma[j] = ma[j] + omb1 * (gj - ma[j]);
+      va[j] = va[j] * b2 + omb2 * gj * gj;
       const float denom = sqrtf(va[j]) / bc2s + eps;
       pa[j] = pa[j] - step_size * (ma[j] / denom);
     }
@@ -67,7 +71,7 @@ __global__ __launch_bounds__(256) void nonfinite_kernel(const float* __restrict_
   const long nv = n / 4;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (long)gridDim.x * blockDim.x) {
     const float4 x = reinterpret_cast<const float4*>(g)[i];
-    bad |= !isfinite(x.x) | !isfinite(x.y) | !isfinite(x.z) | !isfinite(x.w);
+    bad |= (int)!isfinite(x.x) | (int)!isfinite(x.y) | (int)!isfinite(x.z) | (int)!isfinite(x.w);
   }
   if (__syncthreads_or(bad) && threadIdx.x == 0) *found = 1.f;
 }
@@ -89,15 +93,15 @@ extern "C" {
 
 // n must be a multiple of 64; step_ptr is incremented by this call before use (torch order)
 int cmx_adamw_step(float* p, const float* g, float* m, float* v, void* shadow_bf16, const uint8_t* decay64, int64_t n,
-                   const float* lr_ptr, float* step_ptr, float beta1, float beta2, float eps, float weight_decay,
+                   const float* lr_ptr, float* step_ptr, double beta1, double beta2, float eps, double weight_decay,
                    float grad_scale, hipStream_t s) {
   return cmx_adamw_step_scaled(p, g, m, v, shadow_bf16, decay64, n, lr_ptr, step_ptr, beta1, beta2, eps, weight_decay,
                                grad_scale, nullptr, nullptr, s);
 }
 
 int cmx_adamw_step_scaled(float* p, const float* g, float* m, float* v, void* shadow_bf16, const uint8_t* decay64,
-                          int64_t n, const float* lr_ptr, float* step_ptr, float beta1, float beta2, float eps,
-                          float weight_decay, float grad_scale, const float* loss_scale, const float* found_inf,
+                          int64_t n, const float* lr_ptr, float* step_ptr, double beta1, double beta2, float eps,
+                          double weight_decay, float grad_scale, const float* loss_scale, const float* found_inf,
                           hipStream_t s) {
   CMX_REQUIRE(n % 64 == 0, CMX_ERR_SHAPE, "adamw: n must be a multiple of 64");
   hipLaunchKernelGGL(step_incr_kernel, dim3(1), dim3(1), 0, s, step_ptr, found_inf);

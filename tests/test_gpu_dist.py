@@ -67,6 +67,7 @@ def test_dp_world1_graph_step_equals_plain_step(dev, payload):
     flags[1, 0, 1] = 0.0
     d2 = torch.ones(2, 256)
     d2[0, :7] = 0.0
+    flags, d2 = flags.to(dev), d2.to(dev)            # device-resident: no H2D copy inside the capture
     plain.forced_masks = {"droppath": flags, "dropout2d": d2}
     p0 = plain.store.flat.clone()
     ref = _run(plain, FusedAdamW(plain), batch)

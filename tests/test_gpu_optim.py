@@ -55,8 +55,8 @@ def _gpu_moments(opt, model):
     sd = opt.state_dict()
     order = opt._order
     names = {id(p): n for n, p in model.named_parameters()}
-    return {names[id(p)]: (sd["state"][i]["exp_avg"], sd["state"][i]["exp_avg_sq"], float(sd["state"][i]["step"]))
-            for i, p in enumerate(order)}
+    return {names[id(p)]: (sd["state"][i]["exp_avg"].cpu(), sd["state"][i]["exp_avg_sq"].cpu(),
+                           float(sd["state"][i]["step"])) for i, p in enumerate(order)}
 
 
 def test_fused_adamw_matches_torch_adamw_on_shared_gradients(dev):
