@@ -129,6 +129,15 @@ int cmx_bn_bwd_apply(const void* dy, const void* x, const float* mean, const flo
 int cmx_bilinear_fwd_nhwc(const void* in, void* out, int NB, int Hi, int Wi, int Ho, int Wo, int C, int64_t out_pix_stride, int dtype, hipStream_t stream);
 int cmx_bilinear_fwd_nchw_f32(const void* in, float* out, int NB, int Hi, int Wi, int Ho, int Wo, int C, int dtype, hipStream_t stream);
 int cmx_bilinear_adjoint_1d(const void* in, void* out, int64_t P, int Lo, int Li, int Q, int64_t sp, int64_t so, const float* a1, const float* a2, float alpha0, int in_dtype, int out_dtype, hipStream_t stream);
+/* DecoderHead.linear_fuse (MLPDecoder.py:66-77) without the (B, N1, 4E) concat: the 1x1 conv commutes with the
+ * bilinear upsample (linear, weights sum to 1), so Z = e1 Wf[:, 3E:]^T + bias + up(z4) + up(z3) + up(z2) with the
+ * low-resolution products z_i = e_i Wf[:, slot_i]^T (B, h_i, w_i, E) added by the GEMM epilogue (z_i may be NULL).
+ * e1 (B*H1*W1, E); Wf_c1 points at column 3E of the (E, ldw) weight; Z (B*H1*W1, E). */
+/* dx of the SRA spatial-reduction conv Attention.sr (kernel = stride = R, pad 0; dual_segformer.py:95-96): the
+ * dgrad GEMM dy (G, NIg*Ho*Wo, N) @ W (G, N, R*R*C) with the col2im folded into its epilogue as an address remap
+ * (non-overlapping patches).  dx (G*NIg, H, W, C) NHWC; pixels outside the Ho*R x Wo*R window are not written. */
+int cmx_conv_patch_dgrad(const void* dy, const void* Wt, void* dx, int G, int NIg, int H, int W, int C, int R, int Ho, int Wo, int N, int64_t sdy, int64_t sW, int64_t sdx, int dtype, hipStream_t stream);
+int cmx_decoder_fuse_fwd(const void* e1, const void* Wf_c1, void* Z, const float* bias, const void* z4, const void* z3, const void* z2, int B, int H1, int W1, int h4, int w4, int h3, int w3, int h2, int w2, int E, int64_t ldw, int dtype, hipStream_t stream);
 
 /* ---- fused final upsample + CrossEntropyLoss(mean, ignore_index=255) (builder.py:233,249). */
 size_t cmx_upsample_ce_workspace(int B, int H, int W);

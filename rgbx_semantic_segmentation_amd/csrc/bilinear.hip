@@ -11,13 +11,7 @@
 namespace {
 
 __device__ __forceinline__ void src_index(int dst, float scale, int in, int& i0, int& i1, float& l0, float& l1) {
-  float s = (dst + 0.5f) * scale - 0.5f;
-  if (s < 0.f) s = 0.f;
-  i0 = (int)s;
-  if (i0 > in - 1) i0 = in - 1;
-  i1 = i0 + (i0 < in - 1 ? 1 : 0);
-  l1 = s - (float)i0;
-  l0 = 1.f - l1;
+  cmx_bilin_src(dst, scale, in, i0, i1, l0, l1);
 }
 
 // in (NB, Hi, Wi, C) dense; out pixel p at out + ((n*Ho + y)*Wo + x)*ops + c

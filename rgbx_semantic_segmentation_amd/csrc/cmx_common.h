@@ -223,6 +223,19 @@ __device__ __forceinline__ cmx_f2 act2_grad(cmx_f2 z) {
     }                                                                           \
   } while (0)
 
+// bilinear source index of F.interpolate(align_corners=False), PyTorch's rule:
+//   src = max(0, (dst + 0.5) * in/out - 0.5); i0 = floor(src); i1 = min(i0 + 1, in - 1)
+// (scale = (float)in / out, as PyTorch forms it); weights l0 = 1 - (src - i0), l1 = src - i0
+__device__ __forceinline__ void cmx_bilin_src(int dst, float scale, int in, int& i0, int& i1, float& l0, float& l1) {
+  float s = (dst + 0.5f) * scale - 0.5f;
+  if (s < 0.f) s = 0.f;
+  i0 = (int)s;
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l1 = s - (float)i0;
+  l0 = 1.f - l1;
+}
+
 static inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
 
 // dtype dispatch helper for launch wrappers

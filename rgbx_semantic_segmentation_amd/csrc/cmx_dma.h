@@ -12,9 +12,16 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 // hipcc cannot tell the DMA's LDS range from the buffer being read and waits vmcnt(0)
 // before every ds_read, which serialises the prefetch with the MFMAs.  The kernel orders
 // the DMA itself: `s_waitcnt vmcnt(0)` + barrier before a staged buffer is read.
+// The resource is wave-uniform at every call site; readfirstlane pins it to SGPRs even when the
+// compiler cannot prove that (e.g. a record loaded through a searched index).
 __device__ __forceinline__ void dma16(const i32x4 rsrc, uint32_t lds, int voffset) {
+  i32x4 r;
+  r.x = __builtin_amdgcn_readfirstlane(rsrc.x);
+  r.y = __builtin_amdgcn_readfirstlane(rsrc.y);
+  r.z = __builtin_amdgcn_readfirstlane(rsrc.z);
+  r.w = __builtin_amdgcn_readfirstlane(rsrc.w);
   asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
-               :: "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voffset), "s"(rsrc) : "memory");   // m0 is reserved: hipcc uses it for nothing else in these kernels
+               :: "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voffset), "s"(r) : "memory");   // m0 is reserved: hipcc uses it for nothing else in these kernels
 }
 
 constexpr int OOB = (int)0x80000000;            // voffset past num_records -> the load returns 0

@@ -53,6 +53,14 @@ struct GemmArgs {
   //   conv = 1: A(i = output pixel, k = (kh, kw, c)) gathered from x (forward, no im2col);
   //   conv = 2: B(j = c, k = output pixel) = x at tap `ctap` of pixel k (weight gradient of one tap)
   int conv, cH, cW, cC, cKW, cst, cpad, cHo, cWo, ctap;
+  // upsample-add epilogue (cmx_decoder_fuse_fwd): v += sum_s bilinear_s(up[s]) at output row i =
+  // pixel (n, y, x) of an uoH x uoW grid; up[s] is (NB, uh[s], uw[s], N) in C's dtype
+  const void* up[3];
+  int uh[3], uw[3], nup, uoH, uoW;
+  // scatter epilogue (cmx_conv_patch_dgrad): row i = patch (n, oy, ox) of an scHo x scWo grid,
+  // column j = (kh, kw, c) of an scR x scR patch of scC channels -> C pixel (n, oy*scR + kh,
+  // ox*scR + kw) of an scH x scW NHWC image (col2im of a non-overlapping patchify conv)
+  int scatter, scH, scW, scC, scR, scHo, scWo;
 };
 
 // block id -> tile id, giving each of the 8 XCDs (hardware deals block b to XCD b % 8) a
@@ -63,11 +71,94 @@ __device__ __forceinline__ int xcd_tile(int b, int nt) {
 }
 
 // ---------------------------------------------------------------------------- epilogue
+// bilinear taps of output row i in low-res map s: 4 element offsets (units of rows) + weights
+struct UpTaps {
+  long r00, r01, r10, r11;
+  float w00, w01, w10, w11;
+};
+__device__ __forceinline__ UpTaps up_taps(const GemmArgs& p, int s, int i) {
+  const int hw = p.uoH * p.uoW;
+  const int n = i / hw, r = i - n * hw, y = r / p.uoW, x = r - y * p.uoW;
+  const int h = p.uh[s], w = p.uw[s];
+  int y0, y1, x0, x1;
+  float ly0, ly1, lx0, lx1;
+  cmx_bilin_src(y, (float)h / p.uoH, h, y0, y1, ly0, ly1);
+  cmx_bilin_src(x, (float)w / p.uoW, w, x0, x1, lx0, lx1);
+  const long b = (long)n * h * w;
+  return UpTaps{b + (long)y0 * w + x0, b + (long)y0 * w + x1, b + (long)y1 * w + x0, b + (long)y1 * w + x1,
+                ly0 * lx0, ly0 * lx1, ly1 * lx0, ly1 * lx1};
+}
+
+// (the source loops are fully unrolled with `s < p.nup` guards: a runtime index into the
+// argument struct's arrays would demote the whole struct to scratch memory)
 template <typename T>
+__device__ __forceinline__ float up_add1(const GemmArgs& p, int i, int j) {
+  float v = 0.f;
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    if (s >= p.nup) break;
+    const UpTaps t = up_taps(p, s, i);
+    const T* u = reinterpret_cast<const T*>(p.up[s]) + j;
+    const long ld = p.N;
+    v += t.w00 * to_f32(u[t.r00 * ld]) + t.w01 * to_f32(u[t.r01 * ld]) + t.w10 * to_f32(u[t.r10 * ld]) +
+         t.w11 * to_f32(u[t.r11 * ld]);
+  }
+  return v;
+}
+
+// 8 consecutive columns (16-B rows of the maps: N % 8 == 0 checked at launch)
+template <typename T>
+__device__ __forceinline__ void up_add8(const GemmArgs& p, int i, int j, float* v) {
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    if (s >= p.nup) break;
+    const UpTaps t = up_taps(p, s, i);
+    const T* u = reinterpret_cast<const T*>(p.up[s]) + j;
+    const long ld = p.N;
+    float a[8], b[8], c[8], d[8];
+    load_vec<T>(u + t.r00 * ld, a);
+    load_vec<T>(u + t.r01 * ld, b);
+    load_vec<T>(u + t.r10 * ld, c);
+    load_vec<T>(u + t.r11 * ld, d);
+    if constexpr (sizeof(T) == 4) {
+      load_vec<T>(u + t.r00 * ld + 4, a + 4);
+      load_vec<T>(u + t.r01 * ld + 4, b + 4);
+      load_vec<T>(u + t.r10 * ld + 4, c + 4);
+      load_vec<T>(u + t.r11 * ld + 4, d + 4);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += t.w00 * a[e] + t.w01 * b[e] + t.w10 * c[e] + t.w11 * d[e];
+  }
+}
+
+// element offset of C(g, i, j) under the patch scatter
+__device__ __forceinline__ long scatter_offset(const GemmArgs& p, int g, int i, int j) {
+  const int hw = p.scHo * p.scWo;
+  const int n = i / hw, r = i - n * hw, oy = r / p.scWo, ox = r - oy * p.scWo;
+  const int tap = j / p.scC, c = j - tap * p.scC, kh = tap / p.scR, kw = tap - kh * p.scR;
+  return (long)g * p.sC + (((long)n * p.scH + oy * p.scR + kh) * p.scW + ox * p.scR + kw) * p.scC + c;
+}
+
+// element offset of C(g, i, j): row-major with ldc, or (EXT instantiations only) the patch scatter
+template <bool EXT = true>
+__device__ __forceinline__ long c_offset(const GemmArgs& p, int g, int i, int j) {
+  if constexpr (EXT) {
+    if (p.scatter) return scatter_offset(p, g, i, j);
+  }
+  return (long)g * p.sC + (long)i * p.ldc + j;
+}
+
+// per-element epilogue of the generic (register-staged) kernel; the upsample-add and scatter
+// extensions only in its EXT instantiations (inlined into the 16 x tiles unrolled epilogue
+// loop they would spill the plain kernels' registers)
+template <typename T, bool EXT = false>
 __device__ __forceinline__ void epi_store(const GemmArgs& p, int g, int i, int j, float acc) {
   const float bj = p.bias ? p.bias[(long)g * p.sbias + j] : 0.f;
+  if constexpr (EXT) {
+    if (p.nup) acc += up_add1<T>(p, i, j);
+  }
   float v = act_fwd(acc + bj, p.act);
-  const long off = (long)g * p.sC + (long)i * p.ldc + j;
+  const long off = c_offset<EXT>(p, g, i, j);
   if (p.R) {
     const float sc = p.rscale ? p.rscale[((long)g * p.M + i) / p.rows_per_sample] : 1.f;
     v = to_f32(reinterpret_cast<const T*>(p.R)[off]) + sc * v;
@@ -87,7 +178,7 @@ __device__ __forceinline__ void dbias_store(const GemmArgs& p, int g, int i, flo
 template <typename T>
 __device__ __forceinline__ void epi_store8(const GemmArgs& p, int g, int i, int j, int nv, float* v) {
   if (nv < 8 || !p.cvec) {
-    for (int e = 0; e < nv; ++e) epi_store<T>(p, g, i, j + e, v[e]);
+    for (int e = 0; e < nv; ++e) epi_store<T, true>(p, g, i, j + e, v[e]);
     return;
   }
   if (p.bias) {
@@ -95,11 +186,12 @@ __device__ __forceinline__ void epi_store8(const GemmArgs& p, int g, int i, int 
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] += bp[e];
   }
+  if (p.nup) up_add8<T>(p, i, j, v);
   if (p.act) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = act_fwd(v[e], p.act);
   }
-  const long off = (long)g * p.sC + (long)i * p.ldc + j;
+  const long off = c_offset(p, g, i, j);
   if (p.R) {
     const float sc = p.rscale ? p.rscale[((long)g * p.M + i) / p.rows_per_sample] : 1.f;
     float rv[8];
@@ -611,7 +703,7 @@ struct TileLoader {
   }
 };
 
-template <typename T, int BM, int BN, bool TA, bool TB>
+template <typename T, int BM, int BN, bool TA, bool TB, bool EXT>
 __global__ __launch_bounds__(256) void gemm_generic_kernel(const GemmArgs p) {
   typedef MF<T> mf;
   constexpr int LD = BK + Stage<T>::PAD;
@@ -712,7 +804,7 @@ __global__ __launch_bounds__(256) void gemm_generic_kernel(const GemmArgs p) {
         const int i = i0 + wm * (BM / 2) + a * 32 + accrow(q, h);
         if (i >= p.M) continue;
         if (dbcol) dbias_store(p, g, i, acc[a][b][q]);
-        else epi_store<T>(p, g, i, j, acc[a][b][q]);
+        else epi_store<T, EXT>(p, g, i, j, acc[a][b][q]);
       }
     }
   }
@@ -802,15 +894,21 @@ void launch_bf16_ns(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStr
   else launch_bf16<BM, BN, 2>(a, G, nsplit, tA, tB, s);
 }
 
-template <typename T, int BM, int BN>
-void launch_generic(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream_t s) {
+template <typename T, int BM, int BN, bool EXT>
+void launch_generic_x(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream_t s) {
   dim3 grid(a.tiles_m * a.tiles_n, G, nsplit);
-#define CMX_GEMM_LAUNCH(TA, TB) hipLaunchKernelGGL((gemm_generic_kernel<T, BM, BN, TA, TB>), grid, dim3(256), 0, s, a)
+#define CMX_GEMM_LAUNCH(TA, TB) hipLaunchKernelGGL((gemm_generic_kernel<T, BM, BN, TA, TB, EXT>), grid, dim3(256), 0, s, a)
   if (!tA && !tB) CMX_GEMM_LAUNCH(false, false);
   else if (!tA && tB) CMX_GEMM_LAUNCH(false, true);
   else if (tA && tB) CMX_GEMM_LAUNCH(true, true);
   else CMX_GEMM_LAUNCH(true, false);
 #undef CMX_GEMM_LAUNCH
+}
+
+template <typename T, int BM, int BN>
+void launch_generic(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream_t s) {
+  if (a.nup || a.scatter) launch_generic_x<T, BM, BN, true>(a, G, nsplit, tA, tB, s);
+  else launch_generic_x<T, BM, BN, false>(a, G, nsplit, tA, tB, s);
 }
 
 // the bf16 fast path needs every operand row to be whole 16-B chunks on 16-B boundaries
@@ -905,11 +1003,21 @@ int cmx_gemm_splitk(int G, int M, int N, int K, int ones_col, int dtype) {
   return s < 1 ? 1 : (int)s;
 }
 
-int cmx_gemm(const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R,
-             const float* rscale, float* dbias, float* workspace, int G, int M, int N, int K, int K1, int64_t lda,
-             int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias,
-             int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode, int ones_col, int splitk,
-             int dtype, hipStream_t s) {
+}  // extern "C"
+
+namespace {
+// upsample-add sources of the epilogue (nup = 0: none)
+struct UpSpec {
+  const void* src[3];
+  int h[3], w[3], n, oH, oW;
+};
+
+int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R,
+              const float* rscale, float* dbias, float* workspace, int G, int M, int N, int K, int K1, int64_t lda,
+              int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias,
+              int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode, int ones_col, int splitk,
+              int dtype, hipStream_t s, const UpSpec* up, int scR = 0, int scH = 0, int scW = 0, int scC = 0,
+              int scHo = 0, int scWo = 0) {
   CMX_REQUIRE(G > 0 && M > 0 && N > 0 && K > 0, CMX_ERR_SHAPE, "gemm: empty problem G=%d M=%d N=%d K=%d", G, M, N, K);
   CMX_REQUIRE(dtype == 0 || dtype == 1, CMX_ERR_DTYPE, "gemm: unsupported dtype %d", dtype);
   CMX_REQUIRE(out_mode >= 0 && out_mode <= 2 && act >= 0 && act <= 3, CMX_ERR_ARG, "gemm: out_mode/act");
@@ -940,6 +1048,23 @@ int cmx_gemm(const void* A, const void* A2, const void* B, void* C, const float*
            (!R || (uintptr_t)R % 16 == 0);
   a.lda = lda; a.lda2 = lda2; a.ldb = ldb; a.ldc = ldc; a.sA = sA; a.sA2 = sA2; a.sB = sB; a.sC = sC;
   a.sbias = sbias; a.sdb = sdb;
+  if (up && up->n > 0) {
+    CMX_REQUIRE(up->n <= 3 && G == 1 && !ones_col && N % 8 == 0 && (long)up->oH * up->oW > 0 &&
+                M % (up->oH * up->oW) == 0, CMX_ERR_ARG, "gemm: upsample-add epilogue needs G = 1, N %% 8 == 0 and "
+                "M a whole number of %d x %d grids", up->oH, up->oW);
+    for (int q = 0; q < up->n; ++q) {
+      CMX_REQUIRE(up->src[q] && ((uintptr_t)up->src[q] & 15) == 0 && up->h[q] > 0 && up->w[q] > 0, CMX_ERR_ARG,
+                  "gemm: upsample-add source %d", q);
+      a.up[q] = up->src[q]; a.uh[q] = up->h[q]; a.uw[q] = up->w[q];
+    }
+    a.nup = up->n; a.uoH = up->oH; a.uoW = up->oW;
+  }
+  if (scR > 0) {
+    CMX_REQUIRE(G == 1 || sC > 0, CMX_ERR_ARG, "gemm: scatter");
+    CMX_REQUIRE(!R && out_mode == 0 && !ones_col && N == scR * scR * scC && M % (scHo * scWo) == 0, CMX_ERR_ARG,
+                "gemm: patch scatter needs a plain store of N = R*R*C columns");
+    a.scatter = 1; a.scH = scH; a.scW = scW; a.scC = scC; a.scR = scR; a.scHo = scHo; a.scWo = scWo;
+  }
   const int kstep = fast ? FBK : BK;
   const int nk = (K + kstep - 1) / kstep;
   a.kt_per_split = (nk + splitk - 1) / splitk;
@@ -975,6 +1100,56 @@ int cmx_gemm(const void* A, const void* A2, const void* B, void* C, const float*
     else launch_reduce<float>(a, G, work, s);
   }
   return cmx_check_launch("gemm");
+}
+}  // namespace
+
+extern "C" {
+
+int cmx_gemm(const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R,
+             const float* rscale, float* dbias, float* workspace, int G, int M, int N, int K, int K1, int64_t lda,
+             int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias,
+             int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode, int ones_col, int splitk,
+             int dtype, hipStream_t s) {
+  return gemm_impl(A, A2, B, C, bias, R, rscale, dbias, workspace, G, M, N, K, K1, lda, lda2, ldb, ldc, sA, sA2, sB,
+                   sC, sbias, sdb, rows_per_sample, transA, transB, act, out_mode, ones_col, splitk, dtype, s, nullptr);
+}
+
+// dx of a non-overlapping patchify conv (stride == kernel == R, pad 0: Attention.sr,
+// dual_segformer.py:95-96) in ONE launch: dx[g] = col2im(dy[g] @ W[g]) with the col2im folded
+// into the GEMM epilogue as an address remap (every input pixel belongs to at most one patch,
+// so there is no overlap to sum).  dy (G, NIg*Ho*Wo, N), W (G, N, R*R*C) tap-major, dx
+// (G*NIg, H, W, C) NHWC.  Pixels outside the Ho*R x Wo*R window (H or W not a multiple of R)
+// are not written: the caller zeroes dx for such shapes.
+int cmx_conv_patch_dgrad(const void* dy, const void* Wt, void* dx, int G, int NIg, int H, int Wd, int C, int R, int Ho,
+                         int Wo, int N, int64_t sdy, int64_t sW, int64_t sdx, int dtype, hipStream_t s) {
+  CMX_REQUIRE(G > 0 && NIg > 0 && C % 8 == 0 && R > 0 && Ho == H / R && Wo == Wd / R && Ho > 0 && Wo > 0, CMX_ERR_SHAPE,
+              "conv_patch_dgrad: H=%d W=%d R=%d Ho=%d Wo=%d C=%d", H, Wd, R, Ho, Wo, C);
+  const int M = NIg * Ho * Wo, Kc = R * R * C;
+  return gemm_impl(dy, nullptr, Wt, dx, nullptr, nullptr, nullptr, nullptr, nullptr, G, M, Kc, N, N, N, 0, Kc, Kc, sdy,
+                   0, sW, sdx, 0, 0, 1, 0, 1, 0, 0, 0, 1, dtype, s, nullptr, R, H, Wd, C, Ho, Wo);
+}
+
+// DecoderHead.linear_fuse on the restructured decoder (MLPDecoder.py:66-77):
+//   Z = e1 @ Wf[:, 3E:4E]^T + bias + up(z4) + up(z3) + up(z2)
+// where z_i = e_i @ Wf[:, slot_i]^T are the low-resolution products of the upsampled branches
+// (bilinear interpolation is linear with weights summing to 1, so it commutes with the 1x1
+// conv: W up(e) = up(W e)).  e1 (B*H1*W1, E), z_i (B, h_i, w_i, E), Wf (E, ldw) with the c1
+// slice at column 3E; Z (B*H1*W1, E).  The (B, N1, 4E) concat of the reference is never formed.
+int cmx_decoder_fuse_fwd(const void* e1, const void* Wf_c1, void* Z, const float* bias, const void* z4, const void* z3,
+                         const void* z2, int B, int H1, int W1, int h4, int w4, int h3, int w3, int h2, int w2, int E,
+                         int64_t ldw, int dtype, hipStream_t s) {
+  CMX_REQUIRE(B > 0 && H1 > 0 && W1 > 0 && E > 0 && E % 8 == 0, CMX_ERR_SHAPE, "decoder_fuse_fwd: B=%d E=%d", B, E);
+  UpSpec up{};
+  const void* src[3] = {z4, z3, z2};
+  const int hh[3] = {h4, h3, h2}, ww[3] = {w4, w3, w2};
+  for (int q = 0; q < 3; ++q) {
+    if (!src[q]) continue;
+    up.src[up.n] = src[q]; up.h[up.n] = hh[q]; up.w[up.n] = ww[q]; ++up.n;
+  }
+  up.oH = H1; up.oW = W1;
+  const int M = B * H1 * W1;
+  return gemm_impl(e1, nullptr, Wf_c1, Z, bias, nullptr, nullptr, nullptr, nullptr, 1, M, E, E, E, E, 0, ldw, E, 0, 0,
+                   0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 1, dtype, s, &up);
 }
 
 

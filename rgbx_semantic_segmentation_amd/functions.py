@@ -417,7 +417,14 @@ class ConvF(Function):
         else:
             _wgrad_into(dy, cols, Wg, bg)
         dx = None
-        if ctx.needs_input_grad[0] and not nchw:
+        if ctx.needs_input_grad[0] and not nchw and KH == KW == st and pad == 0 and H // st == Ho and Wd // st == Wo:
+            # non-overlapping patches (Attention.sr): col2im folded into the dgrad GEMM's epilogue
+            exact = H % st == 0 and Wd % st == 0
+            dx = (torch.empty if exact else torch.zeros)(NI, H, Wd, C, dtype=dy.dtype, device=dy.device)
+            K.call("cmx_conv_patch_dgrad", K.ptr(dy), K.ptr(W), K.ptr(dx), G, NI // G, H, Wd, C, st, Ho, Wo, W.shape[1],
+                   dy.stride(0), W.stride(0), NI // G * H * Wd * C, K.dtype_code(dy), K.stream())
+            dx = dx.view(ctx.xshape)
+        elif ctx.needs_input_grad[0] and not nchw:
             dcols = _dgrad(dy, W, torch.empty(G, NI // G * Ho * Wo, W.shape[-1], dtype=dy.dtype, device=dy.device))
             dx = torch.empty(NI, H, Wd, C, dtype=dy.dtype, device=dy.device)
             K.call("cmx_col2im_nhwc", K.ptr(dcols), K.ptr(dx), NI, H, Wd, C, KH, KW, st, pad, Ho, Wo, W.shape[-1],
@@ -646,45 +653,69 @@ def batchnorm(store, bn, x, training, res=None, act="none", dscale=None, rps=1, 
     return BatchNormF.apply(x, res, prm, training, act, dscale, rps, group, bn.weight)
 
 
-# ---------------------------------------------------------------------------- decoder gather
-class DecoderGatherF(Function):
-    """Bilinear upsample of c4, c3, c2 to the 1/4 grid + concat [c4, c3, c2, c1]
-    (MLPDecoder.py:66-77) written straight into one (B, N1, 4E) buffer."""
+# ---------------------------------------------------------------------------- decoder fuse
+def _adjoint_to(dZ, B, H1, W1, h, w, E):
+    """up^T dZ: the bilinear adjoint of the (h, w) -> (H1, W1) upsample, (B, h*w, E) in dZ's
+    dtype (two separable 1-D gather passes, fp32 in between, no atomics)."""
+    dt = K.dtype_code(dZ)
+    tmp = torch.empty(B * H1, w, E, dtype=torch.float32, device=dZ.device)
+    K.call("cmx_bilinear_adjoint_1d", K.ptr(dZ), K.ptr(tmp), B * H1, W1, w, E, W1 * E, E, 0, 0, 1.0, dt, 0, K.stream())
+    g = torch.empty(B, h * w, E, dtype=dZ.dtype, device=dZ.device)
+    K.call("cmx_bilinear_adjoint_1d", K.ptr(tmp), K.ptr(g), B, H1, h, w * E, H1 * w * E, w * E, 0, 0, 1.0, 0, dt,
+           K.stream())
+    return g
+
+
+class DecoderFuseF(Function):
+    """DecoderHead's upsample + concat + linear_fuse 1x1 conv (MLPDecoder.py:66-77) without the
+    (B, N1, 4E) concat.  The 1x1 conv is linear and bilinear interpolation is linear with
+    weights summing to 1, so for each upsampled branch  W_i up(e_i) = up(W_i e_i):
+
+        Z = e1 W_c1^T + b + up(e4 W_c4^T) + up(e3 W_c3^T) + up(e2 W_c2^T)
+
+    The three branch products run at their own (low) resolution and the GEMM of the c1 branch
+    adds their bilinear upsample in its epilogue (cmx_decoder_fuse_fwd).  Backward: dZ feeds
+    the c1 dgrad / wgrad and the bias gradient at full resolution; each upsampled branch gets
+    dz_i = up^T dZ (bilinear adjoint) and then its dgrad / wgrad at low resolution.
+    Executed FLOPs: 38400 x 512 x 512 + low-res products instead of 38400 x 2048 x 512 (B2, bs=2);
+    the step roofline keeps the reference's op-by-op count (flops.py)."""
 
     @staticmethod
-    def forward(ctx, c4, c3, c2, c1, sizes):
-        B, N1, E = c1.shape
+    def forward(ctx, e4, e3, e2, e1, Wf, Wfg, bf, bfg, sizes, anchor):
+        B, N1, E = e1.shape
+        (H1, W1), hw = sizes[0], sizes[1:]        # hw: grids of c2, c3, c4
+        W = Wf[0]                                 # (E, 4E): column slots [c4 | c3 | c2 | c1]
+        zs = []
+        for slot, (e, (h, w)) in enumerate(zip((e4, e3, e2), (hw[2], hw[1], hw[0]))):
+            z = torch.empty(1, B * h * w, E, dtype=e.dtype, device=e.device)
+            K.gemm(e.reshape(1, B * h * w, E), W[None, :, slot * E:(slot + 1) * E], z)
+            zs.append(z)
+        Z = torch.empty(B * N1, E, dtype=e1.dtype, device=e1.device)
+        Wc1 = W[:, 3 * E:]
+        K.call("cmx_decoder_fuse_fwd", K.ptr(_c(e1)), Wc1.data_ptr(), K.ptr(Z), K.ptr(bf), K.ptr(zs[0]), K.ptr(zs[1]),
+               K.ptr(zs[2]), B, H1, W1, hw[2][0], hw[2][1], hw[1][0], hw[1][1], hw[0][0], hw[0][1], E, W.stride(0),
+               K.dtype_code(e1), K.stream())
+        ctx.save_for_backward(e4, e3, e2, e1, Wf)
+        ctx.meta = (Wfg, bfg, sizes)
+        return Z
+
+    @staticmethod
+    def backward(ctx, dZ):
+        e4, e3, e2, e1, Wf = ctx.saved_tensors
+        Wfg, bfg, sizes = ctx.meta
+        B, N1, E = e1.shape
         (H1, W1), hw = sizes[0], sizes[1:]
-        cat = torch.empty(B, N1, 4 * E, dtype=c1.dtype, device=c1.device)
-        dt = K.dtype_code(c1)
-        esz = cat.element_size()
-        for slot, (t, (h, w)) in enumerate(zip((c4, c3, c2, c1), (hw[2], hw[1], hw[0], (H1, W1)))):
-            K.call("cmx_bilinear_fwd_nhwc", K.ptr(_c(t)), cat.data_ptr() + slot * E * esz, B, h, w, H1, W1, E, 4 * E,
-                   dt, K.stream())
-        ctx.sizes = sizes
-        ctx.E = E
-        return cat
-
-    @staticmethod
-    def backward(ctx, dcat):
-        dcat = _c(dcat)
-        (H1, W1), hw = ctx.sizes[0], ctx.sizes[1:]
-        E = ctx.E
-        B = dcat.shape[0]
-        dt = K.dtype_code(dcat)
-        esz = dcat.element_size()
+        dZ = _c(dZ).view(1, B * N1, E)
         grads = []
-        for slot, (h, w) in enumerate((hw[2], hw[1], hw[0])):
-            base = dcat.data_ptr() + slot * E * esz
-            tmp = torch.empty(B * H1, w, E, dtype=torch.float32, device=dcat.device)
-            K.call("cmx_bilinear_adjoint_1d", base, K.ptr(tmp), B * H1, W1, w, E, W1 * 4 * E, 4 * E, 0, 0, 1.0, dt, 0,
-                   K.stream())
-            g = torch.empty(B, h * w, E, dtype=dcat.dtype, device=dcat.device)
-            K.call("cmx_bilinear_adjoint_1d", K.ptr(tmp), K.ptr(g), B, H1, h, w * E, H1 * w * E, w * E, 0, 0, 1.0, 0,
-                   dt, K.stream())
-            grads.append(g)
-        g1 = dcat[..., 3 * E:].contiguous()
-        return grads[0], grads[1], grads[2], g1, None
+        for slot, (e, (h, w)) in enumerate(zip((e4, e3, e2), (hw[2], hw[1], hw[0]))):
+            dz = _adjoint_to(dZ, B, H1, W1, h, w, E).view(1, B * h * w, E)
+            sl = slice(slot * E, (slot + 1) * E)
+            grads.append(_dgrad(dz, Wf[:, :, sl], torch.empty_like(dz)).view(e.shape))
+            _wgrad_into(dz, e.reshape(1, B * h * w, E), Wfg[:, :, sl])
+        e1f = e1.reshape(1, B * N1, E)
+        de1 = _dgrad(dZ, Wf[:, :, 3 * E:], torch.empty_like(e1f)).view(e1.shape)
+        _wgrad_into(dZ, e1f, Wfg[:, :, 3 * E:], bfg)
+        return grads[0], grads[1], grads[2], de1, None, None, None, None, None, None
 
 
 # ---------------------------------------------------------------------------- final upsample + CE

@@ -1,9 +1,10 @@
 """SegFormer all-MLP decode head (reference: models/decoders/MLPDecoder.py:8-81).
 
-Execution on tokens: linear_c{1..4} GEMMs, bilinear upsample of c2..c4 written straight
-into the channel slices of one (B, N1, 4E) buffer (no torch.cat), linear_fuse GEMM,
-BatchNorm (SyncBN across ranks when a process group is given) + ReLU + Dropout2d fused
-into one apply kernel, linear_pred GEMM.  Returns low-resolution logits (B*N1, K).
+Execution on tokens: linear_c{1..4} GEMMs; the upsample + concat + linear_fuse 1x1 conv as
+functions.DecoderFuseF (the conv applied to each branch at its own resolution and the
+bilinear upsample added in the c1 GEMM's epilogue: the (B, N1, 4E) concat is never formed);
+BatchNorm (SyncBN across ranks when a process group is given) + ReLU + Dropout2d fused into
+one apply kernel; linear_pred GEMM.  Returns low-resolution logits (B*N1, K).
 """
 from __future__ import annotations
 
@@ -44,9 +45,15 @@ class DecoderHead(nn.Module):
             t = F.glinear(store, lin[i].proj.weight, lin[i].proj.bias, feats[i].view(1, -1, feats[i].shape[-1]))
             proj.append(t.view(B, -1, E))
         H1, W1 = grids[0]
-        cat = F.DecoderGatherF.apply(proj[3], proj[2], proj[1], proj[0], [grids[0]] + list(grids[1:]))
         M = B * H1 * W1
-        f = F.glinear(store, self.linear_fuse[0].weight, self.linear_fuse[0].bias, cat.view(1, M, 4 * E))
+        conv = self.linear_fuse[0]
+        G = 1
+        Wf = store.w(conv.weight).view(G, E, 4 * E)
+        Wfg = store.g(conv.weight).view(G, E, 4 * E)
+        bf = store.w(conv.bias, compute=False).view(G, E)
+        bfg = store.g(conv.bias).view(G, E)
+        f = F.DecoderFuseF.apply(proj[3], proj[2], proj[1], proj[0], Wf, Wfg, bf, bfg, [grids[0]] + list(grids[1:]),
+                                 conv.weight)
         f = F.batchnorm(store, self.linear_fuse[1], f.view(M, E), training, act="relu", dscale=dscale,
                         rps=H1 * W1, group=group)
         return F.glinear(store, self.linear_pred.weight, self.linear_pred.bias, f.view(1, M, E)).view(M, -1)

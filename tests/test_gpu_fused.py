@@ -1,0 +1,87 @@
+"""Fused kernels of round 2 against plain PyTorch fp32 references of the same ops.
+
+* functions.DecoderFuseF (cmx_decoder_fuse_fwd + low-resolution branch GEMMs + bilinear
+  adjoints): DecoderHead's upsample + concat + linear_fuse 1x1 conv (MLPDecoder.py:66-77) with
+  the conv commuted ahead of the upsample -- forward and every input / weight / bias gradient.
+* cmx_conv_patch_dgrad: dx of the SRA spatial-reduction conv (kernel = stride = R, pad 0,
+  dual_segformer.py:95-96) with the col2im folded into the GEMM epilogue, incl. grids that R
+  does not divide (the remainder pixels get zero gradient, as torch's conv backward gives).
+Tolerances: fp32 1e-5 relative; bf16 2e-2 (bf16 storage of the low-resolution products and
+of the outputs)."""
+import pytest
+import torch
+import torch.nn.functional as TF
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    return ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,H1,W1,E", [(2, 120, 160, 64), (1, 32, 40, 128), (2, 30, 17, 32)])
+def test_decoder_fuse_matches_upsample_concat_conv(dev, dtype, B, H1, W1, E):
+    from rgbx_semantic_segmentation_amd import deferred
+    from rgbx_semantic_segmentation_amd import functions as Fn
+    torch.manual_seed(0)
+    grids = [(H1, W1), ((H1 + 1) // 2, (W1 + 1) // 2), ((H1 + 3) // 4, (W1 + 3) // 4), ((H1 + 7) // 8, (W1 + 7) // 8)]
+    es = [torch.randn(B, h * w, E, device=dev) for (h, w) in grids]           # e1, e2, e3, e4
+    Wf = torch.randn(1, E, 4 * E, device=dev) * (4 * E) ** -0.5
+    bf = torch.randn(1, E, device=dev) * 0.1
+    dZ = torch.randn(B * H1 * W1, E, device=dev)
+    # reference: up(e4), up(e3), up(e2), e1 concatenated -> 1x1 conv (fp32 autograd on the rounded inputs)
+    er = [e.to(dtype).float().requires_grad_(True) for e in es]
+    Wr = Wf.to(dtype).float().requires_grad_(True)
+    br = bf.clone().requires_grad_(True)
+
+    def nchw(e, hw):
+        return e.view(B, hw[0], hw[1], E).permute(0, 3, 1, 2)
+    ups = [TF.interpolate(nchw(er[i], grids[i]), size=(H1, W1), mode="bilinear", align_corners=False)
+           for i in (3, 2, 1)]
+    cat = torch.cat(ups + [nchw(er[0], grids[0])], 1)
+    Zr = TF.conv2d(cat, Wr[0].view(E, 4 * E, 1, 1), br[0]).permute(0, 2, 3, 1).reshape(B * H1 * W1, E)
+    Zr.backward(dZ.to(dtype).float())
+    # product
+    eq = [e.to(dtype).requires_grad_(True) for e in es]
+    Wq = Wf.to(dtype)
+    Wg = torch.zeros(1, E, 4 * E, device=dev)
+    bg = torch.zeros(1, E, device=dev)
+    anchor = torch.nn.Parameter(torch.zeros(1, device=dev))
+    Z = Fn.DecoderFuseF.apply(eq[3], eq[2], eq[1], eq[0], Wq, Wg, bf, bg, grids, anchor)
+    Z.backward(dZ.to(dtype))
+    deferred.flush()
+    torch.cuda.synchronize()
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert rel(Z, Zr) < tol, rel(Z, Zr)
+    for i in range(4):
+        assert rel(eq[i].grad, er[i].grad) < tol, (i, rel(eq[i].grad, er[i].grad))
+    assert rel(Wg, Wr.grad) < tol, rel(Wg, Wr.grad)
+    assert rel(bg, br.grad) < tol, rel(bg, br.grad)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("NI,G,H,W,C,R,N", [(4, 2, 120, 160, 64, 8, 64), (4, 2, 60, 80, 128, 4, 128),
+                                            (2, 2, 30, 40, 320, 2, 320), (2, 1, 60, 81, 32, 8, 32),
+                                            (4, 2, 13, 9, 64, 2, 64)])
+def test_conv_patch_dgrad_matches_conv_backward(dev, dtype, NI, G, H, W, C, R, N):
+    from rgbx_semantic_segmentation_amd import kernels as Kn
+    torch.manual_seed(1)
+    Ho, Wo = H // R, W // R
+    NIg = NI // G
+    Wt = torch.randn(G, N, R, R, C, device=dev) * (R * R * C) ** -0.5          # tap-major storage
+    dy = torch.randn(G, NIg * Ho * Wo, N, device=dev)
+    Wq, dyq = Wt.to(dtype), dy.to(dtype)
+    ref = []
+    for g in range(G):
+        w = Wq[g].float().permute(0, 3, 1, 2)                                     # (N, C, R, R)
+        d = dyq[g].float().view(NIg, Ho, Wo, N).permute(0, 3, 1, 2)
+        ref.append(torch.nn.grad.conv2d_input((NIg, C, H, W), w, d, stride=R).permute(0, 2, 3, 1))
+    ref = torch.cat(ref)
+    exact = H % R == 0 and W % R == 0
+    dx = (torch.empty if exact else torch.zeros)(NI, H, W, C, dtype=dtype, device=dev)
+    Kn.call("cmx_conv_patch_dgrad", Kn.ptr(dyq), Kn.ptr(Wq), Kn.ptr(dx), G, NIg, H, W, C, R, Ho, Wo, N,
+            dyq.stride(0), Wq.stride(0), NIg * H * W * C, Kn.dtype_code(dyq), Kn.stream())
+    torch.cuda.synchronize()
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel(dx, ref) < tol, rel(dx, ref)
