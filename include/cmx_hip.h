@@ -103,16 +103,23 @@ int cmx_ffm_rowmat(const void* X, const float* M, void* out, int Bt, int N, int 
  *      + tiny-M MLP (:16-20), SpatialWeights 1x1 C->2 + sigmoid (:74-83), rectification. */
 size_t cmx_frm_pool_workspace(int B, int N, int C);
 int cmx_frm_pool_fwd(const void* x, float* pooled, int* argmax, float* workspace, int B, int N, int C, int dtype, hipStream_t stream);
-int cmx_frm_pool_bwd(const float* dpooled, const int* argmax, void* dx, int B, int N, int C, int dtype, hipStream_t stream);
+/* dx += pooling backward; dpooled (B, 4C) given as partial slices dp[b][k] = sum_s part[s*slice_stride + b*4C + k] */
+int cmx_frm_pool_bwd(const float* dpooled_part, int nslice, int64_t slice_stride, const int* argmax, void* dx, int B, int N, int C, int dtype, hipStream_t stream);
+/* tiny-M linear y = act(x w^T + b) (x (M, K) fp32, M <= 8); backward in one pass over w: dy given as partial slabs
+ * dy[m][n] = sum_s part[s*dy_slice_stride + m*dy_row_stride + n]; writes dw / db; dx as cmx_small_linear_nslice()
+ * partial slices (nslice, M, K) in dx_part (NULL: skip) */
 int cmx_small_linear_fwd(const float* x, const float* w, const float* b, float* y, int M, int K, int Nout, int act, hipStream_t stream);
+int cmx_small_linear_nslice(void);
 size_t cmx_small_linear_bwd_workspace(int M, int K, int Nout);
-int cmx_small_linear_bwd(const float* dy, const float* y, const float* x, const float* w, float* dx, float* dw, float* db, float* dz_ws, int M, int K, int Nout, int act, int accumulate, hipStream_t stream);
-int cmx_frm_spatial_fwd(const void* h, const float* w2, const float* b2, float* sw, int64_t rows, int C, int dtype, hipStream_t stream);
-size_t cmx_frm_spatial_bwd_workspace(int64_t rows, int C);
-int cmx_frm_spatial_bwd(const float* dsw, const float* sw, const void* h, const float* w2, void* dh, float* dw2, float* db2, float* workspace, int64_t rows, int C, int accumulate, int dtype, hipStream_t stream);
-int cmx_frm_combine_fwd(const void* x, const float* cw, const float* sw, void* out, int B, int N, int C, int dtype, hipStream_t stream);
-size_t cmx_frm_combine_bwd_workspace(int B, int N, int C);
-int cmx_frm_combine_bwd(const void* dout, const void* x, const float* cw, const float* sw, void* dx, float* dsw, float* dcw, float* workspace, int B, int N, int C, int dtype, hipStream_t stream);
+int cmx_small_linear_bwd(const float* dy_part, int dy_nslice, int64_t dy_slice_stride, int64_t dy_row_stride, const float* y, const float* x, const float* w, float* dx_part, float* dw, float* db, int M, int K, int Nout, int act, int accumulate, hipStream_t stream);
+/* rectification fused with SpatialWeights' C -> 2 conv + sigmoid: h (B*N, C) = the 2C -> C conv output (pre-ReLU),
+ * w2 (2, C), b2 (2) fp32; writes sw (B*N, 2) (saved for the backward) and out (2, B, N, C) */
+int cmx_frm_combine_fwd(const void* x, const float* cw, const void* h, const float* w2, const float* b2, float* sw, void* out, int B, int N, int C, int dtype, hipStream_t stream);
+/* backward: dx direct path (2,B,N,C), dh (B*N, C); workspace = dcw partials (B, nblk, 2C) followed by the
+ * [dw2 (2C) | db2 (2)] partials (B*nblk, 2C+2); nblk = cmx_frm_combine_bwd_nblk(N, C, dtype) */
+int cmx_frm_combine_bwd_nblk(int N, int C, int dtype);
+size_t cmx_frm_combine_bwd_workspace(int B, int N, int C, int dtype);
+int cmx_frm_combine_bwd(const void* dout, const void* x, const float* cw, const float* sw, const void* h, const float* w2, void* dx, void* dh, float* workspace, int B, int N, int C, int dtype, hipStream_t stream);
 
 /* ---- BatchNorm (ChannelEmbed BNs net_utils.py:319-329, decoder SyncBN MLPDecoder.py:51-55):
  *      fp64 channel sums -> (all-reduce for SyncBN) -> finalize; fused residual / act / Dropout2d. */

@@ -243,7 +243,12 @@ class ChannelWeights(nn.Module):                           # net_utils.py:10-30
     def forward(self, x1, x2):
         B = x1.shape[0]
         x = torch.cat((x1, x2), 1)
-        y = torch.cat((x.mean(dim=(2, 3)), x.amax(dim=(2, 3))), 1)
+        # AdaptiveAvgPool2d(1) / AdaptiveMaxPool2d(1) (net_utils.py:14-15,25-26): the max pool
+        # routes its gradient to ONE index (the first maximum in scan order), unlike amax
+        # which splits it over ties
+        avg = F.adaptive_avg_pool2d(x, 1).view(B, 2 * self.dim)
+        mx = F.adaptive_max_pool2d(x, 1).view(B, 2 * self.dim)
+        y = torch.cat((avg, mx), 1)
         return self.mlp(y).view(B, 2, self.dim, 1, 1).permute(1, 0, 2, 3, 4)
 
 

@@ -5,29 +5,83 @@
 //              pooled (B, 4C) = [avg x1 | avg x2 | max x1 | max x2]; argmax (B, 2C) int32 keeps
 //              the FIRST maximal token (the index PyTorch's CPU max pool routes gradient to).
 //  small_linear  y = act(x W^T + b) for the tiny-M channel MLP (B rows, :16-20) - a GEMV
-//              with one wave per output feature; backward writes dW/db straight into the
-//              gradient buffers.
-//  spatial     SpatialWeights second 1x1 conv (C -> 2) + sigmoid on relu(h) (:74-83).
-//  combine     out1 = x1 + 0.5*cw1*x2 + 0.5*sw1*x2 ; out2 = x2 + 0.5*cw0*x1 + 0.5*sw0*x1
-//              (:147-152) and its backward (direct path + dcw/dsw reductions).
+//              over LDS-staged rows; its backward is ONE pass over W that forms dz from the
+//              producer's partial slabs, writes dW/db and leaves dx as partial slices for
+//              the next consumer (no separate dz / reduce launches).
+//  combine     SpatialWeights' second 1x1 conv (C -> 2) + sigmoid (:74-83) fused with the
+//              rectification out1 = x1 + 0.5*cw1*x2 + 0.5*sw1*x2 ; out2 = x2 + 0.5*cw0*x1 +
+//              0.5*sw0*x1 (:147-152); its backward also runs the spatial head's backward
+//              (dh, dw2 / db2 partials) and leaves the dcw partials for the MLP backward.
+//  The first SpatialWeights 1x1 conv (2C -> C) is a cmx_gemm (forward: two A segments, no cat;
+//  dgrad: both modality slices in one G = 2 launch).
 #include "cmx_common.h"
 
 namespace {
 
-// partial pooling over a token chunk: blockIdx = (chunk, g*B + b); thread = channel
-template <typename T>
-__global__ void pool_partial_kernel(const T* __restrict__ x, float* __restrict__ psum, float* __restrict__ pmax,
-                                    int* __restrict__ pidx, int B, int N, int C, int chunk) {
+// Row-parallel layout shared by the token kernels: a row of C channels is C / V 16-B chunks;
+// TPR lanes per row (the chunk count rounded up to a power of two, at most 64), each lane
+// owning chunks lane, lane + TPR (MAXCH <= 2), RPB = 256 / TPR rows in flight per block.
+constexpr int MAXCH = 2;
+inline int row_lanes(int C, int V) {
+  int tpr = 4;
+  while (tpr < C / V && tpr < 64) tpr <<= 1;
+  return tpr;
+}
+
+// ------------------------------------------------------------------------ pooling (forward)
+// partial avg / max / argmax over a chunk of tokens of one (group, image): blockIdx = (chunk,
+// g*B + b).  16-B loads, rows spread over the block's row slots, the slots combined in LDS
+// (max ties -> the lowest token index, as a sequential scan).
+template <typename T, int TPR>
+__global__ __launch_bounds__(256) void pool_partial_kernel(const T* __restrict__ x, float* __restrict__ psum,
+                                                           float* __restrict__ pmax, int* __restrict__ pidx, int B,
+                                                           int N, int C, int chunk) {
+  constexpr int V = VecT<T>::N, RPB = 256 / TPR;
+  __shared__ float rs[RPB][MAXCH * TPR * V];
+  __shared__ float rm[RPB][MAXCH * TPR * V];
+  __shared__ int ri[RPB][MAXCH * TPR * V];
   const int gb = blockIdx.y, c_ = blockIdx.x;
+  const int lane = threadIdx.x % TPR, slot = threadIdx.x / TPR;
+  const int nch = C / V;
   const int n0 = c_ * chunk, n1 = min(N, n0 + chunk);
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+  float sm[MAXCH][V], mx[MAXCH][V];
+  int ix[MAXCH][V];
+#pragma unroll
+  for (int k = 0; k < MAXCH; ++k)
+#pragma unroll
+    for (int j = 0; j < V; ++j) { sm[k][j] = 0.f; mx[k][j] = -INFINITY; ix[k][j] = 0x7fffffff; }
+  const T* base = x + (long)gb * N * C;
+#pragma unroll 2
+  for (int n = n0 + slot; n < n1; n += RPB) {
+#pragma unroll
+    for (int k = 0; k < MAXCH; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch >= nch) continue;
+      float v[V];
+      load_vec<T>(base + (long)n * C + ch * V, v);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        sm[k][j] += v[j];
+        if (v[j] > mx[k][j]) { mx[k][j] = v[j]; ix[k][j] = n; }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < MAXCH; ++k)
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const int c = (lane + k * TPR) * V + j;
+      if (c < C) { rs[slot][c] = sm[k][j]; rm[slot][c] = mx[k][j]; ri[slot][c] = ix[k][j]; }
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
     float s = 0.f, m = -INFINITY;
-    int mi = n0;
-    const T* p = x + (long)gb * N * C + c;
-    for (int n = n0; n < n1; ++n) {
-      const float v = to_f32(p[(long)n * C]);
-      s += v;
-      if (v > m) { m = v; mi = n; }
+    int mi = 0x7fffffff;
+    for (int q = 0; q < RPB; ++q) {
+      s += rs[q][c];
+      const float v = rm[q][c];
+      const int i = ri[q][c];
+      if (v > m || (v == m && i < mi)) { m = v; mi = i; }
     }
     const long o = ((long)gb * gridDim.x + c_) * C + c;
     psum[o] = s; pmax[o] = m; pidx[o] = mi;
@@ -71,19 +125,56 @@ __global__ __launch_bounds__(256) void pool_final_kernel(const float* __restrict
   argmax[(long)b * 2 * C + g * C + c] = mi;
 }
 
-// one wave per output feature n; M rows
-__global__ void small_linear_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                        const float* __restrict__ b, float* __restrict__ y, int M, int K, int Nout,
-                                        int act) {
-  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (wave >= Nout) return;
-  const float* wr = w + (long)wave * K;
-  for (int m = 0; m < M; ++m) {
-    float s = 0.f;
-    for (int k = lane; k < K; k += 64) s += wr[k] * x[(long)m * K + k];
-    s = wave_sum(s);
-    if (lane == 0) y[(long)m * Nout + wave] = act_fwd(s + (b ? b[wave] : 0.f), act);
+// ------------------------------------------------------------------------ channel MLP
+// y[m][n] = act(x[m] . w[n] + b[n]) for the B-row MLP of ChannelWeights (net_utils.py:16-20):
+// x (M x K) staged once per block in LDS, one wave per 4 output features, float4 weight loads
+// (each weight row read once for all M rows).
+constexpr int MMAX = 8;
+constexpr int LIN_FPW = 1;                      // output features per wave
+__global__ __launch_bounds__(256) void linear_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                         const float* __restrict__ b, float* __restrict__ y, int M,
+                                                         int K, int Nout, int act) {
+  extern __shared__ float xs[];                 // M * K
+  for (int e = threadIdx.x; e < M * K; e += 256) xs[e] = x[e];
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int K4 = K >> 2;
+  const int n = blockIdx.x * 4 + wave;
+  if (n >= Nout) return;
+  const float4* wr = reinterpret_cast<const float4*>(w + (long)n * K);
+  float acc[MMAX];
+#pragma unroll
+  for (int m = 0; m < MMAX; ++m) acc[m] = 0.f;
+  int k4 = lane;
+  for (; k4 + 192 < K4; k4 += 256) {            // four independent 16-B weight loads in flight
+    float4 wv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) wv[u] = wr[k4 + 64 * u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int m = 0; m < MMAX; ++m) {
+        if (m < M) {
+          const float4 xv = *reinterpret_cast<const float4*>(xs + m * K + 4 * (k4 + 64 * u));
+          acc[m] += wv[u].x * xv.x + wv[u].y * xv.y + wv[u].z * xv.z + wv[u].w * xv.w;
+        }
+      }
+  }
+  for (; k4 < K4; k4 += 64) {
+    const float4 wv = wr[k4];
+#pragma unroll
+    for (int m = 0; m < MMAX; ++m) {
+      if (m < M) {
+        const float4 xv = *reinterpret_cast<const float4*>(xs + m * K + 4 * k4);
+        acc[m] += wv.x * xv.x + wv.y * xv.y + wv.z * xv.z + wv.w * xv.w;
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < MMAX; ++m) {
+    if (m >= M) break;
+    const float s = wave_sum(acc[m]);
+    if (lane == 0) y[(long)m * Nout + n] = act_fwd(s + (b ? b[n] : 0.f), act);
   }
 }
 
@@ -94,141 +185,195 @@ __device__ __forceinline__ float act_grad_from_out(float y, int act) {
   return 1.f;
 }
 
-__global__ void small_linear_dz_kernel(const float* __restrict__ dy, const float* __restrict__ y, float* __restrict__ dz,
-                                       long n, int act) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)n; i += gridDim.x * blockDim.x)
-    dz[i] = dy[i] * act_grad_from_out(y[i], act);
-}
-
-// partial dx over an n-slice: ws[slice][m][k] = sum_{n in slice} dz[m][n] w[n][k].
-// Block = 64 k-columns x 4 n-subslices (coalesced W rows), grid = (K/64, NSLICE).
-constexpr int DX_NSLICE = 16;
-constexpr int DX_MMAX = 8;
-__global__ __launch_bounds__(256) void small_linear_dx_kernel(const float* __restrict__ dz, const float* __restrict__ w,
-                                                              float* __restrict__ ws, int M, int K, int Nout) {
-  __shared__ float red[4][DX_MMAX][64];
+// Backward of y = act(x w^T + b) in ONE pass over w: block = 64 k-columns x 4 row lanes over
+// an n-slice of NSLICE.  dy arrives as partial slabs dy[m][n] = sum_s part[s*ss + m*sm + n]
+// (the producer's per-block partials: no separate reduce launch); dz = dy * act'(y).
+//   dx partial  dxp[slice][m][k] = sum_{n in slice} dz[m][n] w[n][k]     (consumer sums slices)
+//   dw[n][k] (+)= sum_m dz[m][n] x[m][k]                                 (written here)
+//   db[n]    (+)= sum_m dz[m][n]                                          (column block 0)
+constexpr int NSLICE = 16;
+constexpr int SLICE_MAX = 256;                  // rows per slice: Nout <= 16 * 256 = 4096
+__global__ __launch_bounds__(256) void linear_bwd_kernel(const float* __restrict__ dyp, int nsl, long ss, long sm,
+                                                         const float* __restrict__ y, const float* __restrict__ x,
+                                                         const float* __restrict__ w, float* __restrict__ dxp,
+                                                         float* __restrict__ dw, float* __restrict__ db, int M, int K,
+                                                         int Nout, int act, int accumulate) {
+  __shared__ float dzs[MMAX][SLICE_MAX];
+  __shared__ float red[4][MMAX][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int k = blockIdx.x * 64 + tx;
-  const int per = (Nout + DX_NSLICE - 1) / DX_NSLICE;
+  const int per = (Nout + NSLICE - 1) / NSLICE;
   const int n0 = blockIdx.y * per, n1 = min(Nout, n0 + per);
-  float acc[DX_MMAX];
-#pragma unroll
-  for (int m = 0; m < DX_MMAX; ++m) acc[m] = 0.f;
-  if (k < K) {
-    for (int n = n0 + ty; n < n1; n += 4) {
-      const float wv = w[(long)n * K + k];
-#pragma unroll
-      for (int m = 0; m < DX_MMAX; ++m)
-        if (m < M) acc[m] += dz[(long)m * Nout + n] * wv;
+  const int rows = n1 > n0 ? n1 - n0 : 0;
+  // dz of the slice: T consecutive lanes sum the nsl partial slabs of one value (strided over
+  // q), combined by shuffles in a fixed order (deterministic)
+  const int nval = M * rows;
+  int T = 1;
+  while (T < 64 && T * 2 * nval <= 256 && T * 2 <= nsl) T <<= 1;
+  for (int base = 0; base < nval * T; base += 256) {
+    const int t = base + threadIdx.x;
+    const int e = t / T, sub = t % T;
+    float d = 0.f;
+    int m = 0, n = n0;
+    if (e < nval) {
+      m = e / rows; n = n0 + e % rows;
+      for (int q = sub; q < nsl; q += T) d += dyp[q * ss + m * sm + n];
+    }
+    d = group_sum(d, T);
+    if (e < nval && sub == 0) dzs[m][n - n0] = d * act_grad_from_out(y[(long)m * Nout + n], act);
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && db) {
+    for (int r = threadIdx.x; r < rows; r += 256) {
+      float sb = 0.f;
+      for (int m = 0; m < M; ++m) sb += dzs[m][r];
+      db[n0 + r] = accumulate ? db[n0 + r] + sb : sb;
     }
   }
+  const int k = blockIdx.x * 64 + tx;
+  float acc[MMAX], xk[MMAX];
 #pragma unroll
-  for (int m = 0; m < DX_MMAX; ++m) red[ty][m][tx] = acc[m];
+  for (int m = 0; m < MMAX; ++m) {
+    acc[m] = 0.f;
+    xk[m] = (m < M && k < K) ? x[(long)m * K + k] : 0.f;
+  }
+  if (k < K) {
+#pragma unroll 4
+    for (int r = ty; r < rows; r += 4) {
+      const int n = n0 + r;
+      const float wv = w[(long)n * K + k];
+      float g = 0.f;
+#pragma unroll
+      for (int m = 0; m < MMAX; ++m) {
+        if (m < M) {
+          const float dz = dzs[m][r];
+          acc[m] += dz * wv;
+          g += dz * xk[m];
+        }
+      }
+      float* d = dw + (long)n * K + k;
+      *d = accumulate ? *d + g : g;
+    }
+  }
+  if (!dxp) return;
+#pragma unroll
+  for (int m = 0; m < MMAX; ++m) red[ty][m][tx] = acc[m];
   __syncthreads();
   if (ty == 0 && k < K) {
     for (int m = 0; m < M; ++m)
-      ws[((long)blockIdx.y * M + m) * K + k] = ((red[0][m][tx] + red[1][m][tx]) + red[2][m][tx]) + red[3][m][tx];
+      dxp[((long)blockIdx.y * M + m) * K + k] = ((red[0][m][tx] + red[1][m][tx]) + red[2][m][tx]) + red[3][m][tx];
   }
 }
 
-// dw[n][k] = sum_m dz[m][n] x[m][k]; db[n] = sum_m dz[m][n]
-__global__ void small_linear_dw_kernel(const float* __restrict__ dz, const float* __restrict__ x, float* __restrict__ dw,
-                                       float* __restrict__ db, int M, int K, int Nout, int accumulate) {
-  const long total = (long)Nout * K;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)total; i += gridDim.x * blockDim.x) {
-    const int k = i % K, n = i / K;
-    float s = 0.f;
-    for (int m = 0; m < M; ++m) s += dz[(long)m * Nout + n] * x[(long)m * K + k];
-    dw[i] = accumulate ? dw[i] + s : s;
-    if (k == 0 && db) {
-      float sb = 0.f;
-      for (int m = 0; m < M; ++m) sb += dz[(long)m * Nout + n];
-      db[n] = accumulate ? db[n] + sb : sb;
+// ------------------------------------------------------------------------ spatial + combine (forward)
+// SpatialWeights' second 1x1 conv + sigmoid (net_utils.py:79-83) fused with the rectification
+// (:147-152): per row, sw = sigmoid(relu(h) . w2 + b2) (saved for the backward), then
+//   out1 = x1 + 0.5*cw1*x2 + 0.5*sw1*x2 ;  out2 = x2 + 0.5*cw0*x1 + 0.5*sw0*x1
+template <typename T, int TPR>
+__global__ __launch_bounds__(256) void combine_fwd_kernel(const T* __restrict__ x, const float* __restrict__ cw,
+                                                          const T* __restrict__ h, const float* __restrict__ w2,
+                                                          const float* __restrict__ b2, float* __restrict__ sw,
+                                                          T* __restrict__ out, int B, int N, int C) {
+  constexpr int V = VecT<T>::N, RPB = 256 / TPR;
+  const int lane = threadIdx.x % TPR, slot = threadIdx.x / TPR;
+  const int nch = C / V;
+  const long rows = (long)B * N, per = rows * C;
+  float wa[MAXCH][V], wb[MAXCH][V];
+#pragma unroll
+  for (int k = 0; k < MAXCH; ++k)
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const int c = (lane + k * TPR) * V + j;
+      const bool ok = lane + k * TPR < nch;
+      wa[k][j] = ok ? w2[c] : 0.f;
+      wb[k][j] = ok ? w2[C + c] : 0.f;
     }
-  }
-}
-
-// sw[row][o] = sigmoid(sum_c relu(h[row][c]) w2[o][c] + b2[o]); 16 lanes per row
-template <typename T>
-__global__ void spatial_fwd_kernel(const T* __restrict__ h, const float* __restrict__ w2, const float* __restrict__ b2,
-                                   float* __restrict__ sw, long rows, int C) {
-  constexpr int V = VecT<T>::N;
-  const int lane = threadIdx.x & 15;
-  const long row = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
-  float s0 = 0.f, s1 = 0.f;
-  if (row < rows) {
-    for (int ch = lane; ch < C / V; ch += 16) {
+  for (long row = (long)blockIdx.x * RPB + slot; row < rows; row += (long)gridDim.x * RPB) {
+    const int b = (int)(row / N);
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXCH; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch >= nch) continue;
       float v[V];
       load_vec<T>(h + row * C + ch * V, v);
 #pragma unroll
       for (int j = 0; j < V; ++j) {
         const float r = v[j] > 0.f ? v[j] : 0.f;
-        s0 += r * w2[ch * V + j];
-        s1 += r * w2[C + ch * V + j];
+        s0 += r * wa[k][j];
+        s1 += r * wb[k][j];
       }
     }
-  }
-  s0 = group_sum(s0, 16);
-  s1 = group_sum(s1, 16);
-  if (row < rows && lane == 0) {
-    sw[row * 2] = 1.f / (1.f + __expf(-(s0 + b2[0])));
-    sw[row * 2 + 1] = 1.f / (1.f + __expf(-(s1 + b2[1])));
-  }
-}
-
-template <typename T>
-__global__ void combine_fwd_kernel(const T* __restrict__ x, const float* __restrict__ cw, const float* __restrict__ sw,
-                                   T* __restrict__ out, int B, int N, int C) {
-  constexpr int V = VecT<T>::N;
-  const long per = (long)B * N * C;
-  const long nvec = per / V;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)nvec; i += gridDim.x * blockDim.x) {
-    const int e = i * V;
-    const int c0 = e % C;
-    const int row = e / C;        // b*N + n
-    const int b = row / N;
-    float a[V], bb[V], o1[V], o2[V];
-    load_vec<T>(x + e, a);
-    load_vec<T>(x + per + e, bb);
-    const float s0 = 0.5f * sw[row * 2], s1 = 0.5f * sw[row * 2 + 1];
+    s0 = group_sum(s0, TPR);
+    s1 = group_sum(s1, TPR);
+    const float sw0 = 1.f / (1.f + __expf(-(s0 + b2[0]))), sw1 = 1.f / (1.f + __expf(-(s1 + b2[1])));
+    if (lane == 0) { sw[row * 2] = sw0; sw[row * 2 + 1] = sw1; }
+    const float h0 = 0.5f * sw0, h1 = 0.5f * sw1;
 #pragma unroll
-    for (int j = 0; j < V; ++j) {
-      const float c0w = 0.5f * cw[(long)b * 2 * C + c0 + j];
-      const float c1w = 0.5f * cw[(long)b * 2 * C + C + c0 + j];
-      o1[j] = (a[j] + c1w * bb[j]) + s1 * bb[j];
-      o2[j] = (bb[j] + c0w * a[j]) + s0 * a[j];
+    for (int k = 0; k < MAXCH; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch >= nch) continue;
+      const long e = row * C + ch * V;
+      float a[V], bb[V], o1[V], o2[V];
+      load_vec<T>(x + e, a);
+      load_vec<T>(x + per + e, bb);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const float c0w = 0.5f * cw[(long)b * 2 * C + ch * V + j];
+        const float c1w = 0.5f * cw[(long)b * 2 * C + C + ch * V + j];
+        o1[j] = (a[j] + c1w * bb[j]) + h1 * bb[j];
+        o2[j] = (bb[j] + c0w * a[j]) + h0 * a[j];
+      }
+      store_vec<T>(out + e, o1);
+      store_vec<T>(out + per + e, o2);
     }
-    store_vec<T>(out + e, o1);
-    store_vec<T>(out + per + e, o2);
   }
 }
 
-// direct-path dx, dsw (row sums) and per-block dcw partials.  blockIdx.y = b.
-// TPR lanes per row; ws (B, nblk, 2C) = [dcw0 | dcw1] partials.
-template <typename T, int TPR>
+// ------------------------------------------------------------------------ combine + spatial (backward)
+// Per row: the direct-path dx of the rectification; dsw (row sums); the spatial head's backward
+// dz2 = dsw * sw (1 - sw), dh = [h > 0] (dz2 . w2).  Per block (blockIdx = (slab, b)): partials
+// dcw (B, nblk, 2C) = [dcw0 | dcw1] and [dw2 (2C) | db2 (2)] (B * nblk, 2C + 2), combined over
+// the block's row slots in LDS (no atomics: deterministic).
+template <typename T, int TPR, int MCH>
 __global__ __launch_bounds__(256) void combine_bwd_kernel(const T* __restrict__ dout, const T* __restrict__ x,
                                                           const float* __restrict__ cw, const float* __restrict__ sw,
-                                                          T* __restrict__ dx, float* __restrict__ dsw,
-                                                          float* __restrict__ ws, int B, int N, int C) {
-  constexpr int V = VecT<T>::N;
-  constexpr int RPB = 256 / TPR;
-  constexpr int MAXCH = 4;  // chunks per lane (C <= 4 * TPR * V)
-  __shared__ float red[2][512];
-  const int b = blockIdx.y;
+                                                          const T* __restrict__ h, const float* __restrict__ w2,
+                                                          T* __restrict__ dx, T* __restrict__ dh,
+                                                          float* __restrict__ pcw, float* __restrict__ psp, int B,
+                                                          int N, int C) {
+  constexpr int V = VecT<T>::N, RPB = 256 / TPR, CMAX = MCH * TPR * V;
+  __shared__ float red[RPB][CMAX];
+  __shared__ float rdb[2][RPB];
+  const int b = blockIdx.y, nblk = gridDim.x;
   const int lane = threadIdx.x % TPR, slot = threadIdx.x / TPR;
   const int nch = C / V;
   const long per = (long)B * N * C;
-  float a0[MAXCH][V], a1[MAXCH][V];
+  float a0[MCH][V], a1[MCH][V], p0[MCH][V], p1[MCH][V];
 #pragma unroll
-  for (int k = 0; k < MAXCH; ++k)
+  for (int k = 0; k < MCH; ++k)
 #pragma unroll
-    for (int j = 0; j < V; ++j) a0[k][j] = a1[k][j] = 0.f;
-  for (int n = blockIdx.x * RPB + slot; n < N; n += gridDim.x * RPB) {
+    for (int j = 0; j < V; ++j) a0[k][j] = a1[k][j] = p0[k][j] = p1[k][j] = 0.f;
+  float db0 = 0.f, db1 = 0.f;
+  // per-channel constants of this block's image (blockIdx.y = b), loaded once
+  float c0h[MCH][V], c1h[MCH][V], wa[MCH][V], wb[MCH][V];
+#pragma unroll
+  for (int k = 0; k < MCH; ++k)
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const int c = (lane + k * TPR) * V + j;
+      const bool ok = lane + k * TPR < nch;
+      c0h[k][j] = ok ? 0.5f * cw[(long)b * 2 * C + c] : 0.f;
+      c1h[k][j] = ok ? 0.5f * cw[(long)b * 2 * C + C + c] : 0.f;
+      wa[k][j] = ok ? w2[c] : 0.f;
+      wb[k][j] = ok ? w2[C + c] : 0.f;
+    }
+  for (int n = blockIdx.x * RPB + slot; n < N; n += nblk * RPB) {
     const long row = (long)b * N + n;
-    const float s0 = 0.5f * sw[row * 2], s1 = 0.5f * sw[row * 2 + 1];
+    const float sw0 = sw[row * 2], sw1 = sw[row * 2 + 1];
+    const float s0 = 0.5f * sw0, s1 = 0.5f * sw1;
     float r0 = 0.f, r1 = 0.f;
 #pragma unroll
-    for (int k = 0; k < MAXCH; ++k) {
+    for (int k = 0; k < MCH; ++k) {
       const int ch = lane + k * TPR;
       if (ch >= nch) continue;
       const long e = row * C + ch * V;
@@ -239,127 +384,148 @@ __global__ __launch_bounds__(256) void combine_bwd_kernel(const T* __restrict__ 
       load_vec<T>(x + per + e, x2);
 #pragma unroll
       for (int j = 0; j < V; ++j) {
-        const int c = ch * V + j;
-        const float c0w = 0.5f * cw[(long)b * 2 * C + c];
-        const float c1w = 0.5f * cw[(long)b * 2 * C + C + c];
+        const float c0w = c0h[k][j], c1w = c1h[k][j];
         o1[j] = d1[j] + (c0w + s0) * d2[j];
         o2[j] = d2[j] + (c1w + s1) * d1[j];
-        const float p1 = d1[j] * x2[j];   // feeds dcw1, dsw1
-        const float p0 = d2[j] * x1[j];   // feeds dcw0, dsw0
-        r1 += p1; r0 += p0;
-        a1[k][j] += p1; a0[k][j] += p0;
+        const float q1 = d1[j] * x2[j];   // feeds dcw1, dsw1
+        const float q0 = d2[j] * x1[j];   // feeds dcw0, dsw0
+        r1 += q1; r0 += q0;
+        a1[k][j] += q1; a0[k][j] += q0;
       }
       store_vec<T>(dx + e, o1);
       store_vec<T>(dx + per + e, o2);
     }
     r0 = group_sum(r0, TPR);
     r1 = group_sum(r1, TPR);
-    if (lane == 0) { dsw[row * 2] = 0.5f * r0; dsw[row * 2 + 1] = 0.5f * r1; }
+    const float g0 = 0.5f * r0 * sw0 * (1.f - sw0), g1 = 0.5f * r1 * sw1 * (1.f - sw1);
+    if (lane == 0) { db0 += g0; db1 += g1; }
+#pragma unroll
+    for (int k = 0; k < MCH; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch >= nch) continue;
+      const long e = row * C + ch * V;
+      float v[V], o[V];
+      load_vec<T>(h + e, v);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const bool pos = v[j] > 0.f;
+        o[j] = pos ? g0 * wa[k][j] + g1 * wb[k][j] : 0.f;
+        const float r = pos ? v[j] : 0.f;
+        p0[k][j] += g0 * r;
+        p1[k][j] += g1 * r;
+      }
+      store_vec<T>(dh + e, o);
+    }
   }
-  // reduce column partials over row slots, 512 columns at a time
-  float* out = ws + ((long)b * gridDim.x + blockIdx.x) * 2 * C;
-  for (int base = 0; base < C; base += 512) {
-    for (int e = threadIdx.x; e < 2 * 512; e += 256) (&red[0][0])[e] = 0.f;
+  // slot-combine the four per-channel partials, one quantity at a time through LDS
+  float* outc = pcw + ((long)b * nblk + blockIdx.x) * 2 * C;
+  float* outs = psp + ((long)b * nblk + blockIdx.x) * (2 * C + 2);
+  for (int qn = 0; qn < 4; ++qn) {
+#pragma unroll
+    for (int k = 0; k < MCH; ++k)
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int c = (lane + k * TPR) * V + j;
+        const float v = qn == 0 ? a0[k][j] : qn == 1 ? a1[k][j] : qn == 2 ? p0[k][j] : p1[k][j];
+        if (c < C) red[slot][c] = v;
+      }
     __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256) {
+      float t = 0.f;
+      for (int q = 0; q < RPB; ++q) t += red[q][c];
+      if (qn < 2) outc[qn * C + c] = 0.5f * t;
+      else outs[(qn - 2) * C + c] = t;
+    }
+    __syncthreads();
+  }
+  if (lane == 0) { rdb[0][slot] = db0; rdb[1][slot] = db1; }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    float t = 0.f;
+    for (int q = 0; q < RPB; ++q) t += rdb[threadIdx.x][q];
+    outs[2 * C + threadIdx.x] = t;
+  }
+}
+
+// ------------------------------------------------------------------------ pooling (backward)
+// dx[g][b][n][c] += dpooled_avg[b][gC+c] / N + (n == argmax[b][gC+c]) * dpooled_max[b][2C+gC+c];
+// dpooled arrives as partial slices dp[b][k] = sum_s part[s*ss + b*sm + k].
+template <typename T, int TPR>
+__global__ __launch_bounds__(256) void pool_bwd_kernel(const float* __restrict__ part, int nsl, long ss, long sm,
+                                                       const int* __restrict__ argmax, T* __restrict__ dx, int B,
+                                                       int N, int C) {
+  constexpr int V = VecT<T>::N, RPB = 256 / TPR;
+  __shared__ float sdp[2 * 1024];                 // [avg | max] gradient of this (g, b), C <= 1024
+  const int gb = blockIdx.y, g = gb / B, b = gb % B;
+  const int lane = threadIdx.x % TPR, slot = threadIdx.x / TPR;
+  const int nch = C / V;
+  // the block's 2C dpooled values, each summed over the nsl partial slices, once per block
+  for (int e = threadIdx.x; e < 2 * C; e += 256) {
+    const int k = e < C ? g * C + e : 2 * C + g * C + (e - C);
+    const float* p = part + b * sm + k;
+    float t = 0.f;
+    for (int q = 0; q < nsl; ++q) t += p[q * ss];
+    sdp[e] = e < C ? t / N : t;
+  }
+  __syncthreads();
+  float dav[MAXCH][V], dmx[MAXCH][V];
+  int am[MAXCH][V];
+#pragma unroll
+  for (int k = 0; k < MAXCH; ++k)
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const int c = (lane + k * TPR) * V + j;
+      const bool ok = lane + k * TPR < nch;
+      dav[k][j] = ok ? sdp[c] : 0.f;
+      dmx[k][j] = ok ? sdp[C + c] : 0.f;
+      am[k][j] = ok ? argmax[(long)b * 2 * C + g * C + c] : -1;
+    }
+  T* base = dx + (long)gb * N * C;
+  for (int n = blockIdx.x * RPB + slot; n < N; n += gridDim.x * RPB) {
 #pragma unroll
     for (int k = 0; k < MAXCH; ++k) {
       const int ch = lane + k * TPR;
+      if (ch >= nch) continue;
+      float v[V];
+      T* p = base + (long)n * C + ch * V;
+      load_vec<T>(p, v);
 #pragma unroll
-      for (int j = 0; j < V; ++j) {
-        const int c = ch * V + j - base;
-        if (ch < nch && c >= 0 && c < 512) {
-          atomicAdd(&red[0][c], a0[k][j]);
-          atomicAdd(&red[1][c], a1[k][j]);
-        }
-      }
+      for (int j = 0; j < V; ++j) v[j] += dav[k][j] + (am[k][j] == n ? dmx[k][j] : 0.f);
+      store_vec<T>(p, v);
     }
-    __syncthreads();
-    for (int c = threadIdx.x; c < 512 && base + c < C; c += 256) {
-      out[base + c] = 0.5f * red[0][c];
-      out[C + base + c] = 0.5f * red[1][c];
-    }
-    __syncthreads();
-  }
-}
-
-// spatial backward: dz2 = dsw * sw(1-sw); dh = [h>0] * (dz2 @ w2); partials of
-// dw2 (2, C) = sum dz2^T relu(h) and db2 (2) into ws (nblk, 2C + 2).  16 lanes per row.
-template <typename T>
-__global__ __launch_bounds__(256) void spatial_bwd_kernel(const float* __restrict__ dsw, const float* __restrict__ sw,
-                                                          const T* __restrict__ h, const float* __restrict__ w2,
-                                                          T* __restrict__ dh, float* __restrict__ ws, long rows, int C) {
-  constexpr int V = VecT<T>::N;
-  __shared__ float red[2 * 512 + 2];
-  for (int e = threadIdx.x; e < 2 * C + 2; e += 256) red[e] = 0.f;
-  __syncthreads();
-  const int lane = threadIdx.x & 15;
-  float db0 = 0.f, db1 = 0.f;
-  for (long row = (long)blockIdx.x * 16 + (threadIdx.x >> 4); row < rows; row += (long)gridDim.x * 16) {
-    const float g0 = dsw[row * 2] * sw[row * 2] * (1.f - sw[row * 2]);
-    const float g1 = dsw[row * 2 + 1] * sw[row * 2 + 1] * (1.f - sw[row * 2 + 1]);
-    if (lane == 0) { db0 += g0; db1 += g1; }
-    for (int ch = lane; ch < C / V; ch += 16) {
-      float v[V], o[V];
-      load_vec<T>(h + row * C + ch * V, v);
-#pragma unroll
-      for (int j = 0; j < V; ++j) {
-        const int c = ch * V + j;
-        const bool pos = v[j] > 0.f;
-        o[j] = pos ? g0 * w2[c] + g1 * w2[C + c] : 0.f;
-        const float r = pos ? v[j] : 0.f;
-        atomicAdd(&red[c], g0 * r);
-        atomicAdd(&red[C + c], g1 * r);
-      }
-      store_vec<T>(dh + row * C + ch * V, o);
-    }
-  }
-  if (lane == 0) { atomicAdd(&red[2 * C], db0); atomicAdd(&red[2 * C + 1], db1); }
-  __syncthreads();
-  for (int e = threadIdx.x; e < 2 * C + 2; e += 256) ws[(long)blockIdx.x * (2 * C + 2) + e] = red[e];
-}
-
-// dx[g][b][n][c] += dpooled_avg[b][gC+c] / N + (n == argmax[b][gC+c]) * dpooled_max[b][2C+gC+c]
-template <typename T>
-__global__ void pool_bwd_kernel(const float* __restrict__ dpooled, const int* __restrict__ argmax, T* __restrict__ dx,
-                                int B, int N, int C) {
-  const long total = 2L * B * N * C;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)total; i += gridDim.x * blockDim.x) {
-    const int c = i % C;
-    const int n = (i / C) % N;
-    const int gb = i / (C * N);
-    const int g = gb / B, b = gb % B;
-    float v = dpooled[(long)b * 4 * C + g * C + c] / N;
-    if (argmax[(long)b * 2 * C + g * C + c] == n) v += dpooled[(long)b * 4 * C + 2 * C + g * C + c];
-    dx[i] = from_f32<T>(to_f32(dx[i]) + v);
   }
 }
 
 int pool_nchunk(int N, int GB) {
-  long nc = (1024 + GB - 1) / GB;
-  const long maxc = (N + 63) / 64;
+  long nc = (512 + GB - 1) / GB;
+  const long maxc = (N + 15) / 16;
   if (nc > maxc) nc = maxc;
   return nc < 1 ? 1 : (int)nc;
 }
-unsigned gridcap(long total) {
-  const unsigned g = cdiv(total, 256);
-  return g < 8192 ? (g ? g : 1) : 8192;
-}
-int combine_nblk(int N, int rpb) {              // <= 256 blocks per image (partials reduced after)
+int combine_nblk(int N, int C, int V) {        // blocks per image of the backward (<= 256: its partials are
+  const int rpb = 256 / row_lanes(C, V);       // summed by the channel-MLP backward's prologue)
   int nb = (N + rpb - 1) / rpb;
   return nb < 256 ? nb : 256;
 }
-int spatial_nblk(long rows) {
-  long nb = (rows + 15) / 16;
-  return (int)(nb < 256 ? nb : 256);
+unsigned rows_grid(long rows, int rpb) {
+  const long g = (rows + rpb - 1) / rpb;
+  return (unsigned)(g < 4096 ? (g > 0 ? g : 1) : 4096);
 }
+
+#define FRM_TPR_DISPATCH(tpr, TPR, ...)                   \
+  do {                                                    \
+    switch (tpr) {                                        \
+      case 4: { constexpr int TPR = 4; __VA_ARGS__; break; }   \
+      case 8: { constexpr int TPR = 8; __VA_ARGS__; break; }   \
+      case 16: { constexpr int TPR = 16; __VA_ARGS__; break; } \
+      case 32: { constexpr int TPR = 32; __VA_ARGS__; break; } \
+      default: { constexpr int TPR = 64; __VA_ARGS__; break; } \
+    }                                                     \
+  } while (0)
+
 }  // namespace
 
 extern "C" {
-
-// dz_ws of cmx_small_linear_bwd: M*Nout + 16*M*K floats
-size_t cmx_small_linear_bwd_workspace(int M, int K, int Nout) {
-  return ((size_t)M * Nout + (size_t)DX_NSLICE * M * K) * sizeof(float);
-}
 
 size_t cmx_frm_pool_workspace(int B, int N, int C) {
   const int nc = pool_nchunk(N, 2 * B);
@@ -368,123 +534,108 @@ size_t cmx_frm_pool_workspace(int B, int N, int C) {
 
 int cmx_frm_pool_fwd(const void* x, float* pooled, int* argmax, float* workspace, int B, int N, int C, int dtype,
                      hipStream_t s) {
-  CMX_REQUIRE(B > 0 && N > 0 && C > 0, CMX_ERR_SHAPE, "frm_pool: shape");
+  const int V = dtype == 0 ? 4 : 8;
+  CMX_REQUIRE(B > 0 && N > 0 && C > 0 && C % V == 0 && C / V <= MAXCH * 64, CMX_ERR_SHAPE, "frm_pool: B=%d N=%d C=%d",
+              B, N, C);
   const int nc = pool_nchunk(N, 2 * B);
   const int chunk = (N + nc - 1) / nc;
   float* psum = workspace;
   float* pmax = psum + (size_t)2 * B * nc * C;
   int* pidx = (int*)(pmax + (size_t)2 * B * nc * C);
+  const int tpr = row_lanes(C, V);
   CMX_DISPATCH(dtype, T, {
-    hipLaunchKernelGGL(pool_partial_kernel<T>, dim3(nc, 2 * B), dim3(C < 256 ? 64 * ((C + 63) / 64) : 256), 0, s,
-                       (const T*)x, psum, pmax, pidx, B, N, C, chunk);
+    FRM_TPR_DISPATCH(tpr, TPR, hipLaunchKernelGGL((pool_partial_kernel<T, TPR>), dim3(nc, 2 * B), dim3(256), 0, s,
+                                                  (const T*)x, psum, pmax, pidx, B, N, C, chunk));
   });
   hipLaunchKernelGGL(pool_final_kernel, dim3(cdiv(C, 64), 2 * B), dim3(256), 0, s, psum, pmax, pidx, pooled, argmax,
                      B, N, C, nc);
   return cmx_check_launch("frm_pool_fwd");
 }
 
-int cmx_frm_pool_bwd(const float* dpooled, const int* argmax, void* dx, int B, int N, int C, int dtype, hipStream_t s) {
+int cmx_frm_pool_bwd(const float* dpooled_part, int nslice, int64_t slice_stride, const int* argmax, void* dx, int B,
+                     int N, int C, int dtype, hipStream_t s) {
+  const int V = dtype == 0 ? 4 : 8;
+  CMX_REQUIRE(C % V == 0 && C / V <= MAXCH * 64 && C <= 1024 && nslice > 0, CMX_ERR_SHAPE, "frm_pool_bwd: C=%d", C);
+  const int tpr = row_lanes(C, V);
+  const int rpb = 256 / tpr;
+  long nb = (N + rpb - 1) / rpb;
+  const long want = (512 + 2 * B - 1) / (2 * B);
+  if (nb > want) nb = want;
   CMX_DISPATCH(dtype, T, {
-    hipLaunchKernelGGL(pool_bwd_kernel<T>, dim3(gridcap(2L * B * N * C)), dim3(256), 0, s, dpooled, argmax, (T*)dx,
-                       B, N, C);
+    FRM_TPR_DISPATCH(tpr, TPR, hipLaunchKernelGGL((pool_bwd_kernel<T, TPR>), dim3((unsigned)nb, 2 * B), dim3(256), 0,
+                                                  s, dpooled_part, nslice, (long)slice_stride, (long)4 * C, argmax,
+                                                  (T*)dx, B, N, C));
   });
   return cmx_check_launch("frm_pool_bwd");
 }
 
 int cmx_small_linear_fwd(const float* x, const float* w, const float* b, float* y, int M, int K, int Nout, int act,
                          hipStream_t s) {
-  hipLaunchKernelGGL(small_linear_fwd_kernel, dim3(cdiv((long)Nout * 64, 256)), dim3(256), 0, s, x, w, b, y, M, K,
+  CMX_REQUIRE(M > 0 && M <= MMAX && K % 4 == 0 && (long)M * K * 4 <= 64 * 1024 && ((uintptr_t)w & 15) == 0 &&
+              ((uintptr_t)x & 15) == 0, CMX_ERR_SHAPE, "small_linear_fwd: M=%d K=%d", M, K);
+  const unsigned grid = cdiv(Nout, 4 * LIN_FPW);
+  hipLaunchKernelGGL(linear_fwd_kernel, dim3(grid), dim3(256), (size_t)M * K * sizeof(float), s, x, w, b, y, M, K,
                      Nout, act);
   return cmx_check_launch("small_linear_fwd");
 }
 
-// dz_ws: M*Nout floats; dx may be NULL
-int cmx_small_linear_bwd(const float* dy, const float* y, const float* x, const float* w, float* dx, float* dw,
-                         float* db, float* dz_ws, int M, int K, int Nout, int act, int accumulate, hipStream_t s) {
-  hipLaunchKernelGGL(small_linear_dz_kernel, dim3(gridcap((long)M * Nout)), dim3(256), 0, s, dy, y, dz_ws,
-                     (long)M * Nout, act);
-  CMX_REQUIRE(M <= DX_MMAX, CMX_ERR_SHAPE, "small_linear_bwd: M=%d > %d", M, DX_MMAX);
-  if (dx) {
-    float* part = dz_ws + (size_t)M * Nout;   // DX_NSLICE * M * K floats after dz
-    hipLaunchKernelGGL(small_linear_dx_kernel, dim3(cdiv(K, 64), DX_NSLICE), dim3(256), 0, s, dz_ws, w, part, M, K,
-                       Nout);
-    const int st = cmx_reduce_partials(part, dx, 1, DX_NSLICE, M * K, 0, 1.f, s);
-    if (st) return st;
-  }
-  hipLaunchKernelGGL(small_linear_dw_kernel, dim3(gridcap((long)Nout * K)), dim3(256), 0, s, dz_ws, x, dw, db, M, K,
-                     Nout, accumulate);
+int cmx_small_linear_nslice(void) { return NSLICE; }
+
+size_t cmx_small_linear_bwd_workspace(int M, int K, int Nout) { return (size_t)NSLICE * M * K * sizeof(float); }
+
+int cmx_small_linear_bwd(const float* dy_part, int dy_nslice, int64_t dy_slice_stride, int64_t dy_row_stride,
+                         const float* y, const float* x, const float* w, float* dx_part, float* dw, float* db, int M,
+                         int K, int Nout, int act, int accumulate, hipStream_t s) {
+  CMX_REQUIRE(M > 0 && M <= MMAX && dy_nslice > 0 && (Nout + NSLICE - 1) / NSLICE <= SLICE_MAX, CMX_ERR_SHAPE,
+              "small_linear_bwd: M=%d Nout=%d", M, Nout);
+  hipLaunchKernelGGL(linear_bwd_kernel, dim3(cdiv(K, 64), NSLICE), dim3(256), 0, s, dy_part, dy_nslice,
+                     (long)dy_slice_stride, (long)dy_row_stride, y, x, w, dx_part, dw, db, M, K, Nout, act,
+                     accumulate);
   return cmx_check_launch("small_linear_bwd");
 }
 
-int cmx_frm_spatial_fwd(const void* h, const float* w2, const float* b2, float* sw, int64_t rows, int C, int dtype,
-                        hipStream_t s) {
-  CMX_REQUIRE(C % 8 == 0, CMX_ERR_SHAPE, "frm_spatial: C");
-  CMX_DISPATCH(dtype, T, {
-    hipLaunchKernelGGL(spatial_fwd_kernel<T>, dim3(cdiv(rows, 16)), dim3(256), 0, s, (const T*)h, w2, b2, sw,
-                       (long)rows, C);
-  });
-  return cmx_check_launch("frm_spatial_fwd");
-}
-
-size_t cmx_frm_spatial_bwd_workspace(int64_t rows, int C) {
-  return (size_t)spatial_nblk(rows) * (2 * C + 2) * sizeof(float);
-}
-
-// dw2 (2, C), db2 (2) fp32 written (or accumulated)
-int cmx_frm_spatial_bwd(const float* dsw, const float* sw, const void* h, const float* w2, void* dh, float* dw2,
-                        float* db2, float* workspace, int64_t rows, int C, int accumulate, int dtype, hipStream_t s) {
-  CMX_REQUIRE(C % 8 == 0 && C <= 512, CMX_ERR_SHAPE, "frm_spatial_bwd: C");
-  const int nb = spatial_nblk(rows);
-  CMX_DISPATCH(dtype, T, {
-    hipLaunchKernelGGL(spatial_bwd_kernel<T>, dim3(nb), dim3(256), 0, s, dsw, sw, (const T*)h, w2, (T*)dh, workspace,
-                       (long)rows, C);
-  });
-  int st = cmx_check_launch("frm_spatial_bwd");
-  if (st) return st;
-  st = cmx_reduce_partials_strided(workspace, dw2, nb, 2 * C, 2 * C + 2, accumulate, s);
-  if (st) return st;
-  return cmx_reduce_partials_strided(workspace + 2 * C, db2, nb, 2, 2 * C + 2, accumulate, s);
-}
-
-int cmx_frm_combine_fwd(const void* x, const float* cw, const float* sw, void* out, int B, int N, int C, int dtype,
-                        hipStream_t s) {
+int cmx_frm_combine_fwd(const void* x, const float* cw, const void* h, const float* w2, const float* b2, float* sw,
+                        void* out, int B, int N, int C, int dtype, hipStream_t s) {
   const int V = dtype == 0 ? 4 : 8;
-  CMX_REQUIRE(C % V == 0, CMX_ERR_SHAPE, "frm_combine: C");
+  CMX_REQUIRE(C % V == 0 && C / V <= MAXCH * 64, CMX_ERR_SHAPE, "frm_combine: C=%d", C);
+  const int tpr = row_lanes(C, V);
+  const unsigned grid = rows_grid((long)B * N, 256 / tpr);
   CMX_DISPATCH(dtype, T, {
-    hipLaunchKernelGGL(combine_fwd_kernel<T>, dim3(gridcap((long)B * N * C / V)), dim3(256), 0, s, (const T*)x, cw, sw,
-                       (T*)out, B, N, C);
+    FRM_TPR_DISPATCH(tpr, TPR, hipLaunchKernelGGL((combine_fwd_kernel<T, TPR>), dim3(grid), dim3(256), 0, s,
+                                                  (const T*)x, cw, (const T*)h, w2, b2, sw, (T*)out, B, N, C));
   });
   return cmx_check_launch("frm_combine_fwd");
 }
 
-size_t cmx_frm_combine_bwd_workspace(int B, int N, int C) {
-  return (size_t)B * combine_nblk(N, 16) * 2 * C * sizeof(float);
+int cmx_frm_combine_bwd_nblk(int N, int C, int dtype) { return combine_nblk(N, C, dtype == 0 ? 4 : 8); }
+
+size_t cmx_frm_combine_bwd_workspace(int B, int N, int C, int dtype) {
+  const int nb = combine_nblk(N, C, dtype == 0 ? 4 : 8);
+  return ((size_t)B * nb * 2 * C + (size_t)B * nb * (2 * C + 2)) * sizeof(float);
 }
 
-// dx (2,B,N,C) direct path; dsw (B,N,2); dcw (B, 2C) = [dcw0 | dcw1] (overwritten)
-int cmx_frm_combine_bwd(const void* dout, const void* x, const float* cw, const float* sw, void* dx, float* dsw,
-                        float* dcw, float* workspace, int B, int N, int C, int dtype, hipStream_t s) {
+// dx (2,B,N,C) direct path, dh (B*N, C); workspace: dcw partials (B, nblk, 2C) then the
+// [dw2 | db2] partials (B * nblk, 2C + 2)
+int cmx_frm_combine_bwd(const void* dout, const void* x, const float* cw, const float* sw, const void* h,
+                        const float* w2, void* dx, void* dh, float* workspace, int B, int N, int C, int dtype,
+                        hipStream_t s) {
   const int V = dtype == 0 ? 4 : 8;
-  CMX_REQUIRE(C % V == 0 && C / V <= 4 * 64, CMX_ERR_SHAPE, "frm_combine_bwd: C=%d", C);
-  const int nb = combine_nblk(N, 16);
-  // lanes per row = the row's 16-B chunks rounded up to a power of two (C = 64 bf16: 8 lanes,
-  // 32 rows per block in flight), capped at a wave
-  const int chunks = C / V;
-  int tpr = 4;
-  while (tpr < chunks && tpr < 64) tpr <<= 1;
-#define CMB(TPR) hipLaunchKernelGGL((combine_bwd_kernel<T, TPR>), dim3(nb, B), dim3(256), 0, s, (const T*)dout, \
-                                    (const T*)x, cw, sw, (T*)dx, dsw, workspace, B, N, C)
+  CMX_REQUIRE(C % V == 0 && C / V <= MAXCH * 64, CMX_ERR_SHAPE, "frm_combine_bwd: C=%d", C);
+  const int nb = combine_nblk(N, C, V);
+  const int tpr = row_lanes(C, V);
+  float* pcw = workspace;
+  float* psp = workspace + (size_t)B * nb * 2 * C;
+  // chunks per lane: 1 unless the row has more than 64 chunks (fp32 with C > 256); the
+  // one-chunk instantiation keeps the per-channel accumulators at half the registers
+#define CMX_CB(MCH_) FRM_TPR_DISPATCH(tpr, TPR, hipLaunchKernelGGL((combine_bwd_kernel<T, TPR, MCH_>), dim3(nb, B), \
+                                                  dim3(256), 0, s, (const T*)dout, (const T*)x, cw, sw, (const T*)h, \
+                                                  w2, (T*)dx, (T*)dh, pcw, psp, B, N, C))
   CMX_DISPATCH(dtype, T, {
-    if (tpr == 4) CMB(4);
-    else if (tpr == 8) CMB(8);
-    else if (tpr == 16) CMB(16);
-    else if (tpr == 32) CMB(32);
-    else CMB(64);
+    if (C / V <= tpr) CMX_CB(1);
+    else CMX_CB(2);
   });
-#undef CMB
-  int st = cmx_check_launch("frm_combine_bwd");
-  if (st) return st;
-  return cmx_reduce_partials(workspace, dcw, B, nb, 2 * C, 0, 1.f, s);
+#undef CMX_CB
+  return cmx_check_launch("frm_combine_bwd");
 }
 
 }  // extern "C"

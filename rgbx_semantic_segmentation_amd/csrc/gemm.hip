@@ -96,12 +96,13 @@ __device__ __forceinline__ float up_add1(const GemmArgs& p, int i, int j) {
   float v = 0.f;
 #pragma unroll
   for (int s = 0; s < 3; ++s) {
-    if (s >= p.nup) break;
-    const UpTaps t = up_taps(p, s, i);
-    const T* u = reinterpret_cast<const T*>(p.up[s]) + j;
-    const long ld = p.N;
-    v += t.w00 * to_f32(u[t.r00 * ld]) + t.w01 * to_f32(u[t.r01 * ld]) + t.w10 * to_f32(u[t.r10 * ld]) +
-         t.w11 * to_f32(u[t.r11 * ld]);
+    if (s < p.nup) {
+      const UpTaps t = up_taps(p, s, i);
+      const T* u = reinterpret_cast<const T*>(p.up[s]) + j;
+      const long ld = p.N;
+      v += t.w00 * to_f32(u[t.r00 * ld]) + t.w01 * to_f32(u[t.r01 * ld]) + t.w10 * to_f32(u[t.r10 * ld]) +
+           t.w11 * to_f32(u[t.r11 * ld]);
+    }
   }
   return v;
 }
@@ -111,7 +112,7 @@ template <typename T>
 __device__ __forceinline__ void up_add8(const GemmArgs& p, int i, int j, float* v) {
 #pragma unroll
   for (int s = 0; s < 3; ++s) {
-    if (s >= p.nup) break;
+    if (s >= p.nup) continue;
     const UpTaps t = up_taps(p, s, i);
     const T* u = reinterpret_cast<const T*>(p.up[s]) + j;
     const long ld = p.N;

@@ -497,7 +497,16 @@ class CrossAttentionF(Function):
 
 # ---------------------------------------------------------------------------- FRM
 class FRMF(Function):
-    """FeatureRectifyModule (net_utils.py:124-152) on x (2, B, N, C)."""
+    """FeatureRectifyModule (net_utils.py:124-152) on x (2, B, N, C).
+
+    Forward (6 launches): avg || max pooling (partial + final), the two-layer channel MLP
+    (ChannelWeights, :16-30), the SpatialWeights 2C -> C 1x1 conv as a cat-free GEMM, and ONE
+    kernel for SpatialWeights' C -> 2 conv + sigmoid fused with the rectification.
+    Backward (7 launches): one kernel for the rectification + spatial-head backward (dx direct
+    path, dh, dcw / dw2 partials), one G = 2 dgrad GEMM adding both modality slices of the 2C -> C
+    conv into dx, the dcw partial sum, the channel MLP backward as one pass over each weight
+    matrix (dz formed from the producer's partial slices, dW / db written, dx left as partial
+    slices), and the pooling backward summing those slices itself."""
 
     @staticmethod
     def forward(ctx, x, prm, anchor):
@@ -517,9 +526,9 @@ class FRMF(Function):
         K.gemm(x[0].view(1, B * N, C), W0[None], h, bias=b0[None], A2=x[1].view(1, B * N, C))
         h = h[0]
         sw = torch.empty(B * N, 2, dtype=torch.float32, device=x.device)
-        K.call("cmx_frm_spatial_fwd", K.ptr(h), K.ptr(w2s), K.ptr(b2s), K.ptr(sw), B * N, C, dt, K.stream())
         out = torch.empty_like(x)
-        K.call("cmx_frm_combine_fwd", K.ptr(x), K.ptr(cw), K.ptr(sw), K.ptr(out), B, N, C, dt, K.stream())
+        K.call("cmx_frm_combine_fwd", K.ptr(x), K.ptr(cw), K.ptr(h), K.ptr(w2s), K.ptr(b2s), K.ptr(sw), K.ptr(out), B,
+               N, C, dt, K.stream())
         ctx.save_for_backward(x, pooled, argmax, y1, cw, h, sw)
         ctx.prm = prm
         return out
@@ -529,34 +538,40 @@ class FRMF(Function):
         x, pooled, argmax, y1, cw, h, sw = ctx.saved_tensors
         (W1, b1, W2, b2, W0, b0, w2s, b2s) = ctx.prm["w"]
         (gW1, gb1, gW2, gb2, gW0, gb0, gw2s, gb2s) = ctx.prm["g"]
-        W1f, W2f, w2sf = ctx.prm["w32"]
         G, B, N, C = x.shape
         dt = K.dtype_code(x)
         dout = _c(dout)
         dx = torch.empty_like(x)
-        dsw = torch.empty(B * N, 2, dtype=torch.float32, device=x.device)
-        dcw = torch.empty(B, 2 * C, dtype=torch.float32, device=x.device)
-        ws = K._ws(K.query("cmx_frm_combine_bwd_workspace", B, N, C), x.device)
-        K.call("cmx_frm_combine_bwd", K.ptr(dout), K.ptr(x), K.ptr(cw), K.ptr(sw), K.ptr(dx), K.ptr(dsw), K.ptr(dcw),
-               K.ptr(ws), B, N, C, dt, K.stream())
         dh = torch.empty_like(h)
-        ws2 = K._ws(K.query("cmx_frm_spatial_bwd_workspace", B * N, C), x.device)
-        K.call("cmx_frm_spatial_bwd", K.ptr(dsw), K.ptr(sw), K.ptr(h), K.ptr(w2sf), K.ptr(dh), K.ptr(gw2s),
-               K.ptr(gb2s), K.ptr(ws2), B * N, C, 0, dt, K.stream())
-        for i in range(2):          # dx_i += dh @ W0[:, iC:(i+1)C] (residual epilogue, in place)
-            dxi = dx[i].view(1, B * N, C)
-            K.gemm(dh[None], W0[None, :, i * C:(i + 1) * C].transpose(1, 2), dxi, residual=dxi)
+        nb = K.query("cmx_frm_combine_bwd_nblk", N, C, dt)
+        ws = K._ws(K.query("cmx_frm_combine_bwd_workspace", B, N, C, dt), x.device)
+        K.call("cmx_frm_combine_bwd", K.ptr(dout), K.ptr(x), K.ptr(cw), K.ptr(sw), K.ptr(h), K.ptr(w2s), K.ptr(dx),
+               K.ptr(dh), K.ptr(ws), B, N, C, dt, K.stream())
+        psp = ws[B * nb * 2 * C:B * nb * 2 * C + B * nb * (2 * C + 2)]
+        if deferred.ENABLED:          # [dw2 | db2] partials: weight gradients, summed by the grouped reduce
+            deferred.reduce(psp, gw2s, gb2s, 1, B * nb, 0, 2 * C + 2, 1, 2 * C + 2, 2 * C, 0, 0, 0, 0)
+        else:
+            tmp = torch.empty(2 * C + 2, dtype=torch.float32, device=x.device)
+            K.call("cmx_partials_sum", K.ptr(psp), K.ptr(tmp), 1, B * nb, 2 * C + 2, 0, 1.0, K.stream())
+            gw2s.view(-1).copy_(tmp[:2 * C])
+            gb2s.view(-1).copy_(tmp[2 * C:])
+        # dx_g += dh @ W0[:, gC:(g+1)C] for both modalities in one launch (A = dh for both groups)
+        Wd = W0.view(C, 2, C).permute(1, 0, 2)                          # (2, C_out, C_in), strides (C, 2C, 1)
+        dx2 = dx.view(2, B * N, C)
+        K.gemm(dh[None].expand(2, B * N, C), Wd.transpose(1, 2), dx2, residual=dx2)
         _wgrad_into(dh[None], x[0].view(1, B * N, C), gW0[None, :, :C], gb0.view(1, C))
         _wgrad_into(dh[None], x[1].view(1, B * N, C), gW0[None, :, C:])
-        # channel MLP backward (sigmoid then relu), then pooling backward
-        dz = K._ws(K.query("cmx_small_linear_bwd_workspace", B, 4 * C, 4 * C), x.device)
-        dy1 = torch.empty(B, 4 * C, dtype=torch.float32, device=x.device)
-        K.call("cmx_small_linear_bwd", K.ptr(dcw), K.ptr(cw), K.ptr(y1), K.ptr(W2f), K.ptr(dy1), K.ptr(gW2),
-               K.ptr(gb2), K.ptr(dz), B, 4 * C, 2 * C, 3, 0, K.stream())
-        dpooled = torch.empty(B, 4 * C, dtype=torch.float32, device=x.device)
-        K.call("cmx_small_linear_bwd", K.ptr(dy1), K.ptr(y1), K.ptr(pooled), K.ptr(W1f), K.ptr(dpooled), K.ptr(gW1),
-               K.ptr(gb1), K.ptr(dz), B, 4 * C, 4 * C, 2, 0, K.stream())
-        K.call("cmx_frm_pool_bwd", K.ptr(dpooled), K.ptr(argmax), K.ptr(dx), B, N, C, dt, K.stream())
+        # channel MLP backward: dcw partial slabs (B, nb, 2C) -> W2 pass -> W1 pass -> pooling
+        ns = K.query("cmx_small_linear_nslice")
+        dcw = torch.empty(B, 2 * C, dtype=torch.float32, device=x.device)      # sum of the nb partial slabs
+        K.call("cmx_partials_sum", K.ptr(ws), K.ptr(dcw), B, nb, 2 * C, 0, 1.0, K.stream())
+        dy1p = torch.empty(ns, B, 4 * C, dtype=torch.float32, device=x.device)
+        K.call("cmx_small_linear_bwd", K.ptr(dcw), 1, 0, 2 * C, K.ptr(cw), K.ptr(y1), K.ptr(W2), K.ptr(dy1p),
+               K.ptr(gW2), K.ptr(gb2), B, 4 * C, 2 * C, 3, 0, K.stream())
+        dpp = torch.empty(ns, B, 4 * C, dtype=torch.float32, device=x.device)
+        K.call("cmx_small_linear_bwd", K.ptr(dy1p), ns, B * 4 * C, 4 * C, K.ptr(y1), K.ptr(pooled), K.ptr(W1),
+               K.ptr(dpp), K.ptr(gW1), K.ptr(gb1), B, 4 * C, 4 * C, 2, 0, K.stream())
+        K.call("cmx_frm_pool_bwd", K.ptr(dpp), ns, B * 4 * C, K.ptr(argmax), K.ptr(dx), B, N, C, dt, K.stream())
         return dx, None, None
 
 
@@ -567,13 +582,12 @@ def frm(store, mod, x):
     cmp = lambda p: store.w(p, stacked=False)
     g = lambda p: store.g(p, stacked=False)
     prm = {
-        # fp32 for the small MLP / spatial head (computed on the VALU in fp32);
-        # compute dtype for the spatial 1x1 GEMM
+        # fp32 for the channel MLP / spatial head (VALU GEMVs and row dots in fp32);
+        # compute dtype for the spatial 2C -> C GEMM
         "w": (f32(cwm[0].weight), f32(cwm[0].bias), f32(cwm[2].weight), f32(cwm[2].bias),
               cmp(swm[0].weight).view(C, 2 * C), f32(swm[0].bias), f32(swm[2].weight).view(2, C), f32(swm[2].bias)),
         "g": (g(cwm[0].weight), g(cwm[0].bias), g(cwm[2].weight), g(cwm[2].bias),
               g(swm[0].weight).view(C, 2 * C), g(swm[0].bias), g(swm[2].weight).view(2, C), g(swm[2].bias)),
-        "w32": (f32(cwm[0].weight), f32(cwm[2].weight), f32(swm[2].weight).view(2, C)),
     }
     return FRMF.apply(x, prm, cwm[0].weight)
 

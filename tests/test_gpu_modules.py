@@ -14,6 +14,11 @@ def rel(a, b, floor=0.0):
     return ((a - b).abs().max() / max(b.abs().max().item(), floor)).item()
 
 
+def rel_l2(a, b, floor=0.0):
+    a = a.detach().double().cpu(); b = b.detach().double().cpu()
+    return ((a - b).norm() / max(b.norm().item(), floor)).item()
+
+
 def _pair(ref_mod, prod_mod):
     from rgbx_semantic_segmentation_amd.params import ParamStore
     prod_mod.load_state_dict(ref_mod.state_dict())
@@ -61,32 +66,66 @@ def test_ffm(dev, C, heads, B, H, W):
     assert errs[0][0] < 1e-3, errs[:4]
 
 
-@pytest.mark.parametrize("C,B,H,W", [(32, 2, 32, 40), (64, 2, 16, 20), (320, 2, 8, 10)])
-def test_frm(dev, C, B, H, W):
-    from rgbx_semantic_segmentation_amd.models.net_utils import FeatureRectifyModule, init_segformer
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("C,B,H,W", [(32, 2, 32, 40), (64, 2, 16, 20), (320, 2, 8, 10), (512, 2, 15, 20),
+                                     (64, 1, 120, 160), (128, 4, 9, 7)])
+def test_frm(dev, C, B, H, W, dtype):
+    """fp32: max-abs relative 1e-4 on outputs / input grads, 1e-3 on parameter grads.
+    bf16 storage: each tensor's error against fp64 within 4x (floor 5e-3) of the error of the
+    same oracle module run in fp32 with bf16 storage emulated (oracle/bf16_emul.py).  The bf16
+    GEMM moves the spatial head's pre-ReLU h across 0 at a few elements, and with
+    SpatialWeights' std-1 init of the C -> 2 conv each flip moves a whole dh element: only an
+    implementation that rounds like the kernels shows the same kinks, so the bound is relative
+    to the emulation, not absolute."""
+    import copy
+    from rgbx_semantic_segmentation_amd.models.net_utils import FeatureRectifyModule
+    from rgbx_semantic_segmentation_amd.params import ParamStore
     from rgbx_semantic_segmentation_amd import functions as F
+    from rgbx_semantic_segmentation_amd import deferred
+    from oracle.bf16_emul import emulate_bf16
     torch.manual_seed(0)
-    ref = R.FeatureRectifyModule(C)
-    ref.apply(R.segformer_init)
-    ref = ref.double()
+    ref32 = R.FeatureRectifyModule(C)
+    ref32.apply(R.segformer_init)
+    ref = copy.deepcopy(ref32).double()
     prod = FeatureRectifyModule(C)
-    store = _pair(ref, prod)
-    x1 = torch.randn(B, C, H, W, dtype=torch.float64, requires_grad=True)
-    x2 = torch.randn(B, C, H, W, dtype=torch.float64, requires_grad=True)
-    w1 = torch.randn(B, C, H, W, dtype=torch.float64)
-    w2 = torch.randn(B, C, H, W, dtype=torch.float64)
+    prod.load_state_dict(ref.state_dict())
+    cdt = torch.float32 if dtype == "float32" else torch.bfloat16
+    store = ParamStore(prod, "cuda", cdt)
+    # the oracle sees the inputs the kernels see (rounded to the storage dtype): the max pool's
+    # gradient then lands on the same token
+    x1 = torch.randn(B, C, H, W).to(cdt).double().requires_grad_(True)
+    x2 = torch.randn(B, C, H, W).to(cdt).double().requires_grad_(True)
+    w1 = torch.randn(B, C, H, W).to(cdt).double()
+    w2 = torch.randn(B, C, H, W).to(cdt).double()
     o1, o2 = ref(x1, x2)
     ((o1 * w1).sum() + (o2 * w2).sum()).backward()
     tok = lambda t: t.detach().flatten(2).transpose(1, 2)
-    r = torch.stack([tok(x1), tok(x2)]).contiguous().float().cuda().requires_grad_(True)
+    r = torch.stack([tok(x1), tok(x2)]).contiguous().to(cdt).cuda().requires_grad_(True)
     out = F.frm(store, prod, r)
-    assert rel(out[0], tok(o1)) < 1e-4 and rel(out[1], tok(o2)) < 1e-4
-    wt = torch.stack([tok(w1), tok(w2)]).float().cuda()
+    wt = torch.stack([tok(w1), tok(w2)]).to(cdt).cuda()
     (out * wt).sum().backward()
+    deferred.flush()
     torch.cuda.synchronize()
-    assert rel(r.grad[0], tok(x1.grad)) < 1e-4, rel(r.grad[0], tok(x1.grad))
-    assert rel(r.grad[1], tok(x2.grad)) < 1e-4, rel(r.grad[1], tok(x2.grad))
     refp = dict(ref.named_parameters())
-    errs = sorted(((rel(p.grad, refp[n].grad, 1e-8), n) for n, p in prod.named_parameters()), reverse=True)
-    print(errs[:4])
-    assert errs[0][0] < 1e-3, errs[:4]
+    got = {"out1": (out[0], tok(o1)), "out2": (out[1], tok(o2)), "dx1": (r.grad[0], tok(x1.grad)),
+           "dx2": (r.grad[1], tok(x2.grad))}
+    got.update({n: (p.grad, refp[n].grad) for n, p in prod.named_parameters()})
+    if dtype == "float32":
+        for k, (a, b) in got.items():
+            tol = 1e-4 if k in ("out1", "out2", "dx1", "dx2") else 1e-3
+            assert rel(a, b, 1e-8) < tol, (k, rel(a, b, 1e-8))
+        return
+    emu = emulate_bf16(copy.deepcopy(ref32))
+    e1 = x1.detach().float().requires_grad_(True)
+    e2 = x2.detach().float().requires_grad_(True)
+    q1, q2 = emu(e1, e2)
+    ((q1 * w1.float()).sum() + (q2 * w2.float()).sum()).backward()
+    emp = dict(emu.named_parameters())
+    emu_t = {"out1": tok(q1), "out2": tok(q2), "dx1": tok(e1.grad), "dx2": tok(e2.grad)}
+    emu_t.update({n: emp[n].grad for n in refp})
+    bad = []
+    for k, (a, b) in got.items():
+        eg, ee = rel(a, b, 1e-8), rel(emu_t[k], b, 1e-8)
+        if eg > max(4 * ee, 5e-3):
+            bad.append((k, eg, ee))
+    assert not bad, bad
