@@ -420,8 +420,9 @@ __global__ __launch_bounds__(256) void combine_bwd_kernel(const T* __restrict__ 
   // slot-combine the four per-channel partials, one quantity at a time through LDS
   float* outc = pcw + ((long)b * nblk + blockIdx.x) * 2 * C;
   float* outs = psp + ((long)b * nblk + blockIdx.x) * (2 * C + 2);
-  for (int qn = 0; qn < 4; ++qn) {
 #pragma unroll
+  for (int qn = 0; qn < 4; ++qn) {             // unrolled: a runtime pick among the four arrays
+#pragma unroll                                   // would put them in scratch memory
     for (int k = 0; k < MCH; ++k)
 #pragma unroll
       for (int j = 0; j < V; ++j) {
