@@ -94,10 +94,13 @@ int cmx_col2im_nhwc(const void* cols, void* dx, int NI, int H, int W, int C, int
 
 /* ---- FFM cross attention (CrossAttention.forward, net_utils.py:199-214):
  *      ctx = softmax_{-2}(k^T v * scale) per (g, b, head); out_1 = q_1 ctx_2, out_2 = q_2 ctx_1.
- *      ctx_reduce mode 0: alpha*X^T Y, 1: softmax_{-2}(alpha*X^T Y), 2: softmax backward. */
-size_t cmx_ffm_ctx_workspace(int BH, int N, int D);
-int cmx_ffm_ctx_reduce(const void* X, const void* Y, const float* ctx, float* out, float* workspace, int Bt, int N, int heads, int D, int64_t xs, int64_t ys, int mode, float alpha, int swapB, int dtype, hipStream_t stream);
-int cmx_ffm_rowmat(const void* X, const float* M, void* out, int Bt, int N, int heads, int D, int64_t xs, int64_t os, int trans, float alpha, int accumulate, int swapB, int dtype, hipStream_t stream);
+ *      The token contractions are batched cmx_gemm calls over (g, b) with C x C operands; these
+ *      two kernels sit between them.  kv / dbd: (G*B, C, C) fp32 GEMM results (k^T v, u^T dout);
+ *      ctx (G*B, heads, D, D) fp32; bdt / da: (G*B, C, C) block-diagonal operands in the compute
+ *      dtype, bdt[(1-g)*B + b][h*D + j][h*D + i] = ctx_{g,b,h}[i][j] (crossed, transposed),
+ *      da[g*B + b][h*D + i][h*D + j] = scale * softmax_bwd (zeros off the diagonal blocks). */
+int cmx_ffm_ctx_fwd(const float* kv, float* ctx, void* bdt, int G, int B, int heads, int D, float scale, int dtype, hipStream_t stream);
+int cmx_ffm_ctx_bwd(const float* ctx, const float* dbd, void* da, int G, int B, int heads, int D, float scale, int dtype, hipStream_t stream);
 
 /* ---- CM-FRM (FeatureRectifyModule, net_utils.py:124-152): ChannelWeights pooling (:22-27)
  *      + tiny-M MLP (:16-20), SpatialWeights 1x1 C->2 + sigmoid (:74-83), rectification. */

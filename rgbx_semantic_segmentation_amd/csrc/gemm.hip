@@ -919,7 +919,10 @@ bool fast_ok(const void* A, const void* A2, const void* B, int M, int N, int K, 
   const int nb = ones_col ? N - 1 : N;
   auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
   if (!al(A) || !al(B) || (A2 && !al(A2))) return false;
-  if (lda % 8 || ldb % 8 || sA % 8 || sB % 8 || K % 8) return false;
+  // a k-contiguous operand is staged in 8-element k chunks (K % 8 keeps the last chunk inside
+  // the row); with both operands row-contiguous k is the row index and any K works
+  // (FFM k^T v / u^T dout over 300-token stage-4 images)
+  if (lda % 8 || ldb % 8 || sA % 8 || sB % 8 || (K % 8 && !(tA && tB))) return false;
   if (tA ? M % 8 : false) return false;
   if (tB ? nb % 8 : false) return false;
   if (A2 && (K1 % FBK || lda2 % 8 || sA2 % 8 || tA)) return false;

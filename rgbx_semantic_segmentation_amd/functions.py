@@ -451,47 +451,51 @@ def conv(store, mod, x, G, NI, H, W, C, stride, pad, nchw=False):
 class CrossAttentionF(Function):
     """CrossAttention.forward (net_utils.py:199-214) on grouped tensors:
     u (G=2, M, C) is the query (raw, no projection), kv (2, M, 2C) = [k | v].
-    ctx_g = softmax_{-2}(k_g^T v_g * s); out_g = u_g @ ctx_{1-g}."""
+    ctx_g = softmax_{-2}(k_g^T v_g * s); out_g = u_g @ ctx_{1-g}.
+
+    Every token contraction is a batched MFMA GEMM over the G * B (modality, image) pairs with
+    K = C (csrc/ffm_attn.hip explains the block-diagonal operands): forward KV = k^T v (fp32),
+    the softmax + crossing kernel, out = u @ BDt^T; backward du = dout @ BD, dBD = u^T dout,
+    the softmax-backward kernel, dk = v @ dA^T and dv = k @ dA written into the halves of dkv."""
 
     @staticmethod
     def forward(ctx, u, kv, B, N, heads, D):
         G, M, C = u.shape
-        BH = G * B * heads
+        GB = G * B
         scale = D ** -0.5
-        cx = torch.empty(BH, D, D, dtype=torch.float32, device=u.device)
-        ws = K._ws(K.query("cmx_ffm_ctx_workspace", BH, N, D), u.device)
-        dt = K.dtype_code(kv)
-        K.call("cmx_ffm_ctx_reduce", K.ptr(kv), kv.data_ptr() + C * kv.element_size(), 0, K.ptr(cx), K.ptr(ws),
-               G * B, N, heads, D, 2 * C, 2 * C, 1, scale, 0, dt, K.stream())
+        kvb = kv.view(GB, N, 2 * C)
+        k, v = kvb[..., :C], kvb[..., C:]
+        KV = torch.empty(GB, C, C, dtype=torch.float32, device=u.device)
+        K.gemm(k.transpose(1, 2), v.transpose(1, 2), KV, out_mode=1)            # k^T v per (g, b)
+        P = torch.empty(GB, heads, D, D, dtype=torch.float32, device=u.device)
+        bdt = torch.empty(GB, C, C, dtype=u.dtype, device=u.device)
+        K.call("cmx_ffm_ctx_fwd", K.ptr(KV), K.ptr(P), K.ptr(bdt), G, B, heads, D, scale, K.dtype_code(u), K.stream())
         out = torch.empty(G, M, C, dtype=u.dtype, device=u.device)
-        K.call("cmx_ffm_rowmat", K.ptr(u), K.ptr(cx), K.ptr(out), G * B, N, heads, D, u.stride(1), C, 0, 1.0, 0, B,
-               dt, K.stream())
-        ctx.save_for_backward(u, kv, cx)
+        K.gemm(u.view(GB, N, C), bdt, out.view(GB, N, C))                      # u_g @ ctx_{1-g} per head
+        ctx.save_for_backward(u, kv, P, bdt)
         ctx.meta = (B, N, heads, D)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        u, kv, cx = ctx.saved_tensors
+        u, kv, P, bdt = ctx.saved_tensors
         B, N, heads, D = ctx.meta
         G, M, C = u.shape
-        dout = _c(dout)
-        dt = K.dtype_code(dout)
+        GB = G * B
         scale = D ** -0.5
-        BH = G * B * heads
+        dout = _c(dout).view(GB, N, C)
+        ub = u.view(GB, N, C)
         du = torch.empty(G, M, C, dtype=u.dtype, device=u.device)
-        K.call("cmx_ffm_rowmat", K.ptr(dout), K.ptr(cx), K.ptr(du), G * B, N, heads, D, C, C, 1, 1.0, 0, B, dt,
-               K.stream())
-        dA = torch.empty_like(cx)
-        ws = K._ws(K.query("cmx_ffm_ctx_workspace", BH, N, D), u.device)
-        K.call("cmx_ffm_ctx_reduce", K.ptr(u), K.ptr(dout), K.ptr(cx), K.ptr(dA), K.ptr(ws), G * B, N, heads, D,
-               u.stride(1), C, 2, scale, B, dt, K.stream())
+        K.gemm(dout, bdt.transpose(1, 2), du.view(GB, N, C))                  # dout @ BD
+        dBD = torch.empty(GB, C, C, dtype=torch.float32, device=u.device)
+        K.gemm(ub.transpose(1, 2), dout.transpose(1, 2), dBD, out_mode=1)      # u^T dout
+        dA = torch.empty(GB, C, C, dtype=u.dtype, device=u.device)
+        K.call("cmx_ffm_ctx_bwd", K.ptr(P), K.ptr(dBD), K.ptr(dA), G, B, heads, D, scale, K.dtype_code(u), K.stream())
+        kvb = kv.view(GB, N, 2 * C)
         dkv = torch.empty(G, M, 2 * C, dtype=kv.dtype, device=kv.device)
-        kp, vp = kv.data_ptr(), kv.data_ptr() + C * kv.element_size()
-        dkp, dvp = dkv.data_ptr(), dkv.data_ptr() + C * dkv.element_size()
-        # dk = v dA^T, dv = k dA
-        K.call("cmx_ffm_rowmat", vp, K.ptr(dA), dkp, G * B, N, heads, D, 2 * C, 2 * C, 1, 1.0, 0, 0, dt, K.stream())
-        K.call("cmx_ffm_rowmat", kp, K.ptr(dA), dvp, G * B, N, heads, D, 2 * C, 2 * C, 0, 1.0, 0, 0, dt, K.stream())
+        dkvb = dkv.view(GB, N, 2 * C)
+        K.gemm(kvb[..., C:], dA, dkvb[..., :C])                                # dk = v dA^T
+        K.gemm(kvb[..., :C], dA.transpose(1, 2), dkvb[..., C:])                # dv = k dA
         return du, dkv, None, None, None, None
 
 

@@ -31,9 +31,12 @@ def ref_epi(acc, bias, act, residual, rscale, rps):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("G,M,N,K", [(2, 300, 64, 64), (2, 1000, 128, 152), (1, 777, 40, 512), (2, 256, 320, 1280),
-                                     (1, 130, 520, 24)])
+                                     (1, 130, 520, 24), (4, 512, 512, 300), (2, 64, 64, 1203)])
 @pytest.mark.parametrize("tA,tB", [(0, 0), (0, 1), (1, 1), (1, 0)])
 def test_gemm_layouts(dev, dtype, G, M, N, K, tA, tB):
+    """K = 300 / 1203 with both operands transposed: the bf16 fast path takes any K there (k is
+    the row index); the groups are packed back to back, so a k-row past K would read the next
+    group's rows (the FFM k^T v / u^T dout products over 300-token images)."""
     torch.manual_seed(0)
     if (tA and M % 8) or (tB and N % 8):
         pytest.skip("transposed operand needs its contiguous dim % 8 == 0")

@@ -29,41 +29,71 @@ def _pair(ref_mod, prod_mod):
     return ParamStore(prod_mod, "cuda", torch.float32)
 
 
-@pytest.mark.parametrize("C,heads,B,H,W", [(32, 1, 2, 32, 40), (64, 2, 2, 16, 20), (160, 5, 2, 8, 10)])
-def test_ffm(dev, C, heads, B, H, W):
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("C,heads,B,H,W", [(32, 1, 2, 32, 40), (64, 2, 2, 16, 20), (160, 5, 2, 8, 10),
+                                           (64, 1, 2, 120, 160), (320, 5, 2, 30, 40), (512, 8, 2, 15, 20)])
+def test_ffm(dev, C, heads, B, H, W, dtype):
+    """FeatureFusionModule (CrossPath with the MFMA cross attention + ChannelEmbed), train mode,
+    against the fp64 oracle.  The yardstick is the same oracle run at the product's precision
+    (plain fp32 for fp32, the bf16-emulated oracle (oracle/bf16_emul.py) for bf16): each tensor
+    within 4x of that run's error, floors 1e-4 (outputs / input grads) and 1e-3 (parameter
+    grads) for fp32 and 5e-3 for bf16 -- the fp32 floor alone is not enough where the layer is
+    ill-conditioned (C=320 at 30x40: the fp32 oracle's own dx error is 2e-3).  Biases feeding a
+    BatchNorm have mathematically zero gradients: bounded by 4x the low-precision run's
+    magnitude, floor 1e-5 (fp32) / 1e-3 (bf16) of the largest parameter gradient."""
+    import copy
     from rgbx_semantic_segmentation_amd.models.net_utils import FeatureFusionModule
+    from rgbx_semantic_segmentation_amd.params import ParamStore
+    from rgbx_semantic_segmentation_amd import deferred
+    from oracle.bf16_emul import emulate_bf16
     torch.manual_seed(0)
-    ref = R.FeatureFusionModule(C, heads).double().train()
+    ref32 = R.FeatureFusionModule(C, heads).train()
+    ref = copy.deepcopy(ref32).double()
     prod = FeatureFusionModule(C, heads).train()
-    store = _pair(ref, prod)
-    x1 = torch.randn(B, C, H, W, dtype=torch.float64, requires_grad=True)
-    x2 = torch.randn(B, C, H, W, dtype=torch.float64, requires_grad=True)
-    wout = torch.randn(B, C, H, W, dtype=torch.float64)
+    prod.load_state_dict(ref.state_dict())
+    for mod in prod.modules():
+        for k, b in list(mod._buffers.items()):
+            if b is not None:
+                mod._buffers[k] = b.cuda()
+    cdt = torch.float32 if dtype == "float32" else torch.bfloat16
+    store = ParamStore(prod, "cuda", cdt)
+    x1 = torch.randn(B, C, H, W).to(cdt).double().requires_grad_(True)
+    x2 = torch.randn(B, C, H, W).to(cdt).double().requires_grad_(True)
+    wout = torch.randn(B, C, H, W).to(cdt).double()
     out_ref = ref(x1, x2)
     (out_ref * wout).sum().backward()
-    r = torch.stack([x1.detach(), x2.detach()]).flatten(3).transpose(2, 3).contiguous().float().cuda().requires_grad_(True)
+    r = torch.stack([x1.detach(), x2.detach()]).flatten(3).transpose(2, 3).contiguous().to(cdt).cuda().requires_grad_(True)
     out = prod.run(store, r, B, H, W, True)          # (B*N, C)
     o = out.view(B, H * W, C)
-    assert rel(o, out_ref.flatten(2).transpose(1, 2)) < 1e-4
-    (o * wout.flatten(2).transpose(1, 2).float().cuda()).sum().backward()
+    (o * wout.flatten(2).transpose(1, 2).to(cdt).cuda()).sum().backward()
+    deferred.flush()
     torch.cuda.synchronize()
     gx = r.grad.view(2, B, H, W, C).permute(0, 1, 4, 2, 3)
-    assert rel(gx[0], x1.grad) < 1e-4, rel(gx[0], x1.grad)
-    assert rel(gx[1], x2.grad) < 1e-4, rel(gx[1], x2.grad)
+    # the oracle at the product's precision
+    low = copy.deepcopy(ref32) if dtype == "float32" else emulate_bf16(copy.deepcopy(ref32))
+    e1 = x1.detach().float().requires_grad_(True)
+    e2 = x2.detach().float().requires_grad_(True)
+    eo = low(e1, e2)
+    (eo * wout.float()).sum().backward()
+    lowp = dict(low.named_parameters())
     refp = dict(ref.named_parameters())
-    # biases that feed a BatchNorm have mathematically zero gradients: compare those
-    # against a floor of 1e-6 x the largest parameter gradient
     gmax = max(p.grad.abs().max().item() for p in ref.parameters())
-    errs = []
+    got = {"out": (o, out_ref.flatten(2).transpose(1, 2), eo.flatten(2).transpose(1, 2)),
+           "dx1": (gx[0], x1.grad, e1.grad), "dx2": (gx[1], x2.grad, e2.grad)}
+    zfloor = 1e-5 if dtype == "float32" else 1e-3
     for n, p in prod.named_parameters():
-        gr = refp[n].grad
-        if gr.abs().max().item() < 1e-9 * gmax:      # structurally zero (bias -> BatchNorm)
-            assert p.grad.abs().max().item() < 1e-5 * gmax, n
+        if refp[n].grad.abs().max().item() < 1e-9 * gmax:     # structurally zero (bias -> BatchNorm)
+            bound = max(4 * lowp[n].grad.abs().max().item(), zfloor * gmax)
+            assert p.grad.abs().max().item() < bound, (n, p.grad.abs().max().item(), bound)
         else:
-            errs.append((rel(p.grad, gr), n))
-    errs.sort(reverse=True)
-    print(errs[:4])
-    assert errs[0][0] < 1e-3, errs[:4]
+            got[n] = (p.grad, refp[n].grad, lowp[n].grad)
+    bad = []
+    for k, (a, b, e) in got.items():
+        floor = 5e-3 if dtype == "bfloat16" else (1e-4 if k in ("out", "dx1", "dx2") else 1e-3)
+        eg, ee = rel(a, b), rel(e, b)
+        if eg > max(4 * ee, floor):
+            bad.append((k, eg, ee))
+    assert not bad, bad
 
 
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
