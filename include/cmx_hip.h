@@ -203,6 +203,20 @@ int cmx_adamw_step_scaled(float* p, const float* g, float* m, float* v, void* sh
 int cmx_grad_nonfinite(const float* g, int64_t n, float* found_inf, hipStream_t stream);
 int cmx_loss_scale_update(float* scale, int* growth_tracker, float* found_inf, float growth_factor, float backoff_factor, int growth_interval, hipStream_t stream);
 
+/* ---- TrainPre augmentation on the GPU (dataloader/dataloader.py:9-112,
+ *      utils/transforms.py:182-187, RGBXDataset.py:65-68), uint8 HWC images (BGR as cv2 reads them).
+ *      resize: cv2.resize INTER_LINEAR (nearest = 0) / INTER_NEAREST (nearest = 1) of an h x w x C
+ *      image to oh x ow, reading the source mirrored (random_mirror, mirror = 1) and clamped to
+ *      [0, clip_max] (TrainPre's label clip; clip_max < 0: none).  color_jitter: in place, BGR ->
+ *      HSV (8U) -> V*bf, S*sf, H+hadd (fp32) -> clip, truncate -> BGR.  blur5: cv2.GaussianBlur
+ *      5x5 sigma 1 (8U fixed point, BORDER_REFLECT_101), out of place.  finalize: cutout box
+ *      [bx1, bx2) x [by1, by2) (rgb/x -> 0, label -> background; empty box: none) + ensure_size
+ *      resize to oh x ow (linear / nearest) + (v/255 - mean)/std in fp64 -> float CHW; labels -> int64. */
+int cmx_aug_resize_u8(const uint8_t* src, int h, int w, int C, uint8_t* dst, int oh, int ow, int nearest, int mirror, int clip_max, hipStream_t stream);
+int cmx_aug_color_jitter_u8(uint8_t* img, int h, int w, float bf, float sf, float hadd, hipStream_t stream);
+int cmx_aug_blur5_u8(const uint8_t* src, uint8_t* dst, int h, int w, int C, hipStream_t stream);
+int cmx_aug_finalize(const uint8_t* rgb, const uint8_t* x, const uint8_t* gt, int h, int w, int oh, int ow, int bx1, int by1, int bx2, int by2, int background, double m0, double m1, double m2, double s0, double s1, double s2, float* rgb_out, float* x_out, int64_t* gt_out, hipStream_t stream);
+
 /* ---- evaluation (engine/evaluator.py:306-396, utils/metric.py:8-15, eval.py:23-36).
  *      seg_window_accumulate: one sliding-window crop -- acc[k, sy+i, sx+j] += exp(s1[k, m0+i, m2+j]
  *      (+ s2[k, m0+i, cw-1-(m2+j)] when s2, the is_flip pass)), s1/s2 (K, ch, cw) fp32 logits of the crop,

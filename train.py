@@ -8,7 +8,8 @@ Same sequence per iteration as the reference: H2D copy, ``loss = model(rgb, moda
 overwrites the flat gradient buffer), ``loss.backward()``, ``optimizer.step()`` (RCCL
 gradient all-reduce + fused AdamW), THEN the WarmUpPolyLR update (the LR lands one step
 late, as in the reference).  Differences: DistributedDataParallel is replaced by the flat
-gradient all-reduce (dist.py); data is the synthetic dataset unless a Dataset is supplied;
+gradient all-reduce (dist.py); data is the synthetic dataset unless --dataset-path names one
+in the reference's layout (then RGBXDataset + TrainPre on the GPU, augment.py);
 TensorBoard logging is omitted (tensorboardX is not installed).
 """
 from __future__ import annotations
@@ -26,7 +27,7 @@ sys.path.insert(0, HERE)
 
 from rgbx_semantic_segmentation_amd.engine.engine import Engine  # noqa: E402
 from rgbx_semantic_segmentation_amd.engine.logger import get_logger  # noqa: E402
-from rgbx_semantic_segmentation_amd.dataloader import SyntheticRGBXDataset, get_train_loader  # noqa: E402
+from rgbx_semantic_segmentation_amd.dataloader import RGBXDataset, SyntheticRGBXDataset, get_train_loader  # noqa: E402
 from rgbx_semantic_segmentation_amd.utils.lr_policy import WarmUpPolyLR  # noqa: E402
 from rgbx_semantic_segmentation_amd.utils.pyt_utils import all_reduce_tensor  # noqa: E402
 
@@ -52,6 +53,15 @@ def build_parser():
     p.add_argument("--seed", type=int, default=12345)
     p.add_argument("--use-mixed-precision", action="store_true",
                    help="config.use_mixed_precision (config.py:61): dynamic loss scaling (GradScaler, train.py:185-198)")
+    p.add_argument("--dataset-path", default="",
+                   help="a dataset in the reference's layout (config.py:19-33): RGB/, Label/, <x-folder>/, "
+                        "<train-source>; empty: the synthetic dataset")
+    p.add_argument("--x-folder", default="Thermal")
+    p.add_argument("--train-source", default="train_val.txt")
+    p.add_argument("--image-format", default=".png")
+    p.add_argument("--x-multi-channel", action="store_true", help="config.x_is_single_channel = False")
+    p.add_argument("--gt-transform", action="store_true", help="config.gt_transform (label - 1)")
+    p.add_argument("--num-workers", type=int, default=2)
     p.add_argument("--checkpoint-dir", default="")
     p.add_argument("--checkpoint-start-epoch", type=int, default=1)
     p.add_argument("--checkpoint-step", type=int, default=1)
@@ -72,10 +82,25 @@ def main(argv=None):
             raise RuntimeError("train.py runs the HIP path and needs a GPU")
         dev = torch.device("cuda", engine.local_rank)
 
-        config = SimpleNamespace(batch_size=args.batch_size, num_workers=0)
-        dataset = SyntheticRGBXDataset(args.niters_per_epoch * args.batch_size, args.height, args.width,
-                                       args.num_classes, seed=args.seed)
-        train_loader, train_sampler = get_train_loader(engine, dataset, config)
+        if args.dataset_path:
+            # the reference's file dataset + TrainPre on the GPU (dataloader.py:129-165)
+            root = args.dataset_path
+            fmt = args.image_format
+            config = SimpleNamespace(
+                rgb_root_folder=os.path.join(root, "RGB"), rgb_format=fmt, gt_root_folder=os.path.join(root, "Label"),
+                gt_format=fmt, gt_transform=args.gt_transform, x_root_folder=os.path.join(root, args.x_folder),
+                x_format=fmt, x_is_single_channel=not args.x_multi_channel,
+                train_source=os.path.join(root, args.train_source), eval_source=os.path.join(root, args.train_source),
+                background=255, num_classes=args.num_classes, image_height=args.height, image_width=args.width,
+                norm_mean=[0.485, 0.456, 0.406], norm_std=[0.229, 0.224, 0.225],
+                train_scale_array=[0.5, 0.75, 1, 1.25, 1.5, 1.75], batch_size=args.batch_size,
+                niters_per_epoch=args.niters_per_epoch, num_workers=args.num_workers)
+            train_loader, train_sampler = get_train_loader(engine, RGBXDataset, config)
+        else:
+            config = SimpleNamespace(batch_size=args.batch_size, num_workers=0)
+            dataset = SyntheticRGBXDataset(args.niters_per_epoch * args.batch_size, args.height, args.width,
+                                           args.num_classes, seed=args.seed)
+            train_loader, train_sampler = get_train_loader(engine, dataset, config)
 
         from rgbx_semantic_segmentation_amd.models.builder import EncoderDecoder
         from rgbx_semantic_segmentation_amd.optim import FusedAdamW, GradScaler
