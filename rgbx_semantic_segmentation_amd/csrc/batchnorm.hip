@@ -29,8 +29,12 @@ int bn_tpr(int chunks) {
   return t;
 }
 
+// row blocks of the reduce passes: ~16 rows each, at most 256 (the grid is this x the channel
+// blocks; more blocks only lengthen the fp64 fold).  The small maps (stage-3/4 FFM BNs:
+// M = 600 .. 2400 rows) then spread over 38 .. 150 row blocks instead of 5 .. 19 whose few
+// lanes walked all rows serially (bn_bwd_reduce 600 x 512: 21 -> 12 us, 2400 x 320: 22 -> 13).
 int bn_nblk(long M) {
-  long nb = (M + 8 * 16 - 1) / (8 * 16);
+  long nb = (M + 15) / 16;
   return (int)(nb < 256 ? (nb > 0 ? nb : 1) : 256);
 }
 
@@ -225,9 +229,11 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
   const int lane = threadIdx.x % TPR, slot = threadIdx.x / TPR;
   const int ch = blockIdx.y * TPR + lane;
   const bool live = ch * V < C;
-  double s[V], q[V];
+  // a lane sums its ~M / (nblk * RS) <= ~10 rows in fp32 (centred terms: no cancellation);
+  // the block and grid partials are fp64
+  float s[V], q[V];
 #pragma unroll
-  for (int j = 0; j < V; ++j) s[j] = q[j] = 0.0;
+  for (int j = 0; j < V; ++j) s[j] = q[j] = 0.f;
   if (live) {
     const int c0 = ch * V;
     float mu[V], is[V], sc[V], sh[V];
@@ -263,7 +269,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
           float g = d[u][j] * act_grad(pre, act);
           if (dscale) g *= ds[u][j];
           s[j] += g;
-          q[j] += (double)g * ((xv[u][j] - mu[j]) * is[j]);
+          q[j] += g * ((xv[u][j] - mu[j]) * is[j]);
         }
     }
   }

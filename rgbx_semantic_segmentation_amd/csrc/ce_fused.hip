@@ -46,17 +46,27 @@ __global__ __launch_bounds__(256) void ce_fwd_tiled(const T* __restrict__ logits
   src_idx(Y0, sh, h, ly0, t1, f0, f1);
   src_idx(X0, sw, w, lx0, t1, f0, f1);
   const T* base = logits + (long)b * h * w * K;
-  for (int e = threadIdx.x; e < LRF * LRF * K; e += 256) {
+  const int Y = Y0 + threadIdx.x / FT, X = X0 + threadIdx.x % FT;
+  // every global load of the thread (its label, its share of the logits tile) is issued
+  // before the first LDS store: one memory latency per block instead of one per 256 items
+  const long lab = (Y < H && X < W) ? label[((long)b * H + Y) * W + X] : (long)ignore;
+  constexpr int NL = (LRF * LRF * KF + 255) / 256;
+  float v[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int e = threadIdx.x + i * 256;
     const int k = e % K, px = e / K;
     const int yy = ly0 + px / LRF, xx = lx0 + px % LRF;
-    lg[px * KF + k] = (yy < h && xx < w) ? to_f32(base[((long)yy * w + xx) * K + k]) : 0.f;
+    v[i] = (e < LRF * LRF * K && yy < h && xx < w) ? to_f32(base[((long)yy * w + xx) * K + k]) : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int e = threadIdx.x + i * 256;
+    if (e < LRF * LRF * K) lg[(e / K) * KF + e % K] = v[i];
   }
   __syncthreads();
-  const int Y = Y0 + threadIdx.x / FT, X = X0 + threadIdx.x % FT;
   float ls = 0.f, lc = 0.f;
   if (Y < H && X < W) {
-    const long p = ((long)b * H + Y) * W + X;
-    const long lab = label[p];
     if (!(lab == ignore || lab < 0 || lab >= K)) {
       int y0, y1, x0, x1;
       float wy0, wy1, wx0, wx1;
@@ -66,17 +76,19 @@ __global__ __launch_bounds__(256) void ce_fwd_tiled(const T* __restrict__ logits
       const float* pb = lg + ((y0 - ly0) * LRF + (x1 - lx0)) * KF;
       const float* pc = lg + ((y1 - ly0) * LRF + (x0 - lx0)) * KF;
       const float* pd = lg + ((y1 - ly0) * LRF + (x1 - lx0)) * KF;
+      // compile-time trip counts predicated on k < K: the LDS reads of all classes are in
+      // flight together and z stays in registers (a runtime-bound loop waits on each read)
+      float z[KF];
       float m = -INFINITY, zl = 0.f;
-      for (int k = 0; k < K; ++k) {
-        const float z = wy0 * (wx0 * pa[k] + wx1 * pb[k]) + wy1 * (wx0 * pc[k] + wx1 * pd[k]);
-        m = fmaxf(m, z);
-        if (k == lab) zl = z;
+#pragma unroll
+      for (int k = 0; k < KF; ++k) {
+        z[k] = k < K ? wy0 * (wx0 * pa[k] + wx1 * pb[k]) + wy1 * (wx0 * pc[k] + wx1 * pd[k]) : -INFINITY;
+        m = fmaxf(m, z[k]);
+        if (k == lab) zl = z[k];
       }
       float se = 0.f;
-      for (int k = 0; k < K; ++k) {
-        const float z = wy0 * (wx0 * pa[k] + wx1 * pb[k]) + wy1 * (wx0 * pc[k] + wx1 * pd[k]);
-        se += __expf(z - m);
-      }
+#pragma unroll
+      for (int k = 0; k < KF; ++k) se += __expf(z[k] - m);
       ls = m + __logf(se) - zl;
       lc = 1.f;
     }
@@ -129,7 +141,8 @@ __global__ __launch_bounds__(256) void ce_bwd_fused(const T* __restrict__ logits
   constexpr int LW = TX + 2, LP = (TY + 2) * LW;
   __shared__ float lg[KF * LP];                     // low-res logits: tile + 1-pixel halo
   __shared__ T g[KF * RY * RX];                     // full-res softmax gradient of the footprint
-  __shared__ float t1[KF * RY * TX];                // x-adjoint: (class, full-res row, low-res col)
+  constexpr int KP = KF + 1;                        // odd pitch: phase C lanes on consecutive k
+  __shared__ float t1[RY * TX * KP];                // x-adjoint: (full-res row, low-res col, class)
   __shared__ float wy[TY * RY], wx[TX * RX];        // bilinear adjoint weights of the tile
   const int bx = blockIdx.x % tiles_x, by = (blockIdx.x / tiles_x) % tiles_y, b = blockIdx.x / (tiles_x * tiles_y);
   const int y0 = by * TY, x0 = bx * TX;
@@ -142,10 +155,27 @@ __global__ __launch_bounds__(256) void ce_bwd_fused(const T* __restrict__ logits
   const int ry = Yb - Ya + 1, rx = Xb - Xa + 1;       // <= RY, RX (exact x4, host-checked)
   const int np = ry * rx;
   const T* base = logits + (long)b * h * w * K;
-  for (int e = threadIdx.x; e < LP * K; e += 256) {
+  // all global loads first (logits tile + halo, the labels of the thread's footprint pixels),
+  // then the LDS stores: one memory latency per block instead of one per 256 items
+  constexpr int NL = (LP * KF + 255) / 256, NPX = (RY * RX + 255) / 256;
+  float v[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int e = threadIdx.x + i * 256;
     const int k = e % K, px = e / K;                  // coalesced global reads along k
     const int yy = y0 - 1 + px / LW, xx = x0 - 1 + px % LW;
-    lg[k * LP + px] = (yy >= 0 && yy < h && xx >= 0 && xx < w) ? to_f32(base[((long)yy * w + xx) * K + k]) : 0.f;
+    v[i] = (e < LP * K && yy >= 0 && yy < h && xx >= 0 && xx < w) ? to_f32(base[((long)yy * w + xx) * K + k]) : 0.f;
+  }
+  long labs[NPX];
+#pragma unroll
+  for (int i = 0; i < NPX; ++i) {
+    const int pi = threadIdx.x + i * 256;
+    labs[i] = pi < np ? label[((long)b * H + Ya + pi / rx) * W + Xa + pi % rx] : (long)ignore;
+  }
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int e = threadIdx.x + i * 256;
+    if (e < LP * K) lg[(e % K) * LP + e / K] = v[i];
   }
   for (int e = threadIdx.x; e < TY * RY + TX * RX; e += 256) {
     const bool isy = e < TY * RY;
@@ -165,9 +195,12 @@ __global__ __launch_bounds__(256) void ce_bwd_fused(const T* __restrict__ logits
   }
   __syncthreads();
   // phase A: g for every footprint pixel (one pixel per lane)
-  for (int pi = threadIdx.x; pi < np; pi += 256) {
+#pragma unroll
+  for (int i = 0; i < NPX; ++i) {
+    const int pi = threadIdx.x + i * 256;
+    if (pi >= np) break;
     const int Y = Ya + pi / rx, X = Xa + pi % rx;
-    const long lab = label[((long)b * H + Y) * W + X];
+    const long lab = labs[i];
     if (lab == ignore || lab < 0 || lab >= K) {
       for (int k = 0; k < K; ++k) g[k * RY * RX + pi] = from_f32<T>(0.f);
       continue;
@@ -206,17 +239,29 @@ __global__ __launch_bounds__(256) void ce_bwd_fused(const T* __restrict__ logits
     const int xl = e % nx, row = (e / nx) % ry, k = e / (nx * ry);
     const T* gr = g + k * RY * RX + row * rx;
     const float* wr = wx + xl * RX;
+    // exact x4 (align_corners=False): low-res column x takes full-res X in [4x - 2, 4x + 6)
+    // only (the borders' clamped taps included); the other footprint weights are zero
+    const int jb = 4 * (x0 + xl) - 2 - Xa;
     float acc = 0.f;
-    for (int j = 0; j < rx; ++j) acc += wr[j] * to_f32(gr[j]);
-    t1[(k * RY + row) * TX + xl] = acc;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int j = jb + jj;
+      acc += (j >= 0 && j < rx) ? wr[j] * to_f32(gr[j]) : 0.f;
+    }
+    t1[(row * TX + xl) * KP + k] = acc;
   }
   __syncthreads();
   // phase C: y-adjoint, write the tile (k fastest: coalesced along the NHWC row)
   for (int e = threadIdx.x; e < ny * nx * K; e += 256) {
     const int k = e % K, xl = (e / K) % nx, yl = e / (K * nx);
     const float* wr = wy + yl * RY;
+    const int jb = 4 * (y0 + yl) - 2 - Ya;              // rows [4y - 2, 4y + 6), as above
     float acc = 0.f;
-    for (int j = 0; j < ry; ++j) acc += wr[j] * t1[(k * RY + j) * TX + xl];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int j = jb + jj;
+      acc += (j >= 0 && j < ry) ? wr[j] * t1[(j * TX + xl) * KP + k] : 0.f;
+    }
     dlogits[((long)b * h * w + (long)(y0 + yl) * w + x0 + xl) * K + k] = from_f32<T>(acc);
   }
 }

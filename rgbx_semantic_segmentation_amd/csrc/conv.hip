@@ -47,29 +47,41 @@ __global__ void zero_pad_cols_kernel(T* __restrict__ cols, long rows, int K, lon
     cols[(i / padw) * ldc + K + i % padw] = from_f32<T>(0.f);
 }
 
-// NCHW fp32 image -> cols in (c, kh, kw) order (= reference weight flatten order)
+// NCHW fp32 image -> cols in (c, kh, kw) order (= reference weight flatten order).  One thread
+// per 8 consecutive columns of one row (ldc % 8 == 0, host-checked): the row and the first
+// column are decoded once, the next 7 columns step (kw, kh, c) incrementally, and the 8 values
+// leave as one 16-B (bf16) / two 16-B (fp32) stores.  The gathers hit the 7.4 MB image in L2.
 template <typename T>
-__global__ void im2col_nchw_kernel(const float* __restrict__ x, T* __restrict__ cols, int NI, int C, int H,
-                                   int W, int KH, int KW, int stride, int pad, int Ho, int Wo, long ldc) {
+__global__ __launch_bounds__(256) void im2col_nchw_kernel(const float* __restrict__ x, T* __restrict__ cols, int NI,
+                                                          int C, int H, int W, int KH, int KW, int stride, int pad,
+                                                          int Ho, int Wo, long ldc) {
   const int K = C * KH * KW;
-  const long total = (long)NI * Ho * Wo * ldc;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)total; i += gridDim.x * blockDim.x) {
-    const int k = i % (int)ldc;
-    const int row = i / (int)ldc;
-    float v = 0.f;
-    if (k < K) {
-      const int c = k / (KH * KW);
-      const int kh = (k / KW) % KH;
-      const int kw = k % KW;
-      const int ox = row % Wo;
-      const int oy = (row / Wo) % Ho;
-      const int n = row / (Wo * Ho);
-      const int iy = oy * stride - pad + kh;
-      const int ix = ox * stride - pad + kw;
-      if (iy >= 0 && iy < H && ix >= 0 && ix < W) v = x[(((long)n * C + c) * H + iy) * W + ix];
+  const int cpr = (int)(ldc / 8);
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)NI * Ho * Wo * cpr) return;
+  const long row = i / cpr;
+  const int k0 = (int)(i - row * cpr) * 8;
+  const int ox = (int)(row % Wo);
+  const int oy = (int)((row / Wo) % Ho);
+  const int n = (int)(row / ((long)Wo * Ho));
+  int c = k0 / (KH * KW), kh = (k0 / KW) % KH, kw = k0 % KW;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float t = 0.f;
+    if (k0 + j < K) {
+      const int iy = oy * stride - pad + kh, ix = ox * stride - pad + kw;
+      if (iy >= 0 && iy < H && ix >= 0 && ix < W) t = x[(((long)n * C + c) * H + iy) * W + ix];
     }
-    cols[i] = from_f32<T>(v);
+    v[j] = t;
+    if (++kw == KW) {
+      kw = 0;
+      if (++kh == KH) { kh = 0; ++c; }
+    }
   }
+  T* o = cols + row * ldc + k0;
+  store_vec<T>(o, v);
+  if constexpr (sizeof(T) == 4) store_vec<T>(o + 4, v + 4);
 }
 
 template <typename T>
@@ -134,11 +146,13 @@ int cmx_im2col_nhwc(const void* x, void* cols, int NI, int H, int W, int C, int 
 
 int cmx_im2col_nchw_f32(const float* x, void* cols, int NI, int C, int H, int W, int KH, int KW, int stride,
                         int pad, int Ho, int Wo, int64_t ldc, int dtype, hipStream_t s) {
-  CMX_REQUIRE(ldc >= (long)KH * KW * C, CMX_ERR_SHAPE, "im2col_nchw: ldc");
+  CMX_REQUIRE(ldc >= (long)KH * KW * C && ldc % 8 == 0, CMX_ERR_SHAPE, "im2col_nchw: ldc %ld (>= K, multiple of 8)",
+              (long)ldc);
   CMX_REQUIRE(Ho == (H + 2 * pad - KH) / stride + 1 && Wo == (W + 2 * pad - KW) / stride + 1, CMX_ERR_SHAPE,
               "im2col_nchw: output size mismatch");
   CMX_DISPATCH(dtype, T, {
-    hipLaunchKernelGGL(im2col_nchw_kernel<T>, dim3(grid_for((long)NI * Ho * Wo * ldc)), dim3(256), 0, s, x,
+    hipLaunchKernelGGL(im2col_nchw_kernel<T>, dim3((unsigned)(((long)NI * Ho * Wo * (ldc / 8) + 255) / 256)), dim3(256),
+                       0, s, x,
                        (T*)cols, NI, C, H, W, KH, KW, stride, pad, Ho, Wo, (long)ldc);
   });
   return cmx_check_launch("im2col_nchw");

@@ -1,0 +1,66 @@
+"""Standalone timings of single kernels at the CMX-B2 480x640 bs=2 shapes (HIP events over
+many back-to-back launches on one stream), for iterating on one kernel without the step's
+run-to-run scheduling noise.  Usage: python scripts/bench_ops.py [name ...]"""
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from rgbx_semantic_segmentation_amd import kernels as K  # noqa: E402
+
+
+def timeit(fn, iters=50):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3
+
+
+def ce():
+    B, h, w, Kc = 2, 120, 160, 40
+    H, W = 4 * h, 4 * w
+    logits = torch.randn(B, h * w, Kc, device="cuda").to(torch.bfloat16)
+    label = torch.randint(0, Kc, (B, H, W), device="cuda")
+    label[:, :20, :20] = 255
+    out = torch.empty(3, device="cuda")
+    ws = K._ws(K.query("cmx_upsample_ce_workspace", B, H, W), "cuda")
+    fwd = lambda: K.call("cmx_upsample_ce_fwd", K.ptr(logits), K.ptr(label), 0, K.ptr(out), K.ptr(ws), B, h, w, H, W,
+                         Kc, 255, 1, K.stream())
+    dloss = torch.ones(1, device="cuda")
+    dl = torch.empty_like(logits)
+    fwd()
+    bwd = lambda: K.call("cmx_upsample_ce_bwd", K.ptr(logits), K.ptr(label), K.ptr(dloss), K.ptr(out), K.ptr(dl), B, h,
+                         w, H, W, Kc, 255, 1, K.stream())
+    return {"ce_fwd": timeit(fwd), "ce_bwd": timeit(bwd)}
+
+
+def bn():
+    res = {}
+    for M, C in [(38400, 512), (2400, 320), (600, 512), (38400, 64)]:
+        x = torch.randn(M, C, device="cuda").to(torch.bfloat16)
+        dy = torch.randn(M, C, device="cuda").to(torch.bfloat16)
+        mean = torch.zeros(C, device="cuda")
+        invstd = torch.ones(C, device="cuda")
+        gamma = torch.ones(C, device="cuda")
+        beta = torch.zeros(C, device="cuda")
+        ws = torch.empty(max(1, K.query("cmx_bn_workspace", M, C) // 8), dtype=torch.float64, device="cuda")
+        sums = torch.empty(2, C, dtype=torch.float64, device="cuda")
+        dg = torch.empty(C, device="cuda")
+        db = torch.empty(C, device="cuda")
+        f = lambda: K.call("cmx_bn_bwd_reduce", K.ptr(dy), K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(gamma),
+                           K.ptr(beta), 0, 0, K.ptr(sums), K.ptr(dg), K.ptr(db), K.ptr(ws), M, C, 1, 0, 0, 1, K.stream())
+        res[f"bn_bwd_reduce {M}x{C}"] = timeit(f)
+    return res
+
+
+if __name__ == "__main__":
+    want = sys.argv[1:] or ["ce", "bn"]
+    for name in want:
+        for k, v in globals()[name]().items():
+            print(f"{k:32s} {v:8.2f} us")
