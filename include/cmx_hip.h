@@ -203,6 +203,21 @@ int cmx_adamw_step_scaled(float* p, const float* g, float* m, float* v, void* sh
 int cmx_grad_nonfinite(const float* g, int64_t n, float* found_inf, hipStream_t stream);
 int cmx_loss_scale_update(float* scale, int* growth_tracker, float* found_inf, float growth_factor, float backoff_factor, int growth_interval, hipStream_t stream);
 
+/* ---- IFRM (ImprovedFeatureRectifyModule, net_utils.py:155-180; config.py:57 'IFRM').
+ *      mul2: out = a * b (fp32; the channel gate y * sigmoid(gate(y)), :61-63), bwd da = d*b, db = d*a.
+ *      combine: o1 = x1 + (lc*cw[1] + ls*sw[1]) * x2, o2 = x2 + (lc*cw[0] + ls*sw[0]) * x1 (:174-175);
+ *      x / out (2, B, N, C), cw (B, 2C) fp32, sw (B*N, 2) un-squashed spatial logits, lc / ls device scalars.
+ *      bwd: dx, dsw directly; part (nblk, 2C) per-block dcw partials (blocks image-major: B x nblk/B),
+ *      lpart (2, nblk) per-block dlc / dls partials; nblk = cmx_ifrm_combine_nblk (cmx_partials_sum folds them). */
+int cmx_mul2(const float* a, const float* b, float* out, int64_t n, hipStream_t stream);
+/* LayerNorm of R fp32 rows of any width C (ImprovedChannelWeights' LN(4C) / LN(2C), :42,45); bwd writes dgamma / dbeta */
+int cmx_rowln_fwd(const float* x, const float* gamma, const float* beta, float* y, float* mean, float* rstd, int R, int C, float eps, hipStream_t stream);
+int cmx_rowln_bwd(const float* dy, const float* x, const float* gamma, const float* mean, const float* rstd, float* dx, float* dgamma, float* dbeta, int R, int C, hipStream_t stream);
+int cmx_mul2_bwd(const float* d, const float* a, const float* b, float* da, float* db, int64_t n, hipStream_t stream);
+int cmx_ifrm_combine_nblk(int B, int N);
+int cmx_ifrm_combine_fwd(const void* x, const float* cw, const void* sw, const float* lc, const float* ls, void* out, int B, int N, int C, int dtype, hipStream_t stream);
+int cmx_ifrm_combine_bwd(const void* dout, const void* x, const float* cw, const void* sw, const float* lc, const float* ls, void* dx, void* dsw, float* part, float* lpart, int B, int N, int C, int dtype, hipStream_t stream);
+
 /* ---- TrainPre augmentation on the GPU (dataloader/dataloader.py:9-112,
  *      utils/transforms.py:182-187, RGBXDataset.py:65-68), uint8 HWC images (BGR as cv2 reads them).
  *      resize: cv2.resize INTER_LINEAR (nearest = 0) / INTER_NEAREST (nearest = 1) of an h x w x C

@@ -66,6 +66,8 @@ class CMXConfig:
     weight_decay: float = 0.01
     drop_path_rate: float = DROP_PATH_RATE
     decoder_dropout: float = 0.1  # MLPDecoder.py:26
+    feature_rectify_module: str = "FRM"   # config.py:57 (FRM | IFRM)
+    feature_fusion_module: str = "FFM"    # config.py:58 (FFM | IFFM)
 
 
 def drop_path_table(depths: List[int], rate: float = DROP_PATH_RATE):
@@ -351,8 +353,127 @@ class FeatureFusionModule(nn.Module):                      # net_utils.py:354-38
         return self.channel_emb(torch.cat((a, b), -1), H, W)
 
 
+# ---- improved variants (config.py:57-58, dual_segformer.py:316-329) ----------------------
+class ImprovedChannelWeights(nn.Module):                   # net_utils.py:33-66
+    def __init__(self, dim):
+        super().__init__()
+        self.dim = dim
+        self.mlp = nn.Sequential(nn.Linear(4 * dim, 4 * dim), nn.LayerNorm(4 * dim), nn.GELU(),
+                                 nn.Linear(4 * dim, 2 * dim), nn.LayerNorm(2 * dim))
+        self.gate = nn.Sequential(nn.Linear(2 * dim, 2 * dim), nn.Sigmoid())
+
+    def forward(self, x1, x2):
+        B = x1.shape[0]
+        x = torch.cat((x1, x2), 1)
+        avg = F.adaptive_avg_pool2d(x, 1).view(B, 2 * self.dim)
+        mx = F.adaptive_max_pool2d(x, 1).view(B, 2 * self.dim)
+        y = self.mlp(torch.cat((avg, mx), 1))
+        y = y * self.gate(y)                                # gating (:61-63)
+        return y.view(B, 2, self.dim, 1, 1).permute(1, 0, 2, 3, 4)
+
+
+class ImprovedSpatialWeights(nn.Module):                   # net_utils.py:86-121
+    def __init__(self, dim):
+        super().__init__()
+        self.conv1 = nn.Conv2d(2 * dim, dim, 1)
+        self.norm1 = nn.BatchNorm2d(dim)
+        self.conv2 = nn.Conv2d(dim, dim, 1)
+        self.norm2 = nn.BatchNorm2d(dim)
+        self.conv3 = nn.Conv2d(dim, 2, 1)
+
+    def forward(self, x1, x2):
+        B, _, H, W = x1.shape
+        y = F.gelu(self.norm1(self.conv1(torch.cat((x1, x2), 1))))
+        y = F.gelu(self.norm2(self.conv2(y))) + y           # residual (:107-115)
+        return self.conv3(y).view(B, 2, 1, H, W).permute(1, 0, 2, 3, 4)     # no sigmoid (:118)
+
+
+class ImprovedFeatureRectifyModule(nn.Module):             # net_utils.py:155-180
+    def __init__(self, dim):
+        super().__init__()
+        self.channel_weights = ImprovedChannelWeights(dim)
+        self.spatial_weights = ImprovedSpatialWeights(dim)
+        self.lambda_channel = nn.Parameter(torch.tensor(0.5))
+        self.lambda_spatial = nn.Parameter(torch.tensor(0.5))
+        self.norm = nn.LayerNorm(dim)                       # eps 1e-5, shared by both outputs
+
+    def forward(self, x1, x2):
+        cw = self.channel_weights(x1, x2)
+        sw = self.spatial_weights(x1, x2)
+        o1 = x1 + self.lambda_channel * cw[1] * x2 + self.lambda_spatial * sw[1] * x2
+        o2 = x2 + self.lambda_channel * cw[0] * x1 + self.lambda_spatial * sw[0] * x1
+        o1 = self.norm(o1.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+        o2 = self.norm(o2.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+        return o1, o2
+
+
+class ImprovedCrossAttention(nn.Module):                   # net_utils.py:216-257
+    def __init__(self, dim, num_heads):
+        super().__init__()
+        self.num_heads = num_heads
+        self.scale = (dim // num_heads) ** -0.5
+        self.q1 = nn.Linear(dim, dim, bias=False)
+        self.kv1 = nn.Linear(dim, 2 * dim, bias=False)
+        self.q2 = nn.Linear(dim, dim, bias=False)
+        self.kv2 = nn.Linear(dim, 2 * dim, bias=False)
+        self.proj1 = nn.Linear(dim, dim)
+        self.proj2 = nn.Linear(dim, dim)                    # attn_drop / proj_drop: p = 0
+
+    def forward(self, x1, x2):
+        B, N, C = x1.shape
+        h, d = self.num_heads, C // self.num_heads
+        q1 = self.q1(x1).view(B, N, h, d).transpose(1, 2)
+        k1, v1 = self.kv1(x1).view(B, N, 2, h, d).permute(2, 0, 3, 1, 4)
+        q2 = self.q2(x2).view(B, N, h, d).transpose(1, 2)
+        k2, v2 = self.kv2(x2).view(B, N, 2, h, d).permute(2, 0, 3, 1, 4)
+        a1 = ((q1 @ k2.transpose(-2, -1)) * self.scale).softmax(dim=-1)
+        a2 = ((q2 @ k1.transpose(-2, -1)) * self.scale).softmax(dim=-1)
+        o1 = self.proj1((a1 @ v2).transpose(1, 2).reshape(B, N, C))
+        o2 = self.proj2((a2 @ v1).transpose(1, 2).reshape(B, N, C))
+        return o1, o2
+
+
+class ImprovedCrossPath(nn.Module):                        # net_utils.py:283-306
+    def __init__(self, dim, num_heads):
+        super().__init__()
+        self.channel_proj1 = nn.Linear(dim, 2 * dim)
+        self.channel_proj2 = nn.Linear(dim, 2 * dim)
+        self.cross_attn = ImprovedCrossAttention(dim, num_heads)
+        self.end_proj1 = nn.Linear(2 * dim, dim)
+        self.end_proj2 = nn.Linear(2 * dim, dim)
+        self.norm1 = nn.LayerNorm(dim)
+        self.norm2 = nn.LayerNorm(dim)
+
+    def forward(self, x1, x2):
+        y1, u1 = F.gelu(self.channel_proj1(x1)).chunk(2, dim=-1)
+        y2, u2 = F.gelu(self.channel_proj2(x2)).chunk(2, dim=-1)
+        v1, v2 = self.cross_attn(u1, u2)
+        o1 = self.norm1(x1 + self.end_proj1(torch.cat((y1, v1), -1)))
+        o2 = self.norm2(x2 + self.end_proj2(torch.cat((y2, v2), -1)))
+        return o1, o2
+
+
+class ImprovedChannelEmbed(ChannelEmbed):                  # net_utils.py:331-351: GELU for ReLU
+    def __init__(self, cin, cout):
+        super().__init__(cin, cout)
+        self.channel_embed[2] = nn.GELU()
+
+
+class ImprovedFeatureFusionModule(nn.Module):              # net_utils.py:387-417
+    def __init__(self, dim, num_heads):
+        super().__init__()
+        self.cross = ImprovedCrossPath(dim, num_heads)
+        self.channel_emb = ImprovedChannelEmbed(2 * dim, dim)
+        self.apply(segformer_init)
+
+    def forward(self, x1, x2):
+        B, C, H, W = x1.shape
+        a, b = self.cross(x1.flatten(2).transpose(1, 2), x2.flatten(2).transpose(1, 2))
+        return self.channel_emb(torch.cat((a, b), -1), H, W)
+
+
 class RGBXTransformer(nn.Module):                          # dual_segformer.py:228-446
-    def __init__(self, embed_dims, depths, drop_path_rate=DROP_PATH_RATE):
+    def __init__(self, embed_dims, depths, drop_path_rate=DROP_PATH_RATE, frm="FRM", ffm="FFM"):
         super().__init__()
         self.depths = depths
         dp = drop_path_table(depths, drop_path_rate)
@@ -368,9 +489,11 @@ class RGBXTransformer(nn.Module):                          # dual_segformer.py:2
                     [Block(embed_dims[s], NUM_HEADS[s], SR_RATIOS[s], probs[i])
                      for i in range(depths[s])]))
                 setattr(self, f"{pre}norm{s + 1}", nn.LayerNorm(embed_dims[s], eps=1e-6))
-        self.FRMs = nn.ModuleList([FeatureRectifyModule(d) for d in embed_dims])
-        self.FFMs = nn.ModuleList([FeatureFusionModule(d, NUM_HEADS[s])
-                                   for s, d in enumerate(embed_dims)])
+        # dual_segformer.py:316-340: anything but 'FRM' / 'FFM' selects the improved variant
+        rect = FeatureRectifyModule if frm == "FRM" else ImprovedFeatureRectifyModule
+        fuse = FeatureFusionModule if ffm == "FFM" else ImprovedFeatureFusionModule
+        self.FRMs = nn.ModuleList([rect(d) for d in embed_dims])
+        self.FFMs = nn.ModuleList([fuse(d, NUM_HEADS[s]) for s, d in enumerate(embed_dims)])
         self.apply(segformer_init)
 
     def forward(self, x_rgb, x_e, return_stages=False):
@@ -454,7 +577,8 @@ class EncoderDecoder(nn.Module):                           # builder.py:14-253
         spec = MIT_SPECS[cfg.backbone]
         self.cfg = cfg
         self.channels = list(spec["embed_dims"])
-        self.backbone = RGBXTransformer(spec["embed_dims"], spec["depths"], cfg.drop_path_rate)
+        self.backbone = RGBXTransformer(spec["embed_dims"], spec["depths"], cfg.drop_path_rate,
+                                        cfg.feature_rectify_module, cfg.feature_fusion_module)
         self.aux_head = None
         self.decode_head = DecoderHead(self.channels, cfg.num_classes, cfg.decoder_embed_dim,
                                        cfg.decoder_dropout, cfg.bn_eps, cfg.bn_momentum)

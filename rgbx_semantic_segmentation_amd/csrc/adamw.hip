@@ -10,8 +10,9 @@
 // the bias corrections are formed in double and rounded to fp32 once (as torch rounds its
 // Python-float scalars), so 1 - 0.999 is 0.001f and not 1.f - 0.999f (1.3e-5 apart).
 // lr and t are read from device memory so the step can be replayed from a HIP graph while
-// WarmUpPolyLR changes lr.  The per-64-element decay flag follows the flat layout (every
-// parameter starts on a 64-element boundary).  Optionally emits the bf16 weight shadow for
+// WarmUpPolyLR changes lr.  The per-64-element flag follows the flat layout (every parameter
+// starts on a 64-element boundary): 1 = decay, 0 = none, 2 = in neither of group_weight's groups
+// (IFRM's lambdas, which the reference's optimizer never sees): left untouched.  Optionally emits the bf16 weight shadow for
 // the next step's GEMMs and scales the gradient (1/world_size after a SUM all-reduce).
 // HBM-bound: 16 B read (p,g,m,v) + 12 B written (p,m,v) [+2 B shadow] per parameter.
 #include "cmx_common.h"
@@ -37,7 +38,9 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
     float4 gg = *reinterpret_cast<const float4*>(g + e);
     float4 mm = *reinterpret_cast<float4*>(m + e);
     float4 vv = *reinterpret_cast<float4*>(v + e);
-    const float dec = decay64[e >> 6] ? decf : 1.f;
+    const uint8_t flag = decay64[e >> 6];              // 0: no decay, 1: decay, 2: frozen
+    if (flag == 2) continue;
+    const float dec = flag ? decf : 1.f;
     float pa[4] = {pp.x, pp.y, pp.z, pp.w}, ga[4] = {gg.x, gg.y, gg.z, gg.w};
     float ma[4] = {mm.x, mm.y, mm.z, mm.w}, va[4] = {vv.x, vv.y, vv.z, vv.w};
 #pragma unroll

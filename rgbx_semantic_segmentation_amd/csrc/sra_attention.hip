@@ -444,7 +444,7 @@ void sra_fwd_fast_launch(const void* q, const void* k, const void* v, void* o, f
 void sra_dq_fast_launch(const void* q, const void* k, const void* v, const void* o, const void* dout,
                         const float* lse, float* Dws, void* dq, int Bt, int N, int Nk, int heads, long qs, long kvs,
                         long os, long dos, long dqs, float sl2, float scale, hipStream_t s);
-int sra_dkv_fast_chunks(int Bt, int N, int heads);
+int sra_dkv_fast_chunks(int Bt, int N, int Nk, int heads);
 void sra_dkv_fast_launch(const void* q, const void* k, const void* v, const void* dout, const float* lse,
                          const float* Dws, float* ws_dk, float* ws_dv, int Bt, int N, int Nk, int heads, long qs,
                          long kvs, long dos, int nchunk, float sl2, float scale, hipStream_t s);
@@ -483,7 +483,7 @@ int cmx_sra_attn_fwd(const void* q, const void* k, const void* v, void* o, float
 
 size_t cmx_sra_attn_bwd_workspace(int Bt, int N, int Nk, int heads, int D) {
   int nc = bwd_nchunk(Bt, N, Nk, heads);
-  const int ncf = sra_dkv_fast_chunks(Bt, N, heads);   // the bf16 fast path may take either
+  const int ncf = sra_dkv_fast_chunks(Bt, N, Nk, heads);   // the bf16 fast path may take either
   if (ncf > nc) nc = ncf;
   const size_t slab = (size_t)nc * Bt * heads * Nk * D;
   return ((size_t)Bt * heads * N + 2 * slab) * sizeof(float);
@@ -502,7 +502,7 @@ int cmx_sra_attn_bwd(const void* q, const void* k, const void* v, const void* o,
   // fast path for any Nk: dQ streams K / V in LDS-sized chunks, dK / dV splits keys over workgroups
   const bool fast = sra_fast_fwd_ok(D, Nk, dtype, ptrs, 6, strides, 5);
   const bool fast_dq = fast;
-  const int nc = fast ? sra_dkv_fast_chunks(Bt, N, heads) : bwd_nchunk(Bt, N, Nk, heads);
+  const int nc = fast ? sra_dkv_fast_chunks(Bt, N, Nk, heads) : bwd_nchunk(Bt, N, Nk, heads);
   const int qc = bwd_qc(N, nc);
   float* Dws = workspace;
   float* ws_dk = Dws + (size_t)Bt * heads * N;

@@ -517,9 +517,12 @@ void sra_dq_fast_launch(const void* q, const void* k, const void* v, const void*
 }
 
 // partial dK / dV slabs of the query chunks (layout of sra_attention.hip's generic path)
-int sra_dkv_fast_chunks(int Bt, int N, int heads) {
-  const long base = (long)Bt * heads;
-  long nc = (256 + base - 1) / base;              // ~one workgroup per CU
+int sra_dkv_fast_chunks(int Bt, int N, int Nk, int heads) {
+  // query chunks per (image, head, 320-key chunk): ~one workgroup per CU over the whole grid
+  // (the SRA layers have one key chunk; IFFM's full cross attention has Nk / 320 of them,
+  // which already fill the chip, and every extra query chunk is another Nk x D slab to reduce)
+  const long base = (long)Bt * heads * ((Nk + NKP_MAX - 1) / NKP_MAX);
+  long nc = (256 + base - 1) / base;
   const long maxc = (N + QT - 1) / QT;
   if (nc > maxc) nc = maxc;
   if (nc > 64) nc = 64;

@@ -299,6 +299,165 @@ class SRAttentionF(Function):
         return dq.view(q.shape), dkv.view(kv.shape), None, None, None, None, None
 
 
+class ActF(Function):
+    """Elementwise activation with the pre-activation saved for the backward: the GELU of
+    ImprovedCrossPath.act1/2 (net_utils.py:288-293, 301-302) and ImprovedChannelWeights
+    (:42), on tensors a GEMM epilogue cannot keep (its pre-activation is needed later)."""
+
+    @staticmethod
+    def forward(ctx, z, act):
+        ctx.act = act
+        ctx.save_for_backward(z)
+        return K.act_fwd(z, act)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (z,) = ctx.saved_tensors
+        return K.act_bwd(_c(dy), z, ctx.act), None
+
+
+class CrossFlashAttnF(Function):
+    """ImprovedCrossAttention's core (net_utils.py:236-257) on grouped tensors q (2, M, C) and
+    kv (2, M, 2C), M = B * N: o_g = softmax(q_g k_{1-g}^T d^-1/2) v_{1-g} (attn_drop p = 0), full
+    token-to-token attention (Nk = N, no spatial reduction).  The SRA flash kernels run it with
+    the OTHER modality's keys / values, one launch per direction (forward and backward)."""
+
+    @staticmethod
+    def forward(ctx, q, kv, B, N, heads, D):
+        G, M, C = q.shape
+        assert G == 2 and M == B * N and kv.shape == (2, M, 2 * C) and q.is_contiguous() and kv.is_contiguous()
+        dt = K.dtype_code(q)
+        esz = kv.element_size()
+        o = torch.empty_like(q)
+        lse = torch.empty(2, B, heads, N, dtype=torch.float32, device=q.device)
+        for g in range(2):
+            src = kv[1 - g]
+            K.call("cmx_sra_attn_fwd", K.ptr(q[g]), K.ptr(src), src.data_ptr() + C * esz, K.ptr(o[g]), K.ptr(lse[g]),
+                   B, N, N, heads, D, C, 2 * C, C, D ** -0.5, dt, K.stream())
+        ctx.save_for_backward(q, kv, o, lse)
+        ctx.dims = (B, N, heads, D)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, kv, o, lse = ctx.saved_tensors
+        B, N, heads, D = ctx.dims
+        C = heads * D
+        do = _c(do)
+        dt = K.dtype_code(q)
+        esz = kv.element_size()
+        dq = torch.empty_like(q)
+        dkv = torch.empty_like(kv)
+        ws = K._ws(K.query("cmx_sra_attn_bwd_workspace", B, N, N, heads, D), q.device)
+        for g in range(2):
+            src, dsrc = kv[1 - g], dkv[1 - g]
+            K.call("cmx_sra_attn_bwd", K.ptr(q[g]), K.ptr(src), src.data_ptr() + C * esz, K.ptr(o[g]), K.ptr(do[g]),
+                   K.ptr(lse[g]), K.ptr(dq[g]), K.ptr(dsrc), dsrc.data_ptr() + C * esz, K.ptr(ws), B, N, N, heads, D,
+                   C, 2 * C, C, C, C, 2 * C, D ** -0.5, dt, K.stream())
+        return dq, dkv, None, None, None, None
+
+
+def _rowln(x, g, b, eps):
+    R, C = x.shape
+    y = torch.empty_like(x)
+    mean = torch.empty(R, dtype=torch.float32, device=x.device)
+    rstd = torch.empty_like(mean)
+    K.call("cmx_rowln_fwd", K.ptr(x), K.ptr(g), K.ptr(b), K.ptr(y), K.ptr(mean), K.ptr(rstd), R, C, float(eps), K.stream())
+    return y, mean, rstd
+
+
+def _rowln_bwd(dy, x, g, mean, rstd, gg, gb):
+    R, C = x.shape
+    dx = torch.empty_like(x)
+    K.call("cmx_rowln_bwd", K.ptr(dy), K.ptr(x), K.ptr(g), K.ptr(mean), K.ptr(rstd), K.ptr(dx), K.ptr(gg), K.ptr(gb),
+           R, C, K.stream())
+    return dx
+
+
+class IFRMF(Function):
+    """ImprovedFeatureRectifyModule (net_utils.py:155-180) up to its LayerNorm, on x (2, B, N, C)
+    with the spatial logits sw (B*N, 2) (ImprovedSpatialWeights' conv3 output, computed by the
+    caller's GEMM / BatchNorm chain):
+      ImprovedChannelWeights (:33-66): avg || max pool -> Linear -> LN -> GELU -> Linear -> LN
+        -> y * sigmoid(gate(y)), on (B, 4C) / (B, 2C) fp32 vectors (cmx_frm_pool_*,
+        cmx_small_linear_*, cmx_layernorm_*, cmx_act_*, cmx_mul2*);
+      the rectification with the learnable lambdas and un-squashed sw (cmx_ifrm_combine_*).
+    The lambdas are in neither of group_weight's groups (init_func.py:33-57 only collects
+    Linear / Conv / norm parameters), so the reference's optimizer never updates them: their
+    gradients are computed, the fused AdamW leaves them alone (ParamStore frozen slots)."""
+
+    @staticmethod
+    def forward(ctx, x, sw, prm, anchor):
+        (W1, b1, g1, e1, W3, b3, g4, e4, Wg, bgt, lc, ls, eps1, eps4) = prm["w"]
+        G, B, N, C = x.shape
+        dt = K.dtype_code(x)
+        f32 = dict(dtype=torch.float32, device=x.device)
+        pooled = torch.empty(B, 4 * C, **f32)
+        argmax = torch.empty(B, 2 * C, dtype=torch.int32, device=x.device)
+        ws = K._ws(K.query("cmx_frm_pool_workspace", B, N, C), x.device)
+        K.call("cmx_frm_pool_fwd", K.ptr(x), K.ptr(pooled), K.ptr(argmax), K.ptr(ws), B, N, C, dt, K.stream())
+        h1 = torch.empty(B, 4 * C, **f32)
+        K.call("cmx_small_linear_fwd", K.ptr(pooled), K.ptr(W1), K.ptr(b1), K.ptr(h1), B, 4 * C, 4 * C, 0, K.stream())
+        n1, m1, r1 = _rowln(h1, g1, e1, eps1)
+        a1 = K.act_fwd(n1, "gelu")
+        h2 = torch.empty(B, 2 * C, **f32)
+        K.call("cmx_small_linear_fwd", K.ptr(a1), K.ptr(W3), K.ptr(b3), K.ptr(h2), B, 4 * C, 2 * C, 0, K.stream())
+        y, m2, r2 = _rowln(h2, g4, e4, eps4)
+        gt = torch.empty(B, 2 * C, **f32)
+        K.call("cmx_small_linear_fwd", K.ptr(y), K.ptr(Wg), K.ptr(bgt), K.ptr(gt), B, 2 * C, 2 * C, 3, K.stream())
+        cw = torch.empty(B, 2 * C, **f32)
+        K.call("cmx_mul2", K.ptr(y), K.ptr(gt), K.ptr(cw), B * 2 * C, K.stream())
+        out = torch.empty_like(x)
+        K.call("cmx_ifrm_combine_fwd", K.ptr(x), K.ptr(cw), K.ptr(sw), K.ptr(lc), K.ptr(ls), K.ptr(out), B, N, C, dt,
+               K.stream())
+        ctx.save_for_backward(x, sw, pooled, argmax, h1, m1, r1, n1, a1, h2, m2, r2, y, gt, cw)
+        ctx.prm = prm
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, sw, pooled, argmax, h1, m1, r1, n1, a1, h2, m2, r2, y, gt, cw = ctx.saved_tensors
+        (W1, b1, g1, e1, W3, b3, g4, e4, Wg, bgt, lc, ls, eps1, eps4) = ctx.prm["w"]
+        (gW1, gb1, gg1, ge1, gW3, gb3, gg4, ge4, gWg, gbg, glc, gls) = ctx.prm["g"]
+        G, B, N, C = x.shape
+        dt = K.dtype_code(x)
+        f32 = dict(dtype=torch.float32, device=x.device)
+        dout = _c(dout)
+        dx = torch.empty_like(x)
+        dsw = torch.empty_like(sw)
+        nb = K.query("cmx_ifrm_combine_nblk", B, N)
+        part = torch.empty(nb, 2 * C, **f32)
+        lpart = torch.empty(2, nb, **f32)
+        K.call("cmx_ifrm_combine_bwd", K.ptr(dout), K.ptr(x), K.ptr(cw), K.ptr(sw), K.ptr(lc), K.ptr(ls), K.ptr(dx),
+               K.ptr(dsw), K.ptr(part), K.ptr(lpart), B, N, C, dt, K.stream())
+        K.call("cmx_partials_sum", K.ptr(lpart[0]), K.ptr(glc), 1, nb, 1, 0, 1.0, K.stream())
+        K.call("cmx_partials_sum", K.ptr(lpart[1]), K.ptr(gls), 1, nb, 1, 0, 1.0, K.stream())
+        dcw = torch.empty(B, 2 * C, **f32)
+        K.call("cmx_partials_sum", K.ptr(part), K.ptr(dcw), B, nb // B, 2 * C, 0, 1.0, K.stream())
+        # cw = y * gt, gt = sigmoid(y Wg^T + bg)
+        dy = torch.empty_like(y)
+        dgt = torch.empty_like(gt)
+        K.call("cmx_mul2_bwd", K.ptr(dcw), K.ptr(y), K.ptr(gt), K.ptr(dy), K.ptr(dgt), B * 2 * C, K.stream())
+        ns = K.query("cmx_small_linear_nslice")
+        dyp = torch.empty(ns, B, 2 * C, **f32)
+        K.call("cmx_small_linear_bwd", K.ptr(dgt), 1, 0, 2 * C, K.ptr(gt), K.ptr(y), K.ptr(Wg), K.ptr(dyp),
+               K.ptr(gWg), K.ptr(gbg), B, 2 * C, 2 * C, 3, 0, K.stream())
+        K.call("cmx_partials_sum", K.ptr(dyp), K.ptr(dy), 1, ns, B * 2 * C, 1, 1.0, K.stream())     # dy += gate path
+        dh2 = _rowln_bwd(dy, h2, g4, m2, r2, gg4, ge4)
+        dap = torch.empty(ns, B, 4 * C, **f32)
+        K.call("cmx_small_linear_bwd", K.ptr(dh2), 1, 0, 2 * C, K.ptr(h2), K.ptr(a1), K.ptr(W3), K.ptr(dap),
+               K.ptr(gW3), K.ptr(gb3), B, 4 * C, 2 * C, 0, 0, K.stream())
+        da1 = torch.empty(B, 4 * C, **f32)
+        K.call("cmx_partials_sum", K.ptr(dap), K.ptr(da1), 1, ns, B * 4 * C, 0, 1.0, K.stream())
+        dn1 = K.act_bwd(da1, n1, "gelu")
+        dh1 = _rowln_bwd(dn1, h1, g1, m1, r1, gg1, ge1)
+        dpp = torch.empty(ns, B, 4 * C, **f32)
+        K.call("cmx_small_linear_bwd", K.ptr(dh1), 1, 0, 4 * C, K.ptr(h1), K.ptr(pooled), K.ptr(W1), K.ptr(dpp),
+               K.ptr(gW1), K.ptr(gb1), B, 4 * C, 4 * C, 0, 0, K.stream())
+        K.call("cmx_frm_pool_bwd", K.ptr(dpp), ns, B * 4 * C, K.ptr(argmax), K.ptr(dx), B, N, C, dt, K.stream())
+        return dx, dsw, None, None
+
+
 # ---------------------------------------------------------------------------- depthwise
 class DWConvF(Function):
     """Depthwise 3x3 + bias + act (Mix-FFN DWConv+GELU, ChannelEmbed DW+ReLU)."""

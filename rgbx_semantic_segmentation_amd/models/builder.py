@@ -74,11 +74,10 @@ class EncoderDecoder(nn.Module):
         decoder = _get(cfg, "decoder", "MLPDecoder")
         if decoder != "MLPDecoder":
             raise NotImplementedError(f"decoder {decoder!r}: only MLPDecoder is on the CMX hot path")
-        # config.py:57-58 selects the rectify / fusion blocks (dual_segformer.py:316-329)
-        for key, supported in (("feature_rectify_module", "FRM"), ("feature_fusion_module", "FFM")):
-            sel = _get(cfg, key, supported)
-            if sel != supported:
-                raise NotImplementedError(f"{key} {sel!r}: only {supported!r} is on the CMX hot path")
+        # config.py:57-58 selects the rectify / fusion blocks (dual_segformer.py:316-329: 'FRM' / 'FFM'
+        # the originals, any other value the improved IFRM / IFFM, as there)
+        frm = _get(cfg, "feature_rectify_module", "FRM")
+        ffm = _get(cfg, "feature_fusion_module", "FFM")
         if criterion is None:
             criterion = nn.CrossEntropyLoss(reduction="mean", ignore_index=int(_get(cfg, "background", 255)))
         if not isinstance(criterion, nn.CrossEntropyLoss) or criterion.reduction != "mean" or \
@@ -90,7 +89,7 @@ class EncoderDecoder(nn.Module):
         self.ignore_index = int(criterion.ignore_index)
         self.backbone_name = backbone
         self.channels = list(MIT_SPECS[backbone]["embed_dims"])
-        self.backbone = BACKBONES[backbone](norm_fuse=norm_layer)
+        self.backbone = BACKBONES[backbone](norm_fuse=norm_layer, frm=frm, ffm=ffm)
         self.aux_head = None
         self.num_classes = int(_get(cfg, "num_classes", 40))
         self.decode_head = DecoderHead(in_channels=self.channels, num_classes=self.num_classes,

@@ -18,7 +18,8 @@ import torch.nn as nn
 
 from ... import functions as F
 from ... import streams
-from ..net_utils import FeatureRectifyModule, FeatureFusionModule, init_segformer
+from ..net_utils import (FeatureRectifyModule, FeatureFusionModule, ImprovedFeatureRectifyModule,
+                         ImprovedFeatureFusionModule, init_segformer)
 
 MIT_SPECS = {
     "mit_b0": dict(embed_dims=[32, 64, 160, 256], depths=[2, 2, 2, 2]),
@@ -95,7 +96,7 @@ class OverlapPatchEmbed(nn.Module):               # dual_segformer.py:183-225
 
 
 class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
-    def __init__(self, embed_dims, depths, drop_path_rate=0.1):
+    def __init__(self, embed_dims, depths, drop_path_rate=0.1, frm="FRM", ffm="FFM"):
         super().__init__()
         self.embed_dims, self.depths = list(embed_dims), list(depths)
         self.dp = drop_path_probs(depths, drop_path_rate)
@@ -109,8 +110,12 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
                 setattr(self, f"{pre}block{s + 1}", nn.ModuleList(
                     [Block(embed_dims[s], NUM_HEADS[s], SR_RATIOS[s], probs[i]) for i in range(depths[s])]))
                 setattr(self, f"{pre}norm{s + 1}", nn.LayerNorm(embed_dims[s], eps=1e-6))
-        self.FRMs = nn.ModuleList([FeatureRectifyModule(d) for d in embed_dims])
-        self.FFMs = nn.ModuleList([FeatureFusionModule(d, NUM_HEADS[s]) for s, d in enumerate(embed_dims)])
+        # config.feature_rectify_module / feature_fusion_module (dual_segformer.py:316-340):
+        # anything but 'FRM' / 'FFM' selects the improved variant, as in the reference
+        rect = FeatureRectifyModule if frm == "FRM" else ImprovedFeatureRectifyModule
+        fuse = FeatureFusionModule if ffm == "FFM" else ImprovedFeatureFusionModule
+        self.FRMs = nn.ModuleList([rect(d) for d in embed_dims])
+        self.FFMs = nn.ModuleList([fuse(d, NUM_HEADS[s]) for s, d in enumerate(embed_dims)])
         self.apply(init_segformer)
 
     # ------------------------------------------------------------------------ execution
@@ -186,7 +191,11 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
             x, _, _ = F.layernorm_res(store, getattr(self, f"norm{s + 1}"), x, G, scale=prev[0], rps=Hc * Wc,
                                       tap=prev[1])
             C = self.embed_dims[s]
-            r = F.frm(store, self.FRMs[s], x.view(G, B, Hc * Wc, C))
+            fr = self.FRMs[s]
+            if isinstance(fr, ImprovedFeatureRectifyModule):
+                r = fr.rectify(store, x.view(G, B, Hc * Wc, C), training)
+            else:
+                r = F.frm(store, fr, x.view(G, B, Hc * Wc, C))
             if side is not None:
                 # FFM_s only feeds the decoder: run it beside stage s + 1 on the side stream
                 # (its backward then runs there too, beside the encoder's backward)
@@ -206,33 +215,33 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
 
 
 class mit_b0(RGBXTransformer):
-    def __init__(self, fuse_cfg=None, **kwargs):
-        super().__init__(**MIT_SPECS["mit_b0"], drop_path_rate=0.1)
+    def __init__(self, fuse_cfg=None, frm="FRM", ffm="FFM", **kwargs):
+        super().__init__(**MIT_SPECS["mit_b0"], drop_path_rate=0.1, frm=frm, ffm=ffm)
 
 
 class mit_b1(RGBXTransformer):
-    def __init__(self, fuse_cfg=None, **kwargs):
-        super().__init__(**MIT_SPECS["mit_b1"], drop_path_rate=0.1)
+    def __init__(self, fuse_cfg=None, frm="FRM", ffm="FFM", **kwargs):
+        super().__init__(**MIT_SPECS["mit_b1"], drop_path_rate=0.1, frm=frm, ffm=ffm)
 
 
 class mit_b2(RGBXTransformer):
-    def __init__(self, fuse_cfg=None, **kwargs):
-        super().__init__(**MIT_SPECS["mit_b2"], drop_path_rate=0.1)
+    def __init__(self, fuse_cfg=None, frm="FRM", ffm="FFM", **kwargs):
+        super().__init__(**MIT_SPECS["mit_b2"], drop_path_rate=0.1, frm=frm, ffm=ffm)
 
 
 class mit_b3(RGBXTransformer):
-    def __init__(self, fuse_cfg=None, **kwargs):
-        super().__init__(**MIT_SPECS["mit_b3"], drop_path_rate=0.1)
+    def __init__(self, fuse_cfg=None, frm="FRM", ffm="FFM", **kwargs):
+        super().__init__(**MIT_SPECS["mit_b3"], drop_path_rate=0.1, frm=frm, ffm=ffm)
 
 
 class mit_b4(RGBXTransformer):
-    def __init__(self, fuse_cfg=None, **kwargs):
-        super().__init__(**MIT_SPECS["mit_b4"], drop_path_rate=0.1)
+    def __init__(self, fuse_cfg=None, frm="FRM", ffm="FFM", **kwargs):
+        super().__init__(**MIT_SPECS["mit_b4"], drop_path_rate=0.1, frm=frm, ffm=ffm)
 
 
 class mit_b5(RGBXTransformer):
-    def __init__(self, fuse_cfg=None, **kwargs):
-        super().__init__(**MIT_SPECS["mit_b5"], drop_path_rate=0.1)
+    def __init__(self, fuse_cfg=None, frm="FRM", ffm="FFM", **kwargs):
+        super().__init__(**MIT_SPECS["mit_b5"], drop_path_rate=0.1, frm=frm, ffm=ffm)
 
 
 BACKBONES = {"mit_b0": mit_b0, "mit_b1": mit_b1, "mit_b2": mit_b2, "mit_b3": mit_b3, "mit_b4": mit_b4,

@@ -53,7 +53,7 @@ class FusedAdamW:
         self.grad_sync = grad_sync          # callable(flat_grad) -> grad scale, or None
         names = list(store.params.keys())
         decay = [store.params[n] for n in names if store.slots[n].decay]
-        no_decay = [store.params[n] for n in names if not store.slots[n].decay]
+        no_decay = [store.params[n] for n in names if not store.slots[n].decay and not store.slots[n].frozen]
         self._order = decay + no_decay      # index order used by state_dict (group_weight order)
         self.param_groups = [
             _Group(self, params=decay, lr=float(lr), betas=self.betas, eps=self.eps, weight_decay=self.weight_decay,

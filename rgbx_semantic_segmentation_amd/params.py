@@ -38,7 +38,8 @@ def partner_name(name: str) -> Optional[str]:
     if m:
         return f"backbone.extra_{m.group(1)}{m.group(2)}"
     for a, b in (("channel_proj1", "channel_proj2"), ("end_proj1", "end_proj2"),
-                 ("cross_attn.kv1", "cross_attn.kv2"), ("cross.norm1", "cross.norm2")):
+                 ("cross_attn.kv1", "cross_attn.kv2"), ("cross.norm1", "cross.norm2"),
+                 ("cross_attn.q1", "cross_attn.q2"), ("cross_attn.proj1", "cross_attn.proj2")):      # IFFM
         if a in name:
             return name.replace(a, b)
     return None
@@ -54,6 +55,7 @@ class Slot:
     storage_shape: Tuple[int, ...]
     kind: str             # "plain", "conv_taps", "conv_pad"
     decay: bool
+    frozen: bool = False  # in neither group_weight group: the optimizer never updates it
 
 
 class ParamStore:
@@ -73,10 +75,16 @@ class ParamStore:
         for mname, mod in model.named_modules():
             for pname, _ in mod.named_parameters(recurse=False):
                 owner[f"{mname}.{pname}" if mname else pname] = (mod, pname)
-        decay_ids = set()
+        # utils/init_func.py:33-57 group_weight: Linear / Conv weights decay; their biases and
+        # norm affine parameters do not; any other parameter (IFRM's lambdas) is in NEITHER
+        # group, so the reference's optimizer never steps it: a frozen slot here
+        decay_ids, grouped = set(), set()
         for mod in model.modules():
             if isinstance(mod, (nn.Linear, nn.Conv2d)):
                 decay_ids.add(id(mod.weight))
+                grouped.update(id(p) for p in mod.parameters(recurse=False))
+            elif isinstance(mod, (nn.BatchNorm2d, nn.LayerNorm, nn.GroupNorm, nn.SyncBatchNorm)):
+                grouped.update(id(p) for p in mod.parameters(recurse=False))
 
         self.slots: Dict[str, Slot] = {}
         placed = set()
@@ -103,7 +111,8 @@ class ParamStore:
             stride = numel if len(group) == 2 else _pad(numel)
             for i, n in enumerate(group):
                 assert by_name[n].shape == p.shape, (name, n)
-                self.slots[n] = Slot(n, off, stride, len(group), i, sshape, kind, id(by_name[n]) in decay_ids)
+                self.slots[n] = Slot(n, off, stride, len(group), i, sshape, kind, id(by_name[n]) in decay_ids,
+                                     id(by_name[n]) not in grouped)
                 placed.add(n)
             off += _pad(stride * len(group))
             seg_bounds[sid][1] = off
@@ -119,8 +128,8 @@ class ParamStore:
         self.params: Dict[str, nn.Parameter] = {}
         for name, p in named:
             s = self.slots[name]
-            if s.decay:
-                self.decay64[s.offset // ALIGN:(s.offset + _pad(s.stride * s.count)) // ALIGN] = 1
+            if s.decay or s.frozen:         # 1: decay, 2: frozen (the AdamW kernel skips it)
+                self.decay64[s.offset // ALIGN:(s.offset + _pad(s.stride * s.count)) // ALIGN] = 2 if s.frozen else 1
             with torch.no_grad():
                 self._param_view(self.flat, s).copy_(p.detach().to(self.device))
             newp = nn.Parameter(self._param_view(self.flat, s))
@@ -142,7 +151,7 @@ class ParamStore:
             return "conv_taps", (co, kh, kw, ci)
         if p.dim() == 4:                           # 1x1 conv / depthwise: same memory order
             return "plain", (p.shape[0], p.shape[1] * p.shape[2] * p.shape[3])
-        return "plain", tuple(p.shape)
+        return "plain", tuple(p.shape) or (1,)          # 0-dim (IFRM's lambdas): one element
 
     def _storage_view(self, buf, s: Slot, stacked: bool):
         n = 1
@@ -162,7 +171,7 @@ class ParamStore:
             ref = self._ref_shape[s.name]
             k = ref[1] * ref[2] * ref[3]
             return st[:, :k].as_strided(ref, (kp, ref[2] * ref[3], ref[3], 1))
-        return st.view(self._ref_shape[s.name])
+        return st.view(torch.Size(self._ref_shape[s.name]))
 
     # ------------------------------------------------------------------ accessors
     def slot(self, p: nn.Parameter) -> Slot:

@@ -100,12 +100,23 @@ def test_load_dualpath_model_duplicates_mit_keys(tmp_path):
             assert torch.equal(sd[k], fsd[k]), k
 
 
-def test_builder_refuses_unbuilt_fusion_modules():
-    """config.py:57-58 selects IFRM / IFFM (dual_segformer.py:316-329): not on the HIP path,
-    so the builder refuses instead of silently building FRM / FFM."""
+def test_builder_selects_improved_fusion_modules():
+    """config.py:57-58 selects IFRM / IFFM (dual_segformer.py:316-329: 'FRM' / 'FFM' the
+    originals, anything else the improved modules); the state_dict keys match the oracle's."""
     from rgbx_semantic_segmentation_amd.models.builder import EncoderDecoder
-    with pytest.raises(NotImplementedError):
-        EncoderDecoder(dict(backbone="mit_b0", num_classes=9, feature_rectify_module="IFRM"))
-    with pytest.raises(NotImplementedError):
-        EncoderDecoder(dict(backbone="mit_b0", num_classes=9, feature_fusion_module="IFFM"))
-    EncoderDecoder(dict(backbone="mit_b0", num_classes=9, feature_rectify_module="FRM", feature_fusion_module="FFM"))
+    from rgbx_semantic_segmentation_amd.models import net_utils as N
+    from oracle.cmx_ref import EncoderDecoder as RefModel, CMXConfig
+    m = EncoderDecoder(dict(backbone="mit_b0", num_classes=9, feature_rectify_module="IFRM",
+                            feature_fusion_module="IFFM"))
+    assert all(isinstance(f, N.ImprovedFeatureRectifyModule) for f in m.backbone.FRMs)
+    assert all(isinstance(f, N.ImprovedFeatureFusionModule) for f in m.backbone.FFMs)
+    ref = RefModel(CMXConfig(backbone="mit_b0", num_classes=9, feature_rectify_module="IFRM",
+                             feature_fusion_module="IFFM"))
+    assert list(m.state_dict().keys()) == list(ref.state_dict().keys())
+    m.load_state_dict(ref.state_dict(), strict=True)
+    plain = EncoderDecoder(dict(backbone="mit_b0", num_classes=9, feature_rectify_module="FRM",
+                                feature_fusion_module="FFM"))
+    assert isinstance(plain.backbone.FRMs[0], N.FeatureRectifyModule)
+    mixed = EncoderDecoder(dict(backbone="mit_b0", num_classes=9, feature_fusion_module="IFFM"))
+    assert isinstance(mixed.backbone.FRMs[0], N.FeatureRectifyModule)
+    assert isinstance(mixed.backbone.FFMs[0], N.ImprovedFeatureFusionModule)
