@@ -497,12 +497,11 @@ __device__ __forceinline__ void rs_step(const float (&v)[N], float (&o)[N / 2], 
 // are reduce-scattered over the lanes of its quad inside the wave, then summed over the 4
 // waves through LDS (reusing the dz image) into the block's (group, tile) slab.
 template <typename T, int CB>
-__device__ __forceinline__ void stage_dz_h(const T* __restrict__ da, const T* __restrict__ gp,
-                                           const T* __restrict__ h, T* dzs, T* hs, int ty0, int tx0, int H, int W,
-                                           int C) {
-  constexpr int NCG = CB / 8, NE = EYB * EXB, NIN = TYB * TXB;
-  constexpr int ITE = (NCG * NE + 255) / 256, ITI = (NCG * NIN + 255) / 256;
-  V8<T> a[ITE], g[ITE], hv[ITI];
+__device__ __forceinline__ void stage_dz(const T* __restrict__ da, const T* __restrict__ gp, T* dzs, int ty0, int tx0,
+                                         int H, int W, int C) {
+  constexpr int NCG = CB / 8, NE = EYB * EXB;
+  constexpr int ITE = (NCG * NE + 255) / 256;
+  V8<T> a[ITE], g[ITE];
 #pragma unroll
   for (int k = 0; k < ITE; ++k) {
     const int it = threadIdx.x + k * 256;
@@ -517,14 +516,6 @@ __device__ __forceinline__ void stage_dz_h(const T* __restrict__ da, const T* __
     }
   }
 #pragma unroll
-  for (int k = 0; k < ITI; ++k) {
-    const int it = threadIdx.x + k * 256;
-    const int cg = it % NCG, px = it / NCG;
-    const int y = ty0 + px / TXB, x = tx0 + px % TXB;
-    hv[k] = v8_zero<T>();
-    if (it < NCG * NIN && y < H && x < W) hv[k] = v8_load<T>(h + ((long)y * W + x) * C + cg * 8);
-  }
-#pragma unroll
   for (int k = 0; k < ITE; ++k) {
     const int it = threadIdx.x + k * 256;
     if (it < NCG * NE) {
@@ -536,15 +527,10 @@ __device__ __forceinline__ void stage_dz_h(const T* __restrict__ da, const T* __
       v8_store<T>(dzs + it * 8, v8_pack<T>(d));
     }
   }
-#pragma unroll
-  for (int k = 0; k < ITI; ++k) {
-    const int it = threadIdx.x + k * 256;
-    if (it < NCG * NIN) v8_store<T>(hs + it * 8, hv[k]);
-  }
 }
 
 template <typename T, int CB>
-__global__ __launch_bounds__(256, 2) void dw2_bwdg_kernel(const T* __restrict__ da, const T* __restrict__ h,
+__global__ __launch_bounds__(256, 3) void dw2_bwdg_kernel(const T* __restrict__ da, const T* __restrict__ h,
                                                        const T* __restrict__ gprime, const float* __restrict__ w,
                                                        T* __restrict__ dh, float* __restrict__ part, int ipg, int H,
                                                        int W, int C, int tiles_x, int tiles_y, int ncb, int nsp) {
@@ -552,30 +538,42 @@ __global__ __launch_bounds__(256, 2) void dw2_bwdg_kernel(const T* __restrict__ 
   constexpr int NE = EYB * EXB, NIN = TYB * TXB;
   constexpr int LPQ = 64 / NCQ;                     // lanes of one quad in a wave (4 or 8)
   constexpr int NV = LPQ == 4 ? 10 : 5;             // partials per lane after the in-wave reduce-scatter
+  // only the dz image lives in LDS (41 KB at CB = 64: three blocks per CU); each thread's h
+  // pixels (4 channels, 16 lanes of a pixel = one 128-B row segment) go straight to registers
+  constexpr int NIT = NIN / PPI;
   __shared__ __attribute__((aligned(16))) T dzs[NE * CB];
-  __shared__ __attribute__((aligned(16))) T hs[NIN * CB];
   static_assert(sizeof(dzs) >= 4 * 64 * NV * sizeof(float), "cross-wave reduce buffer");
+  static_assert(NIN % PPI == 0, "pixel rounds");
   const Tile2 t = tile2_of<TYB, TXB>(CB, ipg, tiles_x, tiles_y, ncb);
   const long ibase = ((long)t.g * ipg + t.img) * H * W * C + t.cb0;
-  stage_dz_h<T, CB>(da + ibase, gprime + ibase, h + ibase, dzs, hs, t.ty0, t.tx0, H, W, C);
+  stage_dz<T, CB>(da + ibase, gprime + ibase, dzs, t.ty0, t.tx0, H, W, C);
   const int cq = threadIdx.x % NCQ, pl = threadIdx.x / NCQ;
   const int c0 = t.cb0 + cq * 4;
+  V4<T> hreg[NIT];
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int it = pl + k * PPI;
+    const int y = t.ty0 + it / TXB, x = t.tx0 + it % TXB;
+    hreg[k].a = {};
+    if (y < H && x < W) hreg[k] = v4_load<T>(h + ibase + ((long)y * W + x) * C + cq * 4);
+  }
   __syncthreads();
   cmx_f2 wr[2][9];
   load_w36(w + ((long)t.g * C + c0) * 9, wr);
-  const T* hc = hs + cq * 4;
   const T* dzc = dzs + cq * 4;
   cmx_f2 acc[2][10];
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int k = 0; k < 10; ++k) acc[u][k] = pk_splat(0.f);
-  for (int it = pl; it < NIN; it += PPI) {
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int it = pl + k * PPI;
     const int r = it / TXB, c = it % TXB;
     const int y = t.ty0 + r, x = t.tx0 + c;
     if (y >= H || x >= W) continue;
     cmx_f2 hv[2];
-    v4_unpack<T>(v4_load<T>(hc + it * CB), hv);
+    v4_unpack<T>(hreg[k], hv);
     cmx_f2 g[2] = {pk_splat(0.f), pk_splat(0.f)};
 #pragma unroll
     for (int i = 0; i < 3; ++i)

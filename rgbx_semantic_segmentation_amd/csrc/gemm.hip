@@ -300,16 +300,20 @@ __device__ __forceinline__ bf16x8 frag_r(const char* img, int rb, int s, int lan
 // NS = LDS stages in the DMA ring: 2 for grids of >= 2 blocks per CU (the co-resident block
 // hides the DMA latency), 4 for grids of at most one block per CU (the ring must hide it).
 // LDS bytes of one block: the NS-stage DMA ring, reused by the fp32 epilogue tile
-template <int BM, int BN, int NS>
+// KW = k-groups of 4 waves: KW = 2 runs 8 waves on one tile, group g multiplying the g-th 64-deep
+// half of each 128-deep ring slot (twice the DMA and MFMA issue per tile: a small-grid GEMM
+// with one 4-wave block per CU is bound by that issue rate, not by the CU's memory path)
+template <int BM, int BN, int NS, int KW = 1>
 constexpr int gemm_smem_bytes() {
-  return NS * (BM + BN) * FBK * 2 > BM * (BN + 4) * 4 ? NS * (BM + BN) * FBK * 2 : BM * (BN + 4) * 4;
+  return NS * KW * (BM + BN) * FBK * 2 > KW * BM * (BN + 4) * 4 ? NS * KW * (BM + BN) * FBK * 2
+                                                                 : KW * BM * (BN + 4) * 4;
 }
 
 // One output tile (of one split / group) of problem p.  `lin` = the block's linear index
 // within the problem, in (split, group, tile) order; smem = gemm_smem_bytes<BM, BN, NS>().
-template <int BM, int BN, bool TA, bool TB, int NS>
+template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1>
 __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin, char* smem) {
-  constexpr int A_BYTES = BM * FBK * 2, STAGE = (BM + BN) * FBK * 2;
+  constexpr int A_BYTES = BM * FBK * 2, STAGE = (BM + BN) * FBK * 2, SLOT = KW * STAGE;
   constexpr int TM = BM / 64, TN = BN / 64;
 
   const int ntile = p.tiles_m * p.tiles_n;
@@ -321,9 +325,9 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
   const i32x4 rA = make_rsrc(Ag), rA2 = make_rsrc(A2g), rB = make_rsrc(Bg);
   const int i0 = tm * BM, j0 = tn * BN;
   const int nreal = p.ones_col ? p.N - 1 : p.N;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = (threadIdx.x >> 6) & 3, kg = KW == 1 ? 0 : threadIdx.x >> 8;
   const int wm = w >> 1, wn = w & 1;
-  const bool do_db = p.ones_col && tn == 0 && wn == 0;   // this wave also sums its A rows
+  const bool do_db = KW == 1 && p.ones_col && tn == 0 && wn == 0;   // this wave also sums its A rows
 
   f32x16 acc[TM][TN], accd[TM];
 #pragma unroll
@@ -334,7 +338,7 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
   }
   const bf16x8 ones = __builtin_bit_cast(bf16x8, make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u));
 
-  const int nk = (p.K + FBK - 1) / FBK;
+  const int nk = (p.K + FBK * KW - 1) / (FBK * KW);   // ring slots of KW x 64 k
   const int kt0 = z * p.kt_per_split;
   const int kt1 = min(nk, kt0 + p.kt_per_split);
 
@@ -356,7 +360,8 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
   }
 
   auto stage = [&](int kt, char* buf) {
-    const int k0 = kt * FBK;
+    const int k0 = (kt * KW + kg) * FBK;
+    buf += kg * STAGE;
     if constexpr (TA) {
       stage_r<BM>(rA, buf, p.lda, i0, p.M, k0, p.K, w, lane);
     } else {
@@ -407,6 +412,7 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
   };
 
   auto compute = [&](const char* buf) {
+    buf += kg * STAGE;
     const char* ai = buf;
     const char* bi = buf + A_BYTES;
 #pragma unroll
@@ -441,21 +447,25 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
   // refilled was last read in the previous iteration, which every wave has left.
   constexpr int PER = BM / 32 + BN / 32;        // LDS-DMA instructions per stage per wave
   auto wait_keep = [](int keep) {               // all but the `keep` most recent tiles landed
-    if (keep >= 2) vm_wait<2 * PER>();
+    if (NS > 7 && keep >= 6) vm_wait<6 * PER>();
+    else if (NS > 6 && keep == 5) vm_wait<5 * PER>();
+    else if (NS > 5 && keep == 4) vm_wait<4 * PER>();
+    else if (NS > 4 && keep == 3) vm_wait<3 * PER>();
+    else if (keep >= 2) vm_wait<2 * PER>();
     else if (keep == 1) vm_wait<PER>();
     else vm_wait<0>();
   };
   const int pro = min(NS - 1, kt1 - kt0);
 #pragma unroll
   for (int q = 0; q < NS - 1; ++q)
-    if (q < pro) stage(kt0 + q, smem + q * STAGE);
+    if (q < pro) stage(kt0 + q, smem + q * SLOT);
   wait_keep(pro - 1);
   __syncthreads();
   int cur = 0;
   for (int kt = kt0; kt < kt1; ++kt) {
     const int nxt = cur == 0 ? NS - 1 : cur - 1;
-    if (kt + NS - 1 < kt1) stage(kt + NS - 1, smem + nxt * STAGE);
-    compute(smem + cur * STAGE);
+    if (kt + NS - 1 < kt1) stage(kt + NS - 1, smem + nxt * SLOT);
+    compute(smem + cur * SLOT);
     // tiles kt+1 .. kt+ahead are in flight; retire tile kt+1, keep the rest
     const int ahead = min(NS - 1, kt1 - 1 - kt);
     wait_keep(ahead - 1);
@@ -471,7 +481,7 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
   // (fp32) row-contiguous stores, the epilogue applied on the way.
   const int r = lane & 31, h = lane >> 5;
   constexpr int CP = BN + 4;
-  float* cs = reinterpret_cast<float*>(smem);
+  float* cs = reinterpret_cast<float*>(smem) + kg * BM * CP;     // one fp32 image per k-group
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -494,26 +504,33 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
     }
   }
   __syncthreads();
-  constexpr int TPR = BN / 8, RPP = 256 / TPR;
+  cs = reinterpret_cast<float*>(smem);
+  constexpr int TPR = BN / 8, RPP = 256 * KW / TPR, NPASS = (BM + RPP - 1) / RPP;
   const int jl = (threadIdx.x % TPR) * 8;
   const int j = j0 + jl;
   if (j >= nreal) return;
   const int nv = min(8, nreal - j);
   float* wsz = p.nsplit > 1 ? slab(p, g, z) : nullptr;
 #pragma unroll 2
-  for (int pass = 0; pass < BM / RPP; ++pass) {
+  for (int pass = 0; pass < NPASS; ++pass) {
     const int il = pass * RPP + threadIdx.x / TPR;
     const int i = i0 + il;
-    if (i >= p.M) break;
+    if (il >= BM || i >= p.M) break;
     float v[8];
     const float4 u0 = *reinterpret_cast<const float4*>(cs + il * CP + jl);
     const float4 u1 = *reinterpret_cast<const float4*>(cs + il * CP + jl + 4);
     v[0] = u0.x; v[1] = u0.y; v[2] = u0.z; v[3] = u0.w; v[4] = u1.x; v[5] = u1.y; v[6] = u1.z; v[7] = u1.w;
+#pragma unroll
+    for (int q = 1; q < KW; ++q) {              // the other k-groups' partial images
+      const float4 w0 = *reinterpret_cast<const float4*>(cs + q * BM * CP + il * CP + jl);
+      const float4 w1 = *reinterpret_cast<const float4*>(cs + q * BM * CP + il * CP + jl + 4);
+      v[0] += w0.x; v[1] += w0.y; v[2] += w0.z; v[3] += w0.w; v[4] += w1.x; v[5] += w1.y; v[6] += w1.z; v[7] += w1.w;
+    }
     if (wsz) {
       float* d = wsz + (long)i * nreal + j;
       if (nv == 8 && (nreal & 3) == 0) {
-        reinterpret_cast<float4*>(d)[0] = u0;
-        reinterpret_cast<float4*>(d)[1] = u1;
+        reinterpret_cast<float4*>(d)[0] = make_float4(v[0], v[1], v[2], v[3]);
+        reinterpret_cast<float4*>(d)[1] = make_float4(v[4], v[5], v[6], v[7]);
       } else {
         for (int e = 0; e < nv; ++e) d[e] = v[e];
       }
@@ -525,10 +542,10 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
 
 // 1-D grid over (split, group, tile); each XCD gets a contiguous run of that order, i.e.
 // neighbouring tiles of one (split, group): they share A row panels and the B k-slice in L2
-template <int BM, int BN, bool TA, bool TB, int NS>
-__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const GemmArgs p) {
-  __shared__ __attribute__((aligned(1024))) char smem[gemm_smem_bytes<BM, BN, NS>()];
-  gemm_bf16_body<BM, BN, TA, TB, NS>(p, xcd_tile(blockIdx.x, p.tiles_m * p.tiles_n * p.G * p.nsplit), smem);
+template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1>
+__global__ __launch_bounds__(256 * KW, KW == 4 ? 1 : 2) void gemm_bf16_kernel(const GemmArgs p) {
+  __shared__ __attribute__((aligned(1024))) char smem[gemm_smem_bytes<BM, BN, NS, KW>()];
+  gemm_bf16_body<BM, BN, TA, TB, NS, KW>(p, xcd_tile(blockIdx.x, p.tiles_m * p.tiles_n * p.G * p.nsplit), smem);
 }
 
 // ============================================================================ grouped launch
@@ -874,10 +891,10 @@ void launch_reduce(const GemmArgs& a, int G, long groups, hipStream_t s) {
 }
 
 // ============================================================================ host side
-template <int BM, int BN, int NS>
+template <int BM, int BN, int NS, int KW = 1>
 void launch_bf16(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream_t s) {
   dim3 grid(a.tiles_m * a.tiles_n * G * nsplit);
-#define CMX_GEMM_LAUNCH(TA, TB) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, TA, TB, NS>), grid, dim3(256), 0, s, a)
+#define CMX_GEMM_LAUNCH(TA, TB) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, TA, TB, NS, KW>), grid, dim3(256 * KW), 0, s, a)
   if (!tA && !tB) CMX_GEMM_LAUNCH(false, false);
   else if (!tA && tB) CMX_GEMM_LAUNCH(false, true);
   else if (tA && tB) CMX_GEMM_LAUNCH(true, true);
@@ -891,6 +908,26 @@ void launch_bf16_ns(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStr
   // a 64 x 64 stage is only 16 KB, so a 4-deep ring (64 KB) would still leave two blocks per
   // CU; measured: no gain (2.82 vs 2.95 ms of GEMM per step), so off by default (CMX_GEMM_NS64=4)
   static const int ns64 = [] { const char* e = getenv("CMX_GEMM_NS64"); return e ? atoi(e) : 2; }();
+  // k-group blocks for 64 x 64 tiles without split-K or bias column (CMX_GEMM_KW = the largest
+  // group count allowed, default 2; 1 = off).  Measured (scripts/gemm_sweep.py, G2 M600 N512):
+  // K 2048 20.1 -> 11.9 us, K 512 7.5 -> 5.8 us at KW = 2; grids above 512 blocks and one-slot
+  // problems are slower with it (M9600 N128 K512: 9.7 -> 10.4 us), so they keep 4 waves.
+  static const int kw = [] { const char* e = getenv("CMX_GEMM_KW"); return e ? atoi(e) : 2; }();
+  if constexpr (BM == 64 && BN == 64) {
+    const int nk64 = (a.K + FBK - 1) / FBK;
+    if (kw >= 2 && nsplit == 1 && !a.ones_col && blocks <= 512 && nk64 >= 4) {
+      GemmArgs b = a;
+      if (kw >= 4 && blocks <= 256 && nk64 >= 16) {
+        b.kt_per_split = (b.K + 4 * FBK - 1) / (4 * FBK);
+        launch_bf16<64, 64, 2, 4>(b, G, nsplit, tA, tB, s);
+        return;
+      }
+      b.kt_per_split = (b.K + 2 * FBK - 1) / (2 * FBK);
+      if (blocks <= 256) launch_bf16<64, 64, 4, 2>(b, G, nsplit, tA, tB, s);
+      else launch_bf16<64, 64, 2, 2>(b, G, nsplit, tA, tB, s);
+      return;
+    }
+  }
   if (blocks <= 256 || (BM == 64 && BN == 64 && ns64 == 4)) launch_bf16<BM, BN, 4>(a, G, nsplit, tA, tB, s);
   else launch_bf16<BM, BN, 2>(a, G, nsplit, tA, tB, s);
 }

@@ -165,11 +165,16 @@ __global__ __launch_bounds__(64 * NW) void sra_fwd_fast(const bf16* __restrict__
         }
       rs += __shfl_xor(rs, 32, 64);
       l[u] = l[u] * alpha + rs;
+      // rescale the accumulator only when some lane's running max moved: alpha == 1 exactly
+      // otherwise, and after the first key tiles the max rarely moves (32 multiplies per lane
+      // per tile off the VALU, which bounds this loop beside the MFMAs)
+      if (__builtin_amdgcn_ballot_w64(mn != m[u])) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) acc[u][t][i] *= alpha;
+      }
       m[u] = mn;
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[u][t][i] *= alpha;
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)

@@ -36,7 +36,9 @@ RATIO = 4.0
 OUTLIER_RATIO = 12.0
 
 CONFIGS = {
-    # name: (backbone, H, W, batch, classes)      BASELINE.json configs[1..4]
+    # name: (backbone, H, W, batch, classes)      BASELINE.json configs[0..4] (configs[2] is
+    # configs[1] per GPU: its multi-rank path is test_gpu_dist.py / test_dist_gloo.py)
+    "config1_b0_240x320_bs1": ("mit_b0", 240, 320, 1, 9),
     "config2_b2_480x640_bs2": ("mit_b2", 480, 640, 2, 40),
     "config4_b4_480x640_bs4": ("mit_b4", 480, 640, 4, 9),
     "config5_b5_1024x1024_bs1": ("mit_b5", 1024, 1024, 1, 19),
