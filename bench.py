@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import gc
 import os
 import sys
 import time
@@ -170,8 +171,12 @@ def main():
             with torch.cuda.stream(s):
                 step()
             torch.cuda.current_stream().wait_stream(s)
+            # no garbage collection (and so no pinned-host frees recording events) inside the
+            # capture; other threads' HIP calls cannot invalidate it (thread_local mode)
+            gc.collect()
+            torch.cuda.synchronize()
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
+            with torch.cuda.graph(graph, capture_error_mode="thread_local"):
                 static_loss = step()
         except Exception as e:  # pragma: no cover - reported in the JSON line
             print(f"[bench] graph capture failed, eager mode: {e!r}", file=sys.stderr)

@@ -56,6 +56,11 @@ int cmx_act_fwd(const void* x, void* y, int64_t n, int act, int dtype, hipStream
 int cmx_act_bwd(const void* dy, const void* z, void* dx, int64_t n, int act, int dtype, hipStream_t stream);
 int cmx_partials_sum(const float* ws, float* out, int G, int nblk, int W, int accumulate, float alpha, hipStream_t stream);
 int cmx_cast_f32_bf16(const float* src, void* dst, int64_t n, hipStream_t stream);
+/* All random masks of one training step in one launch (replaces the torch.rand draws of
+   timm DropPath, dual_segformer.py:141-180, and Dropout2d, MLPDecoder.py:63, plus
+   every BatchNorm2d's num_batches_tracked += 1): dp[i] = floor(keep[i] + u) / keep[i],
+   d2[i] = (u >= p) / (1 - p), u = splitmix64(seed, *step, i); *step += 1 on the device. */
+int cmx_step_masks(const float* keep, int nkeep, float* dp, int nd2, float p, float* d2, uint64_t seed, uint64_t* step, int64_t* nbt, int nnbt, hipStream_t stream);
 /* bf16 gradient payload of the DP exchange (replaces DDP's fp32 bucket all-reduce,
    train.py:145-146 / engine.py:56): out = bf16(sum over P chunks of in, fp32 accumulate);
    and the bf16 -> fp32 copy of the gathered sums. */

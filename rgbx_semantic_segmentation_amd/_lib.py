@@ -33,7 +33,7 @@ def _ctype(decl: str):
         return ctypes.c_void_p
     base = decl.rsplit(" ", 1)[0] if " " in decl else decl
     base = base.replace("const", "").strip()
-    return {"int": ctypes.c_int32, "int64_t": ctypes.c_int64, "float": ctypes.c_float,
+    return {"int": ctypes.c_int32, "int64_t": ctypes.c_int64, "uint64_t": ctypes.c_uint64, "float": ctypes.c_float,
             "size_t": ctypes.c_size_t, "double": ctypes.c_double, "hipStream_t": ctypes.c_void_p, "void": None}[base]
 
 

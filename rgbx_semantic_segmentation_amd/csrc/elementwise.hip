@@ -153,6 +153,39 @@ static int colsum_nblk(long M) {
   return (int)(nb < 256 ? nb : 256);
 }
 
+// ---------------------------------------------------------------- per-step stochastic masks
+// One launch draws every random mask of a training step (builder._stochastic):
+//   DropPath (timm drop_path, dual_segformer.py:141-180): dp[i] = floor(keep[i] + u) / keep[i]
+//   Dropout2d (MLPDecoder.py:63, per sample and channel): d2[i] = (u >= p) / (1 - p)
+// and bumps the BN num_batches_tracked counter (BatchNorm2d.forward in train mode).  u is a
+// counter-based uniform draw: splitmix64 of (seed, step, element), the step counter kept on
+// the device, so a HIP-graph replay draws fresh masks with no host involvement.  One block:
+// every thread reads the step before thread 0 advances it.
+__device__ __forceinline__ float u01(unsigned long long seed, unsigned long long step, unsigned long long i) {
+  unsigned long long z = seed ^ (step * 0x9E3779B97F4A7C15ull) ^ (i * 0xD1B54A32D192ED03ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.f / 16777216.f);   // 24 random bits -> [0, 1)
+}
+
+__global__ __launch_bounds__(256) void step_masks_kernel(const float* __restrict__ keep, int nkeep,
+                                                         float* __restrict__ dp, int nd2, float p,
+                                                         float* __restrict__ d2, unsigned long long seed,
+                                                         unsigned long long* __restrict__ step,
+                                                         long long* __restrict__ nbt, int nnbt) {
+  const unsigned long long st = *step;
+  for (int i = threadIdx.x; i < nkeep; i += blockDim.x) {
+    const float k = keep[i];
+    dp[i] = floorf(k + u01(seed, st, (unsigned long long)i)) / k;
+  }
+  for (int i = threadIdx.x; i < nd2; i += blockDim.x)
+    d2[i] = u01(seed ^ 0x5851F42D4C957F2Dull, st, (unsigned long long)i) >= p ? 1.f / (1.f - p) : 0.f;
+  for (int i = threadIdx.x; i < nnbt; i += blockDim.x) nbt[i] += 1;   // one counter per BatchNorm
+  __syncthreads();
+  if (threadIdx.x == 0) *step = st + 1;
+}
+
 extern "C" {
 
 int cmx_residual_add(const void* x, const void* y, const float* scale, void* out, long n_per_sample,
@@ -253,6 +286,15 @@ int cmx_colsum(const void* x, float* out, float* ws, long M, int G, int N, long 
   int st = cmx_check_launch("colsum");
   if (st) return st;
   return cmx_reduce_partials(ws, out, G, nb, N, accumulate, alpha, s);
+}
+
+int cmx_step_masks(const float* keep, int nkeep, float* dp, int nd2, float p, float* d2, uint64_t seed,
+                   uint64_t* step, int64_t* nbt, int nnbt, hipStream_t s) {
+  CMX_REQUIRE(nkeep >= 0 && nd2 >= 0 && step && (nkeep == 0 || (keep && dp)) && (nd2 == 0 || (d2 && p < 1.f)),
+              CMX_ERR_ARG, "step_masks: nkeep=%d nd2=%d p=%f", nkeep, nd2, p);
+  hipLaunchKernelGGL(step_masks_kernel, dim3(1), dim3(256), 0, s, keep, nkeep, dp, nd2, p, d2,
+                     (unsigned long long)seed, (unsigned long long*)step, (long long*)nbt, nbt ? nnbt : 0);
+  return cmx_check_launch("step_masks");
 }
 
 }  // extern "C"

@@ -446,7 +446,8 @@ void sra_dq_fast_launch(const void* q, const void* k, const void* v, const void*
                         long os, long dos, long dqs, float sl2, float scale, hipStream_t s);
 int sra_dkv_fast_chunks(int Bt, int N, int Nk, int heads);
 void sra_dkv_fast_launch(const void* q, const void* k, const void* v, const void* dout, const float* lse,
-                         const float* Dws, float* ws_dk, float* ws_dv, int Bt, int N, int Nk, int heads, long qs,
+                         const float* Dws, float* ws_dk, float* ws_dv, void* dk, void* dv, long dkvs, int Bt, int N,
+                         int Nk, int heads, long qs,
                          long kvs, long dos, int nchunk, float sl2, float scale, hipStream_t s);
 
 #define SRA_D_DISPATCH(D, ...)                                              \
@@ -515,12 +516,14 @@ int cmx_sra_attn_bwd(const void* q, const void* k, const void* v, const void* o,
                          (const T*)q, (const T*)k, (const T*)v, (const T*)o, (const T*)dout, lse, Dws,
                          (T*)dq, N, Nk, heads, qs, kvs, os, dos, dqs, sl2, scale);
     if (fast)
-      sra_dkv_fast_launch(q, k, v, dout, lse, Dws, ws_dk, ws_dv, Bt, N, Nk, heads, qs, kvs, dos, nc, sl2, scale, s);
+      sra_dkv_fast_launch(q, k, v, dout, lse, Dws, ws_dk, ws_dv, dk, dv, dkvs, Bt, N, Nk, heads, qs, kvs, dos, nc, sl2,
+                          scale, s);
     else
       hipLaunchKernelGGL((sra_bwd_dkv_kernel<T, DD>), dim3(cdiv(Nk, BK), heads, Bt * nc), dim3(256), 0, s,
                          (const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse, Dws, ws_dk, ws_dv, Bt,
                          N, Nk, heads, qs, kvs, dos, qc, nc, sl2, scale);
     const long total = (long)Bt * heads * Nk * D;     // D % 4 == 0: 4-wide groups never straddle a row
+    if (!(fast && nc == 1))                           // one chunk: the fast kernel wrote dK / dV
     hipLaunchKernelGGL((sra_dkv_reduce_kernel<T>), dim3(cdiv(total / 4, 64)), dim3(256), 0, s, ws_dk, ws_dv, (T*)dk,
                        (T*)dv, Bt, Nk, heads, D, dkvs, nc);
   }));

@@ -20,6 +20,7 @@
 // cross-half shuffle; each wave owns QW 32-query sub-tiles for MFMA/VALU overlap.
 #include "cmx_mfma.h"
 #include "cmx_dma.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -335,6 +336,7 @@ constexpr int DKV_TILE_BYTES = 2 * QT * ROWB + 2 * QT * 4;   // Q, dO images + l
 __global__ __launch_bounds__(64 * (NKP_MAX / 32)) void sra_dkv_fast(
     const bf16* __restrict__ q, const bf16* __restrict__ k, const bf16* __restrict__ v, const bf16* __restrict__ dout,
     const float* __restrict__ lse, const float* __restrict__ Dws, float* __restrict__ ws_dk, float* __restrict__ ws_dv,
+    bf16* __restrict__ dk, bf16* __restrict__ dv, long dkvs,
     int Bt, int N, int Nk, int heads, long qs, long kvs, long dos, int QC, int nchunk, float sl2, float scale) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * DKV_TILE_BYTES];
   const int nw = blockDim.x >> 6;
@@ -434,6 +436,21 @@ __global__ __launch_bounds__(64 * (NKP_MAX / 32)) void sra_dkv_fast(
     cur ^= 1;
   }
   if (key >= Nk) return;
+  if (nchunk == 1) {            // one query chunk: this workgroup's sums are the gradients
+    bf16* ok = dk + ((long)b * Nk + key) * dkvs + head * HD;
+    bf16* ov = dv + ((long)b * Nk + key) * dkvs + head * HD;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = 32 * t + 8 * g4 + 4 * h;
+        *reinterpret_cast<uint2*>(ok + d) = make_uint2(pack2_bf16(ak[t][4 * g4] * scale, ak[t][4 * g4 + 1] * scale),
+                                                       pack2_bf16(ak[t][4 * g4 + 2] * scale, ak[t][4 * g4 + 3] * scale));
+        *reinterpret_cast<uint2*>(ov + d) = make_uint2(pack2_bf16(av[t][4 * g4], av[t][4 * g4 + 1]),
+                                                       pack2_bf16(av[t][4 * g4 + 2], av[t][4 * g4 + 3]));
+      }
+    return;
+  }
   const long o = ((((long)c * Bt + b) * heads + head) * Nk + key) * HD;
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -527,6 +544,10 @@ int sra_dkv_fast_chunks(int Bt, int N, int Nk, int heads) {
   // (the SRA layers have one key chunk; IFFM's full cross attention has Nk / 320 of them,
   // which already fill the chip, and every extra query chunk is another Nk x D slab to reduce)
   const long base = (long)Bt * heads * ((Nk + NKP_MAX - 1) / NKP_MAX);
+  // short query sequences: one chunk, the gradients written directly (no fp32 slabs, no
+  // reduce launch); CMX_SRA_DKV_DIRECT = the largest N that takes it
+  static const int direct_n = [] { const char* e = getenv("CMX_SRA_DKV_DIRECT"); return e ? atoi(e) : 0; }();
+  if (N <= direct_n) return 1;
   long nc = (256 + base - 1) / base;
   const long maxc = (N + QT - 1) / QT;
   if (nc > maxc) nc = maxc;
@@ -535,13 +556,14 @@ int sra_dkv_fast_chunks(int Bt, int N, int Nk, int heads) {
 }
 
 void sra_dkv_fast_launch(const void* q, const void* k, const void* v, const void* dout, const float* lse,
-                         const float* Dws, float* ws_dk, float* ws_dv, int Bt, int N, int Nk, int heads, long qs,
-                         long kvs, long dos, int nchunk, float sl2, float scale, hipStream_t s) {
+                         const float* Dws, float* ws_dk, float* ws_dv, void* dk, void* dv, long dkvs, int Bt, int N,
+                         int Nk, int heads, long qs, long kvs, long dos, int nchunk, float sl2, float scale,
+                         hipStream_t s) {
   const int nkw = ((Nk < NKP_MAX ? Nk : NKP_MAX) + 31) / 32 * 32;   // one 32-key sub-tile per wave
   const int nkc = (Nk + NKP_MAX - 1) / NKP_MAX;                       // key chunks (Nk > NKP_MAX)
   int qc = (N + nchunk - 1) / nchunk;
   qc = (qc + QT - 1) / QT * QT;
   hipLaunchKernelGGL(sra_dkv_fast, dim3(nchunk * nkc, heads, Bt), dim3(2 * nkw), 0, s, (const bf16*)q, (const bf16*)k,
-                     (const bf16*)v, (const bf16*)dout, lse, Dws, ws_dk, ws_dv, Bt, N, Nk, heads, qs, kvs, dos, qc,
-                     nchunk, sl2, scale);
+                     (const bf16*)v, (const bf16*)dout, lse, Dws, ws_dk, ws_dv, (bf16*)dk, (bf16*)dv, dkvs, Bt, N,
+                     Nk, heads, qs, kvs, dos, qc, nchunk, sl2, scale);
 }

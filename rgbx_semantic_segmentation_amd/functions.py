@@ -607,30 +607,53 @@ def conv(store, mod, x, G, NI, H, W, C, stride, pad, nchw=False):
 
 
 # ---------------------------------------------------------------------------- FFM cross attention
-class CrossAttentionF(Function):
-    """CrossAttention.forward (net_utils.py:199-214) on grouped tensors:
-    u (G=2, M, C) is the query (raw, no projection), kv (2, M, 2C) = [k | v].
-    ctx_g = softmax_{-2}(k_g^T v_g * s); out_g = u_g @ ctx_{1-g}.
+def _cross_attn_fwd(u, kv, B, N, heads, D):
+    """CrossAttention forward (net_utils.py:199-214) on grouped tensors: u (G=2, M, C) is the
+    query (raw, no projection), kv (2, M, 2C) = [k | v]; ctx_g = softmax_{-2}(k_g^T v_g * s),
+    out_g = u_g @ ctx_{1-g}.  Every token contraction is a batched MFMA GEMM over the G * B
+    (modality, image) pairs with K = C (csrc/ffm_attn.hip explains the block-diagonal
+    operands): KV = k^T v (fp32), the softmax + crossing kernel, out = u @ BDt^T."""
+    G, M, C = u.shape
+    GB = G * B
+    kvb = kv.view(GB, N, 2 * C)
+    k, v = kvb[..., :C], kvb[..., C:]
+    KV = torch.empty(GB, C, C, dtype=torch.float32, device=u.device)
+    K.gemm(k.transpose(1, 2), v.transpose(1, 2), KV, out_mode=1)            # k^T v per (g, b)
+    P = torch.empty(GB, heads, D, D, dtype=torch.float32, device=u.device)
+    bdt = torch.empty(GB, C, C, dtype=u.dtype, device=u.device)
+    K.call("cmx_ffm_ctx_fwd", K.ptr(KV), K.ptr(P), K.ptr(bdt), G, B, heads, D, D ** -0.5, K.dtype_code(u), K.stream())
+    out = torch.empty(G, M, C, dtype=u.dtype, device=u.device)
+    K.gemm(u.view(GB, N, C), bdt, out.view(GB, N, C))                      # u_g @ ctx_{1-g} per head
+    return out, P, bdt
 
-    Every token contraction is a batched MFMA GEMM over the G * B (modality, image) pairs with
-    K = C (csrc/ffm_attn.hip explains the block-diagonal operands): forward KV = k^T v (fp32),
-    the softmax + crossing kernel, out = u @ BDt^T; backward du = dout @ BD, dBD = u^T dout,
-    the softmax-backward kernel, dk = v @ dA^T and dv = k @ dA written into the halves of dkv."""
+
+def _cross_attn_bwd(dout, u, kv, P, bdt, B, N, heads, D, du):
+    """Backward of _cross_attn_fwd: du = dout @ BD written into ``du`` (any row stride),
+    dBD = u^T dout, the softmax-backward kernel, dk = v @ dA^T and dv = k @ dA into the halves
+    of the returned dkv."""
+    G, M, C = u.shape
+    GB = G * B
+    dout = _c(dout).view(GB, N, C)
+    K.gemm(dout, bdt.transpose(1, 2), du.view(GB, N, C))                   # dout @ BD
+    dBD = torch.empty(GB, C, C, dtype=torch.float32, device=u.device)
+    K.gemm(u.view(GB, N, C).transpose(1, 2), dout.transpose(1, 2), dBD, out_mode=1)      # u^T dout
+    dA = torch.empty(GB, C, C, dtype=u.dtype, device=u.device)
+    K.call("cmx_ffm_ctx_bwd", K.ptr(P), K.ptr(dBD), K.ptr(dA), G, B, heads, D, D ** -0.5, K.dtype_code(u), K.stream())
+    kvb = kv.view(GB, N, 2 * C)
+    dkv = torch.empty(G, M, 2 * C, dtype=kv.dtype, device=kv.device)
+    dkvb = dkv.view(GB, N, 2 * C)
+    K.gemm(kvb[..., C:], dA, dkvb[..., :C])                                # dk = v dA^T
+    K.gemm(kvb[..., :C], dA.transpose(1, 2), dkvb[..., C:])                # dv = k dA
+    return dkv
+
+
+class CrossAttentionF(Function):
+    """CrossAttention.forward (net_utils.py:199-214) alone (the module test's entry point;
+    the model runs it inside CrossPathF)."""
 
     @staticmethod
     def forward(ctx, u, kv, B, N, heads, D):
-        G, M, C = u.shape
-        GB = G * B
-        scale = D ** -0.5
-        kvb = kv.view(GB, N, 2 * C)
-        k, v = kvb[..., :C], kvb[..., C:]
-        KV = torch.empty(GB, C, C, dtype=torch.float32, device=u.device)
-        K.gemm(k.transpose(1, 2), v.transpose(1, 2), KV, out_mode=1)            # k^T v per (g, b)
-        P = torch.empty(GB, heads, D, D, dtype=torch.float32, device=u.device)
-        bdt = torch.empty(GB, C, C, dtype=u.dtype, device=u.device)
-        K.call("cmx_ffm_ctx_fwd", K.ptr(KV), K.ptr(P), K.ptr(bdt), G, B, heads, D, scale, K.dtype_code(u), K.stream())
-        out = torch.empty(G, M, C, dtype=u.dtype, device=u.device)
-        K.gemm(u.view(GB, N, C), bdt, out.view(GB, N, C))                      # u_g @ ctx_{1-g} per head
+        out, P, bdt = _cross_attn_fwd(u, kv, B, N, heads, D)
         ctx.save_for_backward(u, kv, P, bdt)
         ctx.meta = (B, N, heads, D)
         return out
@@ -639,23 +662,131 @@ class CrossAttentionF(Function):
     def backward(ctx, dout):
         u, kv, P, bdt = ctx.saved_tensors
         B, N, heads, D = ctx.meta
-        G, M, C = u.shape
-        GB = G * B
-        scale = D ** -0.5
-        dout = _c(dout).view(GB, N, C)
-        ub = u.view(GB, N, C)
-        du = torch.empty(G, M, C, dtype=u.dtype, device=u.device)
-        K.gemm(dout, bdt.transpose(1, 2), du.view(GB, N, C))                  # dout @ BD
-        dBD = torch.empty(GB, C, C, dtype=torch.float32, device=u.device)
-        K.gemm(ub.transpose(1, 2), dout.transpose(1, 2), dBD, out_mode=1)      # u^T dout
-        dA = torch.empty(GB, C, C, dtype=u.dtype, device=u.device)
-        K.call("cmx_ffm_ctx_bwd", K.ptr(P), K.ptr(dBD), K.ptr(dA), G, B, heads, D, scale, K.dtype_code(u), K.stream())
-        kvb = kv.view(GB, N, 2 * C)
-        dkv = torch.empty(G, M, 2 * C, dtype=kv.dtype, device=kv.device)
-        dkvb = dkv.view(GB, N, 2 * C)
-        K.gemm(kvb[..., C:], dA, dkvb[..., :C])                                # dk = v dA^T
-        K.gemm(kvb[..., :C], dA.transpose(1, 2), dkvb[..., C:])                # dv = k dA
+        du = torch.empty_like(u)
+        dkv = _cross_attn_bwd(dout, u, kv, P, bdt, B, N, heads, D, du)
         return du, dkv, None, None, None, None
+
+
+def _stacked_w(store, p):
+    W = store.w(p)
+    return W.view(W.shape[0], W.shape[1], -1)
+
+
+def _stacked_g(store, p):
+    Wg = store.g(p)
+    return Wg.view(Wg.shape[0], Wg.shape[1], -1)
+
+
+class CrossPathF(Function):
+    """FFM's CrossPath (net_utils.py:262-281) for both modalities as ONE autograd node:
+    a = relu(channel_proj(x)); y, u = a.chunk(2, -1); v = CrossAttention(u, kv(u));
+    e = x + end_proj(cat(y, v)).
+
+    As separate nodes, x (read by channel_proj and the residual) and u (read by kv and the
+    attention) each collected two gradients that autograd summed in extra passes, and the
+    (y, u) split concatenated its two gradients in a third.  Here the backward writes dy and
+    du straight into the halves of one (G, M, 2C) buffer (strided GEMM outputs), folds kv's
+    dgrad into du and the residual gradient into dx through the GEMM residual epilogue
+    (C = R + A W, in place), so x and u get one gradient each."""
+
+    @staticmethod
+    def forward(ctx, x, Wcp, Wgcp, bcp, bgcp, Wkv, Wgkv, Wend, Wgend, bend, bgend, B, N, heads, anchor):
+        G, M, C = x.shape
+        D = C // heads
+        a = torch.empty(G, M, 2 * C, dtype=x.dtype, device=x.device)
+        _fwd_gemm(x, Wcp, bcp, a, act="relu")
+        y, u = a[..., :C], a[..., C:]
+        kv = torch.empty(G, M, 2 * C, dtype=x.dtype, device=x.device)
+        _fwd_gemm(u, Wkv, None, kv)
+        v, P, bdt = _cross_attn_fwd(u, kv, B, N, heads, D)
+        e = torch.empty(G, M, C, dtype=x.dtype, device=x.device)
+        _fwd_gemm(y, Wend, bend, e, res=x, x2=v)
+        ctx.save_for_backward(x, a, kv, v, P, bdt, Wcp, Wkv, Wend)
+        ctx.meta = (Wgcp, bgcp, Wgkv, Wgend, bgend, B, N, heads, D)
+        return e
+
+    @staticmethod
+    def backward(ctx, de):
+        x, a, kv, v, P, bdt, Wcp, Wkv, Wend = ctx.saved_tensors
+        Wgcp, bgcp, Wgkv, Wgend, bgend, B, N, heads, D = ctx.meta
+        G, M, C = x.shape
+        de = _c(de)
+        y, u = a[..., :C], a[..., C:]
+        da = torch.empty(G, M, 2 * C, dtype=x.dtype, device=x.device)
+        dy, du = da[..., :C], da[..., C:]
+        # end_proj on cat(y, v): dy into the first half of da, dv apart; the residual passes de
+        _dgrad(de, Wend[:, :, :C], dy)
+        dv = _dgrad(de, Wend[:, :, C:], torch.empty_like(v))
+        _wgrad_into(de, y, Wgend[:, :, :C], bgend)
+        _wgrad_into(de, v, Wgend[:, :, C:])
+        # attention: du (second half of da) = dout @ BD, then += dkv @ Wkv (kv's dgrad, in place)
+        dkv = _cross_attn_bwd(dv, u, kv, P, bdt, B, N, heads, D, du)
+        K.gemm(dkv, Wkv.transpose(1, 2), du, residual=du)
+        _wgrad_into(dkv, u, Wgkv)
+        # channel_proj + ReLU: dx = relu'(a) * da @ Wcp + de (residual epilogue)
+        dz = K.act_bwd(da, a, "relu")
+        dx = torch.empty_like(x)
+        K.gemm(dz, Wcp.transpose(1, 2), dx, residual=de)
+        _wgrad_into(dz, x, Wgcp, bgcp)
+        return (dx,) + (None,) * 14
+
+
+def cross_path(store, cp, x, B, N, heads):
+    w = lambda p: _stacked_w(store, p)   # noqa: E731
+    g = lambda p: _stacked_g(store, p)   # noqa: E731
+    G = x.shape[0]
+    pj, kvm, ep = cp.channel_proj1, cp.cross_attn.kv1, cp.end_proj1
+    return CrossPathF.apply(x, w(pj.weight), g(pj.weight), store.w(pj.bias, compute=False).view(G, -1),
+                            store.g(pj.bias).view(G, -1), w(kvm.weight), g(kvm.weight), w(ep.weight), g(ep.weight),
+                            store.w(ep.bias, compute=False).view(G, -1), store.g(ep.bias).view(G, -1), B, N, heads,
+                            pj.weight)
+
+
+class PairEmbedF(Function):
+    """ChannelEmbed's two 1x1 convs on cat(o[0], o[1]) (net_utils.py:318-330: `residual` and
+    `channel_embed[0]`) as ONE autograd node over the modality pair o (2, M, C): both read
+    the same two halves, so as separate nodes each half collected two gradients (two autograd
+    adds) and the pair split concatenated them (a copy).  The backward writes do[g] =
+    dres @ Wres[:, gC:(g+1)C] for both g in one G = 2 GEMM (dres broadcast over g) and adds
+    dt @ Wce0[:, gC:(g+1)C] through the residual epilogue, in place."""
+
+    @staticmethod
+    def forward(ctx, o, Wres, Wgres, Wce, Wgce, bce, bgce, anchor):
+        _, M, C = o.shape
+        res = torch.empty(1, M, C, dtype=o.dtype, device=o.device)
+        _fwd_gemm(o[0:1], Wres, None, res, x2=o[1:2])
+        t = torch.empty(1, M, Wce.shape[1], dtype=o.dtype, device=o.device)
+        _fwd_gemm(o[0:1], Wce, bce, t, x2=o[1:2])
+        ctx.save_for_backward(o, Wres, Wce)
+        ctx.meta = (Wgres, Wgce, bgce)
+        return res, t
+
+    @staticmethod
+    def backward(ctx, dres, dt):
+        o, Wres, Wce = ctx.saved_tensors
+        Wgres, Wgce, bgce = ctx.meta
+        _, M, C = o.shape
+        dres, dt = _c(dres), _c(dt)
+        do = torch.empty_like(o)
+
+        def halves(W):              # (1, N, 2C) -> (2, N, C): [g] = W[:, gC:(g+1)C]
+            return W[0].view(W.shape[1], 2, C).permute(1, 0, 2)
+        K.gemm(dres.expand(2, M, dres.shape[2]), halves(Wres).transpose(1, 2), do)
+        K.gemm(dt.expand(2, M, dt.shape[2]), halves(Wce).transpose(1, 2), do, residual=do)
+        _wgrad_into(dres, o[0:1], Wgres[:, :, :C])
+        _wgrad_into(dres, o[1:2], Wgres[:, :, C:])
+        _wgrad_into(dt, o[0:1], Wgce[:, :, :C], bgce)
+        _wgrad_into(dt, o[1:2], Wgce[:, :, C:])
+        return (do,) + (None,) * 7
+
+
+def pair_embed(store, ce, o):
+    w = lambda p: _stacked_w(store, p)   # noqa: E731
+    g = lambda p: _stacked_g(store, p)   # noqa: E731
+    c0 = ce.channel_embed[0]
+    return PairEmbedF.apply(o, w(ce.residual.weight), g(ce.residual.weight), w(c0.weight), g(c0.weight),
+                            store.w(c0.bias, compute=False).view(1, -1), store.g(c0.bias).view(1, -1),
+                            ce.residual.weight)
 
 
 # ---------------------------------------------------------------------------- FRM

@@ -31,6 +31,7 @@ import torch
 import torch.nn as nn
 
 from .. import functions as F
+from .. import kernels as K
 from ..params import ParamStore
 from .decoders.MLPDecoder import DecoderHead
 from .encoders.dual_segformer import BACKBONES, MIT_SPECS, load_dualpath_model
@@ -189,11 +190,19 @@ class EncoderDecoder(nn.Module):
             d2 = (d2.to(device=device, dtype=torch.float32) / (1 - p)).contiguous() if (p > 0 and d2 is not None) \
                 else None
             return (dp / keep).contiguous(), d2
-        dp = torch.floor(keep + torch.rand(keep.shape, device=device)) / keep
-        d2 = None
-        if p > 0:
-            d2 = (torch.rand(B, E, device=device) >= p).to(torch.float32) / (1 - p)
-        return dp.contiguous(), d2
+        # one launch draws both masks (counter-based RNG, step counter on the device, so graph
+        # replays draw fresh masks) and bumps num_batches_tracked: cmx_step_masks
+        st = self.__dict__.get("_mask_state")
+        if st is None or st[1].device != keep.device:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())       # from torch's host generator
+            st = self.__dict__["_mask_state"] = (seed, torch.zeros(1, dtype=torch.int64, device=device))
+        dp = torch.empty_like(keep)
+        d2 = torch.empty(B, E, device=device) if p > 0 else None
+        nbt = getattr(self, "_nbt", None)
+        K.call("cmx_step_masks", K.ptr(keep), keep.numel(), K.ptr(dp), B * E if d2 is not None else 0, float(p),
+               K.ptr(d2), st[0], K.ptr(st[1]), K.ptr(nbt), nbt.numel() if nbt is not None else 0, K.stream())
+        self._nbt_bumped = True
+        return dp, d2
 
     # ------------------------------------------------------------------ forward
     def _logits_lowres(self, rgb, modal_x):
@@ -204,9 +213,10 @@ class EncoderDecoder(nn.Module):
         if self.training and torch.is_grad_enabled() and not torch.cuda.is_current_stream_capturing():
             self.store.ensure_grads()
         images = torch.cat([rgb, modal_x], 0).to(device=dev, dtype=torch.float32).contiguous()
+        self._nbt_bumped = False
         dp, d2 = self._stochastic(B, dev)
         group = self.process_group if (self.sync_bn and self.training) else None
-        if self.training and getattr(self, "_nbt", None) is not None:
+        if self.training and getattr(self, "_nbt", None) is not None and not self._nbt_bumped:
             self._nbt.add_(1)
         feats, grids = self.backbone.run(self.store, images, B, H, W, self.training, dp)
         logits = self.decode_head.run(self.store, feats, grids, B, self.training, dscale=d2, group=group)

@@ -111,15 +111,10 @@ class FeatureFusionModule(nn.Module):             # net_utils.py:354-384
         cp, ce = self.cross, self.channel_emb
         heads = self.num_heads
         x = r.view(G, M, C)
-        a = F.glinear(store, cp.channel_proj1.weight, cp.channel_proj1.bias, x, act="relu")
-        y, u = F.split(a, C, -1)
-        kv = F.glinear(store, cp.cross_attn.kv1.weight, None, u)
-        v = F.CrossAttentionF.apply(u, kv, B, N, heads, C // heads)
-        e = F.glinear(store, cp.end_proj1.weight, cp.end_proj1.bias, y, v, res=x)     # x + end_proj(cat(y, v))
+        # relu(channel_proj) -> chunk -> kv + cross attention -> x + end_proj(cat(y, v)): one node
+        e = F.cross_path(store, cp, x, B, N, heads)
         o = F.layernorm(store, cp.norm1, e, G)
-        o1, o2 = F.split(o, 1, 0)
-        res = F.glinear(store, ce.residual.weight, None, o1, o2)
-        t = F.glinear(store, ce.channel_embed[0].weight, ce.channel_embed[0].bias, o1, o2)
+        res, t = F.pair_embed(store, ce, o)             # residual / channel_embed[0] on cat(o[0], o[1])
         t = F.dwconv(store, ce.channel_embed[1], t, B, B, H, W, "relu")
         t = F.glinear(store, ce.channel_embed[3].weight, ce.channel_embed[3].bias, t)
         s = F.batchnorm(store, ce.channel_embed[4], t.view(M, C), training, res=res.view(M, C))

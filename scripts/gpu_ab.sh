@@ -4,9 +4,6 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 T="timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu"
-$T tests/test_gpu_gemm.py tests/test_gpu_dwconv.py tests/test_gpu_grouped.py tests/test_gpu_kernels.py > gpurun_out/pt_a.log 2>&1; rc=$?; tail -2 gpurun_out/pt_a.log; [ $rc -le 1 ] || exit $rc
-CMX_GEMM_KW=4 $T tests/test_gpu_gemm.py > gpurun_out/pt_b.log 2>&1; rc=$?; tail -2 gpurun_out/pt_b.log; [ $rc -le 1 ] || exit $rc
-timeout -k 10 120 python -u scripts/bench_dw.py || exit 1
-timeout -k 10 120 python -u scripts/bench_sra.py || exit 1
-CMX_GEMM_KW=4 timeout -k 10 200 python -u scripts/gemm_sweep.py || exit 1
-STEPS=60 VAR=CMX_GEMM_KW VALUES="2 4 2 4" bash scripts/env_sweep.sh
+CMX_SRA_DKV_DIRECT=100000 $T tests/test_gpu_kernels.py tests/test_gpu_improved.py > gpurun_out/pt_a.log 2>&1; rc=$?; tail -2 gpurun_out/pt_a.log; [ $rc -le 1 ] || exit $rc
+for v in 0 300 1200 4800; do echo "CMX_SRA_DKV_DIRECT=$v"; CMX_SRA_DKV_DIRECT=$v timeout -k 10 120 python -u scripts/bench_sra.py 2>/dev/null || exit 1; done
+STEPS=60 VAR=CMX_SRA_DKV_DIRECT VALUES="0 300 1200 0 300 1200" bash scripts/env_sweep.sh

@@ -7,6 +7,7 @@ import random
 
 import numpy as np
 import pytest
+import gc
 import torch
 
 from oracle import augment_ref as A
@@ -120,3 +121,7 @@ def test_train_pre_batch_and_loader(dev, tmp_path):
         assert torch.isfinite(mb["data"]).all() and len(mb["fn"]) == 2
         n += 1
     assert n == 2
+    # release the loader's pinned host buffers now, not at a later test's garbage collection
+    del loader, mb
+    gc.collect()
+    torch.cuda.synchronize()

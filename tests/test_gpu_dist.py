@@ -6,6 +6,7 @@ runs it for N > 1.  At world size 1 every collective is an identity, so the DP s
 equal the plain step (BatchNorm2d, no process group) to rounding.
 
 8-GPU runs are the driver's; this exercises every line of the N > 1 path that one GPU can."""
+import gc
 import os
 
 import pytest
@@ -42,8 +43,10 @@ def _run(model, opt, batch, captured_steps=2):
     with torch.cuda.stream(s):
         step()
     torch.cuda.current_stream().wait_stream(s)
+    gc.collect()                       # no pinned-host frees of earlier tests inside the capture
+    torch.cuda.synchronize()
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
+    with torch.cuda.graph(graph, capture_error_mode="thread_local"):
         step()
     for _ in range(captured_steps):
         graph.replay()
