@@ -984,13 +984,18 @@ int tile_policy() {
   return p;
 }
 
-// Small-K policy (CMX_GEMM_SMALLK=k): problems with K <= k take 64 x 64 tiles whatever their
-// tile count -- a one- or two-k-tile block is a latency chain (DMA, MFMA, epilogue), and the
-// 128 x 128 tile's 67 KB epilogue image allows only two such chains per CU.
+// Small-K policy (CMX_GEMM_SMALLK=k, default 256): problems with K <= k take 64 x 64 tiles
+// whatever their tile count -- a block of one to four k-tiles is a latency chain (DMA, MFMA,
+// epilogue), and the 128 x 128 tile's 67 KB epilogue image allows only two such chains per CU
+// where 64 x 64 blocks (32 KB) run four or more.  Measured on the B2 step's GEMM census
+// (profiles/r02_r_gemm_census.txt): the stage-1/2 MLP and decoder-input GEMMs
+// (M 38400 / 9600, K 64-256) gain 10-25 % each, 2558 -> 2485 us per step at k = 640; the one
+// 512 x 512 decoder GEMM (K 512) is the shape that keeps 128-wide tiles faster, hence 256.
+// A narrow output (N <= 64, K 512: the decoder's class / c1 products) also takes 64 x 64.
 int smallk_policy() {
   static const int p = [] {
     const char* e = getenv("CMX_GEMM_SMALLK");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 256;
   }();
   return p;
 }
@@ -1002,7 +1007,7 @@ void plan_tiles(int G, int M, int nb, int K, int* bm, int* bn) {
     const long t128 = (long)cdiv(M, *bm) * cdiv(nb, *bn) * G;
     if (t128 < 240) *bm = *bn = 64;
   }
-  if (K <= smallk_policy()) *bm = *bn = 64;
+  if (K <= smallk_policy() || (nb <= 64 && smallk_policy() > 0)) *bm = *bn = 64;
 }
 
 // split factor for the bf16 path: one block per CU when the output has few tiles (each split

@@ -89,10 +89,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
                                                      long rps, const T* __restrict__ dy2) {
   constexpr int V = VecT<T>::N;
   constexpr int RPB = 256 / TPR;
-  // column partials meet in LDS in passes of CAP columns (<= 32 KB of LDS for any TPR)
-  constexpr int CAP0 = 4096 / (256 / TPR) < 512 ? 4096 / (256 / TPR) : 512;
-  constexpr int CAP = NCH * TPR * V > CAP0 ? CAP0 : NCH * TPR * V;
-  __shared__ float red[256 / TPR][2][CAP];
+  __shared__ float red[256 / TPR][2][NCH * TPR * V > 512 ? 512 : NCH * TPR * V];
   const int g = blockIdx.y;
   const int lane = threadIdx.x % TPR;
   const int rslot = threadIdx.x / TPR;
@@ -161,21 +158,21 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
   }
   // block reduction of the column partials over the RPB row slots
   float* out = ws + ((long)g * gridDim.x + blockIdx.x) * 2 * C;
-  for (int base = 0; base < C; base += CAP) {
+  for (int base = 0; base < C; base += 512) {
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
       const int ch = lane + k * TPR;
 #pragma unroll
       for (int j = 0; j < V; ++j) {
         const int c = ch * V + j - base;
-        if (ch < nchunk && c >= 0 && c < CAP) {
+        if (ch < nchunk && c >= 0 && c < 512) {
           red[rslot][0][c] = dg[k][j];
           red[rslot][1][c] = db[k][j];
         }
       }
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < CAP && base + c < C; c += 256) {
+    for (int c = threadIdx.x; c < 512 && base + c < C; c += 256) {
       float a = 0.f, b = 0.f;
       for (int r = 0; r < RPB; ++r) { a += red[r][0][c]; b += red[r][1][c]; }
       out[base + c] = a;
@@ -230,27 +227,10 @@ int cmx_reduce_partials_strided(const float* ws, float* out, int nblk, int W, in
   return cmx_check_launch("reduce_partials_strided");
 }
 
-static int ln_tpr_pow2(int chunks) {
+static int ln_tpr(int chunks) {
   int t = 1;
   while (t < chunks && t < 64) t <<= 1;
   return t < 4 ? 4 : t;
-}
-
-// Lanes per row.  Rows wider than 32 chunks (stage 3 / 4: C = 320, 512) would take a whole
-// wave per row, with 24 of 64 lanes idle at C = 320; an exact fit of at most CMX_LN_NCH chunks
-// per lane (instantiated: 8 x 5, 16 x 4, 16 x 5, 32 x 4) packs several rows per wave instead
-// (C = 320 bf16: 8 lanes x 5 chunks, 32 rows per block).  CMX_LN_NCH=1: one wave per row.
-static int ln_tpr(int chunks) {
-  static const int maxn = [] {
-    const char* e = getenv("CMX_LN_NCH");
-    return e ? atoi(e) : 1;
-  }();
-  const int t0 = ln_tpr_pow2(chunks);
-  if (t0 < 64 || maxn < 4) return t0;
-  static const int cand[4][2] = {{8, 5}, {16, 4}, {16, 5}, {32, 4}};
-  for (const auto& c : cand)
-    if (c[0] * c[1] == chunks && c[1] <= maxn) return c[0];
-  return t0;
 }
 
 template <typename T>
@@ -268,7 +248,6 @@ static int ln_fwd_launch(const void* x, const float* g, const float* b, void* y,
     return cmx_check_launch("layernorm_fwd");                                              \
   }
   LNF(4, 1) LNF(8, 1) LNF(16, 1) LNF(32, 1) LNF(64, 1) LNF(64, 2) LNF(64, 4)
-  LNF(8, 5) LNF(16, 4) LNF(16, 5) LNF(32, 4)
 #undef LNF
   cmx_set_error("layernorm_fwd: unsupported C=%d", C);
   return CMX_ERR_SHAPE;
@@ -298,7 +277,6 @@ static int ln_bwd_launch(const void* dy, const void* x, const float* g, const fl
     goto reduce;                                                                            \
   }
   LNB(4, 1) LNB(8, 1) LNB(16, 1) LNB(32, 1) LNB(64, 1) LNB(64, 2) LNB(64, 4)
-  LNB(8, 5) LNB(16, 4) LNB(16, 5) LNB(32, 4)
 #undef LNB
   cmx_set_error("layernorm_bwd: unsupported C=%d", C);
   return CMX_ERR_SHAPE;
