@@ -1020,6 +1020,15 @@ int auto_split(int G, int M, int N, int K, int ones_col) {
   const int nk = (K + FBK - 1) / FBK;
   const long full = tile_policy() == 1 ? 128 : 200;
   if (tiles >= full || nk < 8) return 1;
+  // an under-filled 64 x 64 problem without a bias-gradient column runs as k-group blocks
+  // (launch_bf16_ns, KW waves per tile) instead of split-K slabs + a reducer launch: measured
+  // +1.2 % per step (interleaved A/B, 246.7 / 247.1 -> 249.5 / 250.5 img/s; CMX_GEMM_SPLITKW=0
+  // restores split-K)
+  static const int splitkw = [] {
+    const char* e = getenv("CMX_GEMM_SPLITKW");
+    return e ? atoi(e) : 1;
+  }();
+  if (splitkw && bm == 64 && bn == 64 && !ones_col) return 1;
   long s = (256 + tiles - 1) / tiles;
   s = s < nk / 4 ? s : nk / 4;
   if (s > 128) s = 128;
@@ -1206,8 +1215,12 @@ size_t cmx_gemm_group_record_size(void) { return sizeof(GroupRec); }
 // split only bounds the k-loop of one block (<= 32 k-tiles of 64 = 2048 tokens per block)
 int cmx_gemm_grouped_splitk(int G, int M, int N, int K, int ones_col) {
   if (G <= 0 || M <= 0 || N <= 0 || K <= 0) return 1;
+  static const int kt = [] {
+    const char* e = getenv("CMX_GROUPED_KT");
+    return e ? atoi(e) : 32;
+  }();
   const int nk = (K + FBK - 1) / FBK;
-  int s = (nk + 31) / 32;
+  int s = (nk + kt - 1) / kt;
   if (s > 64) s = 64;
   const int per = (nk + s - 1) / s;
   return (nk + per - 1) / per;
