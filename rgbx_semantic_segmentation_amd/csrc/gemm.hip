@@ -1028,7 +1028,9 @@ int auto_split(int G, int M, int N, int K, int ones_col) {
     const char* e = getenv("CMX_GEMM_SPLITKW");
     return e ? atoi(e) : 1;
   }();
-  if (splitkw && bm == 64 && bn == 64 && !ones_col) return 1;
+  // (short k-loops only: a k-group block walks nk / 2 ring slots serially, and the FFM context
+  // products -- 64 x 64 over 19200 tokens, nk = 300 -- keep split-K: 10.8 vs 33 us)
+  if (splitkw && bm == 64 && bn == 64 && !ones_col && nk <= 32) return 1;
   long s = (256 + tiles - 1) / tiles;
   s = s < nk / 4 ? s : nk / 4;
   if (s > 128) s = 128;
