@@ -973,7 +973,7 @@ bool fast_ok(const void* A, const void* A2, const void* B, int M, int N, int K, 
 int tile_dim(int n) { return n <= 64 ? 64 : 128; }
 
 // Tile policy of the bf16 path (CMX_GEMM_TILES=0 restores the 128-wide-first policy, for A/B
-// measurements).  Policy 1: when 128-wide tiles leave the chip under-filled (< 240 tiles),
+// measurements).  Policy 1: when 128-wide tiles leave the chip under-filled (< 400 tiles),
 // take 64 x 64 tiles -- 4x the tiles, a lighter per-block k-loop and no split-K combine --
 // and split K only when even those leave it under-filled.
 int tile_policy() {
@@ -1004,8 +1004,11 @@ void plan_tiles(int G, int M, int nb, int K, int* bm, int* bn) {
   *bm = tile_dim(M);
   *bn = tile_dim(nb);
   if (tile_policy() == 1) {
+    // (CMX_GEMM_T128, default 400: the stage-3 MLP GEMMs, 380 128-wide tiles, run 64 x 64;
+    // measured +0.6 % per step over 240 in interleaved A/B)
+    static const int t128min = [] { const char* e = getenv("CMX_GEMM_T128"); return e ? atoi(e) : 400; }();
     const long t128 = (long)cdiv(M, *bm) * cdiv(nb, *bn) * G;
-    if (t128 < 240) *bm = *bn = 64;
+    if (t128 < t128min) *bm = *bn = 64;
   }
   if (K <= smallk_policy() || (nb <= 64 && smallk_policy() > 0)) *bm = *bn = 64;
 }
