@@ -160,7 +160,10 @@ def reduce(src: torch.Tensor, dst: torch.Tensor, dst2: torch.Tensor | None, G: i
     arm()
 
 
-_TABLE_BYTES = 256 * 1024        # one pinned record table (> 1000 records)
+# one pinned record table: 1 MiB (> 4000 grouped-GEMM records).  The B5 1024^2 step packs
+# 284 KB of records into one flush; a 256 KB table made its HIP-graph capture fail and the
+# bench fell back to eager launches (78 ms/step instead of ~30)
+_TABLE_BYTES = 1024 * 1024
 _free = []                        # pinned tables ready for reuse
 
 
