@@ -39,9 +39,13 @@ def parse():
     p.add_argument("--classes", type=int, default=40)
     p.add_argument("--dtype", default="bfloat16")
     p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--allow-eager", action="store_true",
+                   help="fall back to eager launches when the HIP-graph capture fails (default: exit 3)")
     p.add_argument("--loss-scaling", action="store_true",
                    help="config 5's AMP step: dynamic loss scaling (GradScaler) inside the captured step")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--dry-run", action="store_true",
+                   help="rehearse the rank launch on the CPU (gloo all-reduce), no GPU work")
     p.add_argument("--cpu-steps", type=int, default=3)
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="0: every CPU this process may use (affinity, capped by the cgroup CPU quota)")
@@ -95,11 +99,58 @@ def cpu_baseline(args):
                                                                                      f"{sec0 * 1e3:.1f} ms/step"}}
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_command(argv, nproc: int, port: int):
+    """The one-process-per-GPU launch of this script (reference: README.md:129,
+    engine/engine.py:56): ``python -m torch.distributed.run`` with ``nproc`` ranks on this node,
+    rendezvous on 127.0.0.1, the same bench arguments forwarded to every rank."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def check_world(gpus: int, env) -> str:
+    """'launch' (spawn the N ranks), 'run' (this process is a rank or the only one) or raise
+    SystemExit when ``--gpus`` disagrees with the launcher's WORLD_SIZE."""
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            raise SystemExit(f"[bench] --gpus {gpus} but WORLD_SIZE={world}: refusing to report "
+                             f"a {world}-rank number as {gpus} GPUs")
+        return "run"
+    return "launch" if gpus > 1 else "run"
+
+
 def main():
     args = parse()
+    # --gpus N > 1 without a launcher: start the N ranks as a child process BEFORE this
+    # process touches the GPU, wait, forward its output and exit with its code
+    if check_world(args.gpus, os.environ) == "launch":
+        import subprocess
+        cmd = launch_command(sys.argv[1:], args.gpus, free_port())
+        print("[bench] " + " ".join(cmd), file=sys.stderr, flush=True)
+        sys.exit(subprocess.call(cmd))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        # launcher rehearsal without a GPU: the ranks rendezvous over gloo, rank 0 reports
+        if world > 1:
+            dist.init_process_group("gloo")
+            t = torch.ones(1)
+            dist.all_reduce(t)
+            world_seen = int(t.item())
+            dist.destroy_process_group()
+        else:
+            world_seen = 1
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": world_seen}))
+        return
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     group = None
@@ -178,8 +229,12 @@ def main():
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph, capture_error_mode="thread_local"):
                 static_loss = step()
-        except Exception as e:  # pragma: no cover - reported in the JSON line
-            print(f"[bench] graph capture failed, eager mode: {e!r}", file=sys.stderr)
+        except Exception as e:  # pragma: no cover - needs a GPU
+            # a BASELINE-config line must not silently degrade to eager launches (a 3x slower
+            # number): fail unless eager was asked for
+            print(f"[bench] HIP graph capture failed: {e!r}", file=sys.stderr)
+            if not args.allow_eager:
+                raise SystemExit(3)
             graph = None
 
     def run_one():

@@ -205,7 +205,10 @@ int cmx_adamw_step(float* p, const float* g, float* m, float* v, void* shadow_bf
  *      skips the whole update (and the step count) when found_inf[0] != 0; loss_scale_update applies backoff /
  *      growth (after growth_interval clean steps) and clears found_inf. */
 int cmx_adamw_step_scaled(float* p, const float* g, float* m, float* v, void* shadow_bf16, const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1, double beta2, float eps, double weight_decay, float grad_scale, const float* loss_scale, const float* found_inf, hipStream_t stream);
-int cmx_grad_nonfinite(const float* g, int64_t n, float* found_inf, hipStream_t stream);
+/* grad_nonfinite: flags64 (nullable) = the per-64-element decay flags of adamw_step; blocks flagged 2
+ *      (frozen slots, in no optimizer group) are not scanned, as GradScaler.unscale_ checks only the
+ *      optimizer's parameters. */
+int cmx_grad_nonfinite(const float* g, int64_t n, const uint8_t* flags64, float* found_inf, hipStream_t stream);
 int cmx_loss_scale_update(float* scale, int* growth_tracker, float* found_inf, float growth_factor, float backoff_factor, int growth_interval, hipStream_t stream);
 
 /* ---- IFRM (ImprovedFeatureRectifyModule, net_utils.py:155-180; config.py:57 'IFRM').

@@ -17,7 +17,12 @@ algorithms below restate OpenCV's published 8-bit implementations:
     source coordinate f = (d + 0.5) * scale - 0.5 in float, s = floor(f), clamped to the
     edge with weight 0; weights round((1-f)*2048), round(f*2048) (11-bit, cvRound = half to
     even); horizontal pass D = S0*a0 + S1*a1 in int32; vertical pass as the x86 SIMD kernel
-    (VResizeLinearVec_32s8u): ((((D0>>4)*b0)>>16) + (((D1>>4)*b1)>>16) + 2) >> 2, saturated.
+    (VResizeLinearVec_32s8u): ((((D0>>4)*b0)>>16) + (((D1>>4)*b1)>>16) + 2) >> 2, saturated,
+    applied to EVERY byte of a row.  cv2 rounds the bytes its vector loop leaves over at the
+    end of a row with the scalar FixedPtCast ((D0*b0 + D1*b1 + (1 << 21)) >> 22) instead, which
+    can differ by 1 LSB: that scalar tail is NOT modelled, so the GPU kernels are bit-exact
+    against this restatement, and within 1 LSB (not bit-exact) of cv2 itself (unpinned: cv2
+    is not installed).
     Same-size resize is a copy (cv2.resize returns src.copyTo for dsize == ssize).
   * cv2.cvtColor BGR2HSV, 8U (RGB2HSV_b): integer V, S = round(diff*255/V) and H via the
     12-bit sdiv/hdiv tables, H in [0, 180).

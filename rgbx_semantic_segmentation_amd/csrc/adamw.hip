@@ -69,10 +69,13 @@ __global__ void step_incr_kernel(float* step, const float* found_inf) {
 
 // found_inf[0] = 1 if any of g[0, n) is inf / nan (left untouched otherwise; reset by the
 // loss-scale update).  Benign race: every writer stores the same 1.
-__global__ __launch_bounds__(256) void nonfinite_kernel(const float* __restrict__ g, long n, float* __restrict__ found) {
+// Blocks of 64 elements flagged 2 in flags64 (frozen slots) are skipped.
+__global__ __launch_bounds__(256) void nonfinite_kernel(const float* __restrict__ g, long n,
+                                                        const uint8_t* __restrict__ flags64, float* __restrict__ found) {
   int bad = 0;
   const long nv = n / 4;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (long)gridDim.x * blockDim.x) {
+    if (flags64 && flags64[i >> 4] == 2) continue;
     const float4 x = reinterpret_cast<const float4*>(g)[i];
     bad |= (int)!isfinite(x.x) | (int)!isfinite(x.y) | (int)!isfinite(x.z) | (int)!isfinite(x.w);
   }
@@ -115,11 +118,12 @@ int cmx_adamw_step_scaled(float* p, const float* g, float* m, float* v, void* sh
   return cmx_check_launch("adamw_step");
 }
 
-int cmx_grad_nonfinite(const float* g, int64_t n, float* found_inf, hipStream_t s) {
-  CMX_REQUIRE(n % 4 == 0 && found_inf, CMX_ERR_SHAPE, "grad_nonfinite: n %% 4");
+int cmx_grad_nonfinite(const float* g, int64_t n, const uint8_t* flags64, float* found_inf, hipStream_t s) {
+  CMX_REQUIRE(n % 4 == 0 && found_inf && (!flags64 || n % 64 == 0), CMX_ERR_SHAPE,
+              "grad_nonfinite: n %% 4 (n %% 64 with flags)");
   long blocks = (n / 4 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(nonfinite_kernel, dim3((unsigned)blocks), dim3(256), 0, s, g, (long)n, found_inf);
+  hipLaunchKernelGGL(nonfinite_kernel, dim3((unsigned)blocks), dim3(256), 0, s, g, (long)n, flags64, found_inf);
   return cmx_check_launch("grad_nonfinite");
 }
 

@@ -183,8 +183,13 @@ def get_train_loader(engine, dataset, config):
     if isinstance(dataset, type):           # the reference passes the Dataset class (train.py:45)
         from .augment import TrainPre
         dataset = dataset(data_setting(config), "train", None, int(config.batch_size * config.niters_per_epoch))
+        # the draws follow torch's seed like the reference's worker-seeded `random`
+        # (train.py --seed -> torch.manual_seed): one generator per rank
+        import random
+        rank = torch.distributed.get_rank() if engine.distributed else 0
+        rng = random.Random(torch.initial_seed() * 1000003 + rank)
         pre = TrainPre(config.norm_mean, config.norm_std, config.num_classes, config.image_height,
-                       config.image_width, getattr(config, "train_scale_array", None), config.background)
+                       config.image_width, getattr(config, "train_scale_array", None), config.background, rng=rng)
     if engine.distributed:
         sampler = DistributedSampler(dataset)
         batch_size = batch_size // engine.world_size

@@ -56,7 +56,9 @@ class BucketedGradSync:
         # collectives of at most ~chunk_mb of payload each (DDP's 25 MB bucket cap): a long
         # segment is exchanged as a sequence of bounded messages
         mb = float(chunk_mb if chunk_mb is not None else os.environ.get("CMX_DP_CHUNK_MB", "25"))
-        self.chunk = max(1024, int(mb * 2 ** 20) // (2 if self.payload == "bf16" else 4))
+        # a multiple of 64 elements, so every chunk of the flat buffer stays 16-byte aligned for
+        # the vectorized cast / shard-sum kernels (a fractional MB would otherwise misalign)
+        self.chunk = max(1024, (int(mb * 2 ** 20) // (2 if self.payload == "bf16" else 4)) // 64 * 64)
         self.ranges = {sid: (a, b) for sid, a, b in store.segments}
         self.works = []
         self.launched = set()
@@ -91,7 +93,9 @@ class BucketedGradSync:
     def _reduce(self, seg: torch.Tensor) -> None:
         for a in range(0, seg.numel(), self.chunk):
             part = seg[a:a + self.chunk]
-            if self.payload == "fp32" or self.world == 1:
+            # the bf16 protocol runs at every world size (at P = 1 the all-to-all and the
+            # all-gather are copies), so a one-GPU run exercises its kernels and collectives
+            if self.payload == "fp32":
                 dist.all_reduce(part, op=dist.ReduceOp.SUM, group=self.group)
             else:
                 self._reduce_bf16(part)

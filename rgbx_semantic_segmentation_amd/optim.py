@@ -81,7 +81,9 @@ class FusedAdamW:
             gscale = float(self.grad_sync(s.grad))
         if scaler is not None and scaler.enabled:
             # GradScaler.step: skip the update if any (scaled) gradient is inf / nan, else unscale
-            call("cmx_grad_nonfinite", ptr(s.grad), s.numel, ptr(scaler.found_inf), stream())
+            # the frozen slots (IFRM lambdas, in no param group) are not checked, as
+            # GradScaler.unscale_ only checks the optimizer's parameters
+            call("cmx_grad_nonfinite", ptr(s.grad), s.numel, ptr(s.decay64), ptr(scaler.found_inf), stream())
             call("cmx_adamw_step_scaled", ptr(s.flat), ptr(s.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq),
                  ptr(s.shadow), ptr(s.decay64), s.numel, ptr(self.lr_t), ptr(self.step_t), self.betas[0],
                  self.betas[1], self.eps, self.weight_decay, gscale, ptr(scaler.scale_t), ptr(scaler.found_inf),

@@ -82,6 +82,23 @@ def _inputs(B, H, W, K, seed=3):
     return make_batch(B, H, W, K, seed=seed)
 
 
+def _record(case, loss, loss64, rows, bad, grad_bad):
+    """The per-tensor margins on record: {case}.json under $CMX_PARITY_OUT (default
+    gpurun_out/parity, copied into profiles/ after a GPU run) with e_gpu, e_emu and their
+    ratio for every compared tensor."""
+    import json
+    import os
+    out = os.environ.get("CMX_PARITY_OUT", os.path.join("gpurun_out", "parity"))
+    os.makedirs(out, exist_ok=True)
+    tab = [{"tensor": n, "e_gpu": e, "e_emu": ee, "ratio": e / max(ee, 1e-30)} for n, e, ee in rows]
+    rs = sorted(t["ratio"] for t in tab)
+    with open(os.path.join(out, f"{case}.json"), "w") as f:
+        json.dump({"case": case, "ratio_bound": RATIO, "outlier_ratio_bound": OUTLIER_RATIO,
+                   "loss_gpu": loss, "loss_fp64": loss64, "n_tensors": len(tab),
+                   "ratio_median": rs[len(rs) // 2], "ratio_max": rs[-1],
+                   "n_over_bound": len(bad) + len(grad_bad), "tensors": tab}, f, indent=1)
+
+
 def _check(name, e_gpu, e_emu, bad, ratio=RATIO):
     ok = e_gpu <= ratio * e_emu
     if not ok:
@@ -159,6 +176,7 @@ def test_bf16_train_step_vs_fp64_oracle(dev, case):
           f"logits e_gpu {e_l:.3e} e_emu {e_le:.3e}; {len(rows)} tensors, gpu/emu error ratio "
           f"median {ratios[len(ratios) // 2][0]:.2f}, max {ratios[-1][0]:.2f} ({ratios[-1][1]})")
     print("worst ratios:", [(round(r, 2), n) for r, n in ratios[-8:]])
+    _record(case, loss.item(), loss64.item(), rows, bad, grad_bad)
     n_allowed = max(2, len(rows) // 100)
     assert not bad, bad
     assert len(grad_bad) <= n_allowed and all(b[0] <= OUTLIER_RATIO for b in grad_bad), grad_bad[:10]

@@ -144,3 +144,16 @@ def test_bucketed_grad_sync_paramstore_unequal_pixels_gloo_world2(payload):
     for p in procs:
         p.join(timeout=60)
     assert all(r[1] and r[2] for r in res), res
+
+
+def test_chunk_is_16B_aligned_for_fractional_mb(monkeypatch):
+    """A fractional CMX_DP_CHUNK_MB must not misalign later chunks for the 16-B vector cast /
+    shard-sum kernels: the chunk is a multiple of 64 elements."""
+    from rgbx_semantic_segmentation_amd import dist as cdist
+
+    class _Store:
+        segments = [(0, 0, 1 << 20)]
+    monkeypatch.setattr(cdist.BucketedGradSync, "_world", lambda self: 2)
+    for mb, payload in ((0.05, "bf16"), (0.05, "fp32"), (0.3, "bf16"), (25, "fp32")):
+        s = cdist.BucketedGradSync(_Store(), None, payload=payload, chunk_mb=mb)
+        assert s.chunk % 64 == 0, (mb, payload, s.chunk)

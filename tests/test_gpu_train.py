@@ -72,46 +72,56 @@ def test_segment_allreduce_sees_final_gradients(dev):
 
 
 @pytest.mark.gpu
-def test_grad_scaler_protocol(dev):
-    """GradScaler (train.py:185-198 AMP path, config 5): a scaled step updates the parameters
-    like an unscaled one (the power-of-two scale is exact in fp32); an inf gradient skips
-    the update and the step count and halves the scale; growth after growth_interval clean
-    steps.  All on device, no host sync inside the step."""
+def test_grad_scaler_matches_torch_grad_scaler(dev):
+    """a15 (train.py:13,56,185-198): the device GradScaler + FusedAdamW against torch's own
+    ``torch.amp.GradScaler('cpu')`` stepping ``torch.optim.AdamW(group_weight(...))`` on the
+    SAME scaled gradients, over a sequence of clean steps and steps with an inf / nan
+    gradient: scale, growth tracker, skipped steps (AdamW's step count) and the parameters after
+    every step.  The HIP side never syncs the host inside a step."""
+    from oracle.cmx_ref import EncoderDecoder as RefModel, CMXConfig
+    from oracle.train_ref import make_optimizer
     from rgbx_semantic_segmentation_amd.models.builder import EncoderDecoder
     from rgbx_semantic_segmentation_amd.optim import FusedAdamW, GradScaler
     torch.manual_seed(0)
+    ccfg = CMXConfig(backbone="mit_b0", num_classes=9)
+    ref = RefModel(ccfg)
+    mod = EncoderDecoder(dict(backbone="mit_b0", num_classes=9, compute_dtype="float32",
+                              decoder_embed_dim=512)).to(dev)
+    mod.load_state_dict(ref.state_dict(), strict=True)
+    ref.eval()
+    mod.eval()
     g = torch.Generator().manual_seed(5)
     rgb = torch.randn(2, 3, 64, 96, generator=g).to(dev)
     x = torch.randn(2, 3, 64, 96, generator=g).to(dev)
     lab = torch.randint(0, 9, (2, 64, 96), generator=g).to(dev)
-    cfg = dict(backbone="mit_b0", num_classes=9, compute_dtype="float32", decoder_embed_dim=256)
-    ref = EncoderDecoder(cfg).to(dev)
-    ref.eval()
-    mod = EncoderDecoder(cfg).to(dev)
-    mod.load_state_dict(ref.state_dict())
-    mod.eval()
-    o_ref, o = FusedAdamW(ref), FusedAdamW(mod)
+    opt_t = make_optimizer(ref, ccfg)
+    opt = FusedAdamW(mod, lr=ccfg.lr, betas=(0.9, 0.999), weight_decay=ccfg.weight_decay)
+    sc_t = torch.amp.GradScaler("cpu", init_scale=2.0 ** 10, growth_interval=2)
     sc = GradScaler(init_scale=2.0 ** 10, growth_interval=2, device=dev)
-    ref(rgb, x, lab).backward()
-    o_ref.step()
-    sc.scale(mod(rgb, x, lab)).backward()
-    sc.step(o)
-    sc.update()
-    torch.cuda.synchronize()
-    d = (mod.store.flat - ref.store.flat).abs().max().item()
-    assert d < 1e-6 * (1 + ref.store.flat.abs().max().item()), d
-    # overflow: the step is skipped, the scale halves
-    before = mod.store.flat.clone()
-    sc.scale(mod(rgb, x, lab)).backward()
-    mod.store.grad[123] = float("inf")
-    sc.step(o)
-    sc.update()
-    torch.cuda.synchronize()
-    assert torch.equal(before, mod.store.flat)
-    assert sc.get_scale() == 2.0 ** 9 and float(o.step_t.item()) == 1.0
-    # two clean steps: growth back to 2**10
-    for _ in range(2):
+    gp = dict(mod.named_parameters())
+    plan = ["clean", "inf", "clean", "clean", "nan", "clean", "clean"]
+    for it, kind in enumerate(plan):
         sc.scale(mod(rgb, x, lab)).backward()
-        sc.step(o)
+        if kind != "clean":                       # one bad element of one parameter's gradient
+            gp["decode_head.linear_pred.weight"].grad.view(-1)[7] = float(kind)
+        torch.cuda.synchronize()
+        sc_t.scale(torch.ones(()))                # torch's scaler initialises lazily in scale()
+        for n, p in ref.named_parameters():       # the SAME scaled gradients on both sides
+            p.grad = gp[n].grad.detach().cpu().clone()
+        sc_t.step(opt_t)
+        sc_t.update()
+        sc.step(opt)
         sc.update()
-    assert sc.get_scale() == 2.0 ** 10 and float(o.step_t.item()) == 3.0
+        torch.cuda.synchronize()
+        steps_t = {float(st["step"]) for st in opt_t.state.values()} or {0.0}
+        assert sc.get_scale() == sc_t.get_scale(), (it, kind, sc.get_scale(), sc_t.get_scale())
+        assert int(sc.tracker.item()) == int(sc_t._growth_tracker.item()), (it, kind)
+        assert steps_t == {float(opt.step_t.item())}, (it, kind, steps_t, opt.step_t.item())
+        worst = 0.0
+        for n, p in ref.named_parameters():
+            q = gp[n].detach().cpu()
+            worst = max(worst, ((q - p.detach()).abs() - 1e-6 * p.detach().abs()).max().item())
+        print(f"step {it} ({kind}): scale {sc.get_scale():g}, tracker {int(sc.tracker.item())}, "
+              f"adamw steps {opt.step_t.item():g}, max(|dp| - 1e-6|p|) {worst:.2e}")
+        assert worst <= 1e-8, (it, kind, worst)
+    assert sc.get_scale() == 2.0 ** 10 and float(opt.step_t.item()) == 5.0
