@@ -37,7 +37,8 @@ def parse():
     p.add_argument("--width", type=int, default=640)
     p.add_argument("--batch", type=int, default=2, help="per-GPU batch")
     p.add_argument("--classes", type=int, default=40)
-    p.add_argument("--dtype", default="bfloat16")
+    p.add_argument("--dtype", default="bfloat16", choices=["bfloat16", "bf16", "float16", "fp16", "float32"],
+                   help="compute dtype; float16 is the reference's AMP step (config 5) and implies --loss-scaling")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--allow-eager", action="store_true",
                    help="fall back to eager launches when the HIP-graph capture fails (default: exit 3)")
@@ -128,6 +129,8 @@ def check_world(gpus: int, env) -> str:
 
 def main():
     args = parse()
+    if args.dtype in ("float16", "fp16"):
+        args.dtype, args.loss_scaling = "float16", True     # autocast fp16 always runs with a GradScaler
     # --gpus N > 1 without a launcher: start the N ranks as a child process BEFORE this
     # process touches the GPU, wait, forward its output and exit with its code
     if check_world(args.gpus, os.environ) == "launch":
@@ -290,7 +293,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16" if args.dtype in ("bfloat16", "bf16") else "fp32",
+            "dtype": {"bfloat16": "bf16", "bf16": "bf16", "float16": "fp16"}.get(args.dtype, "fp32"),
             "data": "synthetic (seeded uint8 RGB + replicated X plane, ImageNet-normalised; uniform labels "
                     "with one 25x25 ignore block per image; random-init weights)",
             "config": {"workload": workload, "model": f"CMX-{args.backbone}",

@@ -56,15 +56,15 @@ int cmx_act_fwd(const void* x, void* y, int64_t n, int act, int dtype, hipStream
 int cmx_act_bwd(const void* dy, const void* z, void* dx, int64_t n, int act, int dtype, hipStream_t stream);
 int cmx_partials_sum(const float* ws, float* out, int G, int nblk, int W, int accumulate, float alpha, hipStream_t stream);
 int cmx_cast_f32_bf16(const float* src, void* dst, int64_t n, hipStream_t stream);
+int cmx_cast_f32_h16(const float* src, void* dst, int64_t n, int dtype, hipStream_t stream);
 /* All random masks of one training step in one launch (replaces the torch.rand draws of
    timm DropPath, dual_segformer.py:141-180, and Dropout2d, MLPDecoder.py:63, plus
    every BatchNorm2d's num_batches_tracked += 1): dp[i] = floor(keep[i] + u) / keep[i],
    d2[i] = (u >= p) / (1 - p), u = splitmix64(seed, *step, i); *step += 1 on the device. */
 int cmx_step_masks(const float* keep, int nkeep, float* dp, int nd2, float p, float* d2, uint64_t seed, uint64_t* step, int64_t* nbt, int nnbt, hipStream_t stream);
 /* bf16 gradient payload of the DP exchange (replaces DDP's fp32 bucket all-reduce,
-   train.py:145-146 / engine.py:56): out = bf16(sum over P chunks of in, fp32 accumulate);
-   and the bf16 -> fp32 copy of the gathered sums. */
-int cmx_shard_sum_bf16(const void* in, void* out, int P, int64_t n, hipStream_t stream);
+   train.py:145-146 / engine.py:56): the bf16 -> fp32 copy of the all-gathered shard sums
+   (cmx_cast_f32_bf16 makes the payload). */
 int cmx_cast_bf16_f32(const void* src, float* dst, int64_t n, hipStream_t stream);
 size_t cmx_colsum_workspace(int64_t M, int G, int N);
 int cmx_colsum(const void* x, float* out, float* workspace, int64_t M, int G, int N, int64_t ld, int accumulate, float alpha, int dtype, hipStream_t stream);
@@ -186,7 +186,8 @@ int cmx_gemm(const void* A, const void* A2, const void* B, void* C, const float*
 size_t cmx_gemm_group_record_size(void);
 int cmx_gemm_grouped_splitk(int G, int M, int N, int K, int ones_col);
 int cmx_gemm_group_pack(void* rec, const void* A, const void* B, void* C, float* dbias, float* workspace, int G, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t sA, int64_t sB, int64_t sC, int64_t sdb, int transA, int transB, int out_mode, int ones_col, int splitk, int blk0);
-int cmx_gemm_grouped(const void* recs, int nrec, int total_blocks, hipStream_t stream);
+/* cmx_gemm_grouped: dtype = the operands' storage type of every record (1 bf16, 2 fp16) */
+int cmx_gemm_grouped(const void* recs, int nrec, int total_blocks, int dtype, hipStream_t stream);
 /* ---- im2col-free convolution on the same GEMM (bf16, NHWC, C % 64 == 0 for the forward): OverlapPatchEmbed.proj
  *      (k3 s2 p1, dual_segformer.py:196-197) and Attention.sr (kR sR, :95-96).  The forward's A operand is DMA'd
  *      tap by tap straight from x (padding = zeros from the buffer range check); the weight gradient is one
@@ -198,13 +199,13 @@ int cmx_reduce_pack(void* rec, const float* src, float* dst, float* dst2, int G,
 int cmx_reduce_grouped(const void* recs, int nrec, int total_blocks, hipStream_t stream);
 
 /* ---- fused AdamW over the flat parameter buffer (train.py:128-129, init_func.py:33-57). */
-int cmx_adamw_step(float* p, const float* g, float* m, float* v, void* shadow_bf16, const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1, double beta2, float eps, double weight_decay, float grad_scale, hipStream_t stream);
+int cmx_adamw_step(float* p, const float* g, float* m, float* v, void* shadow, int shadow_dtype, const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1, double beta2, float eps, double weight_decay, float grad_scale, hipStream_t stream);
 /* ---- dynamic loss scaling: torch.cuda.amp.GradScaler of the reference's AMP path (train.py:13,56,185-198, config 5).
  *      The scale, growth tracker and found-inf flag live on the device, so a scaled step replays from a HIP graph:
  *      grad_nonfinite sets found_inf if any gradient is inf/nan; adamw_step_scaled unscales by 1/loss_scale[0] and
  *      skips the whole update (and the step count) when found_inf[0] != 0; loss_scale_update applies backoff /
  *      growth (after growth_interval clean steps) and clears found_inf. */
-int cmx_adamw_step_scaled(float* p, const float* g, float* m, float* v, void* shadow_bf16, const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1, double beta2, float eps, double weight_decay, float grad_scale, const float* loss_scale, const float* found_inf, hipStream_t stream);
+int cmx_adamw_step_scaled(float* p, const float* g, float* m, float* v, void* shadow, int shadow_dtype, const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1, double beta2, float eps, double weight_decay, float grad_scale, const float* loss_scale, const float* found_inf, hipStream_t stream);
 /* grad_nonfinite: flags64 (nullable) = the per-64-element decay flags of adamw_step; blocks flagged 2
  *      (frozen slots, in no optimizer group) are not scanned, as GradScaler.unscale_ checks only the
  *      optimizer's parameters. */

@@ -98,4 +98,6 @@ def dtype_code(t: torch.Tensor) -> int:
         return 0
     if t.dtype == torch.bfloat16:
         return 1
+    if t.dtype == torch.float16:
+        return 2
     raise CMXError(f"unsupported dtype {t.dtype}")

@@ -17,8 +17,10 @@
 // HBM-bound: 16 B read (p,g,m,v) + 12 B written (p,m,v) [+2 B shadow] per parameter.
 #include "cmx_common.h"
 
+// S = the weight shadow's 16-bit type (bf16 or f16, the compute dtype's GEMM operand)
+template <typename S>
 __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                             float* __restrict__ v, bf16* __restrict__ shadow, const uint8_t* __restrict__ decay64,
+                             float* __restrict__ v, S* __restrict__ shadow, const uint8_t* __restrict__ decay64,
                              long n, const float* __restrict__ lr_ptr, const float* __restrict__ step_ptr, double b1d,
                              double b2d, float eps, double wd, float gscale, const float* __restrict__ loss_scale,
                              const float* __restrict__ found_inf) {
@@ -56,8 +58,8 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
     *reinterpret_cast<float4*>(m + e) = make_float4(ma[0], ma[1], ma[2], ma[3]);
     *reinterpret_cast<float4*>(v + e) = make_float4(va[0], va[1], va[2], va[3]);
     if (shadow) {
-      uint32_t a = pack2_bf16(pa[0], pa[1]);
-      uint32_t b = pack2_bf16(pa[2], pa[3]);
+      uint32_t a = pack2<S>(pa[0], pa[1]);
+      uint32_t b = pack2<S>(pa[2], pa[3]);
       *reinterpret_cast<uint2*>(shadow + e) = make_uint2(a, b);
     }
   }
@@ -98,23 +100,28 @@ __global__ void loss_scale_update_kernel(float* scale, int* tracker, float* foun
 extern "C" {
 
 // n must be a multiple of 64; step_ptr is incremented by this call before use (torch order)
-int cmx_adamw_step(float* p, const float* g, float* m, float* v, void* shadow_bf16, const uint8_t* decay64, int64_t n,
-                   const float* lr_ptr, float* step_ptr, double beta1, double beta2, float eps, double weight_decay,
-                   float grad_scale, hipStream_t s) {
-  return cmx_adamw_step_scaled(p, g, m, v, shadow_bf16, decay64, n, lr_ptr, step_ptr, beta1, beta2, eps, weight_decay,
-                               grad_scale, nullptr, nullptr, s);
+int cmx_adamw_step(float* p, const float* g, float* m, float* v, void* shadow, int shadow_dtype, const uint8_t* decay64,
+                   int64_t n, const float* lr_ptr, float* step_ptr, double beta1, double beta2, float eps,
+                   double weight_decay, float grad_scale, hipStream_t s) {
+  return cmx_adamw_step_scaled(p, g, m, v, shadow, shadow_dtype, decay64, n, lr_ptr, step_ptr, beta1, beta2, eps,
+                               weight_decay, grad_scale, nullptr, nullptr, s);
 }
 
-int cmx_adamw_step_scaled(float* p, const float* g, float* m, float* v, void* shadow_bf16, const uint8_t* decay64,
-                          int64_t n, const float* lr_ptr, float* step_ptr, double beta1, double beta2, float eps,
-                          double weight_decay, float grad_scale, const float* loss_scale, const float* found_inf,
-                          hipStream_t s) {
+int cmx_adamw_step_scaled(float* p, const float* g, float* m, float* v, void* shadow, int shadow_dtype,
+                          const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1,
+                          double beta2, float eps, double weight_decay, float grad_scale, const float* loss_scale,
+                          const float* found_inf, hipStream_t s) {
   CMX_REQUIRE(n % 64 == 0, CMX_ERR_SHAPE, "adamw: n must be a multiple of 64");
+  CMX_REQUIRE(!shadow || shadow_dtype == 1 || shadow_dtype == 2, CMX_ERR_DTYPE, "adamw: shadow dtype %d", shadow_dtype);
   hipLaunchKernelGGL(step_incr_kernel, dim3(1), dim3(1), 0, s, step_ptr, found_inf);
   long blocks = (n / 4 + 255) / 256;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, g, m, v, (bf16*)shadow_bf16, decay64,
-                     (long)n, lr_ptr, step_ptr, beta1, beta2, eps, weight_decay, grad_scale, loss_scale, found_inf);
+  if (shadow_dtype == 2)
+    hipLaunchKernelGGL(adamw_kernel<f16>, dim3((unsigned)blocks), dim3(256), 0, s, p, g, m, v, (f16*)shadow, decay64,
+                       (long)n, lr_ptr, step_ptr, beta1, beta2, eps, weight_decay, grad_scale, loss_scale, found_inf);
+  else
+    hipLaunchKernelGGL(adamw_kernel<bf16>, dim3((unsigned)blocks), dim3(256), 0, s, p, g, m, v, (bf16*)shadow, decay64,
+                       (long)n, lr_ptr, step_ptr, beta1, beta2, eps, weight_decay, grad_scale, loss_scale, found_inf);
   return cmx_check_launch("adamw_step");
 }
 

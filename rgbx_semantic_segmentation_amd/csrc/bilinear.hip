@@ -168,7 +168,7 @@ int cmx_bilinear_fwd_nchw_f32(const void* in, float* out, int NB, int Hi, int Wi
   return cmx_check_launch("bilinear_fwd_nchw");
 }
 
-// in/out dtypes independent (0 fp32, 1 bf16); alpha = alpha0 * (*a1) * (*a2) (NULL -> 1)
+// in/out dtypes independent (0 fp32, 1 bf16, 2 fp16); alpha = alpha0 * (*a1) * (*a2) (NULL -> 1)
 int cmx_bilinear_adjoint_1d(const void* in, void* out, int64_t P, int Lo, int Li, int Q, int64_t sp, int64_t so,
                             const float* a1, const float* a2, float alpha0, int in_dtype, int out_dtype,
                             hipStream_t s) {
@@ -188,6 +188,9 @@ int cmx_bilinear_adjoint_1d(const void* in, void* out, int64_t P, int Lo, int Li
   else if (in_dtype == 0 && out_dtype == 1) ADJ(float, bf16);
   else if (in_dtype == 1 && out_dtype == 0) ADJ(bf16, float);
   else if (in_dtype == 1 && out_dtype == 1) ADJ(bf16, bf16);
+  else if (in_dtype == 0 && out_dtype == 2) ADJ(float, f16);
+  else if (in_dtype == 2 && out_dtype == 0) ADJ(f16, float);
+  else if (in_dtype == 2 && out_dtype == 2) ADJ(f16, f16);
   else { cmx_set_error("bilinear_adjoint: dtype"); return CMX_ERR_DTYPE; }
 #undef ADJ
   return cmx_check_launch("bilinear_adjoint_1d");

@@ -1,11 +1,13 @@
 // Shared helpers for the CMX gfx950 kernels (C-ABI library libcmx_hip.so).
 //
-// Storage types: float (fp32 parity mode) and bf16 (performance mode); every kernel
-// accumulates in fp32.  dtype codes on the C-ABI: 0 = fp32, 1 = bf16.
+// Storage types: float (fp32 parity mode), bf16 (performance mode) and f16 (IEEE half:
+// the reference's AMP / config-5 dtype); every kernel accumulates in fp32.  dtype codes on
+// the C-ABI: 0 = fp32, 1 = bf16, 2 = fp16.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
+#include <type_traits>
 #include "../../include/cmx_hip.h"  // compiler-checks every definition against the ABI header
 
 #define CMX_ABI_VERSION 1
@@ -54,10 +56,43 @@ __device__ __forceinline__ uint32_t pack2_bf16(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((cmx_f2){a, b}, cmx_bf2));
 }
 
-// 16-byte vectors: VEC<float> = 4 elements, VEC<bf16> = 8 elements.
+// ---------------------------------------------------------------- f16 (IEEE half)
+struct f16 {
+  uint16_t x;
+};
+typedef _Float16 cmx_h2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float to_f32(f16 v) { return (float)__builtin_bit_cast(_Float16, v.x); }
+// fp32 -> fp16 round-to-nearest-even (v_cvt_f16_f32), overflow -> inf like a cast in torch
+template <> __device__ __forceinline__ f16 from_f32<f16>(float v) {
+  f16 r;
+  r.x = __builtin_bit_cast(uint16_t, (_Float16)v);
+  return r;
+}
+__device__ __forceinline__ uint32_t pack2_f16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((cmx_f2){a, b}, cmx_h2));
+}
+
+// 16-bit storage types (bf16, f16) share every 2-byte code path; these convert a packed pair.
+template <typename T> constexpr bool is_h16 = std::is_same<T, bf16>::value || std::is_same<T, f16>::value;
+template <typename T> __device__ __forceinline__ uint32_t pack2(float a, float b) {
+  if constexpr (std::is_same<T, bf16>::value) return pack2_bf16(a, b);
+  else return pack2_f16(a, b);
+}
+template <typename T> __device__ __forceinline__ cmx_f2 unpack2(uint32_t u) {
+  if constexpr (std::is_same<T, bf16>::value) {
+    return (cmx_f2){__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+  } else {
+    return __builtin_convertvector(__builtin_bit_cast(cmx_h2, u), cmx_f2);
+  }
+}
+// the stored 16-bit pattern of 1.0 (a constant MFMA operand)
+template <typename T> constexpr uint16_t one_bits = std::is_same<T, bf16>::value ? 0x3f80 : 0x3c00;
+
+// 16-byte vectors: VEC<float> = 4 elements, VEC<bf16 / f16> = 8 elements.
 template <typename T> struct VecT;
 template <> struct VecT<float> { static constexpr int N = 4; typedef float4 raw; };
 template <> struct VecT<bf16> { static constexpr int N = 8; typedef uint4 raw; };
+template <> struct VecT<f16> { static constexpr int N = 8; typedef uint4 raw; };
 
 template <typename T>
 __device__ __forceinline__ void load_vec(const T* p, float* out) {
@@ -69,8 +104,9 @@ __device__ __forceinline__ void load_vec(const T* p, float* out) {
     uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      out[2 * i] = __uint_as_float(w[i] << 16);
-      out[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+      const cmx_f2 f = unpack2<T>(w[i]);
+      out[2 * i] = f.x;
+      out[2 * i + 1] = f.y;
     }
   }
 }
@@ -83,7 +119,7 @@ __device__ __forceinline__ void store_vec(T* p, const float* in) {
     uint32_t w[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      w[i] = pack2_bf16(in[2 * i], in[2 * i + 1]);
+      w[i] = pack2<T>(in[2 * i], in[2 * i + 1]);
     }
     *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
   }
@@ -243,6 +279,7 @@ static inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b)
   do {                                                                \
     if ((dtype) == 0) { typedef float T; __VA_ARGS__; }               \
     else if ((dtype) == 1) { typedef bf16 T; __VA_ARGS__; }           \
+    else if ((dtype) == 2) { typedef f16 T; __VA_ARGS__; }            \
     else { cmx_set_error("unsupported dtype %d", (int)(dtype)); return CMX_ERR_DTYPE; } \
   } while (0)
 

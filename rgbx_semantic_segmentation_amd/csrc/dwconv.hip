@@ -37,8 +37,8 @@ __device__ __forceinline__ void ld4(const T* p, Px& v) {
     v[1] = (cmx_f2){a.z, a.w};
   } else {
     const uint2 a = *reinterpret_cast<const uint2*>(p);
-    v[0] = (cmx_f2){__uint_as_float(a.x << 16), __uint_as_float(a.x & 0xffff0000u)};
-    v[1] = (cmx_f2){__uint_as_float(a.y << 16), __uint_as_float(a.y & 0xffff0000u)};
+    v[0] = unpack2<T>(a.x);
+    v[1] = unpack2<T>(a.y);
   }
 }
 
@@ -47,18 +47,17 @@ __device__ __forceinline__ void st4(T* p, const Px& v) {
   if constexpr (sizeof(T) == 4) {
     *reinterpret_cast<float4*>(p) = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
   } else {
-    *reinterpret_cast<uint2*>(p) = make_uint2(pack2_bf16(v[0].x, v[0].y), pack2_bf16(v[1].x, v[1].y));
+    *reinterpret_cast<uint2*>(p) = make_uint2(pack2<T>(v[0].x, v[0].y), pack2<T>(v[1].x, v[1].y));
   }
 }
 
-// the pair as it is stored in T (bf16 round-to-nearest-even)
+// the pair as it is stored in T (16-bit types: round-to-nearest-even)
 template <typename T>
 __device__ __forceinline__ cmx_f2 stored(cmx_f2 v) {
   if constexpr (sizeof(T) == 4) {
     return v;
   } else {
-    const uint32_t u = pack2_bf16(v.x, v.y);
-    return (cmx_f2){__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+    return unpack2<T>(pack2<T>(v.x, v.y));
   }
 }
 
@@ -277,6 +276,7 @@ constexpr int TYB = 16, TXB = 16, EYB = TYB + 2, EXB = TXB + 2;
 
 template <typename T> struct V8;                  // 8 channels as stored
 template <> struct V8<bf16> { uint4 a; };
+template <> struct V8<f16> { uint4 a; };
 template <> struct V8<float> { float4 a, b; };
 
 template <typename T>
@@ -304,7 +304,7 @@ __device__ __forceinline__ void v8_unpack(const V8<T>& v, cmx_f2 (&o)[4]) {
   if constexpr (sizeof(T) == 2) {
     const uint32_t w[4] = {v.a.x, v.a.y, v.a.z, v.a.w};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = (cmx_f2){__uint_as_float(w[i] << 16), __uint_as_float(w[i] & 0xffff0000u)};
+    for (int i = 0; i < 4; ++i) o[i] = unpack2<T>(w[i]);
   } else {
     o[0] = (cmx_f2){v.a.x, v.a.y}; o[1] = (cmx_f2){v.a.z, v.a.w};
     o[2] = (cmx_f2){v.b.x, v.b.y}; o[3] = (cmx_f2){v.b.z, v.b.w};
@@ -314,8 +314,8 @@ template <typename T>
 __device__ __forceinline__ V8<T> v8_pack(const cmx_f2 (&o)[4]) {
   V8<T> v;
   if constexpr (sizeof(T) == 2) {
-    v.a = make_uint4(pack2_bf16(o[0].x, o[0].y), pack2_bf16(o[1].x, o[1].y), pack2_bf16(o[2].x, o[2].y),
-                     pack2_bf16(o[3].x, o[3].y));
+    v.a = make_uint4(pack2<T>(o[0].x, o[0].y), pack2<T>(o[1].x, o[1].y), pack2<T>(o[2].x, o[2].y),
+                     pack2<T>(o[3].x, o[3].y));
   } else {
     v.a = make_float4(o[0].x, o[0].y, o[1].x, o[1].y);
     v.b = make_float4(o[2].x, o[2].y, o[3].x, o[3].y);
@@ -380,6 +380,7 @@ __device__ __forceinline__ void stage_region(const T* __restrict__ base, T* img,
 // 128-B (bf16, CB = 64) row segment -- not one 8-B / 16-B piece per lane at a C-element stride.
 template <typename T> struct V4;                  // 4 channels as stored
 template <> struct V4<bf16> { uint2 a; };
+template <> struct V4<f16> { uint2 a; };
 template <> struct V4<float> { float4 a; };
 template <typename T>
 __device__ __forceinline__ V4<T> v4_load(const T* p) {
@@ -391,15 +392,15 @@ __device__ __forceinline__ V4<T> v4_load(const T* p) {
 template <typename T>
 __device__ __forceinline__ void v4_unpack(const V4<T>& v, cmx_f2 (&o)[2]) {
   if constexpr (sizeof(T) == 2) {
-    o[0] = (cmx_f2){__uint_as_float(v.a.x << 16), __uint_as_float(v.a.x & 0xffff0000u)};
-    o[1] = (cmx_f2){__uint_as_float(v.a.y << 16), __uint_as_float(v.a.y & 0xffff0000u)};
+    o[0] = unpack2<T>(v.a.x);
+    o[1] = unpack2<T>(v.a.y);
   } else {
     o[0] = (cmx_f2){v.a.x, v.a.y}; o[1] = (cmx_f2){v.a.z, v.a.w};
   }
 }
 template <typename T>
 __device__ __forceinline__ void v4_store(T* p, const cmx_f2 (&o)[2]) {
-  if constexpr (sizeof(T) == 2) *reinterpret_cast<uint2*>(p) = make_uint2(pack2_bf16(o[0].x, o[0].y), pack2_bf16(o[1].x, o[1].y));
+  if constexpr (sizeof(T) == 2) *reinterpret_cast<uint2*>(p) = make_uint2(pack2<T>(o[0].x, o[0].y), pack2<T>(o[1].x, o[1].y));
   else *reinterpret_cast<float4*>(p) = make_float4(o[0].x, o[0].y, o[1].x, o[1].y);
 }
 // stage a (RY x RX)-pixel region into a pixel-major image img[px][CB]; zeros outside the image
@@ -767,7 +768,7 @@ int bwd_slots(int CQ, int nstrips) {
 
 // LDS-tiled path when the channel count splits into 32-channel blocks (every B0/B2 layer)
 // (fp32 parity mode: 32-channel blocks, so the backward's three tiles fit twice per CU)
-static int tile_cb(int C, int dtype) { return (C % 64 == 0 && dtype == 1) ? 64 : C % 32 == 0 ? 32 : 0; }
+static int tile_cb(int C, int dtype) { return (C % 64 == 0 && (dtype == 1 || dtype == 2)) ? 64 : C % 32 == 0 ? 32 : 0; }
 
 extern "C" {
 

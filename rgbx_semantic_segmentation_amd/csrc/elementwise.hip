@@ -71,6 +71,12 @@ __global__ void cast_f32_bf16_kernel(const float* __restrict__ src, bf16* __rest
     dst[i] = from_f32<bf16>(src[i]);
 }
 
+template <typename S>
+__global__ void cast_f32_h16_kernel(const float* __restrict__ src, S* __restrict__ dst, long n) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    dst[i] = from_f32<S>(src[i]);
+}
+
 // Column sums of x (G, M, N) -> ws partials (G, nblk, N).  TPR lanes span a column tile of
 // TPR*V columns (blockIdx.z), 256/TPR row slots stride over rows.
 template <typename T, int TPR>
@@ -114,23 +120,6 @@ __global__ void colsum_scalar_kernel(const T* __restrict__ x, float* __restrict_
     const T* base = x + (long)g * M * ld + c;
     for (long m = blockIdx.x; m < M; m += gridDim.x) acc += to_f32(base[m * ld]);
     ws[((long)g * gridDim.x + blockIdx.x) * N + c] = acc;
-  }
-}
-
-// bf16 gradient payload of the data-parallel exchange (dist.BucketedGradSync, payload "bf16"):
-// after an all-to-all, rank r holds P bf16 chunks of its shard, one per rank; they are summed
-// in fp32 and the shard is re-emitted in bf16 for the all-gather (fp32 accumulation, half the
-// bytes of an fp32 all-reduce on the wire).  8 elements per thread, 16-B accesses.
-__global__ void shard_sum_bf16_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, int P, long n8) {
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int p = 0; p < P; ++p) {
-      float v[8];
-      load_vec<bf16>(in + ((long)p * n8 + i) * 8, v);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += v[e];
-    }
-    store_vec<bf16>(out + i * 8, acc);
   }
 }
 
@@ -241,14 +230,13 @@ int cmx_cast_f32_bf16(const float* src, void* dst, long n, hipStream_t s) {
   return cmx_check_launch("cast_f32_bf16");
 }
 
-// out[i] = bf16(sum_p in[p * n + i]) in fp32, p < P; n % 8 == 0
-int cmx_shard_sum_bf16(const void* in, void* out, int P, long n, hipStream_t s) {
-  CMX_REQUIRE(P > 0 && n % 8 == 0 && ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0, CMX_ERR_SHAPE,
-              "shard_sum_bf16: P=%d n=%ld (n %% 8, 16-B aligned)", P, n);
+// fp32 -> bf16 (dtype 1) / fp16 (dtype 2), round to nearest even: the weight shadow refresh
+int cmx_cast_f32_h16(const float* src, void* dst, long n, int dtype, hipStream_t s) {
+  CMX_REQUIRE(dtype == 1 || dtype == 2, CMX_ERR_DTYPE, "cast_f32_h16: dtype %d", dtype);
   if (n == 0) return CMX_OK;
-  hipLaunchKernelGGL(shard_sum_bf16_kernel, dim3(ew_grid(n / 8)), dim3(256), 0, s, (const bf16*)in, (bf16*)out, P,
-                     n / 8);
-  return cmx_check_launch("shard_sum_bf16");
+  if (dtype == 2) hipLaunchKernelGGL(cast_f32_h16_kernel<f16>, dim3(ew_grid(n)), dim3(256), 0, s, src, (f16*)dst, n);
+  else hipLaunchKernelGGL(cast_f32_h16_kernel<bf16>, dim3(ew_grid(n)), dim3(256), 0, s, src, (bf16*)dst, n);
+  return cmx_check_launch("cast_f32_h16");
 }
 
 int cmx_cast_bf16_f32(const void* src, float* dst, long n, hipStream_t s) {

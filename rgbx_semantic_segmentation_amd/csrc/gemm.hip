@@ -269,18 +269,21 @@ __device__ __forceinline__ void stage_r(const i32x4 rsrc, char* img, long ld, in
   }
 }
 
+template <typename E> using frag8 = typename MF<E>::frag;
+
 // fragment of sub-tile rows [rb, rb + 32), k16-step s, from a [ROWS][64] image
-__device__ __forceinline__ bf16x8 frag_k(const char* img, int rb, int s, int lane) {
+template <typename E>
+__device__ __forceinline__ frag8<E> frag_k(const char* img, int rb, int s, int lane) {
   const int r = lane & 31, h = lane >> 5;
   const int row = rb + r;
   const int pos = (2 * s + h) ^ ((row >> 1) & 7);
-  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(img + row * 128 + pos * 16));
+  return __builtin_bit_cast(frag8<E>, *reinterpret_cast<const uint4*>(img + row * 128 + pos * 16));
 }
 
 // same fragment from a transposed [64][ROWS] image: two ds_read_b64_tr_b16 (k 0-3, 4-7 of
 // the lane's 8), each delivering column (16*g16 + i) of a 4 x 16 block
-template <int ROWS>
-__device__ __forceinline__ bf16x8 frag_r(const char* img, int rb, int s, int lane) {
+template <typename E, int ROWS>
+__device__ __forceinline__ frag8<E> frag_r(const char* img, int rb, int s, int lane) {
   const int h = lane >> 5, g16 = (lane >> 4) & 1, i = lane & 15, q = i >> 2, pp = i & 3;
   const int col = rb + 16 * g16 + 4 * pp;
   const int chunk = col >> 3;
@@ -294,7 +297,7 @@ __device__ __forceinline__ bf16x8 frag_r(const char* img, int rb, int s, int lan
   }
   typedef short s16x8 __attribute__((ext_vector_type(8)));
   const s16x8 c = __builtin_shufflevector(v[0], v[1], 0, 1, 2, 3, 4, 5, 6, 7);
-  return __builtin_bit_cast(bf16x8, c);
+  return __builtin_bit_cast(frag8<E>, c);
 }
 
 // NS = LDS stages in the DMA ring: 2 for grids of >= 2 blocks per CU (the co-resident block
@@ -311,7 +314,8 @@ constexpr int gemm_smem_bytes() {
 
 // One output tile (of one split / group) of problem p.  `lin` = the block's linear index
 // within the problem, in (split, group, tile) order; smem = gemm_smem_bytes<BM, BN, NS>().
-template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1>
+// E = the 16-bit storage type (bf16 or f16: v_mfma_f32_32x32x16_bf16 / _f16, same tiles and rate)
+template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1, typename E = bf16>
 __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin, char* smem) {
   constexpr int A_BYTES = BM * FBK * 2, STAGE = (BM + BN) * FBK * 2, SLOT = KW * STAGE;
   constexpr int TM = BM / 64, TN = BN / 64;
@@ -319,9 +323,9 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
   const int ntile = p.tiles_m * p.tiles_n;
   const int t = lin % ntile, g = (lin / ntile) % p.G, z = lin / (ntile * p.G);
   const int tm = t / p.tiles_n, tn = t % p.tiles_n;
-  const bf16* Ag = reinterpret_cast<const bf16*>(p.A) + (long)g * p.sA;
-  const bf16* A2g = p.A2 ? reinterpret_cast<const bf16*>(p.A2) + (long)g * p.sA2 : Ag;
-  const bf16* Bg = reinterpret_cast<const bf16*>(p.B) + (long)g * p.sB;
+  const E* Ag = reinterpret_cast<const E*>(p.A) + (long)g * p.sA;
+  const E* A2g = p.A2 ? reinterpret_cast<const E*>(p.A2) + (long)g * p.sA2 : Ag;
+  const E* Bg = reinterpret_cast<const E*>(p.B) + (long)g * p.sB;
   const i32x4 rA = make_rsrc(Ag), rA2 = make_rsrc(A2g), rB = make_rsrc(Bg);
   const int i0 = tm * BM, j0 = tn * BN;
   const int nreal = p.ones_col ? p.N - 1 : p.N;
@@ -336,7 +340,8 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
 #pragma unroll
     for (int b = 0; b < TN; ++b) acc[a][b] = zero16();
   }
-  const bf16x8 ones = __builtin_bit_cast(bf16x8, make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u));
+  constexpr uint32_t one2 = (uint32_t)one_bits<E> * 0x10001u;
+  const frag8<E> ones = __builtin_bit_cast(frag8<E>, make_uint4(one2, one2, one2, one2));
 
   const int nk = (p.K + FBK * KW - 1) / (FBK * KW);   // ring slots of KW x 64 k
   const int kt0 = z * p.kt_per_split;
@@ -417,26 +422,26 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
     const char* bi = buf + A_BYTES;
 #pragma unroll
     for (int s = 0; s < FBK / 16; ++s) {
-      bf16x8 fa[TM], fb[TN];
+      frag8<E> fa[TM], fb[TN];
 #pragma unroll
       for (int a = 0; a < TM; ++a) {
         const int rb = wm * (BM / 2) + a * 32;
-        if constexpr (TA) fa[a] = frag_r<BM>(ai, rb, s, lane);
-        else fa[a] = frag_k(ai, rb, s, lane);
+        if constexpr (TA) fa[a] = frag_r<E, BM>(ai, rb, s, lane);
+        else fa[a] = frag_k<E>(ai, rb, s, lane);
       }
 #pragma unroll
       for (int b = 0; b < TN; ++b) {
         const int rb = wn * (BN / 2) + b * 32;
-        if constexpr (TB) fb[b] = frag_r<BN>(bi, rb, s, lane);
-        else fb[b] = frag_k(bi, rb, s, lane);
+        if constexpr (TB) fb[b] = frag_r<E, BN>(bi, rb, s, lane);
+        else fb[b] = frag_k<E>(bi, rb, s, lane);
       }
 #pragma unroll
       for (int a = 0; a < TM; ++a)
 #pragma unroll
-        for (int b = 0; b < TN; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[b], fa[a], acc[a][b], 0, 0, 0);
+        for (int b = 0; b < TN; ++b) acc[a][b] = MF<E>::mma(fb[b], fa[a], acc[a][b]);
       if (do_db) {
 #pragma unroll
-        for (int a = 0; a < TM; ++a) accd[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fa[a], accd[a], 0, 0, 0);
+        for (int a = 0; a < TM; ++a) accd[a] = MF<E>::mma(ones, fa[a], accd[a]);
       }
     }
   };
@@ -447,24 +452,27 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
   // refilled was last read in the previous iteration, which every wave has left.
   constexpr int PER = BM / 32 + BN / 32;        // LDS-DMA instructions per stage per wave
   auto wait_keep = [](int keep) {               // all but the `keep` most recent tiles landed
-    if (NS > 7 && keep >= 6) vm_wait<6 * PER>();
-    else if (NS > 6 && keep == 5) vm_wait<5 * PER>();
-    else if (NS > 5 && keep == 4) vm_wait<4 * PER>();
-    else if (NS > 4 && keep == 3) vm_wait<3 * PER>();
+    if (NS > 7 && keep >= 7) vm_wait<7 * PER>();
+    else if (NS > 6 && keep >= 6) vm_wait<6 * PER>();
+    else if (NS > 5 && keep == 5) vm_wait<5 * PER>();
+    else if (NS > 4 && keep == 4) vm_wait<4 * PER>();
+    else if (NS > 3 && keep == 3) vm_wait<3 * PER>();
     else if (keep >= 2) vm_wait<2 * PER>();
     else if (keep == 1) vm_wait<PER>();
     else vm_wait<0>();
   };
-  const int pro = min(NS - 1, kt1 - kt0);
+  // a k-range that fits the ring is issued whole in the prologue (every tile in flight at
+  // once, no refills); a longer one keeps NS - 1 tiles ahead and refills the slot just read
+  const int pro = kt1 - kt0 <= NS ? kt1 - kt0 : NS - 1;
 #pragma unroll
-  for (int q = 0; q < NS - 1; ++q)
+  for (int q = 0; q < NS; ++q)
     if (q < pro) stage(kt0 + q, smem + q * SLOT);
   wait_keep(pro - 1);
   __syncthreads();
   int cur = 0;
   for (int kt = kt0; kt < kt1; ++kt) {
     const int nxt = cur == 0 ? NS - 1 : cur - 1;
-    if (kt + NS - 1 < kt1) stage(kt + NS - 1, smem + nxt * SLOT);
+    if (kt + NS - 1 < kt1 && kt + NS - 1 >= kt0 + pro) stage(kt + NS - 1, smem + nxt * SLOT);
     compute(smem + cur * SLOT);
     // tiles kt+1 .. kt+ahead are in flight; retire tile kt+1, keep the rest
     const int ahead = min(NS - 1, kt1 - 1 - kt);
@@ -535,17 +543,17 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
         for (int e = 0; e < nv; ++e) d[e] = v[e];
       }
     } else {
-      epi_store8<bf16>(p, g, i, j, nv, v);
+      epi_store8<E>(p, g, i, j, nv, v);
     }
   }
 }
 
 // 1-D grid over (split, group, tile); each XCD gets a contiguous run of that order, i.e.
 // neighbouring tiles of one (split, group): they share A row panels and the B k-slice in L2
-template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1>
+template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1, typename E = bf16>
 __global__ __launch_bounds__(256 * KW, KW == 4 ? 1 : 2) void gemm_bf16_kernel(const GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[gemm_smem_bytes<BM, BN, NS, KW>()];
-  gemm_bf16_body<BM, BN, TA, TB, NS, KW>(p, xcd_tile(blockIdx.x, p.tiles_m * p.tiles_n * p.G * p.nsplit), smem);
+  gemm_bf16_body<BM, BN, TA, TB, NS, KW, E>(p, xcd_tile(blockIdx.x, p.tiles_m * p.tiles_n * p.G * p.nsplit), smem);
 }
 
 // ============================================================================ grouped launch
@@ -571,6 +579,7 @@ __device__ __forceinline__ int xcd_chunk_tile(int b, int nt, int ch) {
   return ((j / ch) * 8 + x) * ch + j % ch;
 }
 
+template <typename E>
 __global__ __launch_bounds__(256, 2) void gemm_grouped_kernel(const GroupRec* __restrict__ recs, int nrec, int chunk) {
   __shared__ __attribute__((aligned(1024))) char smem[gemm_smem_bytes<128, 128, 2>()];
   const int lin = chunk > 0 ? xcd_chunk_tile(blockIdx.x, gridDim.x, chunk) : xcd_tile(blockIdx.x, gridDim.x);
@@ -582,10 +591,10 @@ __global__ __launch_bounds__(256, 2) void gemm_grouped_kernel(const GroupRec* __
   const GroupRec& r = recs[lo];
   const GemmArgs p = r.a;
   const int local = lin - r.blk0;
-  if (r.bm == 128 && r.bn == 128) gemm_bf16_body<128, 128, true, true, 2>(p, local, smem);
-  else if (r.bm == 128) gemm_bf16_body<128, 64, true, true, 2>(p, local, smem);
-  else if (r.bn == 128) gemm_bf16_body<64, 128, true, true, 2>(p, local, smem);
-  else gemm_bf16_body<64, 64, true, true, 2>(p, local, smem);
+  if (r.bm == 128 && r.bn == 128) gemm_bf16_body<128, 128, true, true, 2, 1, E>(p, local, smem);
+  else if (r.bm == 128) gemm_bf16_body<128, 64, true, true, 2, 1, E>(p, local, smem);
+  else if (r.bn == 128) gemm_bf16_body<64, 128, true, true, 2, 1, E>(p, local, smem);
+  else gemm_bf16_body<64, 64, true, true, 2, 1, E>(p, local, smem);
 }
 
 // ============================================================================ grouped reduce
@@ -649,6 +658,7 @@ constexpr int BK = 32;
 
 template <typename T> struct Stage;
 template <> struct Stage<bf16> { static constexpr int V = 8, PAD = 8; typedef uint4 raw; };
+template <> struct Stage<f16> { static constexpr int V = 8, PAD = 8; typedef uint4 raw; };
 template <> struct Stage<float> { static constexpr int V = 4, PAD = 4; typedef float4 raw; };
 
 template <typename T, int ROWS>
@@ -891,10 +901,10 @@ void launch_reduce(const GemmArgs& a, int G, long groups, hipStream_t s) {
 }
 
 // ============================================================================ host side
-template <int BM, int BN, int NS, int KW = 1>
+template <int BM, int BN, int NS, int KW = 1, typename E = bf16>
 void launch_bf16(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream_t s) {
   dim3 grid(a.tiles_m * a.tiles_n * G * nsplit);
-#define CMX_GEMM_LAUNCH(TA, TB) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, TA, TB, NS, KW>), grid, dim3(256 * KW), 0, s, a)
+#define CMX_GEMM_LAUNCH(TA, TB) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, TA, TB, NS, KW, E>), grid, dim3(256 * KW), 0, s, a)
   if (!tA && !tB) CMX_GEMM_LAUNCH(false, false);
   else if (!tA && tB) CMX_GEMM_LAUNCH(false, true);
   else if (tA && tB) CMX_GEMM_LAUNCH(true, true);
@@ -902,7 +912,7 @@ void launch_bf16(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream
 #undef CMX_GEMM_LAUNCH
 }
 
-template <int BM, int BN>
+template <int BM, int BN, typename E = bf16>
 void launch_bf16_ns(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream_t s) {
   const long blocks = (long)a.tiles_m * a.tiles_n * G * nsplit;
   // a 64 x 64 stage is only 16 KB, so a 4-deep ring (64 KB) would still leave two blocks per
@@ -913,23 +923,43 @@ void launch_bf16_ns(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStr
   // K 2048 20.1 -> 11.9 us, K 512 7.5 -> 5.8 us at KW = 2; grids above 512 blocks and one-slot
   // problems are slower with it (M9600 N128 K512: 9.7 -> 10.4 us), so they keep 4 waves.
   static const int kw = [] { const char* e = getenv("CMX_GEMM_KW"); return e ? atoi(e) : 2; }();
+  // CMX_GEMM_DEEP=1: a 64 x 64 problem whose whole k-range fits a 5- (two blocks per CU) or
+  // 8-slot ring (one block per CU, grids of <= 256 blocks) issues every k-tile at once
+  static const int deep = [] { const char* e = getenv("CMX_GEMM_DEEP"); return e ? atoi(e) : 0; }();
   if constexpr (BM == 64 && BN == 64) {
     const int nk64 = (a.K + FBK - 1) / FBK;
+    if (deep && nsplit == 1 && !a.ones_col && nk64 >= 2) {
+      if (nk64 <= 5 && blocks <= 512) { launch_bf16<64, 64, 5, 1, E>(a, G, nsplit, tA, tB, s); return; }
+      if (nk64 <= 8 && blocks <= 256) { launch_bf16<64, 64, 8, 1, E>(a, G, nsplit, tA, tB, s); return; }
+    }
     if (kw >= 2 && nsplit == 1 && !a.ones_col && blocks <= 512 && nk64 >= 4) {
       GemmArgs b = a;
       if (kw >= 4 && blocks <= 256 && nk64 >= 16) {
         b.kt_per_split = (b.K + 4 * FBK - 1) / (4 * FBK);
-        launch_bf16<64, 64, 2, 4>(b, G, nsplit, tA, tB, s);
+        launch_bf16<64, 64, 2, 4, E>(b, G, nsplit, tA, tB, s);
         return;
       }
       b.kt_per_split = (b.K + 2 * FBK - 1) / (2 * FBK);
-      if (blocks <= 256) launch_bf16<64, 64, 4, 2>(b, G, nsplit, tA, tB, s);
-      else launch_bf16<64, 64, 2, 2>(b, G, nsplit, tA, tB, s);
+      if (blocks <= 256) launch_bf16<64, 64, 4, 2, E>(b, G, nsplit, tA, tB, s);
+      else launch_bf16<64, 64, 2, 2, E>(b, G, nsplit, tA, tB, s);
       return;
     }
   }
-  if (blocks <= 256 || (BM == 64 && BN == 64 && ns64 == 4)) launch_bf16<BM, BN, 4>(a, G, nsplit, tA, tB, s);
-  else launch_bf16<BM, BN, 2>(a, G, nsplit, tA, tB, s);
+  if (blocks <= 256 || (BM == 64 && BN == 64 && ns64 == 4)) launch_bf16<BM, BN, 4, 1, E>(a, G, nsplit, tA, tB, s);
+  else launch_bf16<BM, BN, 2, 1, E>(a, G, nsplit, tA, tB, s);
+}
+
+// the 16-bit fast path for one problem: tile shape (bm, bn), element type from dtype (1 bf16, 2 fp16)
+template <typename E>
+void launch_fast_t(const GemmArgs& a, int bm, int bn, int G, int nsplit, int tA, int tB, hipStream_t s) {
+  if (bm == 64 && bn == 64) launch_bf16_ns<64, 64, E>(a, G, nsplit, tA, tB, s);
+  else if (bm == 64) launch_bf16_ns<64, 128, E>(a, G, nsplit, tA, tB, s);
+  else if (bn == 64) launch_bf16_ns<128, 64, E>(a, G, nsplit, tA, tB, s);
+  else launch_bf16_ns<128, 128, E>(a, G, nsplit, tA, tB, s);
+}
+void launch_fast(const GemmArgs& a, int bm, int bn, int G, int nsplit, int tA, int tB, int dtype, hipStream_t s) {
+  if (dtype == 2) launch_fast_t<f16>(a, bm, bn, G, nsplit, tA, tB, s);
+  else launch_fast_t<bf16>(a, bm, bn, G, nsplit, tA, tB, s);
 }
 
 template <typename T, int BM, int BN, bool EXT>
@@ -1052,7 +1082,7 @@ size_t cmx_gemm_workspace(int G, int M, int N, int splitk) {
 
 int cmx_gemm_splitk(int G, int M, int N, int K, int ones_col, int dtype) {
   if (G <= 0 || M <= 0 || N <= 0 || K <= 0) return 1;
-  if (dtype == 1) return auto_split(G, M, N, K, ones_col);
+  if (dtype == 1 || dtype == 2) return auto_split(G, M, N, K, ones_col);
   // generic path: BK = 32, aim for ~1024 blocks with >= 8 k-tiles per split
   const int nb = ones_col ? N : N;
   const long tiles = (long)cdiv(M, M <= 64 ? 64 : 128) * cdiv(nb, nb <= 64 ? 64 : 128) * G;
@@ -1079,7 +1109,7 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
               int dtype, hipStream_t s, const UpSpec* up, int scR = 0, int scH = 0, int scW = 0, int scC = 0,
               int scHo = 0, int scWo = 0) {
   CMX_REQUIRE(G > 0 && M > 0 && N > 0 && K > 0, CMX_ERR_SHAPE, "gemm: empty problem G=%d M=%d N=%d K=%d", G, M, N, K);
-  CMX_REQUIRE(dtype == 0 || dtype == 1, CMX_ERR_DTYPE, "gemm: unsupported dtype %d", dtype);
+  CMX_REQUIRE(dtype >= 0 && dtype <= 2, CMX_ERR_DTYPE, "gemm: unsupported dtype %d", dtype);
   CMX_REQUIRE(out_mode >= 0 && out_mode <= 2 && act >= 0 && act <= 3, CMX_ERR_ARG, "gemm: out_mode/act");
   CMX_REQUIRE(!(R && out_mode == 2), CMX_ERR_ARG, "gemm: residual with accumulate");
   if (!A2) K1 = K;
@@ -1089,7 +1119,7 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
   CMX_REQUIRE(!ones_col || (transB && dbias && N >= 2 && out_mode != 0 && !bias && !R && act == 0), CMX_ERR_ARG,
               "gemm: ones_col (bias gradient) needs transB, dbias, fp32 output and no epilogue");
   CMX_REQUIRE((long)M * N < (1L << 31) && (long)M * K < (1L << 40), CMX_ERR_SHAPE, "gemm: problem too large");
-  const bool fast = dtype == 1 && fast_ok(A, A2, B, M, N, K, K1, lda, lda2, ldb, sA, sA2, sB, transA, transB, ones_col);
+  const bool fast = dtype != 0 && fast_ok(A, A2, B, M, N, K, K1, lda, lda2, ldb, sA, sA2, sB, transA, transB, ones_col);
   const int V = dtype == 0 ? 4 : 8;
   const int nb = ones_col ? N - 1 : N;
   const bool vec = (transA ? M : K) % V == 0 && (transB ? nb : K) % V == 0 && (K - K1) % V == 0 && (K1 == K || K1 % V == 0) &&
@@ -1103,7 +1133,7 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
   a.G = G; a.M = M; a.N = N; a.K = K; a.K1 = K1; a.rows_per_sample = rows_per_sample > 0 ? rows_per_sample : 1;
   a.act = act; a.out_mode = out_mode; a.ones_col = ones_col; a.vec = vec;
   // 8-column epilogue groups as aligned vectors: C (and R) rows start on 16-B boundaries
-  const long esz = out_mode == 0 ? (dtype == 1 ? 2 : 4) : 4;
+  const long esz = out_mode == 0 ? (dtype != 0 ? 2 : 4) : 4;
   a.cvec = ((uintptr_t)C % 16 == 0) && (ldc * esz) % 16 == 0 && (sC * esz) % 16 == 0 &&
            (!R || (uintptr_t)R % 16 == 0);
   a.lda = lda; a.lda2 = lda2; a.ldb = ldb; a.ldc = ldc; a.sA = sA; a.sA2 = sA2; a.sB = sB; a.sC = sC;
@@ -1134,10 +1164,7 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
     int bm, bn;
     plan_tiles(G, M, nb, K, &bm, &bn);
     a.tiles_m = cdiv(M, bm); a.tiles_n = cdiv(nb, bn);
-    if (bm == 64 && bn == 64) launch_bf16_ns<64, 64>(a, G, splitk, transA, transB, s);
-    else if (bm == 64) launch_bf16_ns<64, 128>(a, G, splitk, transA, transB, s);
-    else if (bn == 64) launch_bf16_ns<128, 64>(a, G, splitk, transA, transB, s);
-    else launch_bf16_ns<128, 128>(a, G, splitk, transA, transB, s);
+    launch_fast(a, bm, bn, G, splitk, transA, transB, dtype, s);
   } else {
     // tile shape: the output's narrow side gets 64 (stage-1 C = 64 outputs, 64-row wgrads)
     const bool m64 = M <= 64, n64 = N <= 64;
@@ -1147,6 +1174,11 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
       else if (m64) launch_generic<bf16, 64, 128>(a, G, splitk, transA, transB, s);
       else if (n64) launch_generic<bf16, 128, 64>(a, G, splitk, transA, transB, s);
       else launch_generic<bf16, 128, 128>(a, G, splitk, transA, transB, s);
+    } else if (dtype == 2) {
+      if (m64 && n64) launch_generic<f16, 64, 64>(a, G, splitk, transA, transB, s);
+      else if (m64) launch_generic<f16, 64, 128>(a, G, splitk, transA, transB, s);
+      else if (n64) launch_generic<f16, 128, 64>(a, G, splitk, transA, transB, s);
+      else launch_generic<f16, 128, 128>(a, G, splitk, transA, transB, s);
     } else {
       if (m64 && n64) launch_generic<float, 64, 64>(a, G, splitk, transA, transB, s);
       else if (m64) launch_generic<float, 64, 128>(a, G, splitk, transA, transB, s);
@@ -1157,6 +1189,7 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
   if (splitk > 1) {
     const long work = (long)M * ((nb + 7) / 8) + (ones_col ? M : 0);
     if (dtype == 1) launch_reduce<bf16>(a, G, work, s);
+    else if (dtype == 2) launch_reduce<f16>(a, G, work, s);
     else launch_reduce<float>(a, G, work, s);
   }
   return cmx_check_launch("gemm");
@@ -1307,8 +1340,8 @@ int cmx_gemm_group_pack_conv_wgrad(void* rec, const void* dy, const void* x, flo
 int cmx_conv_implicit_fwd(const void* x, const void* Wt, void* y, const float* bias, float* workspace, int G, int NIg,
                           int H, int Wd, int C, int KH, int KW, int stride, int pad, int Ho, int Wo, int N, int64_t sx,
                           int64_t sW, int64_t sy, int64_t sbias, int splitk, int dtype, hipStream_t s) {
-  CMX_REQUIRE(dtype == 1 && C % 64 == 0 && N % 8 == 0 && G > 0 && NIg > 0, CMX_ERR_SHAPE,
-              "conv_implicit_fwd: bf16 with C %% 64 == 0 only (C=%d, N=%d)", C, N);
+  CMX_REQUIRE((dtype == 1 || dtype == 2) && C % 64 == 0 && N % 8 == 0 && G > 0 && NIg > 0, CMX_ERR_SHAPE,
+              "conv_implicit_fwd: bf16 / fp16 with C %% 64 == 0 only (C=%d, N=%d)", C, N);
   CMX_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)Wt & 15) == 0 && ((uintptr_t)y & 15) == 0 && sx % 8 == 0 &&
               sW % 8 == 0 && sy % 8 == 0, CMX_ERR_ARG, "conv_implicit_fwd: alignment");
   const long M = (long)NIg * Ho * Wo, K = (long)KH * KW * C;
@@ -1332,15 +1365,16 @@ int cmx_conv_implicit_fwd(const void* x, const void* Wt, void* y, const float* b
   int bm, bn;
   plan_tiles(G, (int)M, N, (int)K, &bm, &bn);
   a.tiles_m = cdiv(M, bm); a.tiles_n = cdiv(N, bn);
-  if (bm == 64 && bn == 64) launch_bf16_ns<64, 64>(a, G, splitk, 0, 0, s);
-  else if (bm == 64) launch_bf16_ns<64, 128>(a, G, splitk, 0, 0, s);
-  else if (bn == 64) launch_bf16_ns<128, 64>(a, G, splitk, 0, 0, s);
-  else launch_bf16_ns<128, 128>(a, G, splitk, 0, 0, s);
-  if (splitk > 1) launch_reduce<bf16>(a, G, (long)M * ((N + 7) / 8), s);
+  launch_fast(a, bm, bn, G, splitk, 0, 0, dtype, s);
+  if (splitk > 1) {
+    if (dtype == 2) launch_reduce<f16>(a, G, (long)M * ((N + 7) / 8), s);
+    else launch_reduce<bf16>(a, G, (long)M * ((N + 7) / 8), s);
+  }
   return cmx_check_launch("conv_implicit_fwd");
 }
 
-int cmx_gemm_grouped(const void* recs, int nrec, int total_blocks, hipStream_t s) {
+int cmx_gemm_grouped(const void* recs, int nrec, int total_blocks, int dtype, hipStream_t s) {
+  CMX_REQUIRE(dtype == 1 || dtype == 2, CMX_ERR_DTYPE, "gemm_grouped: operands bf16 (1) or fp16 (2), got %d", dtype);
   CMX_REQUIRE(recs && nrec > 0 && total_blocks > 0, CMX_ERR_ARG, "gemm_grouped: empty launch");
   // XCD map of the grouped grid: chunked round-robin with 64-tile runs (CMX_GROUPED_CHUNK=n to
   // change the run, 0 = the contiguous xcd_tile map).  Measured on the B2 step's 8174-block
@@ -1351,7 +1385,10 @@ int cmx_gemm_grouped(const void* recs, int nrec, int total_blocks, hipStream_t s
     const char* e = getenv("CMX_GROUPED_CHUNK");
     return e ? atoi(e) : 64;
   }();
-  hipLaunchKernelGGL(gemm_grouped_kernel, dim3(total_blocks), dim3(256), 0, s, (const GroupRec*)recs, nrec, chunk);
+  if (dtype == 2)
+    hipLaunchKernelGGL(gemm_grouped_kernel<f16>, dim3(total_blocks), dim3(256), 0, s, (const GroupRec*)recs, nrec, chunk);
+  else
+    hipLaunchKernelGGL(gemm_grouped_kernel<bf16>, dim3(total_blocks), dim3(256), 0, s, (const GroupRec*)recs, nrec, chunk);
   return cmx_check_launch("gemm_grouped");
 }
 

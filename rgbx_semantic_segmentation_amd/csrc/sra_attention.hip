@@ -90,8 +90,8 @@ __device__ __forceinline__ void store4(T* p, const float* v) {
   if constexpr (sizeof(T) == 4) {
     *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
   } else {
-    uint32_t a = pack2_bf16(v[0], v[1]);
-    uint32_t b = pack2_bf16(v[2], v[3]);
+    uint32_t a = pack2<T>(v[0], v[1]);
+    uint32_t b = pack2<T>(v[2], v[3]);
     *reinterpret_cast<uint2*>(p) = make_uint2(a, b);
   }
 }
@@ -436,19 +436,19 @@ int bwd_qc(int N, int nchunk) {
 
 }  // namespace
 
-// sra_fast.hip: LDS-resident K/V path for bf16, D = 64, Nk <= 320
+// sra_fast.hip: LDS-resident K/V path for bf16 / fp16, D = 64
 bool sra_fast_ok(int D, int Nk, int dtype, const void* const* ptrs, int nptr, const long* strides, int nstr);
 bool sra_fast_fwd_ok(int D, int Nk, int dtype, const void* const* ptrs, int nptr, const long* strides, int nstr);
 void sra_fwd_fast_launch(const void* q, const void* k, const void* v, void* o, float* lse, int Bt, int N, int Nk,
-                         int heads, long qs, long kvs, long os, float sl2, hipStream_t s);
+                         int heads, long qs, long kvs, long os, float sl2, int dtype, hipStream_t s);
 void sra_dq_fast_launch(const void* q, const void* k, const void* v, const void* o, const void* dout,
                         const float* lse, float* Dws, void* dq, int Bt, int N, int Nk, int heads, long qs, long kvs,
-                        long os, long dos, long dqs, float sl2, float scale, hipStream_t s);
+                        long os, long dos, long dqs, float sl2, float scale, int dtype, hipStream_t s);
 int sra_dkv_fast_chunks(int Bt, int N, int Nk, int heads);
 void sra_dkv_fast_launch(const void* q, const void* k, const void* v, const void* dout, const float* lse,
                          const float* Dws, float* ws_dk, float* ws_dv, void* dk, void* dv, long dkvs, int Bt, int N,
                          int Nk, int heads, long qs,
-                         long kvs, long dos, int nchunk, float sl2, float scale, hipStream_t s);
+                         long kvs, long dos, int nchunk, float sl2, float scale, int dtype, hipStream_t s);
 
 #define SRA_D_DISPATCH(D, ...)                                              \
   do {                                                                      \
@@ -470,7 +470,7 @@ int cmx_sra_attn_fwd(const void* q, const void* k, const void* v, void* o, float
     const void* ptrs[] = {q, k, v, o};
     const long strides[] = {qs, kvs, os};
     if (sra_fast_fwd_ok(D, Nk, dtype, ptrs, 4, strides, 3)) {
-      sra_fwd_fast_launch(q, k, v, o, lse, Bt, N, Nk, heads, qs, kvs, os, sl2, s);
+      sra_fwd_fast_launch(q, k, v, o, lse, Bt, N, Nk, heads, qs, kvs, os, sl2, dtype, s);
       return cmx_check_launch("sra_fwd");
     }
   }
@@ -510,14 +510,14 @@ int cmx_sra_attn_bwd(const void* q, const void* k, const void* v, const void* o,
   float* ws_dv = ws_dk + (size_t)nc * Bt * heads * Nk * D;
   SRA_D_DISPATCH(D, CMX_DISPATCH(dtype, T, {
     if (fast_dq)
-      sra_dq_fast_launch(q, k, v, o, dout, lse, Dws, dq, Bt, N, Nk, heads, qs, kvs, os, dos, dqs, sl2, scale, s);
+      sra_dq_fast_launch(q, k, v, o, dout, lse, Dws, dq, Bt, N, Nk, heads, qs, kvs, os, dos, dqs, sl2, scale, dtype, s);
     else
       hipLaunchKernelGGL((sra_bwd_dq_kernel<T, DD>), dim3(cdiv(N, BQ), heads, Bt), dim3(256), 0, s,
                          (const T*)q, (const T*)k, (const T*)v, (const T*)o, (const T*)dout, lse, Dws,
                          (T*)dq, N, Nk, heads, qs, kvs, os, dos, dqs, sl2, scale);
     if (fast)
       sra_dkv_fast_launch(q, k, v, dout, lse, Dws, ws_dk, ws_dv, dk, dv, dkvs, Bt, N, Nk, heads, qs, kvs, dos, nc, sl2,
-                          scale, s);
+                          scale, dtype, s);
     else
       hipLaunchKernelGGL((sra_bwd_dkv_kernel<T, DD>), dim3(cdiv(Nk, BK), heads, Bt * nc), dim3(256), 0, s,
                          (const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse, Dws, ws_dk, ws_dv, Bt,

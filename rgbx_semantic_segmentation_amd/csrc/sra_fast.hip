@@ -24,6 +24,9 @@
 
 namespace {
 
+template <typename E> using frag8 = typename MF<E>::frag;
+
+
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int HD = 64;          // head dim
@@ -38,7 +41,8 @@ __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 // (no register staging; rows >= Nk come back as zeros through the buffer range check).  One
 // wave instruction fills 8 rows (1 KB) in lane order: lane L lands on row 8j + L / 8, slot
 // L % 8, which must hold chunk (L % 8) ^ swz(row).  Completion: vm_wait<0>() + barrier.
-__device__ __forceinline__ void stage_rows(const bf16* __restrict__ g, long ld, int Nk, int nkp, char* img, int wave,
+template <typename E>
+__device__ __forceinline__ void stage_rows(const E* __restrict__ g, long ld, int Nk, int nkp, char* img, int wave,
                                            int lane, int nwaves) {
   const i32x4 rs = make_rsrc(g);
   for (int j = wave; j < nkp / 8; j += nwaves) {
@@ -49,14 +53,16 @@ __device__ __forceinline__ void stage_rows(const bf16* __restrict__ g, long ld, 
 }
 
 // A operand, k = d contiguous: row rb + (lane & 31), d in [16 s + 8 h, +8)
-__device__ __forceinline__ bf16x8 frag_k(const char* img, int rb, int s, int lane) {
+template <typename E>
+__device__ __forceinline__ frag8<E> frag_k(const char* img, int rb, int s, int lane) {
   const int row = rb + (lane & 31), h = lane >> 5;
-  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(img + row * ROWB + (((2 * s + h) ^ swz(row)) << 4)));
+  return frag_bits<E>(*reinterpret_cast<const uint4*>(img + row * ROWB + (((2 * s + h) ^ swz(row)) << 4)));
 }
 
 // A operand from the transposed view: d = db + (lane & 31) on the lane, k = rows
-// kb + 16 s + 4 h + {0..3, 8..11} (the accumulator-as-B order of MF<bf16>::from_acc)
-__device__ __forceinline__ bf16x8 frag_t(const char* img, int kb, int db, int s, int lane) {
+// kb + 16 s + 4 h + {0..3, 8..11} (the accumulator-as-B order of MF<E>::from_acc)
+template <typename E>
+__device__ __forceinline__ frag8<E> frag_t(const char* img, int kb, int db, int s, int lane) {
   const int h = lane >> 5, g16 = (lane >> 4) & 1, i = lane & 15, q = i >> 2, pp = i & 3;
   const int chunk = (db + 16 * g16 + 4 * pp) >> 3;
   s16x4 v[2];
@@ -68,24 +74,25 @@ __device__ __forceinline__ bf16x8 frag_t(const char* img, int kb, int db, int s,
         reinterpret_cast<__attribute__((address_space(3))) s16x4*>(reinterpret_cast<uintptr_t>(img + off)));
   }
   const s16x8 c = __builtin_shufflevector(v[0], v[1], 0, 1, 2, 3, 4, 5, 6, 7);
-  return __builtin_bit_cast(bf16x8, c);
+  return __builtin_bit_cast(frag8<E>, c);
 }
 
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-__device__ __forceinline__ void store_rows(bf16* row_ptr, const f32x16& acc, int t, int h, float mul) {
+template <typename E>
+__device__ __forceinline__ void store_rows(E* row_ptr, const f32x16& acc, int t, int h, float mul) {
 #pragma unroll
   for (int k4 = 0; k4 < 4; ++k4) {
-    const uint32_t a = pack2_bf16(acc[4 * k4] * mul, acc[4 * k4 + 1] * mul);
-    const uint32_t b = pack2_bf16(acc[4 * k4 + 2] * mul, acc[4 * k4 + 3] * mul);
+    const uint32_t a = pack2<E>(acc[4 * k4] * mul, acc[4 * k4 + 1] * mul);
+    const uint32_t b = pack2<E>(acc[4 * k4 + 2] * mul, acc[4 * k4 + 3] * mul);
     *reinterpret_cast<uint2*>(row_ptr + 32 * t + 8 * k4 + 4 * h) = make_uint2(a, b);
   }
 }
 
 // ------------------------------------------------------------------------ forward
-template <int QW, int NW>
-__global__ __launch_bounds__(64 * NW) void sra_fwd_fast(const bf16* __restrict__ q, const bf16* __restrict__ k,
-                                                       const bf16* __restrict__ v, bf16* __restrict__ o,
+template <typename E, int QW, int NW>
+__global__ __launch_bounds__(64 * NW) void sra_fwd_fast(const E* __restrict__ q, const E* __restrict__ k,
+                                                       const E* __restrict__ v, E* __restrict__ o,
                                                        float* __restrict__ lse, int N, int Nk, int nkp, int heads,
                                                        long qs, long kvs, long os, float sl2) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * NKP_MAX * ROWB];
@@ -95,15 +102,15 @@ __global__ __launch_bounds__(64 * NW) void sra_fwd_fast(const bf16* __restrict__
   const int b = blockIdx.z, head = blockIdx.y;
 
   const int q0 = (blockIdx.x * NW + wave) * 32 * QW;
-  const bf16* qb = q + (long)b * N * qs + head * HD;
-  bf16x8 qf[QW][4];
+  const E* qb = q + (long)b * N * qs + head * HD;
+  frag8<E> qf[QW][4];
 #pragma unroll
   for (int u = 0; u < QW; ++u) {
     const int qi = q0 + 32 * u + r;
 #pragma unroll
     for (int s = 0; s < 4; ++s)
-      qf[u][s] = qi < N ? __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(qb + (long)qi * qs + 16 * s + 8 * h))
-                        : zfrag<bf16>();
+      qf[u][s] = qi < N ? frag_bits<E>(*reinterpret_cast<const uint4*>(qb + (long)qi * qs + 16 * s + 8 * h))
+                        : zfrag<E>();
   }
   f32x16 acc[QW][2];
   float m[QW], l[QW];
@@ -128,14 +135,14 @@ __global__ __launch_bounds__(64 * NW) void sra_fwd_fast(const bf16* __restrict__
     f32x16 sa[QW][2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 kf[4];
+      frag8<E> kf[4];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) kf[s] = frag_k(Ki, t0 + 32 * ks, s, lane);
+      for (int s = 0; s < 4; ++s) kf[s] = frag_k<E>(Ki, t0 + 32 * ks, s, lane);
 #pragma unroll
       for (int u = 0; u < QW; ++u) {
         sa[u][ks] = zero16();
 #pragma unroll
-        for (int s = 0; s < 4; ++s) sa[u][ks] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[s], qf[u][s], sa[u][ks], 0, 0, 0);
+        for (int s = 0; s < 4; ++s) sa[u][ks] = MF<E>::mma(kf[s], qf[u][s], sa[u][ks]);
       }
     }
     const bool tail = t0 + KTILE > nc;
@@ -181,13 +188,13 @@ __global__ __launch_bounds__(64 * NW) void sra_fwd_fast(const bf16* __restrict__
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const bf16x8 v0 = frag_t(Vi, t0 + 32 * ks, 0, s, lane);
-        const bf16x8 v1 = frag_t(Vi, t0 + 32 * ks, 32, s, lane);
+        const frag8<E> v0 = frag_t<E>(Vi, t0 + 32 * ks, 0, s, lane);
+        const frag8<E> v1 = frag_t<E>(Vi, t0 + 32 * ks, 32, s, lane);
 #pragma unroll
         for (int u = 0; u < QW; ++u) {
-          const bf16x8 pf = MF<bf16>::from_acc(sa[u][ks], s);
-          acc[u][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v0, pf, acc[u][0], 0, 0, 0);
-          acc[u][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v1, pf, acc[u][1], 0, 0, 0);
+          const frag8<E> pf = MF<E>::from_acc(sa[u][ks], s);
+          acc[u][0] = MF<E>::mma(v0, pf, acc[u][0]);
+          acc[u][1] = MF<E>::mma(v1, pf, acc[u][1]);
         }
       }
   }
@@ -197,7 +204,7 @@ __global__ __launch_bounds__(64 * NW) void sra_fwd_fast(const bf16* __restrict__
     const int qi = q0 + 32 * u + r;
     if (qi >= N) continue;
     const float inv = 1.f / l[u];
-    bf16* ob = o + ((long)b * N + qi) * os + head * HD;
+    E* ob = o + ((long)b * N + qi) * os + head * HD;
     store_rows(ob, acc[u][0], 0, h, inv);
     store_rows(ob, acc[u][1], 1, h, inv);
     if (h == 0 && lse) lse[((long)b * heads + head) * N + qi] = (m[u] + __log2f(l[u])) * 0.69314718055994531f;
@@ -206,11 +213,11 @@ __global__ __launch_bounds__(64 * NW) void sra_fwd_fast(const bf16* __restrict__
 
 // ------------------------------------------------------------------------ backward: dQ (+ Dq)
 // dS^T = P^T o (dP^T - Dq), P^T = exp(S^T - lse), dP^T = V dO^T; dQ^T = K^T dS^T * scale.
-template <int QW, int NW>
-__global__ __launch_bounds__(64 * NW) void sra_dq_fast(const bf16* __restrict__ q, const bf16* __restrict__ k,
-                                                      const bf16* __restrict__ v, const bf16* __restrict__ o,
-                                                      const bf16* __restrict__ dout, const float* __restrict__ lse,
-                                                      float* __restrict__ Dws, bf16* __restrict__ dq, int N, int Nk,
+template <typename E, int QW, int NW>
+__global__ __launch_bounds__(64 * NW) void sra_dq_fast(const E* __restrict__ q, const E* __restrict__ k,
+                                                      const E* __restrict__ v, const E* __restrict__ o,
+                                                      const E* __restrict__ dout, const float* __restrict__ lse,
+                                                      float* __restrict__ Dws, E* __restrict__ dq, int N, int Nk,
                                                       int nkp, int heads, long qs, long kvs, long os, long dos,
                                                       long dqs, float sl2, float scale) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * NKP_MAX * ROWB];
@@ -220,30 +227,30 @@ __global__ __launch_bounds__(64 * NW) void sra_dq_fast(const bf16* __restrict__ 
   const int b = blockIdx.z, head = blockIdx.y;
 
   const int q0 = (blockIdx.x * NW + wave) * 32 * QW;
-  bf16x8 qf[QW][4], df[QW][4];
+  frag8<E> qf[QW][4], df[QW][4];
   float Dq[QW], lse2[QW];
 #pragma unroll
   for (int u = 0; u < QW; ++u) {
     const int qi = q0 + 32 * u + r;
     const bool live = qi < N;
-    const bf16* qrow = q + ((long)b * N + qi) * qs + head * HD;
-    const bf16* orow = o + ((long)b * N + qi) * os + head * HD;
-    const bf16* drow = dout + ((long)b * N + qi) * dos + head * HD;
+    const E* qrow = q + ((long)b * N + qi) * qs + head * HD;
+    const E* orow = o + ((long)b * N + qi) * os + head * HD;
+    const E* drow = dout + ((long)b * N + qi) * dos + head * HD;
     float dot = 0.f;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       if (live) {
         const uint4 qv = *reinterpret_cast<const uint4*>(qrow + 16 * s + 8 * h);
         const uint4 dv = *reinterpret_cast<const uint4*>(drow + 16 * s + 8 * h);
-        qf[u][s] = __builtin_bit_cast(bf16x8, qv);
-        df[u][s] = __builtin_bit_cast(bf16x8, dv);
+        qf[u][s] = frag_bits<E>(qv);
+        df[u][s] = frag_bits<E>(dv);
         float x[8], y[8];
-        load_vec<bf16>(drow + 16 * s + 8 * h, x);
-        load_vec<bf16>(orow + 16 * s + 8 * h, y);
+        load_vec<E>(drow + 16 * s + 8 * h, x);
+        load_vec<E>(orow + 16 * s + 8 * h, y);
 #pragma unroll
         for (int j = 0; j < 8; ++j) dot += x[j] * y[j];
       } else {
-        qf[u][s] = df[u][s] = zfrag<bf16>();
+        qf[u][s] = df[u][s] = zfrag<E>();
       }
     }
     dot += __shfl_xor(dot, 32, 64);
@@ -270,11 +277,11 @@ __global__ __launch_bounds__(64 * NW) void sra_dq_fast(const bf16* __restrict__ 
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int kb = t0 + 32 * ks;
-      bf16x8 kf[4], vf[4];
+      frag8<E> kf[4], vf[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        kf[s] = frag_k(Ki, kb, s, lane);
-        vf[s] = frag_k(Vi, kb, s, lane);
+        kf[s] = frag_k<E>(Ki, kb, s, lane);
+        vf[s] = frag_k<E>(Vi, kb, s, lane);
       }
       f32x16 ds[QW];
 #pragma unroll
@@ -282,8 +289,8 @@ __global__ __launch_bounds__(64 * NW) void sra_dq_fast(const bf16* __restrict__ 
         f32x16 sa = zero16(), dp = zero16();
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[s], qf[u][s], sa, 0, 0, 0);
-          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[s], df[u][s], dp, 0, 0, 0);
+          sa = MF<E>::mma(kf[s], qf[u][s], sa);
+          dp = MF<E>::mma(vf[s], df[u][s], dp);
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -294,13 +301,13 @@ __global__ __launch_bounds__(64 * NW) void sra_dq_fast(const bf16* __restrict__ 
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const bf16x8 k0 = frag_t(Ki, kb, 0, s, lane);
-        const bf16x8 k1 = frag_t(Ki, kb, 32, s, lane);
+        const frag8<E> k0 = frag_t<E>(Ki, kb, 0, s, lane);
+        const frag8<E> k1 = frag_t<E>(Ki, kb, 32, s, lane);
 #pragma unroll
         for (int u = 0; u < QW; ++u) {
-          const bf16x8 sf = MF<bf16>::from_acc(ds[u], s);
-          acc[u][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, sf, acc[u][0], 0, 0, 0);
-          acc[u][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, sf, acc[u][1], 0, 0, 0);
+          const frag8<E> sf = MF<E>::from_acc(ds[u], s);
+          acc[u][0] = MF<E>::mma(k0, sf, acc[u][0]);
+          acc[u][1] = MF<E>::mma(k1, sf, acc[u][1]);
         }
       }
     }
@@ -310,7 +317,7 @@ __global__ __launch_bounds__(64 * NW) void sra_dq_fast(const bf16* __restrict__ 
   for (int u = 0; u < QW; ++u) {
     const int qi = q0 + 32 * u + r;
     if (qi >= N) continue;
-    bf16* out = dq + ((long)b * N + qi) * dqs + head * HD;
+    E* out = dq + ((long)b * N + qi) * dqs + head * HD;
     store_rows(out, acc[u][0], 0, h, scale);
     store_rows(out, acc[u][1], 1, h, scale);
   }
@@ -333,10 +340,11 @@ __device__ __forceinline__ void dma4(const i32x4 rsrc, uint32_t lds, int voffset
 constexpr int QT = 64;                          // queries per tile
 constexpr int DKV_TILE_BYTES = 2 * QT * ROWB + 2 * QT * 4;   // Q, dO images + lse, Dq
 
+template <typename E>
 __global__ __launch_bounds__(64 * (NKP_MAX / 32)) void sra_dkv_fast(
-    const bf16* __restrict__ q, const bf16* __restrict__ k, const bf16* __restrict__ v, const bf16* __restrict__ dout,
+    const E* __restrict__ q, const E* __restrict__ k, const E* __restrict__ v, const E* __restrict__ dout,
     const float* __restrict__ lse, const float* __restrict__ Dws, float* __restrict__ ws_dk, float* __restrict__ ws_dv,
-    bf16* __restrict__ dk, bf16* __restrict__ dv, long dkvs,
+    E* __restrict__ dk, E* __restrict__ dv, long dkvs,
     int Bt, int N, int Nk, int heads, long qs, long kvs, long dos, int QC, int nchunk, float sl2, float scale) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * DKV_TILE_BYTES];
   const int nw = blockDim.x >> 6;
@@ -374,14 +382,14 @@ __global__ __launch_bounds__(64 * (NKP_MAX / 32)) void sra_dkv_fast(
 
   // this wave's 32 keys: K, V fragments as B operands (k = d), lane = key
   const int key = kc0 + 32 * wave + r;
-  bf16x8 kf[4], vf[4];
+  frag8<E> kf[4], vf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     if (key < Nk) {
-      kf[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(k + ((long)b * Nk + key) * kvs + head * HD + 16 * s + 8 * h));
-      vf[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(v + ((long)b * Nk + key) * kvs + head * HD + 16 * s + 8 * h));
+      kf[s] = frag_bits<E>(*reinterpret_cast<const uint4*>(k + ((long)b * Nk + key) * kvs + head * HD + 16 * s + 8 * h));
+      vf[s] = frag_bits<E>(*reinterpret_cast<const uint4*>(v + ((long)b * Nk + key) * kvs + head * HD + 16 * s + 8 * h));
     } else {
-      kf[s] = vf[s] = zfrag<bf16>();
+      kf[s] = vf[s] = zfrag<E>();
     }
   }
   f32x16 ak[2], av[2];
@@ -402,9 +410,9 @@ __global__ __launch_bounds__(64 * (NKP_MAX / 32)) void sra_dkv_fast(
       const int qb = 32 * qt;
       f32x16 sa = zero16(), dp = zero16();
 #pragma unroll
-      for (int s = 0; s < 4; ++s) sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_k(Qi, qb, s, lane), kf[s], sa, 0, 0, 0);
+      for (int s = 0; s < 4; ++s) sa = MF<E>::mma(frag_k<E>(Qi, qb, s, lane), kf[s], sa);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_k(Di, qb, s, lane), vf[s], dp, 0, 0, 0);
+      for (int s = 0; s < 4; ++s) dp = MF<E>::mma(frag_k<E>(Di, qb, s, lane), vf[s], dp);
       const bool tail = q0 + qb + 32 > qend;
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
@@ -422,12 +430,12 @@ __global__ __launch_bounds__(64 * (NKP_MAX / 32)) void sra_dkv_fast(
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const bf16x8 pf = MF<bf16>::from_acc(sa, s);
-        const bf16x8 sf = MF<bf16>::from_acc(dp, s);
+        const frag8<E> pf = MF<E>::from_acc(sa, s);
+        const frag8<E> sf = MF<E>::from_acc(dp, s);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          av[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_t(Di, qb, 32 * t, s, lane), pf, av[t], 0, 0, 0);
-          ak[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_t(Qi, qb, 32 * t, s, lane), sf, ak[t], 0, 0, 0);
+          av[t] = MF<E>::mma(frag_t<E>(Di, qb, 32 * t, s, lane), pf, av[t]);
+          ak[t] = MF<E>::mma(frag_t<E>(Qi, qb, 32 * t, s, lane), sf, ak[t]);
         }
       }
     }
@@ -437,17 +445,17 @@ __global__ __launch_bounds__(64 * (NKP_MAX / 32)) void sra_dkv_fast(
   }
   if (key >= Nk) return;
   if (nchunk == 1) {            // one query chunk: this workgroup's sums are the gradients
-    bf16* ok = dk + ((long)b * Nk + key) * dkvs + head * HD;
-    bf16* ov = dv + ((long)b * Nk + key) * dkvs + head * HD;
+    E* ok = dk + ((long)b * Nk + key) * dkvs + head * HD;
+    E* ov = dv + ((long)b * Nk + key) * dkvs + head * HD;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const int d = 32 * t + 8 * g4 + 4 * h;
-        *reinterpret_cast<uint2*>(ok + d) = make_uint2(pack2_bf16(ak[t][4 * g4] * scale, ak[t][4 * g4 + 1] * scale),
-                                                       pack2_bf16(ak[t][4 * g4 + 2] * scale, ak[t][4 * g4 + 3] * scale));
-        *reinterpret_cast<uint2*>(ov + d) = make_uint2(pack2_bf16(av[t][4 * g4], av[t][4 * g4 + 1]),
-                                                       pack2_bf16(av[t][4 * g4 + 2], av[t][4 * g4 + 3]));
+        *reinterpret_cast<uint2*>(ok + d) = make_uint2(pack2<E>(ak[t][4 * g4] * scale, ak[t][4 * g4 + 1] * scale),
+                                                       pack2<E>(ak[t][4 * g4 + 2] * scale, ak[t][4 * g4 + 3] * scale));
+        *reinterpret_cast<uint2*>(ov + d) = make_uint2(pack2<E>(av[t][4 * g4], av[t][4 * g4 + 1]),
+                                                       pack2<E>(av[t][4 * g4 + 2], av[t][4 * g4 + 3]));
       }
     return;
   }
@@ -482,9 +490,9 @@ int pick_nw(int N, int heads, int Bt, int qw) {
 
 }  // namespace
 
-// the forward streams keys through LDS in NKP_MAX-key chunks: any Nk (bf16, D = 64, 16-B rows)
+// the forward streams keys through LDS in NKP_MAX-key chunks: any Nk (bf16 / fp16, D = 64, 16-B rows)
 bool sra_fast_fwd_ok(int D, int Nk, int dtype, const void* const* ptrs, int nptr, const long* strides, int nstr) {
-  if (dtype != 1 || D != HD || Nk <= 0) return false;
+  if ((dtype != 1 && dtype != 2) || D != HD || Nk <= 0) return false;
   for (int i = 0; i < nptr; ++i)
     if (ptrs[i] && ((uintptr_t)ptrs[i] & 15)) return false;
   for (int i = 0; i < nstr; ++i)
@@ -492,9 +500,9 @@ bool sra_fast_fwd_ok(int D, int Nk, int dtype, const void* const* ptrs, int nptr
   return true;
 }
 
-// bf16, D = 64, Nk <= 320, 16-B aligned rows: the LDS-resident path (sra_attention.hip calls these)
+// bf16 / fp16, D = 64, Nk <= 320, 16-B aligned rows: the LDS-resident path (sra_attention.hip calls these)
 bool sra_fast_ok(int D, int Nk, int dtype, const void* const* ptrs, int nptr, const long* strides, int nstr) {
-  if (dtype != 1 || D != HD || Nk > NKP_MAX || Nk <= 0) return false;
+  if ((dtype != 1 && dtype != 2) || D != HD || Nk > NKP_MAX || Nk <= 0) return false;
   for (int i = 0; i < nptr; ++i)
     if (ptrs[i] && ((uintptr_t)ptrs[i] & 15)) return false;
   for (int i = 0; i < nstr; ++i)
@@ -502,15 +510,16 @@ bool sra_fast_ok(int D, int Nk, int dtype, const void* const* ptrs, int nptr, co
   return true;
 }
 
-void sra_fwd_fast_launch(const void* q, const void* k, const void* v, void* o, float* lse, int Bt, int N, int Nk,
-                         int heads, long qs, long kvs, long os, float sl2, hipStream_t s) {
+template <typename E>
+void sra_fwd_fast_launch_t(const void* q, const void* k, const void* v, void* o, float* lse, int Bt, int N, int Nk,
+                           int heads, long qs, long kvs, long os, float sl2, hipStream_t s) {
   const int nkp = (Nk + KTILE - 1) / KTILE * KTILE;
   const int qw = pick_qw(N, heads, Bt);
   const int nw = pick_nw(N, heads, Bt, qw);
   const dim3 grid(cdiv(N, 32 * nw * qw), heads, Bt);
 #define CMX_SRA_FWD(QW_, NW_)                                                                                       \
-  hipLaunchKernelGGL((sra_fwd_fast<QW_, NW_>), grid, dim3(64 * NW_), 0, s, (const bf16*)q, (const bf16*)k,         \
-                     (const bf16*)v, (bf16*)o, lse, N, Nk, nkp, heads, qs, kvs, os, sl2)
+  hipLaunchKernelGGL((sra_fwd_fast<E, QW_, NW_>), grid, dim3(64 * NW_), 0, s, (const E*)q, (const E*)k,         \
+                     (const E*)v, (E*)o, lse, N, Nk, nkp, heads, qs, kvs, os, sl2)
   if (qw == 2) CMX_SRA_FWD(2, 8);
   else if (nw == 8) CMX_SRA_FWD(1, 8);
   else if (nw == 4) CMX_SRA_FWD(1, 4);
@@ -519,16 +528,17 @@ void sra_fwd_fast_launch(const void* q, const void* k, const void* v, void* o, f
 #undef CMX_SRA_FWD
 }
 
-void sra_dq_fast_launch(const void* q, const void* k, const void* v, const void* o, const void* dout,
-                        const float* lse, float* Dws, void* dq, int Bt, int N, int Nk, int heads, long qs, long kvs,
-                        long os, long dos, long dqs, float sl2, float scale, hipStream_t s) {
+template <typename E>
+void sra_dq_fast_launch_t(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                          const float* lse, float* Dws, void* dq, int Bt, int N, int Nk, int heads, long qs, long kvs,
+                          long os, long dos, long dqs, float sl2, float scale, hipStream_t s) {
   const int nkp = (Nk + KTILE - 1) / KTILE * KTILE;
   const int qw = pick_qw(N, heads, Bt);
   const int nw = pick_nw(N, heads, Bt, qw);
   const dim3 grid(cdiv(N, 32 * nw * qw), heads, Bt);
 #define CMX_SRA_DQ(QW_, NW_)                                                                                        \
-  hipLaunchKernelGGL((sra_dq_fast<QW_, NW_>), grid, dim3(64 * NW_), 0, s, (const bf16*)q, (const bf16*)k,          \
-                     (const bf16*)v, (const bf16*)o, (const bf16*)dout, lse, Dws, (bf16*)dq, N, Nk, nkp, heads, qs,  \
+  hipLaunchKernelGGL((sra_dq_fast<E, QW_, NW_>), grid, dim3(64 * NW_), 0, s, (const E*)q, (const E*)k,          \
+                     (const E*)v, (const E*)o, (const E*)dout, lse, Dws, (E*)dq, N, Nk, nkp, heads, qs,  \
                      kvs, os, dos, dqs, sl2, scale)
   if (qw == 2) CMX_SRA_DQ(2, 8);
   else if (nw == 8) CMX_SRA_DQ(1, 8);
@@ -555,15 +565,44 @@ int sra_dkv_fast_chunks(int Bt, int N, int Nk, int heads) {
   return (int)(nc < 1 ? 1 : nc);
 }
 
-void sra_dkv_fast_launch(const void* q, const void* k, const void* v, const void* dout, const float* lse,
-                         const float* Dws, float* ws_dk, float* ws_dv, void* dk, void* dv, long dkvs, int Bt, int N,
-                         int Nk, int heads, long qs, long kvs, long dos, int nchunk, float sl2, float scale,
-                         hipStream_t s) {
+template <typename E>
+void sra_dkv_fast_launch_t(const void* q, const void* k, const void* v, const void* dout, const float* lse,
+                           const float* Dws, float* ws_dk, float* ws_dv, void* dk, void* dv, long dkvs, int Bt, int N,
+                           int Nk, int heads, long qs, long kvs, long dos, int nchunk, float sl2, float scale,
+                           hipStream_t s) {
   const int nkw = ((Nk < NKP_MAX ? Nk : NKP_MAX) + 31) / 32 * 32;   // one 32-key sub-tile per wave
   const int nkc = (Nk + NKP_MAX - 1) / NKP_MAX;                       // key chunks (Nk > NKP_MAX)
   int qc = (N + nchunk - 1) / nchunk;
   qc = (qc + QT - 1) / QT * QT;
-  hipLaunchKernelGGL(sra_dkv_fast, dim3(nchunk * nkc, heads, Bt), dim3(2 * nkw), 0, s, (const bf16*)q, (const bf16*)k,
-                     (const bf16*)v, (const bf16*)dout, lse, Dws, ws_dk, ws_dv, (bf16*)dk, (bf16*)dv, dkvs, Bt, N,
+  hipLaunchKernelGGL(sra_dkv_fast<E>, dim3(nchunk * nkc, heads, Bt), dim3(2 * nkw), 0, s, (const E*)q, (const E*)k,
+                     (const E*)v, (const E*)dout, lse, Dws, ws_dk, ws_dv, (E*)dk, (E*)dv, dkvs, Bt, N,
                      Nk, heads, qs, kvs, dos, qc, nchunk, sl2, scale);
+}
+
+// dtype 1 = bf16, 2 = fp16 (the callers checked sra_fast_fwd_ok)
+void sra_fwd_fast_launch(const void* q, const void* k, const void* v, void* o, float* lse, int Bt, int N, int Nk,
+                         int heads, long qs, long kvs, long os, float sl2, int dtype, hipStream_t s) {
+  if (dtype == 2) sra_fwd_fast_launch_t<f16>(q, k, v, o, lse, Bt, N, Nk, heads, qs, kvs, os, sl2, s);
+  else sra_fwd_fast_launch_t<bf16>(q, k, v, o, lse, Bt, N, Nk, heads, qs, kvs, os, sl2, s);
+}
+
+void sra_dq_fast_launch(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                        const float* lse, float* Dws, void* dq, int Bt, int N, int Nk, int heads, long qs, long kvs,
+                        long os, long dos, long dqs, float sl2, float scale, int dtype, hipStream_t s) {
+  if (dtype == 2)
+    sra_dq_fast_launch_t<f16>(q, k, v, o, dout, lse, Dws, dq, Bt, N, Nk, heads, qs, kvs, os, dos, dqs, sl2, scale, s);
+  else
+    sra_dq_fast_launch_t<bf16>(q, k, v, o, dout, lse, Dws, dq, Bt, N, Nk, heads, qs, kvs, os, dos, dqs, sl2, scale, s);
+}
+
+void sra_dkv_fast_launch(const void* q, const void* k, const void* v, const void* dout, const float* lse,
+                         const float* Dws, float* ws_dk, float* ws_dv, void* dk, void* dv, long dkvs, int Bt, int N,
+                         int Nk, int heads, long qs, long kvs, long dos, int nchunk, float sl2, float scale,
+                         int dtype, hipStream_t s) {
+  if (dtype == 2)
+    sra_dkv_fast_launch_t<f16>(q, k, v, dout, lse, Dws, ws_dk, ws_dv, dk, dv, dkvs, Bt, N, Nk, heads, qs, kvs, dos,
+                               nchunk, sl2, scale, s);
+  else
+    sra_dkv_fast_launch_t<bf16>(q, k, v, dout, lse, Dws, ws_dk, ws_dv, dk, dv, dkvs, Bt, N, Nk, heads, qs, kvs, dos,
+                                nchunk, sl2, scale, s);
 }

@@ -49,6 +49,7 @@ class _Queue:
         self.reds = []         # argument tuples of cmx_reduce_pack (minus rec / blk0)
         self.keep = []         # tensors the queued work reads or writes
         self.streams = {}      # streams the queued operands were produced on (FFM's side stream)
+        self.dtype = 0         # operand dtype code of the queued GEMMs (1 bf16, 2 fp16; 0 = none yet)
         self.armed = False
 
 
@@ -77,6 +78,18 @@ def arm() -> None:
         torch.autograd.Variable._execution_engine.queue_callback(flush)
 
 
+_H16 = {torch.bfloat16: 1, torch.float16: 2}
+
+
+def _h16_code(*ts) -> int:
+    """1 (bf16) / 2 (fp16) when every operand has that 16-bit dtype and matches the queue's
+    GEMMs, else 0 (not eligible: the caller runs the problem now)."""
+    code = _H16.get(ts[0].dtype, 0)
+    if code == 0 or any(t.dtype != ts[0].dtype for t in ts) or (_q.dtype and _q.dtype != code):
+        return 0
+    return code
+
+
 def _operand(t: torch.Tensor):
     if t.stride(2) == 1:
         return 0, t.stride(1), t.stride(0)
@@ -87,9 +100,12 @@ def _operand(t: torch.Tensor):
 
 def wgrad(dz: torch.Tensor, x: torch.Tensor, Wg: torch.Tensor, bg: torch.Tensor | None = None) -> bool:
     """Queue Wg (fp32 (G, N, k) view) = dz^T x and bg (G, N) = column sums of dz, with
-    dz (G, M, N), x (G, M, k) bf16.  Returns False (nothing queued) when the problem is not
-    eligible for the grouped bf16 path; the caller then runs it immediately."""
-    if not ENABLED or dz.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or not dz.is_cuda:
+    dz (G, M, N), x (G, M, k) bf16 / fp16.  Returns False (nothing queued) when the problem is
+    not eligible for the grouped 16-bit path; the caller then runs it immediately."""
+    if not ENABLED or not dz.is_cuda:
+        return False
+    code = _h16_code(dz, x)
+    if not code:
         return False
     if not _free:
         reserve()
@@ -114,6 +130,7 @@ def wgrad(dz: torch.Tensor, x: torch.Tensor, Wg: torch.Tensor, bg: torch.Tensor 
     if st <= 0:
         return False
     _q.gemms.append(args)
+    _q.dtype = code
     _q.keep.extend((dz, x))
     _note_stream()
     arm()
@@ -123,10 +140,13 @@ def wgrad(dz: torch.Tensor, x: torch.Tensor, Wg: torch.Tensor, bg: torch.Tensor 
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, Wg: torch.Tensor, bg, geom) -> bool:
     """Queue the weight gradient of an NHWC convolution without im2col: one grouped-GEMM
     record per tap, its B operand gathered from x at that tap (cmx_gemm_group_pack_conv_wgrad).
-    dy (G, NIg*Ho*Wo, N) bf16, x (G*NIg, H, W, C) bf16, Wg fp32 (G, N, KH*KW*C), bg (G, N) or None;
+    dy (G, NIg*Ho*Wo, N), x (G*NIg, H, W, C) bf16 / fp16, Wg fp32 (G, N, KH*KW*C), bg (G, N) or None;
     geom = (G, NIg, H, W, C, KH, KW, stride, pad, Ho, Wo).  False: not eligible, run the
     im2col path instead."""
-    if not ENABLED or dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16:
+    if not ENABLED:
+        return False
+    code = _h16_code(dy, x)
+    if not code:
         return False
     G, NIg, H, W, C, KH, KW, st, pad, Ho, Wo = geom
     N = dy.shape[-1]
@@ -141,6 +161,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, Wg: torch.Tensor, bg, geom) ->
     for tap in range(KH * KW):
         b = bg if tap == 0 else None
         _q.convs.append((dy, x, Wg, b, G, NIg, H, W, C, KH, KW, st, pad, Ho, Wo, N, tap, sdy, sx, Wg.stride(0), sdb))
+    _q.dtype = code
     _q.keep.extend((dy, x))
     _note_stream()
     arm()
@@ -217,9 +238,9 @@ def flush() -> None:
     q.armed = False
     if not (q.gemms or q.convs or q.reds):
         return
-    gemms, convs, reds, keep = q.gemms, q.convs, list(q.reds), q.keep
+    gemms, convs, reds, keep, dcode = q.gemms, q.convs, list(q.reds), q.keep, q.dtype
     producers = q.streams
-    q.gemms, q.convs, q.reds, q.keep, q.streams = [], [], [], [], {}
+    q.gemms, q.convs, q.reds, q.keep, q.streams, q.dtype = [], [], [], [], {}, 0
     device = keep[0].device
     cur = torch.cuda.current_stream()
     for sid, st in producers.items():      # operands made on another stream: order after them
@@ -267,12 +288,12 @@ def flush() -> None:
                     reds.append((ws + 4 * G * s * M * Nr, bg.data_ptr(), 0, G, s, s * M, M, 1, M, M, sdb, M, 0, 0, 0))
                 off += (sz + 255) // 256 * 256
         dev = _upload(table, nrec * _GREC, device)
-        call("cmx_gemm_grouped", dev.data_ptr(), nrec, blk, stream())
+        call("cmx_gemm_grouped", dev.data_ptr(), nrec, blk, dcode, stream())
         keep.append(arena)
         if observer is not None:
             # algorithmic work per problem: (G, M, real N, K) and operand / result bytes
             work = [(G, M, N - (1 if hb else 0), K) for (G, M, N, K, hb) in dims]
-            observer(dev, nrec, blk, work, keep)
+            observer(dev, nrec, blk, work, keep, dcode)
     if reds:
         table = _table(len(reds) * _RREC)
         base = table.data_ptr()

@@ -48,8 +48,8 @@ class BucketedGradSync:
         # CMX_DP_OVERLAP=0: one blocking all-reduce per segment at optimizer time (no overlap)
         self.overlap = (os.environ.get("CMX_DP_OVERLAP", "1") == "1") if overlap is None else overlap
         # gradient payload on the wire: "fp32" (SUM all-reduce of the fp32 gradients, DDP's
-        # semantics) or "bf16" (all-to-all of bf16 shards, fp32 accumulation, all-gather of the
-        # bf16 sums: half the bytes over xGMI; the summed gradient is rounded to bf16 once)
+        # semantics) or "bf16" (reduce-scatter + all-gather of bf16 gradients: half the bytes
+        # over xGMI; the sum is rounded to bf16 along the ring)
         self.payload = (payload or os.environ.get("CMX_DP_PAYLOAD", "fp32")).lower()
         if self.payload not in ("fp32", "bf16"):
             raise ValueError(f"gradient payload {self.payload!r}: fp32 or bf16")
@@ -101,37 +101,32 @@ class BucketedGradSync:
                 self._reduce_bf16(part)
 
     def _reduce_bf16(self, t: torch.Tensor) -> None:
-        """SUM over ranks of fp32 ``t`` in place with a bf16 payload and fp32 accumulation:
-        all-to-all of bf16 shards, each rank sums its P received chunks in fp32, all-gather of
-        the bf16 shard sums (2 + 2 bytes per element on the wire vs 8 for a ring fp32
-        all-reduce).  On the GPU the casts and the shard sum are HIP kernels
-        (cmx_cast_f32_bf16 / cmx_shard_sum_bf16 / cmx_cast_bf16_f32); the CPU branch is the
+        """SUM over ranks of fp32 ``t`` in place with a bf16 payload: a reduce-scatter of the
+        bf16 gradients (each rank ends with the sum of its shard) and an all-gather of the summed
+        shards (2 + 2 bytes per element on the wire vs 4 + 4 for an fp32 ring all-reduce).  The
+        sum is formed by the collective's bf16 reduction (RCCL: P - 1 roundings to bf16 along the
+        ring).  Both collectives are safe inside a HIP-graph capture; an all-to-all + local fp32
+        sum was not (RCCL all_to_all_single inside a capture crashed at capture end or hung at
+        exit even at world size 1: scripts/rccl_capture_probe.py, gpurun_out r03_b).  On the GPU
+        the casts are HIP kernels (cmx_cast_f32_bf16 / cmx_cast_bf16_f32); the CPU branch is the
         gloo rehearsal of the same protocol."""
         P = self.world
         n = t.numel()
         shard = -(-n // (8 * P)) * 8                 # per-rank shard, a multiple of 8 elements
         send = torch.zeros(P * shard, dtype=torch.bfloat16, device=t.device)
-        recv = torch.empty_like(send)
         mine = torch.empty(shard, dtype=torch.bfloat16, device=t.device)
         out = torch.empty_like(send)
-        if t.is_cuda:
+        aligned = t.is_cuda and n % 8 == 0
+        if aligned:
             from . import _lib
-            if n % 8 == 0:
-                _lib.call("cmx_cast_f32_bf16", _lib.ptr(t), _lib.ptr(send), n, _lib.stream())
-            else:
-                send[:n].copy_(t)
-            dist.all_to_all_single(recv, send, group=self.group)
-            _lib.call("cmx_shard_sum_bf16", _lib.ptr(recv), _lib.ptr(mine), P, shard, _lib.stream())
-            dist.all_gather_into_tensor(out, mine, group=self.group)
-            if n % 8 == 0:
-                _lib.call("cmx_cast_bf16_f32", _lib.ptr(out), _lib.ptr(t), n, _lib.stream())
-            else:
-                t.copy_(out[:n])
+            _lib.call("cmx_cast_f32_bf16", _lib.ptr(t), _lib.ptr(send), n, _lib.stream())
         else:
             send[:n].copy_(t)
-            dist.all_to_all_single(recv, send, group=self.group)
-            mine.copy_(recv.view(P, shard).float().sum(0))
-            dist.all_gather_into_tensor(out, mine, group=self.group)
+        dist.reduce_scatter_tensor(mine, send, op=dist.ReduceOp.SUM, group=self.group)
+        dist.all_gather_into_tensor(out, mine, group=self.group)
+        if aligned:
+            _lib.call("cmx_cast_bf16_f32", _lib.ptr(out), _lib.ptr(t), n, _lib.stream())
+        else:
             t.copy_(out[:n])
 
     def _finish_backward(self):

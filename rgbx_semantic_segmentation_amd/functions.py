@@ -467,7 +467,7 @@ class DWConvF(Function):
         C = h.shape[-1]
         out = torch.empty_like(h)
         # LDS-tiled channel counts: also save act'(z) so the backward skips the 3x3 recompute
-        tiled = C % (64 if h.dtype == torch.bfloat16 else 32) == 0
+        tiled = C % (64 if h.dtype in (torch.bfloat16, torch.float16) else 32) == 0
         gprime = torch.empty_like(h) if tiled else None
         K.call("cmx_dwconv3x3_fwd_save", K.ptr(h), K.ptr(w), K.ptr(b), K.ptr(out), K.ptr(gprime), NI, ipg, H, W, C,
                K.ACT[act], K.dtype_code(h), K.stream())
@@ -530,7 +530,8 @@ class ConvF(Function):
         # geom: (G, NI, H, Wd, C, KH, KW, stride, pad, Ho, Wo, nchw)
         G, NI, H, Wd, C, KH, KW, st, pad, Ho, Wo, nchw = geom
         Kp = W.shape[-1]
-        if IMPLICIT_CONV and not nchw and x.dtype == torch.bfloat16 and C % 64 == 0 and x.is_contiguous():
+        if IMPLICIT_CONV and not nchw and x.dtype in (torch.bfloat16, torch.float16) and C % 64 == 0 \
+                and x.is_contiguous():
             # im2col-free: the GEMM's A operand is DMA'd tap by tap straight from x
             N = W.shape[1]
             NIg = NI // G

@@ -77,6 +77,12 @@ def act_bwd(dy, z, act: str, out=None):
 def cast_f32_bf16(src: torch.Tensor, dst: torch.Tensor):
     assert src.dtype == torch.float32 and dst.dtype == torch.bfloat16 and src.numel() == dst.numel()
     call("cmx_cast_f32_bf16", ptr(src), ptr(dst), src.numel(), stream())
+
+
+def cast_f32_h16(src: torch.Tensor, dst: torch.Tensor):
+    """fp32 -> bf16 / fp16 (round to nearest even) into ``dst``'s dtype."""
+    assert src.dtype == torch.float32 and dst.dtype in (torch.bfloat16, torch.float16) and src.numel() == dst.numel()
+    call("cmx_cast_f32_h16", ptr(src), ptr(dst), src.numel(), dtype_code(dst), stream())
     return dst
 
 

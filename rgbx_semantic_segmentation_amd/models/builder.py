@@ -10,15 +10,16 @@ API kept from the reference:
 
 Differences by design:
   * ``model.cuda()`` / ``model.to(device)`` flattens the parameters into a ParamStore
-    (one fp32 buffer + gradient buffer + bf16 shadow); parameters remain ``nn.Parameter``
+    (one fp32 buffer + gradient buffer + bf16 / fp16 shadow); parameters remain ``nn.Parameter``
     views with reference shapes.  There is no CPU execution path: forward on a model that
     was not moved to a GPU raises.
   * Decoder input channels come from the encoder's ``embed_dims`` (the reference's
     hard-coded [96,192,384,768] for mit_b4/b5, builder.py:66-75, cannot run; its mit_b1
     entry builds mit_b0, :84-87).
-  * compute dtype: ``cfg.compute_dtype`` ("float32" | "bfloat16"); defaults to bfloat16 when
-    ``cfg.use_mixed_precision`` (the reference's fp16 autocast switch, config.py:61),
-    else float32.
+  * compute dtype: ``cfg.compute_dtype`` ("float32" | "bfloat16" | "float16"); defaults to
+    float16 when ``cfg.use_mixed_precision`` (the reference's fp16 autocast switch,
+    config.py:61, train.py:185-198: fp16 storage, fp32 accumulation, with dynamic loss scaling
+    by optim.GradScaler), else float32.
   * ``backward`` writes parameter gradients straight into the flat gradient buffer
     (overwrite, not accumulate); use the package's ``FusedAdamW``.
 """
@@ -99,9 +100,9 @@ class EncoderDecoder(nn.Module):
         self.bn_momentum = float(_get(cfg, "bn_momentum", 0.1))
         dt = _get(cfg, "compute_dtype", None)
         if dt is None:
-            dt = "bfloat16" if _get(cfg, "use_mixed_precision", False) else "float32"
+            dt = "float16" if _get(cfg, "use_mixed_precision", False) else "float32"
         self.compute_dtype = {"float32": torch.float32, "fp32": torch.float32, "bfloat16": torch.bfloat16,
-                              "bf16": torch.bfloat16}[str(dt)]
+                              "bf16": torch.bfloat16, "float16": torch.float16, "fp16": torch.float16}[str(dt)]
         self.sync_bn = norm_layer is nn.SyncBatchNorm
         self.process_group = None
         self.store: Optional[ParamStore] = None

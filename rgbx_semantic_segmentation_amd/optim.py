@@ -85,12 +85,12 @@ class FusedAdamW:
             # GradScaler.unscale_ only checks the optimizer's parameters
             call("cmx_grad_nonfinite", ptr(s.grad), s.numel, ptr(s.decay64), ptr(scaler.found_inf), stream())
             call("cmx_adamw_step_scaled", ptr(s.flat), ptr(s.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq),
-                 ptr(s.shadow), ptr(s.decay64), s.numel, ptr(self.lr_t), ptr(self.step_t), self.betas[0],
+                 ptr(s.shadow), s.shadow_code, ptr(s.decay64), s.numel, ptr(self.lr_t), ptr(self.step_t), self.betas[0],
                  self.betas[1], self.eps, self.weight_decay, gscale, ptr(scaler.scale_t), ptr(scaler.found_inf),
                  stream())
             return None
         call("cmx_adamw_step", ptr(s.flat), ptr(s.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq), ptr(s.shadow),
-             ptr(s.decay64), s.numel, ptr(self.lr_t), ptr(self.step_t), self.betas[0], self.betas[1], self.eps,
+             s.shadow_code, ptr(s.decay64), s.numel, ptr(self.lr_t), ptr(self.step_t), self.betas[0], self.betas[1], self.eps,
              self.weight_decay, gscale, stream())
         return None
 

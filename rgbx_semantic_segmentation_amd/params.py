@@ -1,4 +1,4 @@
-"""Flat parameter store: one fp32 master buffer, one fp32 gradient buffer, one bf16 shadow.
+"""Flat parameter store: one fp32 master buffer, one fp32 gradient buffer, one bf16 / fp16 shadow.
 
 MI355X-first layout decisions (the reference keeps 66.6 M parameters as ~600 separate
 tensors, ``train.py:104-149``):
@@ -121,8 +121,11 @@ class ParamStore:
         self.segments = [(sid, b[0], b[1]) for sid, b in sorted(seg_bounds.items())]
         self.flat = torch.zeros(off, dtype=torch.float32, device=self.device)
         self.grad = torch.zeros(off, dtype=torch.float32, device=self.device)
-        self.shadow = (torch.zeros(off, dtype=torch.bfloat16, device=self.device)
-                       if compute_dtype == torch.bfloat16 else None)
+        # the GEMM-operand copy of the weights in a 16-bit compute dtype (bf16, or fp16 for the
+        # reference's AMP configuration), refreshed by every optimizer step
+        self.shadow = (torch.zeros(off, dtype=compute_dtype, device=self.device)
+                       if compute_dtype in (torch.bfloat16, torch.float16) else None)
+        self.shadow_code = {torch.bfloat16: 1, torch.float16: 2}.get(compute_dtype, 0)
         self.decay64 = torch.zeros(off // ALIGN, dtype=torch.uint8)
         # copy values, rebind parameters as views
         self.params: Dict[str, nn.Parameter] = {}
@@ -204,4 +207,4 @@ class ParamStore:
     def refresh_shadow(self):
         if self.shadow is not None:
             from . import kernels as K
-            K.cast_f32_bf16(self.flat, self.shadow)
+            K.cast_f32_h16(self.flat, self.shadow)

@@ -57,8 +57,8 @@ def measure_dominant(model, batch, workload: str, iters: int = 20):
     rgb, x, lab = batch
     seen = []
 
-    def obs(dev, nrec, blk, work, keep):
-        seen.append((dev, nrec, blk, list(work), list(keep)))
+    def obs(dev, nrec, blk, work, keep, dcode=1):
+        seen.append((dev, nrec, blk, list(work), list(keep), dcode))
 
     deferred.observer = obs
     try:
@@ -73,11 +73,11 @@ def measure_dominant(model, batch, workload: str, iters: int = 20):
     # each re-timed standalone; the family's algorithmic work over its total time
     flops = nbytes = t = 0.0
     blk = nrec = 0
-    for dev, nr, bl, work, keep in seen:
+    for dev, nr, bl, work, keep, dcode in seen:
         for (G, M, Nr, K) in work:
             flops += 2.0 * G * M * Nr * K
             nbytes += 2.0 * G * (M + Nr) * K + 4.0 * G * M * Nr
-        launch = lambda: _lib.call("cmx_gemm_grouped", dev.data_ptr(), nr, bl, _lib.stream())
+        launch = lambda: _lib.call("cmx_gemm_grouped", dev.data_ptr(), nr, bl, dcode, _lib.stream())
         for _ in range(3):
             launch()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

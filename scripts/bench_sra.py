@@ -33,7 +33,10 @@ def t(fn, iters=20):
 def main():
     Bt, D, Nk = 4, 64, 300
     tot_f = tot_b = 0.0
-    for N, heads, depth in ((19200, 1, 3), (4800, 2, 4), (1200, 5, 6), (300, 8, 3)):
+    stages = ((19200, 1, 3), (4800, 2, 4), (1200, 5, 6), (300, 8, 3))
+    if len(sys.argv) > 2 and sys.argv[1] == "stage":          # one stage (for a rocprofv3 per-kernel split)
+        stages = (stages[int(sys.argv[2]) - 1],)
+    for N, heads, depth in stages:
         C = heads * D
         q = torch.randn(Bt, N, C, device="cuda").bfloat16()
         kv = torch.randn(Bt, Nk, 2 * C, device="cuda").bfloat16()
@@ -66,5 +69,5 @@ def sweep():
 
 if len(sys.argv) > 1 and sys.argv[1] == "sweep":
     sweep()
-elif __name__ == "__main__":
+elif __name__ == "__main__":     # all stages, or `stage S`
     main()

@@ -1,0 +1,51 @@
+"""Which RCCL collectives survive HIP-graph capture at world size 1 (one case per process:
+a crash ends only that case).  Usage: python scripts/rccl_capture_probe.py CASE
+CASE in {a2a_eager, ag_eager, rs_eager, ag_graph, rs_graph, a2a_graph}."""
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+
+def main(case):
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(29400 + os.getpid() % 500))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    n = 1 << 16
+    src = torch.randn(n, device=dev).to(torch.bfloat16)
+    out = torch.empty_like(src)
+
+    def op():
+        if case.startswith("a2a"):
+            dist.all_to_all_single(out, src)
+        elif case.startswith("ag"):
+            dist.all_gather_into_tensor(out, src)
+        else:
+            dist.reduce_scatter_tensor(out, src)
+
+    op()
+    torch.cuda.synchronize()
+    if case.endswith("graph"):
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            op()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        out.zero_()
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            op()
+        g.replay()
+        torch.cuda.synchronize()
+    ok = torch.equal(out, src)
+    print(f"{case}: {'ok' if ok else 'WRONG'}", flush=True)
+    dist.destroy_process_group()
+    sys.exit(0 if ok else 1)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

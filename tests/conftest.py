@@ -19,3 +19,12 @@ def dev():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda", 0)
+
+
+def pytest_make_parametrize_id(config, val, argname):
+    """Readable ids for torch dtypes (``float16`` instead of ``dtype2``), so ``-k float16``
+    selects the fp16 cases."""
+    import torch
+    if isinstance(val, torch.dtype):
+        return str(val).replace("torch.", "")
+    return None

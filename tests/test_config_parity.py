@@ -28,7 +28,7 @@ import pytest
 import torch
 
 from oracle.cmx_ref import EncoderDecoder as RefModel, CMXConfig, DropPath
-from oracle.bf16_emul import emulate_bf16
+from oracle.bf16_emul import emulate_storage
 
 pytestmark = pytest.mark.gpu
 
@@ -36,13 +36,18 @@ RATIO = 4.0
 OUTLIER_RATIO = 12.0
 
 CONFIGS = {
-    # name: (backbone, H, W, batch, classes)      BASELINE.json configs[0..4] (configs[2] is
+    # name: (backbone, H, W, batch, classes, dtype)   BASELINE.json configs[0..4] (configs[2] is
     # configs[1] per GPU: its multi-rank path is test_gpu_dist.py / test_dist_gloo.py)
-    "config1_b0_240x320_bs1": ("mit_b0", 240, 320, 1, 9),
-    "config2_b2_480x640_bs2": ("mit_b2", 480, 640, 2, 40),
-    "config4_b4_480x640_bs4": ("mit_b4", 480, 640, 4, 9),
-    "config5_b5_1024x1024_bs1": ("mit_b5", 1024, 1024, 1, 19),
+    "config1_b0_240x320_bs1": ("mit_b0", 240, 320, 1, 9, "bfloat16"),
+    "config2_b2_480x640_bs2": ("mit_b2", 480, 640, 2, 40, "bfloat16"),
+    "config4_b4_480x640_bs4": ("mit_b4", 480, 640, 4, 9, "bfloat16"),
+    "config5_b5_1024x1024_bs1": ("mit_b5", 1024, 1024, 1, 19, "bfloat16"),
+    # config 5 as BASELINE states it: fp16 storage + dynamic loss scaling (train.py:185-198); the
+    # backward runs on the loss times the GradScaler's initial scale, gradients unscaled after
+    "config5_b5_1024x1024_bs1_fp16": ("mit_b5", 1024, 1024, 1, 19, "float16"),
+    "config1_b0_240x320_bs1_fp16": ("mit_b0", 240, 320, 1, 9, "float16"),
 }
+LOSS_SCALE = 2.0 ** 16          # torch.cuda.amp.GradScaler's init_scale
 
 
 def err(a, b):
@@ -110,7 +115,9 @@ def _check(name, e_gpu, e_emu, bad, ratio=RATIO):
 @pytest.mark.parametrize("case", list(CONFIGS))
 def test_bf16_train_step_vs_fp64_oracle(dev, case):
     from rgbx_semantic_segmentation_amd.models.builder import EncoderDecoder
-    backbone, H, W, B, K = CONFIGS[case]
+    backbone, H, W, B, K, dtype = CONFIGS[case]
+    h16 = {"bfloat16": torch.bfloat16, "float16": torch.float16}[dtype]
+    S = LOSS_SCALE if h16 == torch.float16 else 1.0
     torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
     torch.manual_seed(0)
     ref = RefModel(CMXConfig(backbone=backbone, num_classes=K))
@@ -120,10 +127,10 @@ def test_bf16_train_step_vs_fp64_oracle(dev, case):
             b.copy_(torch.rand(b.shape, generator=g) * 0.2 - 0.1)
         elif n.endswith("running_var"):
             b.copy_(torch.rand(b.shape, generator=g) + 0.5)
-    model = EncoderDecoder(dict(backbone=backbone, num_classes=K, compute_dtype="bfloat16",
+    model = EncoderDecoder(dict(backbone=backbone, num_classes=K, compute_dtype=dtype,
                                 decoder_embed_dim=512)).to(dev)
     model.load_state_dict(ref.state_dict(), strict=True)
-    emu = emulate_bf16(copy.deepcopy(ref))
+    emu = emulate_storage(copy.deepcopy(ref), h16)
     ref64 = ref.double()
     for m in (ref64, emu, model):
         m.train()
@@ -138,11 +145,17 @@ def test_bf16_train_step_vs_fp64_oracle(dev, case):
     loss64 = ref64(rgb.double(), x.double(), lab)
     loss64.backward()
     loss_emu = emu(rgb, x, lab)
-    loss_emu.backward()
+    (loss_emu * S).backward()
+    if S != 1.0:
+        for p in emu.parameters():
+            p.grad.div_(S)
     t_cpu = time.time() - t0
     loss = model(rgb.to(dev), x.to(dev), lab.to(dev))
-    loss.backward()
+    (loss * S).backward()
     torch.cuda.synchronize()
+    if S != 1.0:
+        assert torch.isfinite(model.store.grad).all(), "scaled fp16 backward overflowed"
+        model.store.grad.div_(S)
 
     bad, rows = [], []
     e_l, e_le = err(lo, lo64), err(lo_emu, lo64)

@@ -126,7 +126,7 @@ def _worker_store(rank, world, port, payload, q):
             den = ddp[n].abs().max().clamp_min(1e-12)
             worst = max(worst, ((got - ddp[n]).abs().max() / den).item())
             worst_glob = max(worst_glob, ((ref.get_parameter(n).grad - ddp[n]).abs().max() / den).item())
-        tol = 1e-6 if payload == "fp32" else 8e-3           # bf16: one rounding of the summed gradient
+        tol = 1e-6 if payload == "fp32" else 8e-3           # bf16: payload + ring-sum roundings
         q.put((rank, worst <= tol, worst_glob > 1e-3, worst, worst_glob))
     finally:
         dist.destroy_process_group()

@@ -98,26 +98,18 @@ def test_dp_world1_graph_step_equals_plain_step(dev, payload):
     assert rel < 1e-3, (rel, d)
 
 
-@pytest.mark.parametrize("P", [1, 2, 8])
-def test_bf16_payload_kernels_against_cpu_formula(dev, P):
-    """The three kernels of the bf16 gradient exchange (dist.BucketedGradSync._reduce_bf16) on
-    their own, P ranks emulated in one buffer: cast fp32 -> bf16 (RNE), the per-shard fp32 sum
-    of the P received chunks rounded to bf16 once, cast bf16 -> fp32 -- against the CPU formula
-    (the gloo branch of the same protocol), bit for bit."""
+def test_bf16_payload_casts_against_cpu(dev):
+    """The two kernels of the bf16 gradient exchange (dist.BucketedGradSync._reduce_bf16): the
+    fp32 -> bf16 payload cast (round to nearest even) and the bf16 -> fp32 copy of the gathered
+    sums, bit for bit against torch's CPU casts, over magnitudes 1e-6 .. 1e3."""
     from rgbx_semantic_segmentation_amd import _lib
     n = 8 * 1237
-    g = torch.Generator().manual_seed(P)
-    src = (torch.randn(P, n, generator=g) * torch.logspace(-6, 3, n)).float()
-    send = torch.empty(P, n, dtype=torch.bfloat16, device=dev)
+    g = torch.Generator().manual_seed(3)
+    src = (torch.randn(n, generator=g) * torch.logspace(-6, 3, n)).float()
+    send = torch.empty(n, dtype=torch.bfloat16, device=dev)
     s_dev = src.to(dev)
-    for p in range(P):
-        _lib.call("cmx_cast_f32_bf16", _lib.ptr(s_dev[p]), _lib.ptr(send[p]), n, _lib.stream())
+    _lib.call("cmx_cast_f32_bf16", _lib.ptr(s_dev), _lib.ptr(send), n, _lib.stream())
     assert torch.equal(send.cpu(), src.to(torch.bfloat16))
-    mine = torch.empty(n, dtype=torch.bfloat16, device=dev)
-    _lib.call("cmx_shard_sum_bf16", _lib.ptr(send), _lib.ptr(mine), P, n, _lib.stream())
-    ref = src.to(torch.bfloat16).float().sum(0).to(torch.bfloat16)
-    assert torch.equal(mine.cpu(), ref)
     back = torch.empty(n, dtype=torch.float32, device=dev)
-    _lib.call("cmx_cast_bf16_f32", _lib.ptr(mine), _lib.ptr(back), n, _lib.stream())
-    assert torch.equal(back.cpu(), ref.float())
-
+    _lib.call("cmx_cast_bf16_f32", _lib.ptr(send), _lib.ptr(back), n, _lib.stream())
+    assert torch.equal(back.cpu(), src.to(torch.bfloat16).float())

@@ -29,7 +29,7 @@ def ref_dw(h, w, b, act, G, B, H, W):
     return torch.cat(outs)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("C,H,W", [(64, 30, 44), (256, 17, 16), (160, 9, 33), (320, 8, 10), (36, 12, 12)])
 @pytest.mark.parametrize("act", ["gelu", "relu", "none"])
 def test_dwconv_fwd_bwd(dev, dtype, C, H, W, act):
@@ -65,7 +65,8 @@ def test_dwconv_fwd_bwd(dev, dtype, C, H, W, act):
     assert rel(db, br.grad) < (tol if dtype == torch.float32 else 1e-2)
 
 
-@pytest.mark.parametrize("dtype,C,H,W", [(torch.bfloat16, 64, 30, 44), (torch.bfloat16, 256, 17, 16),
+@pytest.mark.parametrize("dtype,C,H,W", [(torch.float16, 64, 30, 44), (torch.float16, 512, 15, 20),
+                                         (torch.bfloat16, 64, 30, 44), (torch.bfloat16, 256, 17, 16),
                                          (torch.bfloat16, 320, 9, 33), (torch.bfloat16, 512, 15, 20),
                                          (torch.float32, 32, 8, 10), (torch.float32, 160, 9, 33),
                                          (torch.float32, 64, 30, 44)])

@@ -29,7 +29,7 @@ def ref_epi(acc, bias, act, residual, rscale, rps):
     return v
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("G,M,N,K", [(2, 300, 64, 64), (2, 1000, 128, 152), (1, 777, 40, 512), (2, 256, 320, 1280),
                                      (1, 130, 520, 24), (4, 512, 512, 300), (2, 64, 64, 1203)])
 @pytest.mark.parametrize("tA,tB", [(0, 0), (0, 1), (1, 1), (1, 0)])
@@ -51,7 +51,7 @@ def test_gemm_layouts(dev, dtype, G, M, N, K, tA, tB):
     assert rel(C, ref) < (1e-5 if dtype == torch.float32 else 1e-2)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("act", ["none", "gelu", "relu"])
 @pytest.mark.parametrize("res", [False, True])
 @pytest.mark.parametrize("K", [96, 2048])
@@ -72,7 +72,7 @@ def test_gemm_epilogues(dev, dtype, act, res, K):
     assert rel(C, ref) < (1e-5 if dtype == torch.float32 else 1e-2)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_gemm_fp32_out_and_accumulate(dev, dtype):
     torch.manual_seed(2)
     from rgbx_semantic_segmentation_amd import kernels as Kn
@@ -87,7 +87,7 @@ def test_gemm_fp32_out_and_accumulate(dev, dtype):
     assert rel(W, 2 * ref) < 1e-5
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_gemm_two_segment_A(dev, dtype):
     """Linear on cat(x1, x2) without the cat (end_proj / ChannelEmbed)."""
     torch.manual_seed(3)
@@ -103,7 +103,7 @@ def test_gemm_two_segment_A(dev, dtype):
     assert rel(C, ref) < (1e-5 if dtype == torch.float32 else 1e-2)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("splitk", [1, 7, 32])
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_gemm_wgrad_splitk_bias_grad(dev, dtype, splitk, accumulate):
@@ -128,7 +128,7 @@ def test_gemm_wgrad_splitk_bias_grad(dev, dtype, splitk, accumulate):
     assert torch.equal(Wg[:, :, :k0], W0[:, :, :k0]) and torch.equal(Wg[:, :, k0 + Kx:], W0[:, :, k0 + Kx:])
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("tA,tB", [(0, 0), (0, 1)])
 def test_gemm_unaligned_dims(dev, dtype, tA, tB):
     """Row strides / reduction lengths that are not whole 16-B chunks (K = 9 classes of the
@@ -166,7 +166,8 @@ def test_gemm_step_shapes_bf16(dev, G, M, N, K, tA, tB):
 
 @pytest.mark.parametrize("Cin,Cout,k,st,pad,H,W", [(64, 128, 3, 2, 1, 30, 40), (128, 320, 3, 2, 1, 15, 20),
                                                    (64, 64, 8, 8, 0, 120, 160), (320, 320, 2, 2, 0, 30, 40)])
-def test_implicit_conv(dev, Cin, Cout, k, st, pad, H, W):
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_implicit_conv(dev, Cin, Cout, k, st, pad, H, W, dt):
     """im2col-free conv (cmx_conv_implicit_fwd) and its per-tap grouped weight gradient
     (deferred.conv_wgrad) against torch fp32 conv2d: OverlapPatchEmbed k3 s2 p1 and the SRA
     spatial-reduction conv kR sR (dual_segformer.py:95-96, 196-197).  bf16 tolerance 1e-2."""
@@ -175,10 +176,10 @@ def test_implicit_conv(dev, Cin, Cout, k, st, pad, H, W):
     torch.manual_seed(3)
     G, NIg = 2, 2
     Ho, Wo = (H + 2 * pad - k) // st + 1, (W + 2 * pad - k) // st + 1
-    x = torch.randn(G * NIg, H, W, Cin, device=dev).bfloat16()
-    Wt = (torch.randn(G, Cout, k, k, Cin, device=dev) / math.sqrt(k * k * Cin)).bfloat16()
+    x = torch.randn(G * NIg, H, W, Cin, device=dev).to(dt)
+    Wt = (torch.randn(G, Cout, k, k, Cin, device=dev) / math.sqrt(k * k * Cin)).to(dt)
     b = torch.randn(G, Cout, device=dev)
-    y = torch.empty(G, NIg * Ho * Wo, Cout, device=dev, dtype=torch.bfloat16)
+    y = torch.empty(G, NIg * Ho * Wo, Cout, device=dev, dtype=dt)
     M = NIg * Ho * Wo
     sk = K.query("cmx_gemm_splitk", G, M, Cout, k * k * Cin, 0, 1)
     ws = K._ws(K.query("cmx_gemm_workspace", G, M, Cout, sk), dev) if sk > 1 else None
@@ -190,7 +191,7 @@ def test_implicit_conv(dev, Cin, Cout, k, st, pad, H, W):
         got = y[g].view(NIg, Ho, Wo, Cout).permute(0, 3, 1, 2)
         assert rel(got, ref) < 1e-2, rel(got, ref)
     # weight gradient of every tap in one grouped launch
-    dy = torch.randn(G, NIg * Ho * Wo, Cout, device=dev).bfloat16()
+    dy = torch.randn(G, NIg * Ho * Wo, Cout, device=dev).to(dt)
     Wg = torch.full((G, Cout, k * k * Cin), float("nan"), device=dev)
     bg = torch.full((G, Cout), float("nan"), device=dev)
     assert deferred.conv_wgrad(dy, x, Wg, bg, (G, NIg, H, W, Cin, k, k, st, pad, Ho, Wo))

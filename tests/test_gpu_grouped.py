@@ -16,7 +16,8 @@ def rel(a, b):
     return ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-30)).item()
 
 
-def test_grouped_wgrads_and_bias(dev):
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_grouped_wgrads_and_bias(dev, dt):
     from rgbx_semantic_segmentation_amd import deferred
     torch.manual_seed(0)
     shapes = [(2, 38400, 64, 64, True), (2, 38400, 256, 64, True), (2, 38400, 64, 256, True),
@@ -24,8 +25,8 @@ def test_grouped_wgrads_and_bias(dev):
               (2, 1200, 320, 320, True), (2, 600, 40, 512, True)]
     jobs = []
     for G, M, N, k, has_b in shapes:
-        dz = torch.randn(G, M, N, device=dev).bfloat16()
-        x = torch.randn(G, M, k, device=dev).bfloat16()
+        dz = torch.randn(G, M, N, device=dev).to(dt)
+        x = torch.randn(G, M, k, device=dev).to(dt)
         Wg = torch.full((G, N, k), float("nan"), device=dev)
         bg = torch.full((G, N), float("nan"), device=dev) if has_b else None
         queued = deferred.wgrad(dz, x, Wg, bg)
@@ -33,8 +34,8 @@ def test_grouped_wgrads_and_bias(dev):
         jobs.append((dz, x, Wg, bg))
     # a strided column slice of one gradient (FRM: gW0[:, :C] and gW0[:, C:])
     M, N, C = 19200, 64, 64
-    dzs = torch.randn(1, M, N, device=dev).bfloat16()
-    xa, xb = torch.randn(1, M, C, device=dev).bfloat16(), torch.randn(1, M, C, device=dev).bfloat16()
+    dzs = torch.randn(1, M, N, device=dev).to(dt)
+    xa, xb = torch.randn(1, M, C, device=dev).to(dt), torch.randn(1, M, C, device=dev).to(dt)
     W2 = torch.full((1, N, 2 * C), float("nan"), device=dev)
     b2 = torch.full((1, N), float("nan"), device=dev)
     assert deferred.wgrad(dzs, xa, W2[:, :, :C], b2) and deferred.wgrad(dzs, xb, W2[:, :, C:])

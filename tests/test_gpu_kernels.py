@@ -8,8 +8,8 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-TOL = {torch.float32: 1e-4, torch.bfloat16: 3e-2}
-DTYPES = [torch.float32, torch.bfloat16]
+TOL = {torch.float32: 1e-4, torch.bfloat16: 3e-2, torch.float16: 3e-2}
+DTYPES = [torch.float32, torch.bfloat16, torch.float16]
 
 
 def relerr(a, b):

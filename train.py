@@ -47,7 +47,8 @@ def build_parser():
     p.add_argument("--nepochs", type=int, default=1)
     p.add_argument("--niters-per-epoch", type=int, default=10)
     p.add_argument("--warm-up-epoch", type=int, default=10)
-    p.add_argument("--compute-dtype", default="bfloat16", choices=["bfloat16", "float32"])
+    p.add_argument("--compute-dtype", default=None, choices=["bfloat16", "float32", "float16"],
+                   help="default: float16 with --use-mixed-precision (the reference's fp16 autocast), else bfloat16")
     p.add_argument("--criterion", default="CrossEntropyLoss")
     p.add_argument("--optimizer", default="AdamW")
     p.add_argument("--seed", type=int, default=12345)
@@ -107,7 +108,8 @@ def main(argv=None):
         from rgbx_semantic_segmentation_amd import dist as cdist
 
         norm = torch.nn.SyncBatchNorm if engine.distributed else torch.nn.BatchNorm2d
-        cfg = dict(backbone=args.backbone, num_classes=args.num_classes, compute_dtype=args.compute_dtype,
+        dtype = args.compute_dtype or ("float16" if args.use_mixed_precision else "bfloat16")
+        cfg = dict(backbone=args.backbone, num_classes=args.num_classes, compute_dtype=dtype,
                    decoder_embed_dim=512)
         model = EncoderDecoder(cfg, norm_layer=norm).to(dev)
         sync = None
