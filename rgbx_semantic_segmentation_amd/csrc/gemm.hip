@@ -461,18 +461,16 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
     else if (keep == 1) vm_wait<PER>();
     else vm_wait<0>();
   };
-  // a k-range that fits the ring is issued whole in the prologue (every tile in flight at
-  // once, no refills); a longer one keeps NS - 1 tiles ahead and refills the slot just read
-  const int pro = kt1 - kt0 <= NS ? kt1 - kt0 : NS - 1;
+  const int pro = min(NS - 1, kt1 - kt0);
 #pragma unroll
-  for (int q = 0; q < NS; ++q)
+  for (int q = 0; q < NS - 1; ++q)
     if (q < pro) stage(kt0 + q, smem + q * SLOT);
   wait_keep(pro - 1);
   __syncthreads();
   int cur = 0;
   for (int kt = kt0; kt < kt1; ++kt) {
     const int nxt = cur == 0 ? NS - 1 : cur - 1;
-    if (kt + NS - 1 < kt1 && kt + NS - 1 >= kt0 + pro) stage(kt + NS - 1, smem + nxt * SLOT);
+    if (kt + NS - 1 < kt1) stage(kt + NS - 1, smem + nxt * SLOT);
     compute(smem + cur * SLOT);
     // tiles kt+1 .. kt+ahead are in flight; retire tile kt+1, keep the rest
     const int ahead = min(NS - 1, kt1 - 1 - kt);
@@ -923,15 +921,8 @@ void launch_bf16_ns(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStr
   // K 2048 20.1 -> 11.9 us, K 512 7.5 -> 5.8 us at KW = 2; grids above 512 blocks and one-slot
   // problems are slower with it (M9600 N128 K512: 9.7 -> 10.4 us), so they keep 4 waves.
   static const int kw = [] { const char* e = getenv("CMX_GEMM_KW"); return e ? atoi(e) : 2; }();
-  // CMX_GEMM_DEEP=1: a 64 x 64 problem whose whole k-range fits a 5- (two blocks per CU) or
-  // 8-slot ring (one block per CU, grids of <= 256 blocks) issues every k-tile at once
-  static const int deep = [] { const char* e = getenv("CMX_GEMM_DEEP"); return e ? atoi(e) : 0; }();
   if constexpr (BM == 64 && BN == 64) {
     const int nk64 = (a.K + FBK - 1) / FBK;
-    if (deep && nsplit == 1 && !a.ones_col && nk64 >= 2) {
-      if (nk64 <= 5 && blocks <= 512) { launch_bf16<64, 64, 5, 1, E>(a, G, nsplit, tA, tB, s); return; }
-      if (nk64 <= 8 && blocks <= 256) { launch_bf16<64, 64, 8, 1, E>(a, G, nsplit, tA, tB, s); return; }
-    }
     if (kw >= 2 && nsplit == 1 && !a.ones_col && blocks <= 512 && nk64 >= 4) {
       GemmArgs b = a;
       if (kw >= 4 && blocks <= 256 && nk64 >= 16) {

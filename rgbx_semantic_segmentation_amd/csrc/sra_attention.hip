@@ -450,6 +450,16 @@ void sra_dkv_fast_launch(const void* q, const void* k, const void* v, const void
                          int Nk, int heads, long qs,
                          long kvs, long dos, int nchunk, float sl2, float scale, int dtype, hipStream_t s);
 
+bool sra_small_ok(int D, int N, int Nk, int dtype, const void* const* ptrs, int nptr, const long* strides, int nstr);
+void sra_fwd_small_launch(const void* q, const void* k, const void* v, void* o, float* lse, int Bt, int N, int Nk,
+                          int heads, long qs, long kvs, long os, float sl2, int dtype, hipStream_t s);
+void sra_dq_small_launch(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                         const float* lse, float* Dws, void* dq, int Bt, int N, int Nk, int heads, long qs, long kvs,
+                         long os, long dos, long dqs, float sl2, float scale, int dtype, hipStream_t s);
+void sra_dkv_small_launch(const void* q, const void* k, const void* v, const void* dout, const float* lse,
+                          const float* Dws, void* dk, void* dv, long dkvs, int Bt, int N, int Nk, int heads, long qs,
+                          long kvs, long dos, float sl2, float scale, int dtype, hipStream_t s);
+
 #define SRA_D_DISPATCH(D, ...)                                              \
   do {                                                                      \
     if ((D) == 64) { constexpr int DD = 64; __VA_ARGS__; }                  \
@@ -469,6 +479,10 @@ int cmx_sra_attn_fwd(const void* q, const void* k, const void* v, void* o, float
   {
     const void* ptrs[] = {q, k, v, o};
     const long strides[] = {qs, kvs, os};
+    if (sra_small_ok(D, N, Nk, dtype, ptrs, 4, strides, 3)) {
+      sra_fwd_small_launch(q, k, v, o, lse, Bt, N, Nk, heads, qs, kvs, os, sl2, dtype, s);
+      return cmx_check_launch("sra_fwd");
+    }
     if (sra_fast_fwd_ok(D, Nk, dtype, ptrs, 4, strides, 3)) {
       sra_fwd_fast_launch(q, k, v, o, lse, Bt, N, Nk, heads, qs, kvs, os, sl2, dtype, s);
       return cmx_check_launch("sra_fwd");
@@ -500,6 +514,14 @@ int cmx_sra_attn_bwd(const void* q, const void* k, const void* v, const void* o,
   const float sl2 = scale * 1.4426950408889634f;
   const void* ptrs[] = {q, k, v, o, dout, dq};
   const long strides[] = {qs, kvs, os, dos, dqs};
+  if (sra_small_ok(D, N, Nk, dtype, ptrs, 6, strides, 5) && ((uintptr_t)dk & 15) == 0 && ((uintptr_t)dv & 15) == 0 &&
+      dkvs % 8 == 0) {
+    // short sequences: keys split over waves (dQ), query tiles over waves (dK / dV), no slabs
+    float* Dws = workspace;
+    sra_dq_small_launch(q, k, v, o, dout, lse, Dws, dq, Bt, N, Nk, heads, qs, kvs, os, dos, dqs, sl2, scale, dtype, s);
+    sra_dkv_small_launch(q, k, v, dout, lse, Dws, dk, dv, dkvs, Bt, N, Nk, heads, qs, kvs, dos, sl2, scale, dtype, s);
+    return cmx_check_launch("sra_bwd");
+  }
   // fast path for any Nk: dQ streams K / V in LDS-sized chunks, dK / dV splits keys over workgroups
   const bool fast = sra_fast_fwd_ok(D, Nk, dtype, ptrs, 6, strides, 5);
   const bool fast_dq = fast;

@@ -472,6 +472,369 @@ __global__ __launch_bounds__(64 * (NKP_MAX / 32)) void sra_dkv_fast(
     }
 }
 
+// ------------------------------------------------------------------------ short sequences
+// Stages 3 / 4 of B2 / B4 (N = 1200 / 300 queries per (b, head), Nk = 300 keys): the kernels
+// above stage all of a (b, head)'s keys in every workgroup and walk them serially, so with
+// 64 queries per workgroup the K / V staging and the 5-step key loop are a latency chain the
+// chip cannot fill (11-23 us per launch for 0.6-1.8 GFLOP).  Here the keys are split over the
+// waves of a workgroup instead: wave w owns the w-th 64-key tile (its K / V image in its own
+// LDS region, staged and read by that wave alone, so no barrier guards it), and the waves'
+// partial results meet once in LDS at the end.  dK / dV keep the keys on the lanes and split
+// the QUERY tiles over the waves, so every key's gradient is summed inside one workgroup: no
+// partial slabs and no reduce launch.
+constexpr int SKT = NKP_MAX / KTILE;           // key tiles of 64 (Nk <= 320): waves per workgroup
+constexpr int SREG = 2 * KTILE * ROWB;          // per-wave LDS region: two 64-row images (16 KB)
+constexpr int SQW = 8;                          // dK / dV: query-tile waves per workgroup
+constexpr int SDREG = 2 * KTILE * ROWB + 2 * KTILE * 4;   // dK / dV region: Q, dO images + lse, Dq
+
+// fp32 [row][64] tile in a wave's region, 16-B chunks XOR-swizzled by (row & 15): the lanes of
+// one accumulator write (32 rows, one chunk each) spread over the bank row
+__device__ __forceinline__ float* xrow(char* reg, int row, int chunk) {
+  return reinterpret_cast<float*>(reg + row * 256 + ((chunk ^ (row & 15)) << 4));
+}
+
+// acc (lane = row r of the 32-row block rb, registers = 32 columns of column block 32 t) scaled
+// by `mul` -> the wave's fp32 [row][64] tile
+__device__ __forceinline__ void put_tile(char* reg, const f32x16& acc, int rb, int t, int lane, float mul) {
+  const int r = lane & 31, h = lane >> 5, row = rb + r;
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4)
+    *reinterpret_cast<float4*>(xrow(reg, row, 8 * t + 2 * g4 + h)) =
+        make_float4(acc[4 * g4] * mul, acc[4 * g4 + 1] * mul, acc[4 * g4 + 2] * mul, acc[4 * g4 + 3] * mul);
+}
+
+// out row `row`, columns [8 dg, 8 dg + 8) = sum over the nw regions (stride `rs` bytes) * mul
+template <typename E>
+__device__ __forceinline__ void sum_store8(const char* smem, int nw, long rs, int row, int dg, float mul, E* out) {
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int w = 0; w < nw; ++w) {
+    char* reg = const_cast<char*>(smem) + w * rs;
+    const float4 x = *reinterpret_cast<const float4*>(xrow(reg, row, 2 * dg));
+    const float4 y = *reinterpret_cast<const float4*>(xrow(reg, row, 2 * dg + 1));
+    a[0] += x.x; a[1] += x.y; a[2] += x.z; a[3] += x.w; a[4] += y.x; a[5] += y.y; a[6] += y.z; a[7] += y.w;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] *= mul;
+  store_vec<E>(out, a);
+}
+
+// forward: workgroup = 64 queries of one (b, head); wave w = key tile w
+template <typename E>
+__global__ __launch_bounds__(64 * SKT) void sra_fwd_small(const E* __restrict__ q, const E* __restrict__ k,
+                                                         const E* __restrict__ v, E* __restrict__ o,
+                                                         float* __restrict__ lse, int N, int Nk, int heads, long qs,
+                                                         long kvs, long os, float sl2) {
+  __shared__ __attribute__((aligned(1024))) char smem[SKT * SREG];
+  const int nw = blockDim.x >> 6;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int b = blockIdx.z, head = blockIdx.y, q0 = blockIdx.x * 64;
+  char* Ki = smem + wave * SREG;
+  char* Vi = Ki + KTILE * ROWB;
+  const int t0 = wave * KTILE, nkw = min(KTILE, Nk - t0);
+  stage_rows<E>(k + ((long)b * Nk + t0) * kvs + head * HD, kvs, nkw, KTILE, Ki, 0, lane, 1);
+  stage_rows<E>(v + ((long)b * Nk + t0) * kvs + head * HD, kvs, nkw, KTILE, Vi, 0, lane, 1);
+  const E* qb = q + (long)b * N * qs + head * HD;
+  frag8<E> qf[2][4];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int qi = q0 + 32 * u + r;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      qf[u][s] = qi < N ? frag_bits<E>(*reinterpret_cast<const uint4*>(qb + (long)qi * qs + 16 * s + 8 * h)) : zfrag<E>();
+  }
+  vm_wait<0>();                                  // this wave's own images (no other wave reads them)
+  f32x16 sa[2][2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    frag8<E> kf[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) kf[s] = frag_k<E>(Ki, 32 * ks, s, lane);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      sa[u][ks] = zero16();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) sa[u][ks] = MF<E>::mma(kf[s], qf[u][s], sa[u][ks]);
+    }
+  }
+  float m[2], l[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    float mt = -INFINITY;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float x = sa[u][ks][i];
+        if (32 * ks + accrow(i, h) >= nkw) x = -INFINITY;
+        sa[u][ks][i] = x;
+        mt = fmaxf(mt, x);
+      }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
+    float rs = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = fexp2(fmaf(sa[u][ks][i], sl2, -mt));
+        sa[u][ks][i] = p;
+        rs += p;
+      }
+    m[u] = mt;
+    l[u] = rs + __shfl_xor(rs, 32, 64);
+  }
+  // this wave's (max, sum) per query into its K image (K is no longer read)
+  float* st = reinterpret_cast<float*>(Ki);
+  if (h == 0) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) { st[32 * u + r] = m[u]; st[64 + 32 * u + r] = l[u]; }
+  }
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) acc[u][0] = acc[u][1] = zero16();
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const frag8<E> v0 = frag_t<E>(Vi, 32 * ks, 0, s, lane);
+      const frag8<E> v1 = frag_t<E>(Vi, 32 * ks, 32, s, lane);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const frag8<E> pf = MF<E>::from_acc(sa[u][ks], s);
+        acc[u][0] = MF<E>::mma(v0, pf, acc[u][0]);
+        acc[u][1] = MF<E>::mma(v1, pf, acc[u][1]);
+      }
+    }
+  __syncthreads();                               // every wave's (max, sum) is in LDS
+  float mul[2], M[2], L[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    float mx = -INFINITY;
+    for (int w = 0; w < nw; ++w) mx = fmaxf(mx, reinterpret_cast<const float*>(smem + w * SREG)[32 * u + r]);
+    float sum = 0.f;
+    for (int w = 0; w < nw; ++w) {
+      const float* sw = reinterpret_cast<const float*>(smem + w * SREG);
+      sum += sw[64 + 32 * u + r] * fexp2(sw[32 * u + r] - mx);
+    }
+    M[u] = mx;
+    L[u] = sum;
+    mul[u] = fexp2(m[u] - mx) / sum;             // this wave's share of the normalised output
+  }
+  __syncthreads();                               // the statistics are read: the regions take the outputs
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    put_tile(Ki, acc[u][0], 32 * u, 0, lane, mul[u]);
+    put_tile(Ki, acc[u][1], 32 * u, 1, lane, mul[u]);
+    const int qi = q0 + 32 * u + r;
+    if (wave == 0 && h == 0 && lse && qi < N)
+      lse[((long)b * heads + head) * N + qi] = (M[u] + __log2f(L[u])) * 0.69314718055994531f;
+  }
+  __syncthreads();
+  for (int it = threadIdx.x; it < 64 * 8; it += blockDim.x) {
+    const int row = it >> 3, dg = it & 7, qi = q0 + row;
+    if (qi < N) sum_store8<E>(smem, nw, SREG, row, dg, 1.f, o + ((long)b * N + qi) * os + head * HD + 8 * dg);
+  }
+}
+
+// dQ: workgroup = 64 queries of one (b, head); wave w = key tile w; partial dQ summed in LDS
+template <typename E>
+__global__ __launch_bounds__(64 * SKT) void sra_dq_small(const E* __restrict__ q, const E* __restrict__ k,
+                                                        const E* __restrict__ v, const E* __restrict__ o,
+                                                        const E* __restrict__ dout, const float* __restrict__ lse,
+                                                        float* __restrict__ Dws, E* __restrict__ dq, int N, int Nk,
+                                                        int heads, long qs, long kvs, long os, long dos, long dqs,
+                                                        float sl2, float scale) {
+  __shared__ __attribute__((aligned(1024))) char smem[SKT * SREG];
+  const int nw = blockDim.x >> 6;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int b = blockIdx.z, head = blockIdx.y, q0 = blockIdx.x * 64;
+  char* Ki = smem + wave * SREG;
+  char* Vi = Ki + KTILE * ROWB;
+  const int t0 = wave * KTILE, nkw = min(KTILE, Nk - t0);
+  stage_rows<E>(k + ((long)b * Nk + t0) * kvs + head * HD, kvs, nkw, KTILE, Ki, 0, lane, 1);
+  stage_rows<E>(v + ((long)b * Nk + t0) * kvs + head * HD, kvs, nkw, KTILE, Vi, 0, lane, 1);
+  frag8<E> qf[2][4], df[2][4];
+  float Dq[2], lse2[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int qi = q0 + 32 * u + r;
+    const bool live = qi < N;
+    const E* qrow = q + ((long)b * N + qi) * qs + head * HD;
+    const E* orow = o + ((long)b * N + qi) * os + head * HD;
+    const E* drow = dout + ((long)b * N + qi) * dos + head * HD;
+    float dot = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (live) {
+        qf[u][s] = frag_bits<E>(*reinterpret_cast<const uint4*>(qrow + 16 * s + 8 * h));
+        df[u][s] = frag_bits<E>(*reinterpret_cast<const uint4*>(drow + 16 * s + 8 * h));
+        float x[8], y[8];
+        load_vec<E>(drow + 16 * s + 8 * h, x);
+        load_vec<E>(orow + 16 * s + 8 * h, y);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dot += x[j] * y[j];
+      } else {
+        qf[u][s] = df[u][s] = zfrag<E>();
+      }
+    }
+    dot += __shfl_xor(dot, 32, 64);
+    Dq[u] = dot;
+    const long sidx = ((long)b * heads + head) * N + qi;
+    lse2[u] = live ? lse[sidx] * 1.4426950408889634f : 0.f;
+    if (live && h == 0 && wave == 0) Dws[sidx] = dot;
+  }
+  vm_wait<0>();
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) acc[u][0] = acc[u][1] = zero16();
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    frag8<E> kf[4], vf[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kf[s] = frag_k<E>(Ki, 32 * ks, s, lane);
+      vf[s] = frag_k<E>(Vi, 32 * ks, s, lane);
+    }
+    f32x16 ds[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      f32x16 sa = zero16(), dp = zero16();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sa = MF<E>::mma(kf[s], qf[u][s], sa);
+        dp = MF<E>::mma(vf[s], df[u][s], dp);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float p = fexp2(sa[i] * sl2 - lse2[u]);
+        if (32 * ks + accrow(i, h) >= nkw) p = 0.f;
+        ds[u][i] = p * (dp[i] - Dq[u]);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const frag8<E> k0 = frag_t<E>(Ki, 32 * ks, 0, s, lane);
+      const frag8<E> k1 = frag_t<E>(Ki, 32 * ks, 32, s, lane);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const frag8<E> sf = MF<E>::from_acc(ds[u], s);
+        acc[u][0] = MF<E>::mma(k0, sf, acc[u][0]);
+        acc[u][1] = MF<E>::mma(k1, sf, acc[u][1]);
+      }
+    }
+  }
+  // own region: every read of it fed an MFMA whose result is in acc, so it is free
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    put_tile(Ki, acc[u][0], 32 * u, 0, lane, scale);
+    put_tile(Ki, acc[u][1], 32 * u, 1, lane, scale);
+  }
+  __syncthreads();
+  for (int it = threadIdx.x; it < 64 * 8; it += blockDim.x) {
+    const int row = it >> 3, dg = it & 7, qi = q0 + row;
+    if (qi < N) sum_store8<E>(smem, nw, SREG, row, dg, 1.f, dq + ((long)b * N + qi) * dqs + head * HD + 8 * dg);
+  }
+}
+
+// dK / dV: workgroup = 32 keys of one (b, head) on the lanes; wave w sweeps query tiles
+// w, w + nw, ... (its own Q / dO images), and the waves' sums meet in LDS: every key's dK / dV
+// is complete inside the workgroup (written directly, no slabs)
+template <typename E>
+__global__ __launch_bounds__(64 * SQW) void sra_dkv_small(const E* __restrict__ q, const E* __restrict__ k,
+                                                         const E* __restrict__ v, const E* __restrict__ dout,
+                                                         const float* __restrict__ lse, const float* __restrict__ Dws,
+                                                         E* __restrict__ dk, E* __restrict__ dv, long dkvs, int N,
+                                                         int Nk, int heads, long qs, long kvs, long dos, float sl2,
+                                                         float scale) {
+  __shared__ __attribute__((aligned(1024))) char smem[SQW * SDREG];
+  const int nw = blockDim.x >> 6;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int head = blockIdx.y, b = blockIdx.z, k0 = blockIdx.x * 32;
+  const long sbase = ((long)b * heads + head) * N;
+  const i32x4 rq = make_rsrc(q + (long)b * N * qs + head * HD);
+  const i32x4 rd = make_rsrc(dout + (long)b * N * dos + head * HD);
+  const i32x4 rl = make_rsrc(lse + sbase);
+  const i32x4 rD = make_rsrc(Dws + sbase);
+  char* Qi = smem + wave * SDREG;
+  char* Di = Qi + KTILE * ROWB;
+  const float* ls = reinterpret_cast<const float*>(Qi + 2 * KTILE * ROWB);
+  const float* Ds = ls + KTILE;
+  const int key = k0 + r;
+  frag8<E> kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (key < Nk) {
+      kf[s] = frag_bits<E>(*reinterpret_cast<const uint4*>(k + ((long)b * Nk + key) * kvs + head * HD + 16 * s + 8 * h));
+      vf[s] = frag_bits<E>(*reinterpret_cast<const uint4*>(v + ((long)b * Nk + key) * kvs + head * HD + 16 * s + 8 * h));
+    } else {
+      kf[s] = vf[s] = zfrag<E>();
+    }
+  }
+  f32x16 ak[2], av[2];
+  ak[0] = ak[1] = av[0] = av[1] = zero16();
+  const int nqt = (N + KTILE - 1) / KTILE;
+  for (int qt0 = wave; qt0 < nqt; qt0 += nw) {
+    const int q0 = qt0 * KTILE;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the previous tile's image reads are done
+    // this tile's Q / dO rows (8 + 8 instructions) and lse / Dq (one each) into the wave's images
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int row = j * 8 + (lane >> 3), cc = (lane & 7) ^ swz(row), gq = q0 + row;
+      dma16(rq, lds_addr(Qi + j * 1024), gq < N ? (int)(((long)gq * qs + cc * 8) * 2) : OOB);
+      dma16(rd, lds_addr(Di + j * 1024), gq < N ? (int)(((long)gq * dos + cc * 8) * 2) : OOB);
+    }
+    dma4(rl, lds_addr(Qi + 2 * KTILE * ROWB), q0 + lane < N ? (q0 + lane) * 4 : OOB);
+    dma4(rD, lds_addr(Qi + 2 * KTILE * ROWB + KTILE * 4), q0 + lane < N ? (q0 + lane) * 4 : OOB);
+    vm_wait<0>();
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      const int qb = 32 * qh;
+      f32x16 sa = zero16(), dp = zero16();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) sa = MF<E>::mma(frag_k<E>(Qi, qb, s, lane), kf[s], sa);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) dp = MF<E>::mma(frag_k<E>(Di, qb, s, lane), vf[s], dp);
+      const bool tail = q0 + qb + 32 > N;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 l4 = *reinterpret_cast<const float4*>(ls + qb + 8 * g4 + 4 * h);
+        const float4 d4 = *reinterpret_cast<const float4*>(Ds + qb + 8 * g4 + 4 * h);
+        const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * g4 + e;
+          float p = fexp2(fmaf(sa[i], sl2, -lv[e] * 1.4426950408889634f));
+          if (tail && q0 + qb + accrow(i, h) >= N) p = 0.f;
+          sa[i] = p;
+          dp[i] = p * (dp[i] - dv4[e]);
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const frag8<E> pf = MF<E>::from_acc(sa, s);
+        const frag8<E> sf = MF<E>::from_acc(dp, s);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          av[t] = MF<E>::mma(frag_t<E>(Di, qb, 32 * t, s, lane), pf, av[t]);
+          ak[t] = MF<E>::mma(frag_t<E>(Qi, qb, 32 * t, s, lane), sf, ak[t]);
+        }
+      }
+    }
+  }
+  // the waves' partial sums meet in LDS: [key][d] dK tile then dV tile in each wave's region
+  // (its images are dead: every read fed an MFMA whose result is in ak / av)
+  put_tile(Qi, ak[0], 0, 0, lane, scale);
+  put_tile(Qi, ak[1], 0, 1, lane, scale);
+  put_tile(Qi + 32 * 256, av[0], 0, 0, lane, 1.f);
+  put_tile(Qi + 32 * 256, av[1], 0, 1, lane, 1.f);
+  __syncthreads();
+  for (int it = threadIdx.x; it < 2 * 32 * 8; it += blockDim.x) {
+    const int which = it >> 8, row = (it >> 3) & 31, dg = it & 7, kk = k0 + row;
+    if (kk >= Nk) continue;
+    E* out = (which ? dv : dk) + ((long)b * Nk + kk) * dkvs + head * HD + 8 * dg;
+    sum_store8<E>(smem + which * 32 * 256, nw, SDREG, row, dg, 1.f, out);
+  }
+}
+
 int pick_qw(int N, int heads, int Bt) {
   const long wg2 = (long)cdiv(N, 64 * NWAVE) * heads * Bt;   // workgroups at 2 sub-tiles per wave
   return wg2 >= 512 ? 2 : 1;
@@ -605,4 +968,48 @@ void sra_dkv_fast_launch(const void* q, const void* k, const void* v, const void
   else
     sra_dkv_fast_launch_t<bf16>(q, k, v, dout, lse, Dws, ws_dk, ws_dv, dk, dv, dkvs, Bt, N, Nk, heads, qs, kvs, dos,
                                 nchunk, sl2, scale, s);
+}
+
+// ---------------------------------------------------------------- short sequences (sra_*_small)
+// eligible: 16-bit storage, D = 64, Nk <= 320 (one 64-key tile per wave), 16-B aligned rows, and a
+// short query sequence (N <= CMX_SRA_SMALL_N, default 2048: stages 3 / 4 of B2 / B4)
+bool sra_small_ok(int D, int N, int Nk, int dtype, const void* const* ptrs, int nptr, const long* strides, int nstr) {
+  static const int small_n = [] { const char* e = getenv("CMX_SRA_SMALL_N"); return e ? atoi(e) : 2048; }();
+  return N <= small_n && sra_fast_ok(D, Nk, dtype, ptrs, nptr, strides, nstr);
+}
+
+void sra_fwd_small_launch(const void* q, const void* k, const void* v, void* o, float* lse, int Bt, int N, int Nk,
+                          int heads, long qs, long kvs, long os, float sl2, int dtype, hipStream_t s) {
+  const dim3 grid(cdiv(N, 64), heads, Bt), block(64 * cdiv(Nk, KTILE));
+  if (dtype == 2)
+    hipLaunchKernelGGL(sra_fwd_small<f16>, grid, block, 0, s, (const f16*)q, (const f16*)k, (const f16*)v, (f16*)o,
+                       lse, N, Nk, heads, qs, kvs, os, sl2);
+  else
+    hipLaunchKernelGGL(sra_fwd_small<bf16>, grid, block, 0, s, (const bf16*)q, (const bf16*)k, (const bf16*)v,
+                       (bf16*)o, lse, N, Nk, heads, qs, kvs, os, sl2);
+}
+
+void sra_dq_small_launch(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                         const float* lse, float* Dws, void* dq, int Bt, int N, int Nk, int heads, long qs, long kvs,
+                         long os, long dos, long dqs, float sl2, float scale, int dtype, hipStream_t s) {
+  const dim3 grid(cdiv(N, 64), heads, Bt), block(64 * cdiv(Nk, KTILE));
+#define CMX_SRA_DQS(E_)                                                                                            \
+  hipLaunchKernelGGL(sra_dq_small<E_>, grid, block, 0, s, (const E_*)q, (const E_*)k, (const E_*)v, (const E_*)o,   \
+                     (const E_*)dout, lse, Dws, (E_*)dq, N, Nk, heads, qs, kvs, os, dos, dqs, sl2, scale)
+  if (dtype == 2) CMX_SRA_DQS(f16);
+  else CMX_SRA_DQS(bf16);
+#undef CMX_SRA_DQS
+}
+
+void sra_dkv_small_launch(const void* q, const void* k, const void* v, const void* dout, const float* lse,
+                          const float* Dws, void* dk, void* dv, long dkvs, int Bt, int N, int Nk, int heads, long qs,
+                          long kvs, long dos, float sl2, float scale, int dtype, hipStream_t s) {
+  const int nqt = cdiv(N, KTILE);
+  const dim3 grid(cdiv(Nk, 32), heads, Bt), block(64 * (nqt < SQW ? nqt : SQW));
+#define CMX_SRA_DKVS(E_)                                                                                           \
+  hipLaunchKernelGGL(sra_dkv_small<E_>, grid, block, 0, s, (const E_*)q, (const E_*)k, (const E_*)v,                \
+                     (const E_*)dout, lse, Dws, (E_*)dk, (E_*)dv, dkvs, N, Nk, heads, qs, kvs, dos, sl2, scale)
+  if (dtype == 2) CMX_SRA_DKVS(f16);
+  else CMX_SRA_DKVS(bf16);
+#undef CMX_SRA_DKVS
 }

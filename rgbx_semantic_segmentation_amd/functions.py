@@ -537,11 +537,12 @@ class ConvF(Function):
             NIg = NI // G
             y = torch.empty(G, NIg * Ho * Wo, N, dtype=x.dtype, device=x.device)
             M = NIg * Ho * Wo
-            sk = K.query("cmx_gemm_splitk", G, M, N, Kp, 0, 1)
+            dt = K.dtype_code(x)
+            sk = K.query("cmx_gemm_splitk", G, M, N, Kp, 0, dt)
             ws = K._ws(K.query("cmx_gemm_workspace", G, M, N, sk), x.device) if sk > 1 else None
             K.call("cmx_conv_implicit_fwd", K.ptr(x), K.ptr(W), K.ptr(y), K.ptr(b), K.ptr(ws), G, NIg, H, Wd, C, KH, KW,
                    st, pad, Ho, Wo, N, NIg * H * Wd * C, W.stride(0), y.stride(0), b.stride(0) if b is not None else 0,
-                   sk, 1, K.stream())
+                   sk, dt, K.stream())
             ctx.save_for_backward(x, W)
             ctx.meta = (Wg, bg, geom)
             ctx.xshape = x.shape

@@ -9,7 +9,7 @@ import sys
 c = sqlite3.connect(sys.argv[1])
 top = int(sys.argv[2]) if len(sys.argv) > 2 else 40
 rows = c.execute("select start, end, name from kernels order by start").fetchall()
-idx = [i for i, r in enumerate(rows) if r[2].startswith("adamw")]
+idx = [i for i, r in enumerate(rows) if r[2].replace("void ", "").startswith("adamw")]
 seg = rows[idx[-2] + 1:idx[-1] + 1]
 print(f"launches/step {len(seg)}  wall {(seg[-1][1] - seg[0][0]) / 1e3:.0f} us  busy {sum(r[1] - r[0] for r in seg) / 1e3:.0f} us")
 cat = collections.defaultdict(lambda: [0, 0.0])

@@ -8,7 +8,7 @@ import sys
 c = sqlite3.connect(sys.argv[1])
 flt = sys.argv[2] if len(sys.argv) > 2 else None
 rows = c.execute("select start, end, name from kernels order by start").fetchall()
-idx = [i for i, r in enumerate(rows) if r[2].startswith("adamw")]
+idx = [i for i, r in enumerate(rows) if r[2].replace("void ", "").startswith("adamw")]
 seg = rows[idx[-2] + 1:idx[-1] + 1]
 t0 = seg[0][0]
 prev_end = t0

@@ -26,13 +26,15 @@ def _model(dev, norm, state=None):
     return m
 
 
-def _run(model, opt, batch, captured_steps=2):
+def _run(model, opt, batch, captured_steps=2, pre_step=None):
     """bench.py's sequence: 2 eager steps, a side-stream warm-up, capture, replays."""
     rgb, x, lab = batch
 
     def step():
         loss = model(rgb, x, lab)
         loss.backward()
+        if pre_step is not None:
+            pre_step()
         opt.step()
         return loss
 
@@ -73,7 +75,11 @@ def test_dp_world1_graph_step_equals_plain_step(dev, payload):
     flags, d2 = flags.to(dev), d2.to(dev)            # device-resident: no H2D copy inside the capture
     plain.forced_masks = {"droppath": flags, "dropout2d": d2}
     p0 = plain.store.flat.clone()
-    ref = _run(plain, FusedAdamW(plain), batch)
+    # the bf16 payload at world size 1 delivers float(bf16(g)) (a one-rank reduce-scatter and
+    # all-gather are copies): the plain reference rounds its gradients the same way
+    g = plain.store.grad
+    rounding = (lambda: g.copy_(g.to(torch.bfloat16).float())) if payload == "bf16" else None
+    ref = _run(plain, FusedAdamW(plain), batch, pre_step=rounding)
 
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     try:

@@ -184,7 +184,7 @@ def test_implicit_conv(dev, Cin, Cout, k, st, pad, H, W, dt):
     sk = K.query("cmx_gemm_splitk", G, M, Cout, k * k * Cin, 0, 1)
     ws = K._ws(K.query("cmx_gemm_workspace", G, M, Cout, sk), dev) if sk > 1 else None
     K.call("cmx_conv_implicit_fwd", K.ptr(x), K.ptr(Wt), K.ptr(y), K.ptr(b), K.ptr(ws), G, NIg, H, W, Cin, k, k, st,
-           pad, Ho, Wo, Cout, NIg * H * W * Cin, Wt[0].numel(), y.stride(0), Cout, sk, 1, K.stream())
+           pad, Ho, Wo, Cout, NIg * H * W * Cin, Wt[0].numel(), y.stride(0), Cout, sk, K.dtype_code(x), K.stream())
     xr = x.float().view(G, NIg, H, W, Cin).permute(0, 1, 4, 2, 3)
     for g in range(G):
         ref = F.conv2d(xr[g], Wt[g].float().permute(0, 3, 1, 2), b[g], stride=st, padding=pad)   # (NIg, Cout, Ho, Wo)

@@ -57,12 +57,17 @@ def sra_ref(q, kv, heads, D):
                                               (1, 65, 80, 8, 32),
                                               # Nk > 320: the fast forward streams keys in
                                               # LDS-sized chunks (B5 1024 x 1024: Nk = 1024)
-                                              (2, 700, 1024, 2, 64), (1, 333, 650, 1, 64)])
-def test_sra_attention(dev, dtype, Bt, N, Nk, heads, D):
+                                              (2, 700, 1024, 2, 64), (1, 333, 650, 1, 64),
+                                              # short sequences (sra_*_small: keys split over waves):
+                                              # ragged query / key tiles, one-wave and five-wave key
+                                              # splits, the N threshold; N = 4800 stays on the fast path
+                                              (3, 333, 70, 2, 64), (2, 129, 257, 3, 64), (1, 2048, 320, 1, 64),
+                                              (2, 4800, 300, 2, 64), (1, 37, 33, 1, 64)])
+def test_sra_attention(dev, dtype, Bt, N, Nk, heads, D, qmul=1.0):
     from rgbx_semantic_segmentation_amd import kernels as K
     torch.manual_seed(1)
     C = heads * D
-    q = torch.randn(Bt, N, C, dtype=torch.float64)
+    q = torch.randn(Bt, N, C, dtype=torch.float64) * qmul
     kv = torch.randn(Bt, Nk, 2 * C, dtype=torch.float64)
     do = torch.randn(Bt, N, C, dtype=torch.float64)
     qr = q.clone().requires_grad_(True); kvr = kv.clone().requires_grad_(True)
@@ -178,3 +183,12 @@ def test_batchnorm(dev, dtype, M, C, rps, act, use_res, use_ds, training):
         assert relerr(dres, rr.grad) < tol
     if training:
         assert relerr(rm, rmr) < 1e-4 and relerr(rv, rvr) < 1e-4
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("Bt,N,Nk,heads", [(2, 300, 300, 4), (1, 1200, 300, 5), (1, 4800, 300, 2)])
+def test_sra_attention_peaked(dev, dtype, Bt, N, Nk, heads):
+    """Sharply peaked softmax (q x 6): the per-wave maxima of the short-sequence kernels differ by
+    tens of units, so the cross-wave rescale of the partial outputs decides the result; also the
+    fast kernels' online-softmax rescale (rule 26 of the programming guide: force the branch)."""
+    test_sra_attention(dev, dtype, Bt, N, Nk, heads, 64, qmul=6.0)
