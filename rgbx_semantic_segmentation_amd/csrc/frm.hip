@@ -88,20 +88,22 @@ __global__ __launch_bounds__(256) void pool_partial_kernel(const T* __restrict__
   }
 }
 
-// block = 64 channels x 4 chunk slices of one (group, image); the slices meet in LDS.  Max ties
-// resolve to the lowest token index, as the sequential scan over chunks would.
+// block = 16 channels x 16 chunk slices of one (group, image); the slices meet in LDS.  Max ties
+// resolve to the lowest token index, as the sequential scan over chunks would.  (A 64-channel x
+// 4-slice block walked its 128 chunk partials as a 32-step chain of dependent L2 loads: 12 us.)
+constexpr int PF_CH = 16, PF_SL = 16;
 __global__ __launch_bounds__(256) void pool_final_kernel(const float* __restrict__ psum, const float* __restrict__ pmax,
                                                          const int* __restrict__ pidx, float* __restrict__ pooled,
                                                          int* __restrict__ argmax, int B, int N, int C, int nchunk) {
-  __shared__ float rs[3][64], rm[3][64];
-  __shared__ int ri[3][64];
-  const int gb = blockIdx.y, cl = threadIdx.x & 63, zl = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  __shared__ float rs[PF_SL][PF_CH], rm[PF_SL][PF_CH];
+  __shared__ int ri[PF_SL][PF_CH];
+  const int gb = blockIdx.y, cl = threadIdx.x % PF_CH, zl = threadIdx.x / PF_CH;
+  const int c = blockIdx.x * PF_CH + cl;
   float sm = 0.f, m = -INFINITY;
   int mi = 0x7fffffff;
   if (c < C) {
 #pragma unroll 4
-    for (int k = zl; k < nchunk; k += 4) {
+    for (int k = zl; k < nchunk; k += PF_SL) {
       const long o = ((long)gb * nchunk + k) * C + c;
       sm += psum[o];
       const float v = pmax[o];
@@ -109,11 +111,10 @@ __global__ __launch_bounds__(256) void pool_final_kernel(const float* __restrict
       if (v > m || (v == m && ix < mi)) { m = v; mi = ix; }
     }
   }
-  if (zl > 0) { rs[zl - 1][cl] = sm; rm[zl - 1][cl] = m; ri[zl - 1][cl] = mi; }
+  rs[zl][cl] = sm; rm[zl][cl] = m; ri[zl][cl] = mi;
   __syncthreads();
   if (zl > 0 || c >= C) return;
-#pragma unroll
-  for (int q = 0; q < 3; ++q) {
+  for (int q = 1; q < PF_SL; ++q) {
     sm += rs[q][cl];
     const float v = rm[q][cl];
     const int ix = ri[q][cl];
@@ -548,8 +549,8 @@ int cmx_frm_pool_fwd(const void* x, float* pooled, int* argmax, float* workspace
     FRM_TPR_DISPATCH(tpr, TPR, hipLaunchKernelGGL((pool_partial_kernel<T, TPR>), dim3(nc, 2 * B), dim3(256), 0, s,
                                                   (const T*)x, psum, pmax, pidx, B, N, C, chunk));
   });
-  hipLaunchKernelGGL(pool_final_kernel, dim3(cdiv(C, 64), 2 * B), dim3(256), 0, s, psum, pmax, pidx, pooled, argmax,
-                     B, N, C, nc);
+  hipLaunchKernelGGL(pool_final_kernel, dim3(cdiv(C, PF_CH), 2 * B), dim3(256), 0, s, psum, pmax, pidx, pooled,
+                     argmax, B, N, C, nc);
   return cmx_check_launch("frm_pool_fwd");
 }
 

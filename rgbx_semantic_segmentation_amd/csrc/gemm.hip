@@ -61,6 +61,10 @@ struct GemmArgs {
   // column j = (kh, kw, c) of an scR x scR patch of scC channels -> C pixel (n, oy*scR + kh,
   // ox*scR + kw) of an scH x scW NHWC image (col2im of a non-overlapping patchify conv)
   int scatter, scH, scW, scC, scR, scHo, scWo;
+  // direct = 1: the 16-bit fast path stores its tile straight from the accumulators (4 columns
+  // = 8 B per lane and register group) instead of through the fp32 LDS image (set by the host
+  // for plain-layout 16-bit outputs without split-K, k-groups or upsample / scatter epilogues)
+  int direct;
 };
 
 // block id -> tile id, giving each of the 8 XCDs (hardware deals block b to XCD b % 8) a
@@ -477,6 +481,49 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
     wait_keep(ahead - 1);
     __syncthreads();
     cur = cur + 1 == NS ? 0 : cur + 1;
+  }
+
+  if (KW == 1 && p.direct) {
+    // direct epilogue: lane (r, h) holds C(i = r, j = accrow(q, h)) of each 32 x 32 sub-tile;
+    // registers 4 g4 .. 4 g4 + 3 are the 4 consecutive columns 8 g4 + 4 h + (0..3)
+    const int r = lane & 31, h = lane >> 5;
+    if (do_db && h == 0) {
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+        const int i = i0 + wm * (BM / 2) + a * 32 + r;
+        if (i < p.M) dbias_store(p, g, i, accd[a][0]);
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      const int i = i0 + wm * (BM / 2) + a * 32 + r;
+      if (i >= p.M) continue;
+      const float sc = (p.R && p.rscale) ? p.rscale[((long)g * p.M + i) / p.rows_per_sample] : 1.f;
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int j = j0 + wn * (BN / 2) + b * 32 + 8 * g4 + 4 * h;
+          if (j >= nreal) continue;
+          float v[4] = {acc[a][b][4 * g4], acc[a][b][4 * g4 + 1], acc[a][b][4 * g4 + 2], acc[a][b][4 * g4 + 3]};
+          if (p.bias) {
+            const float4 bv = *reinterpret_cast<const float4*>(p.bias + (long)g * p.sbias + j);
+            v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
+          }
+          if (p.act) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = act_fwd(v[e], p.act);
+          }
+          const long off = (long)g * p.sC + (long)i * p.ldc + j;
+          if (p.R) {
+            const uint2 rv = *reinterpret_cast<const uint2*>(reinterpret_cast<const E*>(p.R) + off);
+            const cmx_f2 r0 = unpack2<E>(rv.x), r1 = unpack2<E>(rv.y);
+            v[0] = r0.x + sc * v[0]; v[1] = r0.y + sc * v[1]; v[2] = r1.x + sc * v[2]; v[3] = r1.y + sc * v[3];
+          }
+          *reinterpret_cast<uint2*>(reinterpret_cast<E*>(p.C) + off) = make_uint2(pack2<E>(v[0], v[1]), pack2<E>(v[2], v[3]));
+        }
+    }
+    return;
   }
 
   // epilogue through LDS.  acc[a][b] holds C^T (B fragment fed as the MFMA's A operand), so
@@ -1151,6 +1198,11 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
   a.kt_per_split = (nk + splitk - 1) / splitk;
   splitk = (nk + a.kt_per_split - 1) / a.kt_per_split;      // no empty splits
   a.nsplit = splitk;
+  // CMX_GEMM_DIRECT=1: register epilogue for plain 16-bit outputs (A/B switch, default off)
+  static const int direct_env = [] { const char* e = getenv("CMX_GEMM_DIRECT"); return e ? atoi(e) : 0; }();
+  a.direct = direct_env && fast && splitk == 1 && out_mode == 0 && !ones_col && !a.nup && !a.scatter && nb % 4 == 0 &&
+             ldc % 4 == 0 && sC % 4 == 0 && ((uintptr_t)C & 7) == 0 && (!R || ((uintptr_t)R & 7) == 0) &&
+             (!bias || (sbias % 4 == 0 && ((uintptr_t)bias & 15) == 0));
   if (fast) {
     int bm, bn;
     plan_tiles(G, M, nb, K, &bm, &bn);
