@@ -99,13 +99,14 @@ int cmx_col2im_nhwc(const void* cols, void* dx, int NI, int H, int W, int C, int
 
 /* ---- FFM cross attention (CrossAttention.forward, net_utils.py:199-214):
  *      ctx = softmax_{-2}(k^T v * scale) per (g, b, head); out_1 = q_1 ctx_2, out_2 = q_2 ctx_1.
- *      The token contractions are batched cmx_gemm calls over (g, b) with C x C operands; these
- *      two kernels sit between them.  kv / dbd: (G*B, C, C) fp32 GEMM results (k^T v, u^T dout);
- *      ctx (G*B, heads, D, D) fp32; bdt / da: (G*B, C, C) block-diagonal operands in the compute
- *      dtype, bdt[(1-g)*B + b][h*D + j][h*D + i] = ctx_{g,b,h}[i][j] (crossed, transposed),
- *      da[g*B + b][h*D + i][h*D + j] = scale * softmax_bwd (zeros off the diagonal blocks). */
-int cmx_ffm_ctx_fwd(const float* kv, float* ctx, void* bdt, int G, int B, int heads, int D, float scale, int dtype, hipStream_t stream);
-int cmx_ffm_ctx_bwd(const float* ctx, const float* dbd, void* da, int G, int B, int heads, int D, float scale, int dtype, hipStream_t stream);
+ *      The token contractions are per-head cmx_gemm_h2 calls over (g, b, head) (d x d products,
+ *      the reference's MACs); these two kernels sit between them.  Every array is
+ *      (G*B, heads, D, D): kv / dctx fp32 GEMM results (k^T v, u^T dout), ctx fp32 (saved);
+ *      ctxT[(1-g)*B + b][h][j][i] = ctx_{g,b,h}[i][j] (crossed, transposed) and
+ *      da[g*B + b][h][i][j] = scale * softmax_bwd in the compute dtype; dctx is filed under the
+ *      modality that consumed the context. */
+int cmx_ffm_ctx_fwd(const float* kv, float* ctx, void* ctxT, int G, int B, int heads, int D, float scale, int dtype, hipStream_t stream);
+int cmx_ffm_ctx_bwd(const float* ctx, const float* dctx, void* da, int G, int B, int heads, int D, float scale, int dtype, hipStream_t stream);
 
 /* ---- CM-FRM (FeatureRectifyModule, net_utils.py:124-152): ChannelWeights pooling (:22-27)
  *      + tiny-M MLP (:16-20), SpatialWeights 1x1 C->2 + sigmoid (:74-83), rectification. */
@@ -175,6 +176,11 @@ int cmx_upsample_ce_bwd(const void* logits, const int64_t* label, const float* d
 size_t cmx_gemm_workspace(int G, int M, int N, int splitk);
 int cmx_gemm_splitk(int G, int M, int N, int K, int ones_col, int dtype);
 int cmx_gemm(const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R, const float* rscale, float* dbias, float* workspace, int G, int M, int N, int K, int K1, int64_t lda, int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias, int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode, int ones_col, int splitk, int dtype, hipStream_t stream);
+/* cmx_gemm_h2: cmx_gemm (no A2 / bias / residual / epilogue extras) over a two-level batch of G = Go * gh
+ *      problems: problem g reads / writes at (g / gh) * sX + (g % gh) * sXh -- the per-head k^T v,
+ *      u @ ctx and their backward products of the FFM cross attention (net_utils.py:206-212), one
+ *      (image x modality, head) pair per problem. */
+int cmx_gemm_h2(const void* A, const void* B, void* C, float* workspace, int G, int gh, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t sA, int64_t sAh, int64_t sB, int64_t sBh, int64_t sC, int64_t sCh, int transA, int transB, int out_mode, int splitk, int dtype, hipStream_t stream);
 
 /* ---- grouped (deferred) launches: the weight gradients of a backward segment in ONE GEMM
  *      launch and every partial-sum reduction (split-K slabs, LayerNorm dgamma/dbeta, DWConv

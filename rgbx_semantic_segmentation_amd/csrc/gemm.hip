@@ -61,6 +61,11 @@ struct GemmArgs {
   // column j = (kh, kw, c) of an scR x scR patch of scC channels -> C pixel (n, oy*scR + kh,
   // ox*scR + kw) of an scH x scW NHWC image (col2im of a non-overlapping patchify conv)
   int scatter, scH, scW, scC, scR, scHo, scWo;
+  // two-level batch (cmx_gemm_h2): batch g = (g / gh, g % gh), operand offset
+  // (g / gh) * sX + (g % gh) * sXh -- e.g. (image, head) pairs of per-head products; gh = 1:
+  // the plain stride g * sX
+  int gh;
+  long sAh, sBh, sCh;
   // direct = 1: the 16-bit fast path stores its tile straight from the accumulators (4 columns
   // = 8 B per lane and register group) instead of through the fp32 LDS image (set by the host
   // for plain-layout 16-bit outputs without split-K, k-groups or upsample / scatter epilogues)
@@ -136,6 +141,10 @@ __device__ __forceinline__ void up_add8(const GemmArgs& p, int i, int j, float* 
   }
 }
 
+__device__ __forceinline__ long goff(const GemmArgs& p, int g, long s, long sh) {
+  return p.gh > 1 ? (long)(g / p.gh) * s + (long)(g % p.gh) * sh : (long)g * s;
+}
+
 // element offset of C(g, i, j) under the patch scatter
 __device__ __forceinline__ long scatter_offset(const GemmArgs& p, int g, int i, int j) {
   const int hw = p.scHo * p.scWo;
@@ -150,7 +159,7 @@ __device__ __forceinline__ long c_offset(const GemmArgs& p, int g, int i, int j)
   if constexpr (EXT) {
     if (p.scatter) return scatter_offset(p, g, i, j);
   }
-  return (long)g * p.sC + (long)i * p.ldc + j;
+  return goff(p, g, p.sC, p.sCh) + (long)i * p.ldc + j;
 }
 
 // per-element epilogue of the generic (register-staged) kernel; the upsample-add and scatter
@@ -327,9 +336,9 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
   const int ntile = p.tiles_m * p.tiles_n;
   const int t = lin % ntile, g = (lin / ntile) % p.G, z = lin / (ntile * p.G);
   const int tm = t / p.tiles_n, tn = t % p.tiles_n;
-  const E* Ag = reinterpret_cast<const E*>(p.A) + (long)g * p.sA;
+  const E* Ag = reinterpret_cast<const E*>(p.A) + goff(p, g, p.sA, p.sAh);
   const E* A2g = p.A2 ? reinterpret_cast<const E*>(p.A2) + (long)g * p.sA2 : Ag;
-  const E* Bg = reinterpret_cast<const E*>(p.B) + (long)g * p.sB;
+  const E* Bg = reinterpret_cast<const E*>(p.B) + goff(p, g, p.sB, p.sBh);
   const i32x4 rA = make_rsrc(Ag), rA2 = make_rsrc(A2g), rB = make_rsrc(Bg);
   const int i0 = tm * BM, j0 = tn * BN;
   const int nreal = p.ones_col ? p.N - 1 : p.N;
@@ -514,7 +523,7 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = act_fwd(v[e], p.act);
           }
-          const long off = (long)g * p.sC + (long)i * p.ldc + j;
+          const long off = goff(p, g, p.sC, p.sCh) + (long)i * p.ldc + j;
           if (p.R) {
             const uint2 rv = *reinterpret_cast<const uint2*>(reinterpret_cast<const E*>(p.R) + off);
             const cmx_f2 r0 = unpack2<E>(rv.x), r1 = unpack2<E>(rv.y);
@@ -787,9 +796,9 @@ __global__ __launch_bounds__(256) void gemm_generic_kernel(const GemmArgs p) {
   const int t = xcd_tile(blockIdx.x, p.tiles_m * p.tiles_n);
   const int tm = t / p.tiles_n, tn = t % p.tiles_n;
   const int g = blockIdx.y, z = blockIdx.z;
-  const T* Ag = reinterpret_cast<const T*>(p.A) + (long)g * p.sA;
+  const T* Ag = reinterpret_cast<const T*>(p.A) + goff(p, g, p.sA, p.sAh);
   const T* A2g = p.A2 ? reinterpret_cast<const T*>(p.A2) + (long)g * p.sA2 : nullptr;
-  const T* Bg = reinterpret_cast<const T*>(p.B) + (long)g * p.sB;
+  const T* Bg = reinterpret_cast<const T*>(p.B) + goff(p, g, p.sB, p.sBh);
   const int i0 = tm * BM, j0 = tn * BN;
   const int nreal = p.ones_col ? p.N - 1 : p.N;     // real B rows (the ones row is virtual)
   const int ones_row = p.ones_col ? p.N - 1 : -1;
@@ -1145,7 +1154,7 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
               int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias,
               int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode, int ones_col, int splitk,
               int dtype, hipStream_t s, const UpSpec* up, int scR = 0, int scH = 0, int scW = 0, int scC = 0,
-              int scHo = 0, int scWo = 0) {
+              int scHo = 0, int scWo = 0, int gh = 1, int64_t sAh = 0, int64_t sBh = 0, int64_t sCh = 0) {
   CMX_REQUIRE(G > 0 && M > 0 && N > 0 && K > 0, CMX_ERR_SHAPE, "gemm: empty problem G=%d M=%d N=%d K=%d", G, M, N, K);
   CMX_REQUIRE(dtype >= 0 && dtype <= 2, CMX_ERR_DTYPE, "gemm: unsupported dtype %d", dtype);
   CMX_REQUIRE(out_mode >= 0 && out_mode <= 2 && act >= 0 && act <= 3, CMX_ERR_ARG, "gemm: out_mode/act");
@@ -1157,7 +1166,8 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
   CMX_REQUIRE(!ones_col || (transB && dbias && N >= 2 && out_mode != 0 && !bias && !R && act == 0), CMX_ERR_ARG,
               "gemm: ones_col (bias gradient) needs transB, dbias, fp32 output and no epilogue");
   CMX_REQUIRE((long)M * N < (1L << 31) && (long)M * K < (1L << 40), CMX_ERR_SHAPE, "gemm: problem too large");
-  const bool fast = dtype != 0 && fast_ok(A, A2, B, M, N, K, K1, lda, lda2, ldb, sA, sA2, sB, transA, transB, ones_col);
+  const bool fast = dtype != 0 && fast_ok(A, A2, B, M, N, K, K1, lda, lda2, ldb, sA, sA2, sB, transA, transB, ones_col) &&
+                    sAh % 8 == 0 && sBh % 8 == 0;
   const int V = dtype == 0 ? 4 : 8;
   const int nb = ones_col ? N - 1 : N;
   const bool vec = (transA ? M : K) % V == 0 && (transB ? nb : K) % V == 0 && (K - K1) % V == 0 && (K1 == K || K1 % V == 0) &&
@@ -1176,6 +1186,10 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
            (!R || (uintptr_t)R % 16 == 0);
   a.lda = lda; a.lda2 = lda2; a.ldb = ldb; a.ldc = ldc; a.sA = sA; a.sA2 = sA2; a.sB = sB; a.sC = sC;
   a.sbias = sbias; a.sdb = sdb;
+  CMX_REQUIRE(gh >= 1 && (gh == 1 || (G % gh == 0 && !A2 && !bias && !R && !ones_col && !(up && up->n) && !scR)),
+              CMX_ERR_ARG, "gemm: a two-level batch (gh=%d) takes G %% gh == 0 and no A2 / bias / residual / "
+              "bias-gradient / upsample / scatter", gh);
+  a.gh = gh; a.sAh = sAh; a.sBh = sBh; a.sCh = sCh;
   if (up && up->n > 0) {
     CMX_REQUIRE(up->n <= 3 && G == 1 && !ones_col && N % 8 == 0 && (long)up->oH * up->oW > 0 &&
                 M % (up->oH * up->oW) == 0, CMX_ERR_ARG, "gemm: upsample-add epilogue needs G = 1, N %% 8 == 0 and "
@@ -1256,6 +1270,17 @@ int cmx_gemm(const void* A, const void* A2, const void* B, void* C, const float*
 // so there is no overlap to sum).  dy (G, NIg*Ho*Wo, N), W (G, N, R*R*C) tap-major, dx
 // (G*NIg, H, W, C) NHWC.  Pixels outside the Ho*R x Wo*R window (H or W not a multiple of R)
 // are not written: the caller zeroes dx for such shapes.
+// cmx_gemm over a two-level batch: G = Go * gh problems, problem g = (g / gh, g % gh) at operand
+// offsets (g / gh) * sX + (g % gh) * sXh (per-head products of the FFM cross attention:
+// net_utils.py:206-212, (image x modality, head) pairs with the heads a column slice of a row)
+int cmx_gemm_h2(const void* A, const void* B, void* C, float* workspace, int G, int gh, int M, int N, int K,
+                int64_t lda, int64_t ldb, int64_t ldc, int64_t sA, int64_t sAh, int64_t sB, int64_t sBh, int64_t sC,
+                int64_t sCh, int transA, int transB, int out_mode, int splitk, int dtype, hipStream_t s) {
+  return gemm_impl(A, nullptr, B, C, nullptr, nullptr, nullptr, nullptr, workspace, G, M, N, K, K, lda, 0, ldb, ldc, sA,
+                   0, sB, sC, 0, 0, 1, transA, transB, 0, out_mode, 0, splitk, dtype, s, nullptr, 0, 0, 0, 0, 0, 0, gh,
+                   sAh, sBh, sCh);
+}
+
 int cmx_conv_patch_dgrad(const void* dy, const void* Wt, void* dx, int G, int NIg, int H, int Wd, int C, int R, int Ho,
                          int Wo, int N, int64_t sdy, int64_t sW, int64_t sdx, int dtype, hipStream_t s) {
   CMX_REQUIRE(G > 0 && NIg > 0 && C % 8 == 0 && R > 0 && Ho == H / R && Wo == Wd / R && Ho > 0 && Wo > 0, CMX_ERR_SHAPE,

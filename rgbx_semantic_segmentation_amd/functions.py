@@ -609,43 +609,53 @@ def conv(store, mod, x, G, NI, H, W, C, stride, pad, nchw=False):
 
 
 # ---------------------------------------------------------------------------- FFM cross attention
+def _heads(t, GB, N, heads, D, off=0):
+    """(G, M, W) token rows (unit column stride, rows of stride rs, G * M rows evenly spaced)
+    -> the (GB, heads, N, D) view of columns [off + h*D, off + (h+1)*D): one (image, head) pair
+    per leading index, no copy."""
+    G, M, W = t.shape
+    rs = t.stride(1)
+    assert t.stride(2) == 1 and t.stride(0) == M * rs and M == (GB // G) * N, (t.shape, t.stride(), GB, N)
+    return t.as_strided((GB, heads, N, D), (N * rs, D, rs, 1), t.storage_offset() + off)
+
+
 def _cross_attn_fwd(u, kv, B, N, heads, D):
     """CrossAttention forward (net_utils.py:199-214) on grouped tensors: u (G=2, M, C) is the
     query (raw, no projection), kv (2, M, 2C) = [k | v]; ctx_g = softmax_{-2}(k_g^T v_g * s),
-    out_g = u_g @ ctx_{1-g}.  Every token contraction is a batched MFMA GEMM over the G * B
-    (modality, image) pairs with K = C (csrc/ffm_attn.hip explains the block-diagonal
-    operands): KV = k^T v (fp32), the softmax + crossing kernel, out = u @ BDt^T."""
+    out_g = u_g @ ctx_{1-g}.  Every token contraction is a per-head MFMA GEMM over the
+    (modality, image, head) triples (kernels.gemm_h2: the reference's d x d products, no
+    block-diagonal padding): KV = k^T v (fp32), the softmax + crossing kernel, out = u @ ctx."""
     G, M, C = u.shape
     GB = G * B
-    kvb = kv.view(GB, N, 2 * C)
-    k, v = kvb[..., :C], kvb[..., C:]
-    KV = torch.empty(GB, C, C, dtype=torch.float32, device=u.device)
-    K.gemm(k.transpose(1, 2), v.transpose(1, 2), KV, out_mode=1)            # k^T v per (g, b)
+    kh, vh = _heads(kv, GB, N, heads, D), _heads(kv, GB, N, heads, D, C)        # (GB, h, N, D)
+    KV = torch.empty(GB, heads, D, D, dtype=torch.float32, device=u.device)
+    K.gemm_h2(kh.transpose(2, 3), vh.transpose(2, 3), KV, out_mode=1)          # k_h^T v_h
     P = torch.empty(GB, heads, D, D, dtype=torch.float32, device=u.device)
-    bdt = torch.empty(GB, C, C, dtype=u.dtype, device=u.device)
-    K.call("cmx_ffm_ctx_fwd", K.ptr(KV), K.ptr(P), K.ptr(bdt), G, B, heads, D, D ** -0.5, K.dtype_code(u), K.stream())
+    ctxT = torch.empty(GB, heads, D, D, dtype=u.dtype, device=u.device)
+    K.call("cmx_ffm_ctx_fwd", K.ptr(KV), K.ptr(P), K.ptr(ctxT), G, B, heads, D, D ** -0.5, K.dtype_code(u), K.stream())
     out = torch.empty(G, M, C, dtype=u.dtype, device=u.device)
-    K.gemm(u.view(GB, N, C), bdt, out.view(GB, N, C))                      # u_g @ ctx_{1-g} per head
-    return out, P, bdt
+    K.gemm_h2(_heads(u, GB, N, heads, D), ctxT, _heads(out, GB, N, heads, D))  # u_h @ ctx_h (crossed)
+    return out, P, ctxT
 
 
-def _cross_attn_bwd(dout, u, kv, P, bdt, B, N, heads, D, du):
-    """Backward of _cross_attn_fwd: du = dout @ BD written into ``du`` (any row stride),
-    dBD = u^T dout, the softmax-backward kernel, dk = v @ dA^T and dv = k @ dA into the halves
-    of the returned dkv."""
+def _cross_attn_bwd(dout, u, kv, P, ctxT, B, N, heads, D, du):
+    """Backward of _cross_attn_fwd: du = dout @ ctx^T written into ``du`` (any row stride),
+    dctx = u^T dout, the softmax-backward kernel, dk = v @ dA^T and dv = k @ dA into the halves
+    of the returned dkv -- per head, like the forward."""
     G, M, C = u.shape
     GB = G * B
-    dout = _c(dout).view(GB, N, C)
-    K.gemm(dout, bdt.transpose(1, 2), du.view(GB, N, C))                   # dout @ BD
-    dBD = torch.empty(GB, C, C, dtype=torch.float32, device=u.device)
-    K.gemm(u.view(GB, N, C).transpose(1, 2), dout.transpose(1, 2), dBD, out_mode=1)      # u^T dout
-    dA = torch.empty(GB, C, C, dtype=u.dtype, device=u.device)
-    K.call("cmx_ffm_ctx_bwd", K.ptr(P), K.ptr(dBD), K.ptr(dA), G, B, heads, D, D ** -0.5, K.dtype_code(u), K.stream())
-    kvb = kv.view(GB, N, 2 * C)
+    dout = _c(dout)
+    doh = _heads(dout, GB, N, heads, D)
+    K.gemm_h2(doh, ctxT.transpose(2, 3), _heads(du, GB, N, heads, D))             # dout_h @ ctx_h^T
+    dctx = torch.empty(GB, heads, D, D, dtype=torch.float32, device=u.device)
+    K.gemm_h2(_heads(u, GB, N, heads, D).transpose(2, 3), doh.transpose(2, 3), dctx, out_mode=1)   # u_h^T dout_h
+    dA = torch.empty(GB, heads, D, D, dtype=u.dtype, device=u.device)
+    K.call("cmx_ffm_ctx_bwd", K.ptr(P), K.ptr(dctx), K.ptr(dA), G, B, heads, D, D ** -0.5, K.dtype_code(u),
+           K.stream())
     dkv = torch.empty(G, M, 2 * C, dtype=kv.dtype, device=kv.device)
-    dkvb = dkv.view(GB, N, 2 * C)
-    K.gemm(kvb[..., C:], dA, dkvb[..., :C])                                # dk = v dA^T
-    K.gemm(kvb[..., :C], dA.transpose(1, 2), dkvb[..., C:])                # dv = k dA
+    kh, vh = _heads(kv, GB, N, heads, D), _heads(kv, GB, N, heads, D, C)
+    K.gemm_h2(vh, dA, _heads(dkv, GB, N, heads, D))                            # dk_h = v_h dA_h^T
+    K.gemm_h2(kh, dA.transpose(2, 3), _heads(dkv, GB, N, heads, D, C))         # dv_h = k_h dA_h
     return dkv
 
 
@@ -655,17 +665,17 @@ class CrossAttentionF(Function):
 
     @staticmethod
     def forward(ctx, u, kv, B, N, heads, D):
-        out, P, bdt = _cross_attn_fwd(u, kv, B, N, heads, D)
-        ctx.save_for_backward(u, kv, P, bdt)
+        out, P, ctxT = _cross_attn_fwd(u, kv, B, N, heads, D)
+        ctx.save_for_backward(u, kv, P, ctxT)
         ctx.meta = (B, N, heads, D)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        u, kv, P, bdt = ctx.saved_tensors
+        u, kv, P, ctxT = ctx.saved_tensors
         B, N, heads, D = ctx.meta
         du = torch.empty_like(u)
-        dkv = _cross_attn_bwd(dout, u, kv, P, bdt, B, N, heads, D, du)
+        dkv = _cross_attn_bwd(dout, u, kv, P, ctxT, B, N, heads, D, du)
         return du, dkv, None, None, None, None
 
 
@@ -700,16 +710,16 @@ class CrossPathF(Function):
         y, u = a[..., :C], a[..., C:]
         kv = torch.empty(G, M, 2 * C, dtype=x.dtype, device=x.device)
         _fwd_gemm(u, Wkv, None, kv)
-        v, P, bdt = _cross_attn_fwd(u, kv, B, N, heads, D)
+        v, P, ctxT = _cross_attn_fwd(u, kv, B, N, heads, D)
         e = torch.empty(G, M, C, dtype=x.dtype, device=x.device)
         _fwd_gemm(y, Wend, bend, e, res=x, x2=v)
-        ctx.save_for_backward(x, a, kv, v, P, bdt, Wcp, Wkv, Wend)
+        ctx.save_for_backward(x, a, kv, v, P, ctxT, Wcp, Wkv, Wend)
         ctx.meta = (Wgcp, bgcp, Wgkv, Wgend, bgend, B, N, heads, D)
         return e
 
     @staticmethod
     def backward(ctx, de):
-        x, a, kv, v, P, bdt, Wcp, Wkv, Wend = ctx.saved_tensors
+        x, a, kv, v, P, ctxT, Wcp, Wkv, Wend = ctx.saved_tensors
         Wgcp, bgcp, Wgkv, Wgend, bgend, B, N, heads, D = ctx.meta
         G, M, C = x.shape
         de = _c(de)
@@ -721,8 +731,8 @@ class CrossPathF(Function):
         dv = _dgrad(de, Wend[:, :, C:], torch.empty_like(v))
         _wgrad_into(de, y, Wgend[:, :, :C], bgend)
         _wgrad_into(de, v, Wgend[:, :, C:])
-        # attention: du (second half of da) = dout @ BD, then += dkv @ Wkv (kv's dgrad, in place)
-        dkv = _cross_attn_bwd(dv, u, kv, P, bdt, B, N, heads, D, du)
+        # attention: du (second half of da) = dout @ ctx^T per head, then += dkv @ Wkv (kv's dgrad)
+        dkv = _cross_attn_bwd(dv, u, kv, P, ctxT, B, N, heads, D, du)
         K.gemm(dkv, Wkv.transpose(1, 2), du, residual=du)
         _wgrad_into(dkv, u, Wgkv)
         # channel_proj + ReLU: dx = relu'(a) * da @ Wcp + de (residual epilogue)

@@ -151,6 +151,33 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, bias: torch.Tensor |
     return C
 
 
+def gemm_h2(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, out_mode: int = 0, splitk: int = 0) -> torch.Tensor:
+    """C[o, h] = A[o, h] @ B[o, h]^T over a two-level batch of logical 4-D views A (Go, gh, M, K),
+    B (Go, gh, N, K), C (Go, gh, M, N) (cmx_gemm_h2): e.g. per-head products whose heads are
+    column slices of token rows, so the (image, head) pairs have no single batch stride."""
+    Go, gh, M, K = A.shape
+    N = B.shape[2]
+    assert B.shape == (Go, gh, N, K) and C.shape == (Go, gh, M, N) and C.stride(3) == 1, (A.shape, B.shape, C.shape)
+    assert A.dtype == B.dtype and C.dtype == (A.dtype if out_mode == 0 else torch.float32), (A.dtype, C.dtype)
+
+    def op(t, name):
+        if t.stride(3) == 1:
+            return 0, t.stride(2)
+        if t.stride(2) == 1:
+            return 1, t.stride(3)
+        raise ValueError(f"gemm_h2: operand {name} needs a unit stride along rows or k, got {t.stride()}")
+    tA, lda = op(A, "A")
+    tB, ldb = op(B, "B")
+    G = Go * gh
+    if splitk <= 0:
+        splitk = query("cmx_gemm_splitk", G, M, N, K, 0, dtype_code(A))
+    ws = _ws(query("cmx_gemm_workspace", G, M, N, splitk), A.device) if splitk > 1 else None
+    call("cmx_gemm_h2", ptr(A), ptr(B), ptr(C), ptr(ws), G, gh, M, N, K, lda, ldb, C.stride(2), A.stride(0),
+         A.stride(1), B.stride(0), B.stride(1), C.stride(0), C.stride(1), tA, tB, int(out_mode), int(splitk),
+         dtype_code(A), stream())
+    return C
+
+
 # ------------------------------------------------------------------------------ SRA attention
 def sra_attn_fwd(q, k, v, Bt, N, Nk, heads, D, scale, qs, kvs, save_lse=True):
     """q: base pointer tensor of (Bt, N, *) rows with stride qs; k/v: views into the kv

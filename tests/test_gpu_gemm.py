@@ -205,3 +205,28 @@ def test_implicit_conv(dev, Cin, Cout, k, st, pad, H, W, dt):
         ref_w = wr.grad.permute(0, 2, 3, 1).reshape(Cout, -1)
         assert rel(Wg[g], ref_w) < 1e-2, rel(Wg[g], ref_w)
         assert rel(bg[g], dy[g].float().sum(0)) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("GB,heads,N,D", [(4, 2, 4800, 64), (4, 5, 1200, 64), (2, 8, 300, 64), (4, 1, 333, 32)])
+def test_gemm_h2_per_head(dev, dtype, GB, heads, N, D):
+    """cmx_gemm_h2 (two-level batch) on the FFM cross attention's per-head views: the heads are
+    column slices of token rows (net_utils.py:206-212).  k_h^T v_h (fp32 out, split-K over tokens)
+    and u_h @ ctx_h into a strided output slice, against torch on the same views."""
+    from rgbx_semantic_segmentation_amd import kernels as Kn
+    from rgbx_semantic_segmentation_amd.functions import _heads
+    torch.manual_seed(7)
+    C = heads * D
+    kv = torch.randn(2, GB // 2 * N, 2 * C, device=dev).to(dtype)
+    kh, vh = _heads(kv, GB, N, heads, D), _heads(kv, GB, N, heads, D, C)
+    KV = torch.empty(GB, heads, D, D, device=dev)
+    Kn.gemm_h2(kh.transpose(2, 3), vh.transpose(2, 3), KV, out_mode=1)
+    ref = kh.float().transpose(2, 3) @ vh.float()
+    assert rel(KV, ref) < (1e-5 if dtype == torch.float32 else 2e-3), rel(KV, ref)
+    ctxT = torch.randn(GB, heads, D, D, device=dev).to(dtype)
+    wide = torch.zeros(2, GB // 2 * N, 2 * C, device=dev, dtype=dtype)      # output: second half of wider rows
+    out = _heads(wide[..., C:], GB, N, heads, D)
+    Kn.gemm_h2(kh, ctxT, out)
+    ref = kh.float() @ ctxT.float().transpose(2, 3)
+    assert rel(out, ref) < (1e-5 if dtype == torch.float32 else 1e-2), rel(out, ref)
+    assert not wide[..., :C].abs().any()                                     # the other half untouched
