@@ -34,6 +34,12 @@ int cmx_abi_version(void);
 const char* cmx_last_error(void);
 /* pinned host -> device copy of a packed record table on `stream` (see grouped launches) */
 int cmx_upload(void* dst, const void* src, size_t nbytes, hipStream_t stream);
+/* launch-policy knobs (GEMM_TILES, GEMM_SMALLK, GEMM_T128, GEMM_KW, GEMM_NS64, GEMM_SPLITKW,
+ * GEMM_DIRECT, SRA_SMALL_N, SRA_DKV_DIRECT, GROUPED_KT, GROUPED_CHUNK): initialised from the
+ * CMX_<NAME> environment variable, changed in-process by cmx_tune for interleaved A/B runs;
+ * a knob set before the first launch that reads it keeps the set value.  tune_get: -1 if unset. */
+int cmx_tune(const char* name, int value);
+int cmx_tune_get(const char* name);
 
 /* ---- LayerNorm: nn.LayerNorm in Block.norm1/norm2, stage norms (eps 1e-6,
  *      dual_segformer.py:148,155,257), OverlapPatchEmbed.norm (:198), Attention.norm (:97),
@@ -123,6 +129,19 @@ size_t cmx_small_linear_bwd_workspace(int M, int K, int Nout);
 int cmx_small_linear_bwd(const float* dy_part, int dy_nslice, int64_t dy_slice_stride, int64_t dy_row_stride, const float* y, const float* x, const float* w, float* dx_part, float* dw, float* db, int M, int K, int Nout, int act, int accumulate, hipStream_t stream);
 /* rectification fused with SpatialWeights' C -> 2 conv + sigmoid: h (B*N, C) = the 2C -> C conv output (pre-ReLU),
  * w2 (2, C), b2 (2) fp32; writes sw (B*N, 2) (saved for the backward) and out (2, B, N, C) */
+/* ChannelWeights (net_utils.py:11-30) of FeatureRectifyModule (:145) as ONE launch per direction:
+ * a grid of one workgroup per CU whose phases (pool partial, pool final, GEMV W1 + relu, GEMV W2 +
+ * sigmoid; backward: dcw slab sum * sigmoid', W2 pass, W1 pass, pooling gradient) meet at grid
+ * barriers.  x (2,B,N,C); pooled, y1 (B,4C), argmax, cw (B,2C) fp32/int32; W1 (4C,4C), W2 (2C,4C) fp32.
+ * Backward: dcw_part = the combine backward's (B, nslab, 2C) partials; dW / db written (not
+ * accumulated); the pooling gradient is ADDED into dx.  B <= 8, C % 16 == 0, C <= 512.  One launch
+ * of each direction at a time per device.  barrier_timeouts: count of polls that gave up (0 = every
+ * grid was co-resident; synchronous, for tests). */
+size_t cmx_frm_channel_fwd_workspace(int B, int N, int C);
+int cmx_frm_channel_fwd(const void* x, const float* w1, const float* b1, const float* w2, const float* b2, float* pooled, int* argmax, float* y1, float* cw, float* workspace, int B, int N, int C, int dtype, hipStream_t stream);
+size_t cmx_frm_channel_bwd_workspace(int B, int C);
+int cmx_frm_channel_bwd(const float* dcw_part, int nslab, const float* cw, const float* y1, const float* pooled, const int* argmax, const float* w1, const float* w2, float* dw1, float* db1, float* dw2, float* db2, void* dx, float* workspace, int B, int N, int C, int dtype, hipStream_t stream);
+int cmx_frm_barrier_timeouts(void);
 int cmx_frm_combine_fwd(const void* x, const float* cw, const void* h, const float* w2, const float* b2, float* sw, void* out, int B, int N, int C, int dtype, hipStream_t stream);
 /* backward: dx direct path (2,B,N,C), dh (B*N, C); workspace = dcw partials (B, nblk, 2C) followed by the
  * [dw2 (2C) | db2 (2)] partials (B*nblk, 2C+2); nblk = cmx_frm_combine_bwd_nblk(N, C, dtype) */

@@ -23,6 +23,8 @@ enum cmx_status {
 // ---------------------------------------------------------------- error reporting
 void cmx_set_error(const char* fmt, ...);
 int cmx_check_launch(const char* what);
+// launch-policy knob NAME: a stable reference, initialised from CMX_NAME or `def` (abi.cpp)
+int& cmx_knob(const char* name, int def);
 
 #define CMX_REQUIRE(cond, code, ...)   \
   do {                                 \

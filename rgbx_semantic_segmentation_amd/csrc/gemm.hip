@@ -971,12 +971,12 @@ void launch_bf16_ns(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStr
   const long blocks = (long)a.tiles_m * a.tiles_n * G * nsplit;
   // a 64 x 64 stage is only 16 KB, so a 4-deep ring (64 KB) would still leave two blocks per
   // CU; measured: no gain (2.82 vs 2.95 ms of GEMM per step), so off by default (CMX_GEMM_NS64=4)
-  static const int ns64 = [] { const char* e = getenv("CMX_GEMM_NS64"); return e ? atoi(e) : 2; }();
+  static int& ns64 = cmx_knob("GEMM_NS64", 2);
   // k-group blocks for 64 x 64 tiles without split-K or bias column (CMX_GEMM_KW = the largest
   // group count allowed, default 2; 1 = off).  Measured (scripts/gemm_sweep.py, G2 M600 N512):
   // K 2048 20.1 -> 11.9 us, K 512 7.5 -> 5.8 us at KW = 2; grids above 512 blocks and one-slot
   // problems are slower with it (M9600 N128 K512: 9.7 -> 10.4 us), so they keep 4 waves.
-  static const int kw = [] { const char* e = getenv("CMX_GEMM_KW"); return e ? atoi(e) : 2; }();
+  static int& kw = cmx_knob("GEMM_KW", 2);
   if constexpr (BM == 64 && BN == 64) {
     const int nk64 = (a.K + FBK - 1) / FBK;
     if (kw >= 2 && nsplit == 1 && !a.ones_col && blocks <= 512 && nk64 >= 4) {
@@ -1054,10 +1054,7 @@ int tile_dim(int n) { return n <= 64 ? 64 : 128; }
 // take 64 x 64 tiles -- 4x the tiles, a lighter per-block k-loop and no split-K combine --
 // and split K only when even those leave it under-filled.
 int tile_policy() {
-  static const int p = [] {
-    const char* e = getenv("CMX_GEMM_TILES");
-    return e ? atoi(e) : 1;
-  }();
+  static int& p = cmx_knob("GEMM_TILES", 1);
   return p;
 }
 
@@ -1070,10 +1067,7 @@ int tile_policy() {
 // 512 x 512 decoder GEMM (K 512) is the shape that keeps 128-wide tiles faster, hence 256.
 // A narrow output (N <= 64, K 512: the decoder's class / c1 products) also takes 64 x 64.
 int smallk_policy() {
-  static const int p = [] {
-    const char* e = getenv("CMX_GEMM_SMALLK");
-    return e ? atoi(e) : 256;
-  }();
+  static int& p = cmx_knob("GEMM_SMALLK", 256);
   return p;
 }
 
@@ -1083,7 +1077,7 @@ void plan_tiles(int G, int M, int nb, int K, int* bm, int* bn) {
   if (tile_policy() == 1) {
     // (CMX_GEMM_T128, default 400: the stage-3 MLP GEMMs, 380 128-wide tiles, run 64 x 64;
     // measured +0.6 % per step over 240 in interleaved A/B)
-    static const int t128min = [] { const char* e = getenv("CMX_GEMM_T128"); return e ? atoi(e) : 400; }();
+    static int& t128min = cmx_knob("GEMM_T128", 400);
     const long t128 = (long)cdiv(M, *bm) * cdiv(nb, *bn) * G;
     if (t128 < t128min) *bm = *bn = 64;
   }
@@ -1104,10 +1098,7 @@ int auto_split(int G, int M, int N, int K, int ones_col) {
   // (launch_bf16_ns, KW waves per tile) instead of split-K slabs + a reducer launch: measured
   // +1.2 % per step (interleaved A/B, 246.7 / 247.1 -> 249.5 / 250.5 img/s; CMX_GEMM_SPLITKW=0
   // restores split-K)
-  static const int splitkw = [] {
-    const char* e = getenv("CMX_GEMM_SPLITKW");
-    return e ? atoi(e) : 1;
-  }();
+  static int& splitkw = cmx_knob("GEMM_SPLITKW", 1);
   // (short k-loops only: a k-group block walks nk / 2 ring slots serially, and the FFM context
   // products -- 64 x 64 over 19200 tokens, nk = 300 -- keep split-K: 10.8 vs 33 us)
   if (splitkw && bm == 64 && bn == 64 && !ones_col && nk <= 32) return 1;
@@ -1213,7 +1204,7 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
   splitk = (nk + a.kt_per_split - 1) / a.kt_per_split;      // no empty splits
   a.nsplit = splitk;
   // CMX_GEMM_DIRECT=1: register epilogue for plain 16-bit outputs (A/B switch, default off)
-  static const int direct_env = [] { const char* e = getenv("CMX_GEMM_DIRECT"); return e ? atoi(e) : 0; }();
+  static int& direct_env = cmx_knob("GEMM_DIRECT", 0);
   a.direct = direct_env && fast && splitk == 1 && out_mode == 0 && !ones_col && !a.nup && !a.scatter && nb % 4 == 0 &&
              ldc % 4 == 0 && sC % 4 == 0 && ((uintptr_t)C & 7) == 0 && (!R || ((uintptr_t)R & 7) == 0) &&
              (!bias || (sbias % 4 == 0 && ((uintptr_t)bias & 15) == 0));
@@ -1323,10 +1314,7 @@ int cmx_gemm_grouped_splitk(int G, int M, int N, int K, int ones_col) {
   if (G <= 0 || M <= 0 || N <= 0 || K <= 0) return 1;
   // <= 48 k-tiles of 64 tokens per block (CMX_GROUPED_KT): measured against 16 / 24 / 32 / 64
   // on the B2 step (interleaved A/B: 32 -> 48 is +1.5 %, 64 no better; fewer slabs to reduce)
-  static const int kt = [] {
-    const char* e = getenv("CMX_GROUPED_KT");
-    return e ? atoi(e) : 48;
-  }();
+  static int& kt = cmx_knob("GROUPED_KT", 48);
   const int nk = (K + FBK - 1) / FBK;
   int s = (nk + kt - 1) / kt;
   if (s > 64) s = 64;
@@ -1449,10 +1437,7 @@ int cmx_gemm_grouped(const void* recs, int nrec, int total_blocks, int dtype, hi
   // launch: 695-702 us contiguous, 624-633 us for runs of 4..128 tiles
   // (scripts/grouped_chunk_sweep.sh); PMC HBM bytes per launch 3.13 GB at 16-tile runs,
   // 2.48 GB at 64 (contiguous: 2.43 GB), so 64 keeps the L2 reuse of neighbouring tiles
-  static const int chunk = [] {
-    const char* e = getenv("CMX_GROUPED_CHUNK");
-    return e ? atoi(e) : 64;
-  }();
+  static int& chunk = cmx_knob("GROUPED_CHUNK", 64);
   if (dtype == 2)
     hipLaunchKernelGGL(gemm_grouped_kernel<f16>, dim3(total_blocks), dim3(256), 0, s, (const GroupRec*)recs, nrec, chunk);
   else

@@ -9,7 +9,9 @@
 // of one 16-byte vector.  HBM-bound: fwd reads x once and writes y once (+8 B/row stats).
 #include "cmx_common.h"
 
-template <typename T, int TPR, int NCH>
+// RPT rows per thread, spaced RPB apart: every row's loads are issued before any reduction, so
+// a narrow-row launch (C = 64 / 128: one 16-B chunk per lane) keeps RPT loads in flight per lane
+template <typename T, int TPR, int NCH, int RPT>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x,
                                                      const float* __restrict__ gamma,
                                                      const float* __restrict__ beta,
@@ -20,56 +22,65 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x,
   constexpr int RPB = 256 / TPR;
   const int g = blockIdx.y;
   const int lane = threadIdx.x % TPR;
-  const long row = (long)blockIdx.x * RPB + threadIdx.x / TPR;
-  const bool live = row < R;
-  const long grow = (long)g * R + row;
+  const long row0 = (long)blockIdx.x * RPB * RPT + threadIdx.x / TPR;
   const int nchunk = C / V;
-  float v[NCH][V];
-  float s = 0.f;
+  float v[RPT][NCH][V];
 #pragma unroll
-  for (int k = 0; k < NCH; ++k) {
-    const int ch = lane + k * TPR;
-    if (live && ch < nchunk) {
-      load_vec<T>(x + grow * C + ch * V, v[k]);
+  for (int u = 0; u < RPT; ++u) {
+    const long row = row0 + (long)u * RPB;
 #pragma unroll
-      for (int j = 0; j < V; ++j) s += v[k][j];
-    } else {
+    for (int k = 0; k < NCH; ++k) {
+      const int ch = lane + k * TPR;
+      if (row < R && ch < nchunk) {
+        load_vec<T>(x + ((long)g * R + row) * C + ch * V, v[u][k]);
+      } else {
 #pragma unroll
-      for (int j = 0; j < V; ++j) v[k][j] = 0.f;
+        for (int j = 0; j < V; ++j) v[u][k][j] = 0.f;
+      }
     }
   }
-  s = group_sum(s, TPR);
-  const float mu = s / C;
-  float q = 0.f;
-#pragma unroll
-  for (int k = 0; k < NCH; ++k) {
-    const int ch = lane + k * TPR;
-    if (live && ch < nchunk) {
-#pragma unroll
-      for (int j = 0; j < V; ++j) { float d = v[k][j] - mu; q += d * d; }
-    }
-  }
-  q = group_sum(q, TPR);
-  const float rstd = rsqrtf(q / C + eps);
-  if (!live) return;
   const float* gg = gamma + (long)g * C;
   const float* bb = beta + (long)g * C;
 #pragma unroll
-  for (int k = 0; k < NCH; ++k) {
-    const int ch = lane + k * TPR;
-    if (ch < nchunk) {
-      float o[V];
+  for (int u = 0; u < RPT; ++u) {
+    const long row = row0 + (long)u * RPB;
+    const long grow = (long)g * R + row;
+    float s = 0.f;
 #pragma unroll
-      for (int j = 0; j < V; ++j) {
-        const int c = ch * V + j;
-        o[j] = (v[k][j] - mu) * rstd * gg[c] + bb[c];
+    for (int k = 0; k < NCH; ++k)
+#pragma unroll
+      for (int j = 0; j < V; ++j) s += v[u][k][j];
+    s = group_sum(s, TPR);
+    const float mu = s / C;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch < nchunk) {
+#pragma unroll
+        for (int j = 0; j < V; ++j) { float d = v[u][k][j] - mu; q += d * d; }
       }
-      store_vec<T>(y + grow * C + ch * V, o);
     }
-  }
-  if (lane == 0) {
-    if (mean_out) mean_out[grow] = mu;
-    if (rstd_out) rstd_out[grow] = rstd;
+    q = group_sum(q, TPR);
+    const float rstd = rsqrtf(q / C + eps);
+    if (row >= R) continue;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch < nchunk) {
+        float o[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const int c = ch * V + j;
+          o[j] = (v[u][k][j] - mu) * rstd * gg[c] + bb[c];
+        }
+        store_vec<T>(y + grow * C + ch * V, o);
+      }
+    }
+    if (lane == 0) {
+      if (mean_out) mean_out[grow] = mu;
+      if (rstd_out) rstd_out[grow] = rstd;
+    }
   }
 }
 
@@ -78,7 +89,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x,
 // dual_segformer.py:168-169, summed here instead of by a separate add).  dxs (optional) =
 // sscale[row / rps] * dx: the DropPath-scaled copy the residual branch's own backward needs.
 // Per-block partial column sums of dy*xhat (dgamma) and dy (dbeta) go to ws.
-template <typename T, int TPR, int NCH>
+template <typename T, int TPR, int NCH, int RPT>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                      const float* __restrict__ gamma,
                                                      const float* __restrict__ mean,
@@ -101,57 +112,80 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
 #pragma unroll
     for (int j = 0; j < V; ++j) dg[k][j] = db[k][j] = 0.f;
 
-  for (long row = (long)blockIdx.x * RPB + rslot; row < R; row += (long)gridDim.x * RPB) {
-    const long grow = (long)g * R + row;
-    const float mu = mean[grow], rs = rstd[grow];
-    float xv[NCH][V], gv[NCH][V];
-    float s1 = 0.f, s2 = 0.f;
+  // RPT rows per iteration, all their loads issued before the row reductions
+  const long stride = (long)gridDim.x * RPB;
+  for (long row0 = (long)blockIdx.x * RPB + rslot; row0 < R; row0 += stride * RPT) {
+    float xv[RPT][NCH][V], gv[RPT][NCH][V], dv[RPT][NCH][V];
+    float mu[RPT], rs[RPT];
 #pragma unroll
-    for (int k = 0; k < NCH; ++k) {
-      const int ch = lane + k * TPR;
-      if (ch < nchunk) {
-        float dv[V];
-        load_vec<T>(x + grow * C + ch * V, xv[k]);
-        load_vec<T>(dy + grow * C + ch * V, dv);
-        if (dy2) {              // second consumer of y (q and the SR conv both read norm1's output)
-          float d2[V];
-          load_vec<T>(dy2 + grow * C + ch * V, d2);
+    for (int u = 0; u < RPT; ++u) {
+      const long row = row0 + u * stride;
+      const bool live = row < R;
+      const long grow = (long)g * R + (live ? row : 0);
+      mu[u] = live ? mean[grow] : 0.f;
+      rs[u] = live ? rstd[grow] : 0.f;
 #pragma unroll
-          for (int j = 0; j < V; ++j) dv[j] += d2[j];
-        }
+      for (int k = 0; k < NCH; ++k) {
+        const int ch = lane + k * TPR;
+        if (live && ch < nchunk) {
+          load_vec<T>(x + grow * C + ch * V, xv[u][k]);
+          load_vec<T>(dy + grow * C + ch * V, dv[u][k]);
+          if (dy2) {              // second consumer of y (q and the SR conv both read norm1's output)
+            float d2[V];
+            load_vec<T>(dy2 + grow * C + ch * V, d2);
 #pragma unroll
-        for (int j = 0; j < V; ++j) {
-          const float xh = (xv[k][j] - mu) * rs;
-          xv[k][j] = xh;
-          gv[k][j] = dv[j] * gg[ch * V + j];
-          s1 += gv[k][j];
-          s2 += gv[k][j] * xh;
-          dg[k][j] += dv[j] * xh;
-          db[k][j] += dv[j];
+            for (int j = 0; j < V; ++j) dv[u][k][j] += d2[j];
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < V; ++j) xv[u][k][j] = dv[u][k][j] = 0.f;
         }
       }
     }
-    s1 = group_sum(s1, TPR) / C;
-    s2 = group_sum(s2, TPR) / C;
 #pragma unroll
-    for (int k = 0; k < NCH; ++k) {
-      const int ch = lane + k * TPR;
-      if (ch < nchunk) {
-        float o[V];
+    for (int u = 0; u < RPT; ++u) {
+      const long row = row0 + u * stride;
+      const long grow = (long)g * R + row;
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-        for (int j = 0; j < V; ++j) o[j] = rs * (gv[k][j] - s1 - xv[k][j] * s2);
-        if (dres) {
-          float rv[V];
-          load_vec<T>(dres + grow * C + ch * V, rv);
+      for (int k = 0; k < NCH; ++k) {
+        const int ch = lane + k * TPR;
+        if (ch < nchunk) {
 #pragma unroll
-          for (int j = 0; j < V; ++j) o[j] += rv[j];
+          for (int j = 0; j < V; ++j) {
+            const float xh = (xv[u][k][j] - mu[u]) * rs[u];
+            xv[u][k][j] = xh;
+            gv[u][k][j] = dv[u][k][j] * gg[ch * V + j];
+            s1 += gv[u][k][j];
+            s2 += gv[u][k][j] * xh;
+            dg[k][j] += dv[u][k][j] * xh;
+            db[k][j] += dv[u][k][j];
+          }
         }
-        store_vec<T>(dx + grow * C + ch * V, o);
-        if (dxs) {
-          const float sc = sscale[grow / rps];
+      }
+      s1 = group_sum(s1, TPR) / C;
+      s2 = group_sum(s2, TPR) / C;
+      if (row >= R) continue;
 #pragma unroll
-          for (int j = 0; j < V; ++j) o[j] *= sc;
-          store_vec<T>(dxs + grow * C + ch * V, o);
+      for (int k = 0; k < NCH; ++k) {
+        const int ch = lane + k * TPR;
+        if (ch < nchunk) {
+          float o[V];
+#pragma unroll
+          for (int j = 0; j < V; ++j) o[j] = rs[u] * (gv[u][k][j] - s1 - xv[u][k][j] * s2);
+          if (dres) {
+            float rv[V];
+            load_vec<T>(dres + grow * C + ch * V, rv);
+#pragma unroll
+            for (int j = 0; j < V; ++j) o[j] += rv[j];
+          }
+          store_vec<T>(dx + grow * C + ch * V, o);
+          if (dxs) {
+            const float sc = sscale[grow / rps];
+#pragma unroll
+            for (int j = 0; j < V; ++j) o[j] *= sc;
+            store_vec<T>(dxs + grow * C + ch * V, o);
+          }
         }
       }
     }
@@ -240,14 +274,17 @@ static int ln_fwd_launch(const void* x, const float* g, const float* b, void* y,
   const int chunks = C / V;
   const int tpr = ln_tpr(chunks);
   const int nch = (chunks + tpr - 1) / tpr;
-  const dim3 grid(cdiv(R, 256 / tpr), G);
-#define LNF(TPR, NCH)                                                                      \
-  if (tpr == TPR && nch == NCH) {                                                          \
-    hipLaunchKernelGGL((ln_fwd_kernel<T, TPR, NCH>), grid, dim3(256), 0, s, (const T*)x, g, b, \
-                       (T*)y, mu, rs, R, C, eps);                                          \
-    return cmx_check_launch("layernorm_fwd");                                              \
+  // 4 rows per thread for narrow rows when that still leaves >= 256 blocks (one per CU)
+  const int rpt = (nch == 1 && tpr <= 16 && R * G / ((256 / tpr) * 4) >= 256) ? 4 : 1;
+  const dim3 grid(cdiv(R, (256 / tpr) * rpt), G);
+#define LNF(TPR, NCH, RPT)                                                                  \
+  if (tpr == TPR && nch == NCH && rpt == RPT) {                                             \
+    hipLaunchKernelGGL((ln_fwd_kernel<T, TPR, NCH, RPT>), grid, dim3(256), 0, s, (const T*)x, g, b, \
+                       (T*)y, mu, rs, R, C, eps);                                           \
+    return cmx_check_launch("layernorm_fwd");                                               \
   }
-  LNF(4, 1) LNF(8, 1) LNF(16, 1) LNF(32, 1) LNF(64, 1) LNF(64, 2) LNF(64, 4)
+  LNF(4, 1, 4) LNF(8, 1, 4) LNF(16, 1, 4)
+  LNF(4, 1, 1) LNF(8, 1, 1) LNF(16, 1, 1) LNF(32, 1, 1) LNF(64, 1, 1) LNF(64, 2, 1) LNF(64, 4, 1)
 #undef LNF
   cmx_set_error("layernorm_fwd: unsupported C=%d", C);
   return CMX_ERR_SHAPE;
@@ -269,14 +306,17 @@ static int ln_bwd_launch(const void* dy, const void* x, const float* g, const fl
   const int nch = (chunks + tpr - 1) / tpr;
   const int nb = ln_bwd_blocks(R, 256 / tpr);
   const dim3 grid(nb, G);
-#define LNB(TPR, NCH)                                                                       \
-  if (tpr == TPR && nch == NCH) {                                                           \
-    hipLaunchKernelGGL((ln_bwd_kernel<T, TPR, NCH>), grid, dim3(256), 0, s, (const T*)dy,    \
+  // two rows per iteration where a thread walks more than one (narrow rows, stage 1 / 2)
+  const int rpt = (nch == 1 && tpr <= 16 && R > (long)nb * (256 / tpr)) ? 2 : 1;
+#define LNB(TPR, NCH, RPT)                                                                  \
+  if (tpr == TPR && nch == NCH && rpt == RPT) {                                             \
+    hipLaunchKernelGGL((ln_bwd_kernel<T, TPR, NCH, RPT>), grid, dim3(256), 0, s, (const T*)dy, \
                        (const T*)x, g, mu, rs, (T*)dx, ws, R, C, (const T*)dres, sscale,     \
                        (T*)dxs, rps, (const T*)dy2);                                         \
     goto reduce;                                                                            \
   }
-  LNB(4, 1) LNB(8, 1) LNB(16, 1) LNB(32, 1) LNB(64, 1) LNB(64, 2) LNB(64, 4)
+  LNB(4, 1, 2) LNB(8, 1, 2) LNB(16, 1, 2)
+  LNB(4, 1, 1) LNB(8, 1, 1) LNB(16, 1, 1) LNB(32, 1, 1) LNB(64, 1, 1) LNB(64, 2, 1) LNB(64, 4, 1)
 #undef LNB
   cmx_set_error("layernorm_bwd: unsupported C=%d", C);
   return CMX_ERR_SHAPE;

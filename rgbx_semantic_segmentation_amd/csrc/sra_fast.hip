@@ -28,6 +28,7 @@ template <typename E> using frag8 = typename MF<E>::frag;
 
 
 typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f2 __attribute__((ext_vector_type(2)));     // packed fp32 pair (v_pk_fma / add / mul)
 
 constexpr int HD = 64;          // head dim
 constexpr int ROWB = 128;       // bytes per key row of an image
@@ -75,6 +76,32 @@ __device__ __forceinline__ frag8<E> frag_t(const char* img, int kb, int db, int 
   }
   const s16x8 c = __builtin_shufflevector(v[0], v[1], 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_bit_cast(frag8<E>, c);
+}
+
+// The same reads with the per-lane part of the address precomputed once per kernel: with row
+// bases that are multiples of 16 the swizzle depends only on the lane, so a tile's address is
+// (uniform tile base) + (per-lane offset) + (compile-time sub-tile offset).  A runtime key loop
+// then costs one add per distinct per-lane offset per tile instead of a full recomputation.
+__device__ __forceinline__ int koff(int s, int lane) {
+  const int row = lane & 31, h = lane >> 5;
+  return row * ROWB + (((2 * s + h) ^ swz(row)) << 4);
+}
+__device__ __forceinline__ int toff(int rd, int db, int lane) {
+  const int h = lane >> 5, g16 = (lane >> 4) & 1, i = lane & 15, q = i >> 2, pp = i & 3;
+  const int chunk = (db + 16 * g16 + 4 * pp) >> 3, kk = 4 * h + 8 * rd + q;
+  return kk * ROWB + ((chunk ^ swz(kk)) << 4) + ((pp & 1) << 3);
+}
+template <typename E>
+__device__ __forceinline__ frag8<E> frag_k_o(const char* p) {
+  return frag_bits<E>(*reinterpret_cast<const uint4*>(p));
+}
+template <typename E>
+__device__ __forceinline__ frag8<E> frag_t_o(const char* p0, const char* p1) {
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      reinterpret_cast<__attribute__((address_space(3))) s16x4*>(reinterpret_cast<uintptr_t>(p0)));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      reinterpret_cast<__attribute__((address_space(3))) s16x4*>(reinterpret_cast<uintptr_t>(p1)));
+  return __builtin_bit_cast(frag8<E>, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
@@ -131,13 +158,25 @@ __global__ __launch_bounds__(64 * NW) void sra_fwd_fast(const E* __restrict__ q,
   vm_wait<0>();
   __syncthreads();
 
-  for (int t0 = 0; t0 < nkc; t0 += KTILE) {
+  // whole key tiles, then the ragged tail tile with the key mask: the unmasked tiles carry no
+  // per-score compare / select
+  int ko[4], to[2][2];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) ko[s] = koff(s, lane);
+#pragma unroll
+  for (int rd = 0; rd < 2; ++rd)
+#pragma unroll
+    for (int d = 0; d < 2; ++d) to[rd][d] = toff(rd, 32 * d, lane);
+  auto tile = [&](const int t0, auto masked) {
+    constexpr bool MASK = decltype(masked)::value;
+    const char* Kt = Ki + t0 * ROWB;
+    const char* Vt = Vi + t0 * ROWB;
     f32x16 sa[QW][2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       frag8<E> kf[4];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) kf[s] = frag_k<E>(Ki, t0 + 32 * ks, s, lane);
+      for (int s = 0; s < 4; ++s) kf[s] = frag_k_o<E>(Kt + 32 * ks * ROWB + ko[s]);
 #pragma unroll
       for (int u = 0; u < QW; ++u) {
         sa[u][ks] = zero16();
@@ -145,37 +184,42 @@ __global__ __launch_bounds__(64 * NW) void sra_fwd_fast(const E* __restrict__ q,
         for (int s = 0; s < 4; ++s) sa[u][ks] = MF<E>::mma(kf[s], qf[u][s], sa[u][ks]);
       }
     }
-    const bool tail = t0 + KTILE > nc;
 #pragma unroll
     for (int u = 0; u < QW; ++u) {
+      if constexpr (MASK) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (t0 + 32 * ks + accrow(i, h) >= nc) sa[u][ks][i] = -INFINITY;
+      }
       float mt = -INFINITY;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float x = sa[u][ks][i];
-          if (tail && t0 + 32 * ks + accrow(i, h) >= nc) x = -INFINITY;
-          sa[u][ks][i] = x;
-          mt = fmaxf(mt, x);
-        }
-      // max on the raw scores (the scale is positive), exponent as one FMA per score
+        for (int i = 0; i < 16; ++i) mt = fmaxf(mt, sa[u][ks][i]);
+      // max on the raw scores (the scale is positive), exponent as one packed FMA per 2 scores
       mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
       const float mn = fmaxf(m[u], mt);
       const float alpha = fexp2(m[u] - mn);
-      float rs = 0.f;
+      const f2 sl2v = {sl2, sl2}, nmn = {-mn, -mn};
+      f2 rs2 = {0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float p = fexp2(fmaf(sa[u][ks][i], sl2, -mn));
-          sa[u][ks][i] = p;
-          rs += p;
+        for (int i = 0; i < 16; i += 2) {
+          const f2 x = {sa[u][ks][i], sa[u][ks][i + 1]};
+          const f2 a = x * sl2v + nmn;
+          const f2 p = {fexp2(a.x), fexp2(a.y)};
+          sa[u][ks][i] = p.x;
+          sa[u][ks][i + 1] = p.y;
+          rs2 += p;
         }
+      float rs = rs2.x + rs2.y;
       rs += __shfl_xor(rs, 32, 64);
       l[u] = l[u] * alpha + rs;
       // rescale the accumulator only when some lane's running max moved: alpha == 1 exactly
-      // otherwise, and after the first key tiles the max rarely moves (32 multiplies per lane
-      // per tile off the VALU, which bounds this loop beside the MFMAs)
+      // otherwise, and after the first key tiles the max rarely moves
       if (__builtin_amdgcn_ballot_w64(mn != m[u])) {
 #pragma unroll
         for (int t = 0; t < 2; ++t)
@@ -188,8 +232,9 @@ __global__ __launch_bounds__(64 * NW) void sra_fwd_fast(const E* __restrict__ q,
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const frag8<E> v0 = frag_t<E>(Vi, t0 + 32 * ks, 0, s, lane);
-        const frag8<E> v1 = frag_t<E>(Vi, t0 + 32 * ks, 32, s, lane);
+        const char* vp = Vt + (32 * ks + 16 * s) * ROWB;
+        const frag8<E> v0 = frag_t_o<E>(vp + to[0][0], vp + to[1][0]);
+        const frag8<E> v1 = frag_t_o<E>(vp + to[0][1], vp + to[1][1]);
 #pragma unroll
         for (int u = 0; u < QW; ++u) {
           const frag8<E> pf = MF<E>::from_acc(sa[u][ks], s);
@@ -197,7 +242,10 @@ __global__ __launch_bounds__(64 * NW) void sra_fwd_fast(const E* __restrict__ q,
           acc[u][1] = MF<E>::mma(v1, pf, acc[u][1]);
         }
       }
-  }
+  };
+  const int nfull = nc / KTILE;
+  for (int t0 = 0; t0 < nfull * KTILE; t0 += KTILE) tile(t0, std::false_type{});
+  if (nfull * KTILE < nc) tile(nfull * KTILE, std::true_type{});
   }                                             // key chunks
 #pragma unroll
   for (int u = 0; u < QW; ++u) {
@@ -272,16 +320,26 @@ __global__ __launch_bounds__(64 * NW) void sra_dq_fast(const E* __restrict__ q, 
   vm_wait<0>();
   __syncthreads();
 
-  for (int t0 = 0; t0 < nkc; t0 += KTILE) {
-    const bool tail = t0 + KTILE > nc;
+  // whole key tiles, then the masked tail tile (see the forward)
+  int ko[4], to[2][2];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) ko[s] = koff(s, lane);
+#pragma unroll
+  for (int rd = 0; rd < 2; ++rd)
+#pragma unroll
+    for (int d = 0; d < 2; ++d) to[rd][d] = toff(rd, 32 * d, lane);
+  auto tile = [&](const int t0, auto masked) {
+    constexpr bool MASK = decltype(masked)::value;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int kb = t0 + 32 * ks;
+      const char* Kt = Ki + kb * ROWB;
+      const char* Vt = Vi + kb * ROWB;
       frag8<E> kf[4], vf[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        kf[s] = frag_k<E>(Ki, kb, s, lane);
-        vf[s] = frag_k<E>(Vi, kb, s, lane);
+        kf[s] = frag_k_o<E>(Kt + ko[s]);
+        vf[s] = frag_k_o<E>(Vt + ko[s]);
       }
       f32x16 ds[QW];
 #pragma unroll
@@ -292,17 +350,25 @@ __global__ __launch_bounds__(64 * NW) void sra_dq_fast(const E* __restrict__ q, 
           sa = MF<E>::mma(kf[s], qf[u][s], sa);
           dp = MF<E>::mma(vf[s], df[u][s], dp);
         }
+        const f2 sl2v = {sl2, sl2}, nl = {-lse2[u], -lse2[u]}, nD = {-Dq[u], -Dq[u]};
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float p = fexp2(sa[i] * sl2 - lse2[u]);
-          if (tail && kb + accrow(i, h) >= nc) p = 0.f;
-          ds[u][i] = p * (dp[i] - Dq[u]);
+        for (int i = 0; i < 16; i += 2) {
+          const f2 a = f2{sa[i], sa[i + 1]} * sl2v + nl;
+          f2 p = {fexp2(a.x), fexp2(a.y)};
+          if constexpr (MASK) {
+            if (kb + accrow(i, h) >= nc) p.x = 0.f;
+            if (kb + accrow(i + 1, h) >= nc) p.y = 0.f;
+          }
+          const f2 d = p * (f2{dp[i], dp[i + 1]} + nD);
+          ds[u][i] = d.x;
+          ds[u][i + 1] = d.y;
         }
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const frag8<E> k0 = frag_t<E>(Ki, kb, 0, s, lane);
-        const frag8<E> k1 = frag_t<E>(Ki, kb, 32, s, lane);
+        const char* kp = Kt + 16 * s * ROWB;
+        const frag8<E> k0 = frag_t_o<E>(kp + to[0][0], kp + to[1][0]);
+        const frag8<E> k1 = frag_t_o<E>(kp + to[0][1], kp + to[1][1]);
 #pragma unroll
         for (int u = 0; u < QW; ++u) {
           const frag8<E> sf = MF<E>::from_acc(ds[u], s);
@@ -311,7 +377,10 @@ __global__ __launch_bounds__(64 * NW) void sra_dq_fast(const E* __restrict__ q, 
         }
       }
     }
-  }
+  };
+  const int nfull = nc / KTILE;
+  for (int t0 = 0; t0 < nfull * KTILE; t0 += KTILE) tile(t0, std::false_type{});
+  if (nfull * KTILE < nc) tile(nfull * KTILE, std::true_type{});
   }                                             // key chunks
 #pragma unroll
   for (int u = 0; u < QW; ++u) {
@@ -398,8 +467,17 @@ __global__ __launch_bounds__(64 * (NKP_MAX / 32)) void sra_dkv_fast(
   if (qbeg < qend) issue(qbeg, smem);
   vm_wait<0>();
   __syncthreads();
+  // only the ragged last query tile carries the per-score query mask
+  int ko[4], to[2][2];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) ko[s] = koff(s, lane);
+#pragma unroll
+  for (int rd = 0; rd < 2; ++rd)
+#pragma unroll
+    for (int d = 0; d < 2; ++d) to[rd][d] = toff(rd, 32 * d, lane);
   int cur = 0;
-  for (int q0 = qbeg; q0 < qend; q0 += QT) {
+  auto qtile = [&](const int q0, auto masked) {
+    constexpr bool MASK = decltype(masked)::value;
     if (q0 + QT < qend) issue(q0 + QT, smem + (cur ^ 1) * DKV_TILE_BYTES);
     const char* Qi = smem + cur * DKV_TILE_BYTES;
     const char* Di = Qi + QT * ROWB;
@@ -410,39 +488,50 @@ __global__ __launch_bounds__(64 * (NKP_MAX / 32)) void sra_dkv_fast(
       const int qb = 32 * qt;
       f32x16 sa = zero16(), dp = zero16();
 #pragma unroll
-      for (int s = 0; s < 4; ++s) sa = MF<E>::mma(frag_k<E>(Qi, qb, s, lane), kf[s], sa);
+      for (int s = 0; s < 4; ++s) sa = MF<E>::mma(frag_k_o<E>(Qi + qb * ROWB + ko[s]), kf[s], sa);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) dp = MF<E>::mma(frag_k<E>(Di, qb, s, lane), vf[s], dp);
-      const bool tail = q0 + qb + 32 > qend;
+      for (int s = 0; s < 4; ++s) dp = MF<E>::mma(frag_k_o<E>(Di + qb * ROWB + ko[s]), vf[s], dp);
+      const f2 sl2v = {sl2, sl2}, nlog2e = {-1.4426950408889634f, -1.4426950408889634f};
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const float4 l4 = *reinterpret_cast<const float4*>(ls + qb + 8 * g4 + 4 * h);
         const float4 d4 = *reinterpret_cast<const float4*>(Ds + qb + 8 * g4 + 4 * h);
-        const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int e = 0; e < 4; e += 2) {
           const int i = 4 * g4 + e;
-          float p = fexp2(fmaf(sa[i], sl2, -lv[e] * 1.4426950408889634f));
-          if (tail && q0 + qb + accrow(i, h) >= qend) p = 0.f;
-          sa[i] = p;
-          dp[i] = p * (dp[i] - dv[e]);
+          const f2 lv = e == 0 ? f2{l4.x, l4.y} : f2{l4.z, l4.w};
+          const f2 dv = e == 0 ? f2{d4.x, d4.y} : f2{d4.z, d4.w};
+          const f2 a = f2{sa[i], sa[i + 1]} * sl2v + lv * nlog2e;
+          f2 p = {fexp2(a.x), fexp2(a.y)};
+          if constexpr (MASK) {
+            if (q0 + qb + accrow(i, h) >= qend) p.x = 0.f;
+            if (q0 + qb + accrow(i + 1, h) >= qend) p.y = 0.f;
+          }
+          const f2 d = p * (f2{dp[i], dp[i + 1]} - dv);
+          sa[i] = p.x; sa[i + 1] = p.y;
+          dp[i] = d.x; dp[i + 1] = d.y;
         }
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const frag8<E> pf = MF<E>::from_acc(sa, s);
         const frag8<E> sf = MF<E>::from_acc(dp, s);
+        const char* dpp = Di + (qb + 16 * s) * ROWB;
+        const char* qpp = Qi + (qb + 16 * s) * ROWB;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          av[t] = MF<E>::mma(frag_t<E>(Di, qb, 32 * t, s, lane), pf, av[t]);
-          ak[t] = MF<E>::mma(frag_t<E>(Qi, qb, 32 * t, s, lane), sf, ak[t]);
+          av[t] = MF<E>::mma(frag_t_o<E>(dpp + to[0][t], dpp + to[1][t]), pf, av[t]);
+          ak[t] = MF<E>::mma(frag_t_o<E>(qpp + to[0][t], qpp + to[1][t]), sf, ak[t]);
         }
       }
     }
     vm_wait<0>();
     __syncthreads();
     cur ^= 1;
-  }
+  };
+  const int nfull = (qend - qbeg) / QT;
+  for (int q0 = qbeg; q0 < qbeg + nfull * QT; q0 += QT) qtile(q0, std::false_type{});
+  if (qbeg + nfull * QT < qend) qtile(qbeg + nfull * QT, std::true_type{});
   if (key >= Nk) return;
   if (nchunk == 1) {            // one query chunk: this workgroup's sums are the gradients
     E* ok = dk + ((long)b * Nk + key) * dkvs + head * HD;
@@ -557,28 +646,36 @@ __global__ __launch_bounds__(64 * SKT) void sra_fwd_small(const E* __restrict__ 
     }
   }
   float m[2], l[2];
+  if (nkw < KTILE) {                             // only the last wave's tile is ragged
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (32 * ks + accrow(i, h) >= nkw) sa[u][ks][i] = -INFINITY;
+  }
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     float mt = -INFINITY;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float x = sa[u][ks][i];
-        if (32 * ks + accrow(i, h) >= nkw) x = -INFINITY;
-        sa[u][ks][i] = x;
-        mt = fmaxf(mt, x);
-      }
+      for (int i = 0; i < 16; ++i) mt = fmaxf(mt, sa[u][ks][i]);
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
-    float rs = 0.f;
+    const f2 sl2v = {sl2, sl2}, nmt = {-mt, -mt};
+    f2 rs2 = {0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = fexp2(fmaf(sa[u][ks][i], sl2, -mt));
-        sa[u][ks][i] = p;
-        rs += p;
+      for (int i = 0; i < 16; i += 2) {
+        const f2 a = f2{sa[u][ks][i], sa[u][ks][i + 1]} * sl2v + nmt;
+        const f2 p = {fexp2(a.x), fexp2(a.y)};
+        sa[u][ks][i] = p.x;
+        sa[u][ks][i + 1] = p.y;
+        rs2 += p;
       }
+    const float rs = rs2.x + rs2.y;
     m[u] = mt;
     l[u] = rs + __shfl_xor(rs, 32, 64);
   }
@@ -703,11 +800,18 @@ __global__ __launch_bounds__(64 * SKT) void sra_dq_small(const E* __restrict__ q
         sa = MF<E>::mma(kf[s], qf[u][s], sa);
         dp = MF<E>::mma(vf[s], df[u][s], dp);
       }
+      const f2 sl2v = {sl2, sl2}, nl = {-lse2[u], -lse2[u]}, nD = {-Dq[u], -Dq[u]};
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float p = fexp2(sa[i] * sl2 - lse2[u]);
-        if (32 * ks + accrow(i, h) >= nkw) p = 0.f;
-        ds[u][i] = p * (dp[i] - Dq[u]);
+      for (int i = 0; i < 16; i += 2) {
+        const f2 a = f2{sa[i], sa[i + 1]} * sl2v + nl;
+        f2 p = {fexp2(a.x), fexp2(a.y)};
+        if (nkw < KTILE) {                       // the last wave's ragged tile (uniform branch)
+          if (32 * ks + accrow(i, h) >= nkw) p.x = 0.f;
+          if (32 * ks + accrow(i + 1, h) >= nkw) p.y = 0.f;
+        }
+        const f2 d = p * (f2{dp[i], dp[i + 1]} + nD);
+        ds[u][i] = d.x;
+        ds[u][i + 1] = d.y;
       }
     }
 #pragma unroll
@@ -794,18 +898,25 @@ __global__ __launch_bounds__(64 * SQW) void sra_dkv_small(const E* __restrict__ 
 #pragma unroll
       for (int s = 0; s < 4; ++s) dp = MF<E>::mma(frag_k<E>(Di, qb, s, lane), vf[s], dp);
       const bool tail = q0 + qb + 32 > N;
+      const f2 sl2v = {sl2, sl2}, nlog2e = {-1.4426950408889634f, -1.4426950408889634f};
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const float4 l4 = *reinterpret_cast<const float4*>(ls + qb + 8 * g4 + 4 * h);
         const float4 d4 = *reinterpret_cast<const float4*>(Ds + qb + 8 * g4 + 4 * h);
-        const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int e = 0; e < 4; e += 2) {
           const int i = 4 * g4 + e;
-          float p = fexp2(fmaf(sa[i], sl2, -lv[e] * 1.4426950408889634f));
-          if (tail && q0 + qb + accrow(i, h) >= N) p = 0.f;
-          sa[i] = p;
-          dp[i] = p * (dp[i] - dv4[e]);
+          const f2 lv = e == 0 ? f2{l4.x, l4.y} : f2{l4.z, l4.w};
+          const f2 dv2 = e == 0 ? f2{d4.x, d4.y} : f2{d4.z, d4.w};
+          const f2 a = f2{sa[i], sa[i + 1]} * sl2v + lv * nlog2e;
+          f2 p = {fexp2(a.x), fexp2(a.y)};
+          if (tail) {                            // uniform: only the ragged last query tile
+            if (q0 + qb + accrow(i, h) >= N) p.x = 0.f;
+            if (q0 + qb + accrow(i + 1, h) >= N) p.y = 0.f;
+          }
+          const f2 d = p * (f2{dp[i], dp[i + 1]} - dv2);
+          sa[i] = p.x; sa[i + 1] = p.y;
+          dp[i] = d.x; dp[i + 1] = d.y;
         }
       }
 #pragma unroll
@@ -919,7 +1030,7 @@ int sra_dkv_fast_chunks(int Bt, int N, int Nk, int heads) {
   const long base = (long)Bt * heads * ((Nk + NKP_MAX - 1) / NKP_MAX);
   // short query sequences: one chunk, the gradients written directly (no fp32 slabs, no
   // reduce launch); CMX_SRA_DKV_DIRECT = the largest N that takes it
-  static const int direct_n = [] { const char* e = getenv("CMX_SRA_DKV_DIRECT"); return e ? atoi(e) : 0; }();
+  static int& direct_n = cmx_knob("SRA_DKV_DIRECT", 0);
   if (N <= direct_n) return 1;
   long nc = (256 + base - 1) / base;
   const long maxc = (N + QT - 1) / QT;
@@ -974,7 +1085,7 @@ void sra_dkv_fast_launch(const void* q, const void* k, const void* v, const void
 // eligible: 16-bit storage, D = 64, Nk <= 320 (one 64-key tile per wave), 16-B aligned rows, and a
 // short query sequence (N <= CMX_SRA_SMALL_N, default 2048: stages 3 / 4 of B2 / B4)
 bool sra_small_ok(int D, int N, int Nk, int dtype, const void* const* ptrs, int nptr, const long* strides, int nstr) {
-  static const int small_n = [] { const char* e = getenv("CMX_SRA_SMALL_N"); return e ? atoi(e) : 2048; }();
+  static int& small_n = cmx_knob("SRA_SMALL_N", 2048);
   return N <= small_n && sra_fast_ok(D, Nk, dtype, ptrs, nptr, strides, nstr);
 }
 

@@ -805,14 +805,14 @@ def pair_embed(store, ce, o):
 class FRMF(Function):
     """FeatureRectifyModule (net_utils.py:124-152) on x (2, B, N, C).
 
-    Forward (6 launches): avg || max pooling (partial + final), the two-layer channel MLP
-    (ChannelWeights, :16-30), the SpatialWeights 2C -> C 1x1 conv as a cat-free GEMM, and ONE
-    kernel for SpatialWeights' C -> 2 conv + sigmoid fused with the rectification.
-    Backward (7 launches): one kernel for the rectification + spatial-head backward (dx direct
-    path, dh, dcw / dw2 partials), one G = 2 dgrad GEMM adding both modality slices of the 2C -> C
-    conv into dx, the dcw partial sum, the channel MLP backward as one pass over each weight
-    matrix (dz formed from the producer's partial slices, dW / db written, dx left as partial
-    slices), and the pooling backward summing those slices itself."""
+    Forward (3 launches): ChannelWeights (:11-30) -- avg || max pooling and the two-layer channel
+    MLP -- as ONE grid-barrier kernel (cmx_frm_channel_fwd), the SpatialWeights 2C -> C 1x1 conv
+    as a cat-free GEMM, and ONE kernel for SpatialWeights' C -> 2 conv + sigmoid fused with the
+    rectification.
+    Backward (3 launches + 2 deferred wgrads): one kernel for the rectification + spatial-head
+    backward (dx direct path, dh, dcw / dw2 partials), one G = 2 dgrad GEMM adding both modality
+    slices of the 2C -> C conv into dx, and the channel branch backward as ONE grid-barrier kernel
+    (cmx_frm_channel_bwd: dcw slab sum, W2 pass, W1 pass, pooling gradient into dx)."""
 
     @staticmethod
     def forward(ctx, x, prm, anchor):
@@ -821,12 +821,12 @@ class FRMF(Function):
         dt = K.dtype_code(x)
         pooled = torch.empty(B, 4 * C, dtype=torch.float32, device=x.device)
         argmax = torch.empty(B, 2 * C, dtype=torch.int32, device=x.device)
-        ws = K._ws(K.query("cmx_frm_pool_workspace", B, N, C), x.device)
-        K.call("cmx_frm_pool_fwd", K.ptr(x), K.ptr(pooled), K.ptr(argmax), K.ptr(ws), B, N, C, dt, K.stream())
         y1 = torch.empty(B, 4 * C, dtype=torch.float32, device=x.device)
-        K.call("cmx_small_linear_fwd", K.ptr(pooled), K.ptr(W1), K.ptr(b1), K.ptr(y1), B, 4 * C, 4 * C, 2, K.stream())
         cw = torch.empty(B, 2 * C, dtype=torch.float32, device=x.device)
-        K.call("cmx_small_linear_fwd", K.ptr(y1), K.ptr(W2), K.ptr(b2), K.ptr(cw), B, 4 * C, 2 * C, 3, K.stream())
+        # ChannelWeights (net_utils.py:11-30): avg || max pool + both MLP GEMVs, one launch
+        ws = K._ws(K.query("cmx_frm_channel_fwd_workspace", B, N, C), x.device)
+        K.call("cmx_frm_channel_fwd", K.ptr(x), K.ptr(W1), K.ptr(b1), K.ptr(W2), K.ptr(b2), K.ptr(pooled),
+               K.ptr(argmax), K.ptr(y1), K.ptr(cw), K.ptr(ws), B, N, C, dt, K.stream())
         # h = cat(x1, x2) W0^T + b0 (SpatialWeights' first 1x1 conv, net_utils.py:72-73), cat-free
         h = torch.empty(1, B * N, C, dtype=x.dtype, device=x.device)
         K.gemm(x[0].view(1, B * N, C), W0[None], h, bias=b0[None], A2=x[1].view(1, B * N, C))
@@ -867,17 +867,12 @@ class FRMF(Function):
         K.gemm(dh[None].expand(2, B * N, C), Wd.transpose(1, 2), dx2, residual=dx2)
         _wgrad_into(dh[None], x[0].view(1, B * N, C), gW0[None, :, :C], gb0.view(1, C))
         _wgrad_into(dh[None], x[1].view(1, B * N, C), gW0[None, :, C:])
-        # channel MLP backward: dcw partial slabs (B, nb, 2C) -> W2 pass -> W1 pass -> pooling
-        ns = K.query("cmx_small_linear_nslice")
-        dcw = torch.empty(B, 2 * C, dtype=torch.float32, device=x.device)      # sum of the nb partial slabs
-        K.call("cmx_partials_sum", K.ptr(ws), K.ptr(dcw), B, nb, 2 * C, 0, 1.0, K.stream())
-        dy1p = torch.empty(ns, B, 4 * C, dtype=torch.float32, device=x.device)
-        K.call("cmx_small_linear_bwd", K.ptr(dcw), 1, 0, 2 * C, K.ptr(cw), K.ptr(y1), K.ptr(W2), K.ptr(dy1p),
-               K.ptr(gW2), K.ptr(gb2), B, 4 * C, 2 * C, 3, 0, K.stream())
-        dpp = torch.empty(ns, B, 4 * C, dtype=torch.float32, device=x.device)
-        K.call("cmx_small_linear_bwd", K.ptr(dy1p), ns, B * 4 * C, 4 * C, K.ptr(y1), K.ptr(pooled), K.ptr(W1),
-               K.ptr(dpp), K.ptr(gW1), K.ptr(gb1), B, 4 * C, 4 * C, 2, 0, K.stream())
-        K.call("cmx_frm_pool_bwd", K.ptr(dpp), ns, B * 4 * C, K.ptr(argmax), K.ptr(dx), B, N, C, dt, K.stream())
+        # channel MLP + pooling backward in one launch: dcw partial slabs (B, nb, 2C) -> W2 pass ->
+        # W1 pass -> pooling gradient added into dx
+        cws = K._ws(K.query("cmx_frm_channel_bwd_workspace", B, C), x.device)
+        K.call("cmx_frm_channel_bwd", K.ptr(ws), nb, K.ptr(cw), K.ptr(y1), K.ptr(pooled), K.ptr(argmax), K.ptr(W1),
+               K.ptr(W2), K.ptr(gW1), K.ptr(gb1), K.ptr(gW2), K.ptr(gb2), K.ptr(dx), K.ptr(cws), B, N, C, dt,
+               K.stream())
         return dx, None, None
 
 

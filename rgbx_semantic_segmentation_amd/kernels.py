@@ -15,6 +15,16 @@ from ._lib import call, query, ptr, stream, dtype_code
 ACT = {"none": 0, "gelu": 1, "relu": 2, "sigmoid": 3}
 
 
+def tune(name: str, value: int) -> None:
+    """Set launch-policy knob `name` (e.g. "GEMM_SMALLK"; cmx_tune) for launches planned from now on."""
+    call("cmx_tune", name.encode(), int(value))
+
+
+def tune_get(name: str) -> int:
+    """Current value of knob `name`, -1 if it has not been set or read yet."""
+    return query("cmx_tune_get", name.encode())
+
+
 def _ws(nbytes: int, device) -> torch.Tensor:
     return torch.empty(max(1, (nbytes + 3) // 4), dtype=torch.float32, device=device)
 

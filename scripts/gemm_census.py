@@ -1,6 +1,8 @@
 """GEMM census of one CMX training step: every cmx_gemm call (shape, transposes, epilogue),
 re-timed standalone on its own operands with HIP events, beside torch.bmm (hipBLASLt) on the
-same views.  Usage (GPU box):  python scripts/gemm_census.py [--backbone mit_b2] [--out file]"""
+same views.  Usage (GPU box):  python scripts/gemm_census.py [--backbone mit_b2] [--out file]
+    [--ab KNOB=v1,v2,...]  time every call under each value of a launch-policy knob (cmx_tune),
+                           interleaved call by call, and print per-shape and total deltas"""
 from __future__ import annotations
 
 import argparse
@@ -42,6 +44,7 @@ def main():
     ap.add_argument("--backbone", default="mit_b2")
     ap.add_argument("--out", default="gpurun_out/gemm_census.json")
     ap.add_argument("--no-torch", action="store_true")
+    ap.add_argument("--ab", default="", help="KNOB=v1,v2: interleaved A/B of a cmx_tune knob")
     a = ap.parse_args()
     from rgbx_semantic_segmentation_amd.models.builder import EncoderDecoder
     from rgbx_semantic_segmentation_amd.data import make_batch
@@ -63,6 +66,8 @@ def main():
     loss.backward()
     torch.cuda.synchronize()
     K.gemm = orig
+    if a.ab:
+        return ab_census(calls, orig, a.ab)
     rows = []
     agg = collections.defaultdict(lambda: [0, 0.0, 0.0, 0.0])
     for A, B, C, kw in calls:
@@ -104,6 +109,43 @@ def main():
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(rows, f, indent=0)
+
+
+def ab_census(calls, orig, spec):
+    knob, vals = spec.split("=")
+    vals = [int(v) for v in vals.split(",")]
+    base = K.tune_get(knob)
+    byk = collections.OrderedDict()
+    tot = [0.0] * len(vals)
+    for A, B, C, kw in calls:
+        G, M, K1 = A.shape
+        Kd = K1 + (kw["A2"].shape[2] if kw.get("A2") is not None else 0)
+        N = B.shape[1]
+        tA = int(A.stride(1) == 1 and A.stride(2) != 1)
+        tB = int(B.stride(1) == 1 and B.stride(2) != 1)
+        key = f"G{G} M{M} N{N} K{Kd} tA{tA} tB{tB} om{kw.get('out_mode', 0)} db{int(kw.get('dbias') is not None)}"
+        ts = []
+        for rep in range(2):                   # two interleaved rounds, keep the best of each arm
+            for i, v in enumerate(vals):
+                K.tune(knob, v)
+                t = timeit(lambda: orig(A, B, C, **kw))
+                if rep == 0:
+                    ts.append(t)
+                else:
+                    ts[i] = min(ts[i], t)
+        e = byk.setdefault(key, [0, [0.0] * len(vals)])
+        e[0] += 1
+        for i, t in enumerate(ts):
+            e[1][i] += t
+            tot[i] += t
+    if base >= 0:
+        K.tune(knob, base)
+    print(f"{len(calls)} gemm calls, knob {knob}: " + "  ".join(f"{v}: {t:.0f} us" for v, t in zip(vals, tot)))
+    print(f"  {'shape':48s} {'n':>3} " + " ".join(f"{str(v):>9}" for v in vals))
+    for key, (n, ts) in sorted(byk.items(), key=lambda kv: -max(kv[1][1]) + min(kv[1][1])):
+        if max(ts) - min(ts) < 2.0:
+            continue
+        print(f"  {key:48s} {n:3d} " + " ".join(f"{t:9.1f}" for t in ts))
 
 
 if __name__ == "__main__":

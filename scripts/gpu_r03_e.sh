@@ -25,3 +25,5 @@ for arm in 1 2; do
   timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/bench_${arm}_$TAG.json 2>&1 || exit $?
   echo "bench $(grep -o '"value": [0-9.]*' gpurun_out/bench_${arm}_$TAG.json)"
 done
+timeout -k 10 400 python3 -u scripts/gemm_census.py --ab GEMM_DIRECT=0,1 > gpurun_out/ab_direct_$TAG.txt 2>&1 || exit $?
+head -30 gpurun_out/ab_direct_$TAG.txt

@@ -19,3 +19,31 @@ for s, e, n in seg:
     cat[k][1] += (e - s) / 1e3
 for k, (n, t) in sorted(cat.items(), key=lambda x: -x[1][1])[:top]:
     print(f"{n:5d} {t:8.1f} {t / n:7.2f}  {k[:100]}")
+
+# kernel families of the step (DESIGN.md per-family table)
+FAMILIES = [
+    ("GEMM (MFMA: linear / conv / decoder / attention projections)", r"^gemm_|^splitk_reduce"),
+    ("grouped wgrad + reduce (deferred weight gradients)", r"^gemm_grouped|^reduce_grouped"),
+    ("SRA attention (MFMA)", r"^sra_"),
+    ("depthwise 3x3 conv + GELU (MixFFN)", r"^dw2_|^dw_"),
+    ("LayerNorm", r"^ln_"),
+    ("BatchNorm", r"^bn_"),
+    ("FRM (CM-FRM)", r"^frm_channel|^pool_|^linear_|^combine_|^ifrm"),
+    ("FFM (cross attention contexts)", r"^ffm_"),
+    ("CE loss + upsample", r"^ce_|^upsample_ce"),
+    ("bilinear / col2im / im2col / patch", r"^bilinear|^col2im|^im2col|^patch"),
+    ("optimizer (AdamW, non-finite check, step)", r"^adamw|^nonfinite|^step_"),
+    ("elementwise / casts / partial sums", r"^act_|^residual|^scale_|^cast_|^reduce_partials|^partials|^colsum|^mul2"),
+    ("torch / runtime", r"^at::|^__amd|^void at::"),
+]
+fam = collections.defaultdict(lambda: [0, 0.0])
+for k, (n, t) in cat.items():
+    name = next((f for f, rx in FAMILIES if re.search(rx, k)), "other")
+    if name == "GEMM (MFMA: linear / conv / decoder / attention projections)" and re.search(r"^gemm_grouped", k):
+        name = "grouped wgrad + reduce (deferred weight gradients)"
+    fam[name][0] += n
+    fam[name][1] += t
+busy = sum(t for _, t in fam.values())
+print(f"\nfamily                                                       launches      us   share")
+for f, (n, t) in sorted(fam.items(), key=lambda x: -x[1][1]):
+    print(f"{f:60s} {n:8d} {t:8.1f} {100 * t / busy:6.1f}%")

@@ -117,3 +117,15 @@ def test_encoder_decoder_refuses_cpu_execution():
         m(torch.zeros(1, 3, 32, 32), torch.zeros(1, 3, 32, 32))
     with pytest.raises(NotImplementedError):
         EncoderDecoder(dict(backbone="swin_s"))
+
+
+def test_tune_knobs_roundtrip():
+    """cmx_tune sets a launch-policy knob in-process (no GPU needed); unset knobs read -1."""
+    from rgbx_semantic_segmentation_amd import kernels as K
+    assert K.tune_get("TEST_ONLY_KNOB") == -1
+    K.tune("TEST_ONLY_KNOB", 7)
+    assert K.tune_get("TEST_ONLY_KNOB") == 7
+    K.tune("TEST_ONLY_KNOB", 3)
+    assert K.tune_get("TEST_ONLY_KNOB") == 3
+    with pytest.raises(Exception):
+        K.tune("X" * 40, 1)

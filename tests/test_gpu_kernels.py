@@ -19,6 +19,32 @@ def relerr(a, b):
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("C,R", [(64, 38400), (128, 9600), (32, 20000)])
+def test_layernorm_many_rows(dev, dtype, C, R):
+    """Stage-1 / 2 row counts: the forward's 4-rows-per-thread and the backward's 2-rows-per-
+    iteration paths (with ragged row tails), against fp64 torch."""
+    from rgbx_semantic_segmentation_amd import kernels as K
+    torch.manual_seed(1)
+    G, eps = 2, 1e-6
+    R = R + 37
+    x = torch.randn(G, R, C, dtype=torch.float64) * 2 + 0.5
+    g = torch.randn(G, C, dtype=torch.float64)
+    b = torch.randn(G, C, dtype=torch.float64)
+    dy = torch.randn(G, R, C, dtype=torch.float64)
+    xr = x.clone().requires_grad_(True); gr = g.clone().requires_grad_(True); br = b.clone().requires_grad_(True)
+    yr = torch.stack([torch.nn.functional.layer_norm(xr[i], (C,), gr[i], br[i], eps) for i in range(G)])
+    yr.backward(dy)
+    xd = x.to(dev, dtype)
+    y, mu, rs = K.layernorm_fwd(xd, g.float().to(dev), b.float().to(dev), eps, G=G)
+    assert relerr(y, yr) < TOL[dtype]
+    dg = torch.empty(G, C, device=dev); db = torch.empty(G, C, device=dev)
+    dx = K.layernorm_bwd(dy.to(dev, dtype), xd, g.float().to(dev), mu, rs, G, dg, db)
+    assert relerr(dx, xr.grad) < TOL[dtype] * 3
+    assert relerr(dg, gr.grad) < TOL[dtype] * 3
+    assert relerr(db, br.grad) < TOL[dtype] * 3
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("C,eps", [(32, 1e-6), (64, 1e-6), (160, 1e-5), (320, 1e-6), (512, 1e-5)])
 def test_layernorm(dev, dtype, C, eps):
     from rgbx_semantic_segmentation_amd import kernels as K
