@@ -264,6 +264,15 @@ int cmx_ifrm_combine_bwd(const void* dout, const void* x, const float* cw, const
 int cmx_aug_resize_u8(const uint8_t* src, int h, int w, int C, uint8_t* dst, int oh, int ow, int nearest, int mirror, int clip_max, hipStream_t stream);
 int cmx_aug_color_jitter_u8(uint8_t* img, int h, int w, float bf, float sf, float hadd, hipStream_t stream);
 int cmx_aug_blur5_u8(const uint8_t* src, uint8_t* dst, int h, int w, int C, hipStream_t stream);
+/* the four stages above over a whole minibatch, one launch per stage (TrainPre over the
+ * DataLoader's batch, dataloader.py:85-112 + the default collate).  table: device array of
+ * B records of 24 int64 words: [0] rgb, [1] x (h x w x 3 u8), [2] gt (h x w u8) sources;
+ * [3] rs, [4] xs (sh x sw x 3), [5] gs (sh x sw) scaled images; [6] blur output (sh x sw x 3,
+ * 0 = no blur); [7] rgb_out, [8] x_out (3 x oh x ow f32), [9] gt_out (oh x ow i64) batch slots;
+ * [10] h, [11] w, [12] sh, [13] sw, [14] mirror, [15..18] cutout box bx1, by1, bx2, by2 (all
+ * zero: none); [19] bf, [20] sf, [21] hue add (float bits in the low 32 bits); [22..23] 0.
+ * max_sh / max_sw bound every record's sh / sw. */
+int cmx_aug_batch(const int64_t* table, int B, int max_sh, int max_sw, int oh, int ow, int clip_max, int background, double m0, double m1, double m2, double s0, double s1, double s2, hipStream_t stream);
 int cmx_aug_finalize(const uint8_t* rgb, const uint8_t* x, const uint8_t* gt, int h, int w, int oh, int ow, int bx1, int by1, int bx2, int by2, int background, double m0, double m1, double m2, double s0, double s1, double s2, float* rgb_out, float* x_out, int64_t* gt_out, hipStream_t stream);
 
 /* ---- evaluation (engine/evaluator.py:306-396, utils/metric.py:8-15, eval.py:23-36).

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import random
 
+import numpy as np
 import torch
 
 from . import _lib as L
@@ -111,13 +112,97 @@ class TrainPre:
 
     def batch(self, samples, out=None):
         """Augment a list of (rgb, gt, modal_x) uint8 samples into batch tensors (B,3,H,W) f32,
-        (B,H,W) i64, (B,3,H,W) f32 -- the default collate of the reference's DataLoader."""
+        (B,H,W) i64, (B,3,H,W) f32 -- the default collate of the reference's DataLoader.
+
+        The draws are made sample by sample in the reference's order (as B calls of __call__
+        would); the pixel work is ONE launch per stage for the whole minibatch
+        (``cmx_aug_batch``).  Host samples (numpy / CPU tensors) and the per-sample record table
+        are packed into one pinned staging buffer (two, alternating, reused across batches) and
+        moved to HBM by ONE host-to-device copy; samples already on the device are read in place."""
         B = len(samples)
         dev = self.device
         if out is None:
             out = (torch.empty(B, 3, self.H, self.W, dtype=torch.float32, device=dev),
                    torch.empty(B, self.H, self.W, dtype=torch.int64, device=dev),
                    torch.empty(B, 3, self.H, self.W, dtype=torch.float32, device=dev))
+        ro, go, xo = out
+        assert ro.is_contiguous() and go.is_contiguous() and xo.is_contiguous()
+        assert ro.shape == (B, 3, self.H, self.W) and xo.shape == ro.shape and go.shape == (B, self.H, self.W)
+        rec = np.zeros((B, _AUG_REC), dtype=np.int64)
+        host = []                                    # (array, staging offset)
+        src_off = 0
+        scratch_off = 0
+        max_sh = max_sw = 1
         for b, (rgb, gt, x) in enumerate(samples):
-            self(rgb, gt, x, out=(out[0][b], out[1][b], out[2][b]))
+            h, w = int(rgb.shape[0]), int(rgb.shape[1])
+            if (rgb.ndim != 3 or rgb.shape[2] != 3 or tuple(x.shape) != tuple(rgb.shape)
+                    or tuple(gt.shape) != (h, w)):
+                raise ValueError(f"TrainPre: rgb {tuple(rgb.shape)} / x {tuple(x.shape)} must be HxWx3 and gt "
+                                 f"{tuple(gt.shape)} HxW of the same size")
+            prm = draw_params(h, w, self.scales, self.rng)
+            sh, sw = prm["sh"], prm["sw"]
+            max_sh, max_sw = max(max_sh, sh), max(max_sw, sw)
+            for k, a in enumerate((rgb, x, gt)):
+                if isinstance(a, torch.Tensor) and a.is_cuda:
+                    if a.dtype != torch.uint8 or not a.is_contiguous():
+                        raise TypeError("TrainPre: device samples must be contiguous uint8")
+                    rec[b, k] = a.data_ptr()
+                else:
+                    a = a.numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
+                    if a.dtype != np.uint8:
+                        raise TypeError(f"TrainPre expects uint8 images, got {a.dtype}")
+                    host.append((b, k, a, src_off))
+                    src_off += _align(a.size)
+            n = sh * sw
+            sizes = (3 * n, 3 * n, n, 3 * n if prm["blur"] else 0)
+            for k, sz in enumerate(sizes):
+                rec[b, 3 + k] = scratch_off if sz else -1
+                scratch_off += _align(sz)
+            bx1, by1, bx2, by2 = prm["box"] if prm["box"] is not None else (0, 0, 0, 0)
+            rec[b, 10:19] = (h, w, sh, sw, int(bool(prm["mirror"])), bx1, by1, bx2, by2)
+            rec[b, 19:22] = np.array([prm["bf"], prm["sf"], prm["hf"] * 180], dtype=np.float32).view(np.int32)
+        table_bytes = rec.nbytes
+        stage = torch.empty(src_off + table_bytes, dtype=torch.uint8, device=dev)
+        scratch = torch.empty(max(scratch_off, 1), dtype=torch.uint8, device=dev)
+        sbase, cbase = stage.data_ptr(), scratch.data_ptr()
+        for b, k, a, off in host:
+            rec[b, k] = sbase + off
+        for k in range(4):
+            col = rec[:, 3 + k]
+            rec[:, 3 + k] = np.where(col >= 0, col + cbase, 0)
+        rec[:, 7] = [ro[b].data_ptr() for b in range(B)]
+        rec[:, 8] = [xo[b].data_ptr() for b in range(B)]
+        rec[:, 9] = [go[b].data_ptr() for b in range(B)]
+        pin = self._staging(src_off + table_bytes)
+        view = pin.numpy()
+        for b, k, a, off in host:
+            view[off:off + a.size] = a.reshape(-1)
+        view[src_off:src_off + table_bytes] = rec.reshape(-1).view(np.uint8)
+        st = torch.cuda.current_stream(dev)
+        stage.copy_(pin[:src_off + table_bytes], non_blocking=True)
+        self._events[self._turn].record(st)
+        mn, sd = self.norm_mean, self.norm_std
+        L.call("cmx_aug_batch", sbase + src_off, B, max_sh, max_sw, self.H, self.W, self.num_classes - 1,
+               self.background, mn[0], mn[1], mn[2], sd[0], sd[1], sd[2], st.cuda_stream)
         return out
+
+    def _staging(self, nbytes: int) -> torch.Tensor:
+        """The next of two pinned staging buffers, grown to ``nbytes``; waits until the copy that
+        last read it has finished (its event), so a buffer is never overwritten in flight."""
+        if not hasattr(self, "_pins"):
+            self._pins = [None, None]
+            self._events = [torch.cuda.Event(), torch.cuda.Event()]
+            self._turn = 1
+        self._turn ^= 1
+        t = self._turn
+        self._events[t].synchronize()
+        if self._pins[t] is None or self._pins[t].numel() < nbytes:
+            self._pins[t] = torch.empty(_align(int(nbytes * 1.25)), dtype=torch.uint8).pin_memory()
+        return self._pins[t]
+
+
+_AUG_REC = 24
+
+
+def _align(n: int, a: int = 256) -> int:
+    return (int(n) + a - 1) // a * a

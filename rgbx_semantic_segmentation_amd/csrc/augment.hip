@@ -56,11 +56,9 @@ __device__ __forceinline__ int nn_index(int d, double inv, int ssize) {
 }
 
 template <int C>
-__global__ __launch_bounds__(256) void resize_u8_kernel(const uint8_t* __restrict__ src, int h, int w,
-                                                        uint8_t* __restrict__ dst, int oh, int ow, int nearest,
-                                                        int mirror, int clip_max, double sx, double sy) {
-  const long p = (long)blockIdx.x * 256 + threadIdx.x;
-  if (p >= (long)oh * ow) return;
+__device__ __forceinline__ void resize_px(const uint8_t* __restrict__ src, int h, int w, uint8_t* __restrict__ dst,
+                                          int oh, int ow, int nearest, int mirror, int clip_max, double sx,
+                                          double sy, long p) {
   const int oy = (int)(p / ow), ox = (int)(p - (long)oy * ow);
   auto col = [&](int x) { return mirror ? w - 1 - x : x; };
   uint8_t* o = dst + p * C;
@@ -86,6 +84,15 @@ __global__ __launch_bounds__(256) void resize_u8_kernel(const uint8_t* __restric
     }
     o[c] = (uint8_t)lin_combine(v00 * a0 + v01 * a1, v10 * a0 + v11 * a1, b0, b1);
   }
+}
+
+template <int C>
+__global__ __launch_bounds__(256) void resize_u8_kernel(const uint8_t* __restrict__ src, int h, int w,
+                                                        uint8_t* __restrict__ dst, int oh, int ow, int nearest,
+                                                        int mirror, int clip_max, double sx, double sy) {
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= (long)oh * ow) return;
+  resize_px<C>(src, h, w, dst, oh, ow, nearest, mirror, clip_max, sx, sy, p);
 }
 
 // ---------------------------------------------------------------------------- colour
@@ -135,9 +142,7 @@ __device__ __forceinline__ void hsv2bgr(int H, int S, int V, uint8_t* o) {
 // astype(uint8) (truncation of a non-negative value)
 __device__ __forceinline__ int clip_trunc(float f) { return (int)fminf(fmaxf(f, 0.f), 255.f); }
 
-__global__ __launch_bounds__(256) void jitter_kernel(uint8_t* __restrict__ img, long n, float bf, float sf, float hadd) {
-  const long p = (long)blockIdx.x * 256 + threadIdx.x;
-  if (p >= n) return;
+__device__ __forceinline__ void jitter_px(uint8_t* __restrict__ img, long p, float bf, float sf, float hadd) {
   uint8_t* q = img + p * 3;
   int h, s, v;
   bgr2hsv(q[0], q[1], q[2], h, s, v);
@@ -147,16 +152,20 @@ __global__ __launch_bounds__(256) void jitter_kernel(uint8_t* __restrict__ img, 
   hsv2bgr(h, s, v, q);
 }
 
+__global__ __launch_bounds__(256) void jitter_kernel(uint8_t* __restrict__ img, long n, float bf, float sf, float hadd) {
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= n) return;
+  jitter_px(img, p, bf, sf, hadd);
+}
+
 // ---------------------------------------------------------------------------- blur
 __device__ __forceinline__ int refl101(int i, int n) {
   i = i < 0 ? -i : i;
   return i >= n ? 2 * (n - 1) - i : i;
 }
 
-__global__ __launch_bounds__(256) void blur5_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int h,
-                                                    int w, int C) {
-  const long p = (long)blockIdx.x * 256 + threadIdx.x;
-  if (p >= (long)h * w) return;
+__device__ __forceinline__ void blur5_px(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int h, int w,
+                                         int C, long p) {
   const int y = (int)(p / w), x = (int)(p - (long)y * w);
   const int k[5] = {14, 62, 104, 62, 14};
   int xs[5], ys[5];
@@ -179,6 +188,13 @@ __global__ __launch_bounds__(256) void blur5_kernel(const uint8_t* __restrict__ 
   }
 }
 
+__global__ __launch_bounds__(256) void blur5_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int h,
+                                                    int w, int C) {
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= (long)h * w) return;
+  blur5_px(src, dst, h, w, C, p);
+}
+
 // ---------------------------------------------------------------------------- finalize
 struct FinArgs {
   const uint8_t *rgb, *x, *gt;
@@ -193,10 +209,8 @@ __device__ __forceinline__ bool in_box(const FinArgs& a, int y, int x) {
   return x >= a.bx1 && x < a.bx2 && y >= a.by1 && y < a.by2;
 }
 
-__global__ __launch_bounds__(256) void finalize_kernel(const FinArgs a) {
-  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void finalize_px(const FinArgs& a, long p) {
   const long plane = (long)a.oh * a.ow;
-  if (p >= plane) return;
   const int oy = (int)(p / a.ow), ox = (int)(p - (long)oy * a.ow);
   // label: nearest, cutout box -> background
   {
@@ -222,6 +236,81 @@ __global__ __launch_bounds__(256) void finalize_kernel(const FinArgs a) {
       out[c * plane + p] = (float)f;
     }
   }
+}
+
+__global__ __launch_bounds__(256) void finalize_kernel(const FinArgs a) {
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= (long)a.oh * a.ow) return;
+  finalize_px(a, p);
+}
+
+// ---------------------------------------------------------------------------- minibatch
+// cmx_aug_batch: the four stages over a whole minibatch, one launch per stage, blockIdx.y =
+// sample.  Each sample's record (CMX_AUG_REC int64 words, layout in include/cmx_hip.h) carries
+// its device pointers, sizes and draws; a block past its sample's (smaller) scaled size exits.
+constexpr int AUG_REC = 24;
+
+struct AugRec {
+  const uint8_t *rgb, *x, *gt;
+  uint8_t *rs, *xs, *gs, *rb;
+  float *rgb_out, *x_out;
+  int64_t* gt_out;
+  int h, w, sh, sw, mirror, bx1, by1, bx2, by2;
+  float bf, sf, hadd;
+};
+
+__device__ __forceinline__ AugRec aug_rec(const int64_t* __restrict__ table, int b) {
+  const int64_t* r = table + (long)b * AUG_REC;
+  AugRec a;
+  a.rgb = (const uint8_t*)r[0]; a.x = (const uint8_t*)r[1]; a.gt = (const uint8_t*)r[2];
+  a.rs = (uint8_t*)r[3]; a.xs = (uint8_t*)r[4]; a.gs = (uint8_t*)r[5]; a.rb = (uint8_t*)r[6];
+  a.rgb_out = (float*)r[7]; a.x_out = (float*)r[8]; a.gt_out = (int64_t*)r[9];
+  a.h = (int)r[10]; a.w = (int)r[11]; a.sh = (int)r[12]; a.sw = (int)r[13]; a.mirror = (int)r[14];
+  a.bx1 = (int)r[15]; a.by1 = (int)r[16]; a.bx2 = (int)r[17]; a.by2 = (int)r[18];
+  a.bf = __int_as_float((int)r[19]); a.sf = __int_as_float((int)r[20]); a.hadd = __int_as_float((int)r[21]);
+  return a;
+}
+
+// blockIdx.z: 0 = rgb, 1 = x (bilinear), 2 = label (nearest + clip)
+__global__ __launch_bounds__(256) void resize_batch_kernel(const int64_t* __restrict__ table, int clip_max) {
+  const AugRec a = aug_rec(table, blockIdx.y);
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= (long)a.sh * a.sw) return;
+  const double sx = 1.0 / ((double)a.sw / a.w), sy = 1.0 / ((double)a.sh / a.h);
+  if (blockIdx.z == 2) resize_px<1>(a.gt, a.h, a.w, a.gs, a.sh, a.sw, 1, a.mirror, clip_max, sx, sy, p);
+  else resize_px<3>(blockIdx.z ? a.x : a.rgb, a.h, a.w, blockIdx.z ? a.xs : a.rs, a.sh, a.sw, 0, a.mirror, -1, sx, sy, p);
+}
+
+__global__ __launch_bounds__(256) void jitter_batch_kernel(const int64_t* __restrict__ table) {
+  const AugRec a = aug_rec(table, blockIdx.y);
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= (long)a.sh * a.sw) return;
+  jitter_px(a.rs, p, a.bf, a.sf, a.hadd);
+}
+
+__global__ __launch_bounds__(256) void blur_batch_kernel(const int64_t* __restrict__ table) {
+  const AugRec a = aug_rec(table, blockIdx.y);
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  if (a.rb == nullptr || p >= (long)a.sh * a.sw) return;
+  blur5_px(a.rs, a.rb, a.sh, a.sw, 3, p);
+}
+
+__global__ __launch_bounds__(256) void finalize_batch_kernel(const int64_t* __restrict__ table, int oh, int ow,
+                                                             int background, double m0, double m1, double m2,
+                                                             double s0, double s1, double s2) {
+  const AugRec r = aug_rec(table, blockIdx.y);
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= (long)oh * ow) return;
+  FinArgs a;
+  a.rgb = r.rb ? r.rb : r.rs; a.x = r.xs; a.gt = r.gs;
+  a.h = r.sh; a.w = r.sw; a.oh = oh; a.ow = ow;
+  a.bx1 = r.bx1; a.by1 = r.by1; a.bx2 = r.bx2; a.by2 = r.by2; a.background = background;
+  a.sx = 1.0 / ((double)ow / r.sw); a.sy = 1.0 / ((double)oh / r.sh);
+  a.isx = a.sx; a.isy = a.sy;
+  a.mean[0] = m0; a.mean[1] = m1; a.mean[2] = m2;
+  a.std[0] = s0; a.std[1] = s1; a.std[2] = s2;
+  a.rgb_out = r.rgb_out; a.x_out = r.x_out; a.gt_out = r.gt_out;
+  finalize_px(a, p);
 }
 
 inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
@@ -278,6 +367,20 @@ int cmx_aug_finalize(const uint8_t* rgb, const uint8_t* x, const uint8_t* gt, in
   a.rgb_out = rgb_out; a.x_out = x_out; a.gt_out = gt_out;
   hipLaunchKernelGGL(finalize_kernel, dim3(nblk((long)oh * ow)), dim3(256), 0, s, a);
   return cmx_check_launch("aug_finalize");
+}
+
+int cmx_aug_batch(const int64_t* table, int B, int max_sh, int max_sw, int oh, int ow, int clip_max, int background,
+                  double m0, double m1, double m2, double s0, double s1, double s2, hipStream_t s) {
+  CMX_REQUIRE(table && B > 0 && B <= 65535 && max_sh > 0 && max_sw > 0 && oh > 0 && ow > 0, CMX_ERR_SHAPE,
+              "aug_batch: B=%d max %dx%d -> %dx%d", B, max_sh, max_sw, oh, ow);
+  CMX_REQUIRE(clip_max < 256, CMX_ERR_ARG, "aug_batch: clip_max %d", clip_max);
+  const unsigned gs = nblk((long)max_sh * max_sw);
+  hipLaunchKernelGGL(resize_batch_kernel, dim3(gs, B, 3), dim3(256), 0, s, table, clip_max);
+  hipLaunchKernelGGL(jitter_batch_kernel, dim3(gs, B), dim3(256), 0, s, table);
+  hipLaunchKernelGGL(blur_batch_kernel, dim3(gs, B), dim3(256), 0, s, table);
+  hipLaunchKernelGGL(finalize_batch_kernel, dim3(nblk((long)oh * ow), B), dim3(256), 0, s, table, oh, ow, background,
+                     m0, m1, m2, s0, s1, s2);
+  return cmx_check_launch("aug_batch");
 }
 
 }  // extern "C"

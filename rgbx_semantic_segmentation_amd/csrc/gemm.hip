@@ -610,6 +610,180 @@ __global__ __launch_bounds__(256 * KW, KW == 4 ? 1 : 2) void gemm_bf16_kernel(co
   gemm_bf16_body<BM, BN, TA, TB, NS, KW, E>(p, xcd_tile(blockIdx.x, p.tiles_m * p.tiles_n * p.G * p.nsplit), smem);
 }
 
+// ============================================================================ stream kernel
+// Persistent 64 x 64 tiles for the many-tile, short-k problems of stages 1-2 and the decoder
+// (M 9600-76800 tokens, K 64-512: a handful of k-tiles per output tile).  One block per tile
+// runs DMA -> MFMA -> epilogue as one latency chain, every block of a launch in the same phase,
+// so HBM idles while the tiles are multiplied and stored.  Here a block walks the tiles
+// t = b, b + grid, ... (XCD-aware order: block b's virtual ids stay on its XCD) and the NS-deep
+// LDS-DMA ring runs straight across tile boundaries: the next tiles' operands are in flight
+// while a tile's epilogue stores leave from the accumulators (no LDS image).  The epilogue
+// reads nothing from global memory between DMAs (a younger global load could only be waited
+// for together with every older DMA -- vmcnt counts in issue order): the residual tile rides
+// the ring as a third image, bias and DropPath scales are staged into LDS once per block, and
+// the barriers are raw s_barrier (a __syncthreads fence would drain the ring).
+constexpr int ST_BIAS_MAX = 2048;      // G * N bias floats staged per block
+constexpr int ST_SCALE_MAX = 256;      // DropPath scales (G * M / rows_per_sample)
+
+template <int NS, bool HR>
+constexpr int stream_smem_bytes() {
+  return NS * (HR ? 3 : 2) * 64 * FBK * 2 + (ST_BIAS_MAX + ST_SCALE_MAX) * 4;
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  __builtin_amdgcn_s_waitcnt((15) | (3 << 14) | (7 << 4) | (0 << 8));   // lgkmcnt(0) only
+  __builtin_amdgcn_s_barrier();
+}
+
+template <bool TA, bool TB, int NS, bool HR, typename E>
+__global__ __launch_bounds__(256, 2) void gemm_stream_kernel(const GemmArgs p) {
+  constexpr int TILE = 64 * FBK * 2;                  // one 64 x 64 16-bit image
+  constexpr int SLOT = (HR ? 3 : 2) * TILE;
+  constexpr int PER = HR ? 6 : 4;                      // DMA instructions per wave per ring slot
+  __shared__ __attribute__((aligned(1024))) char smem[stream_smem_bytes<NS, HR>()];
+  float* bias_s = reinterpret_cast<float*>(smem + NS * SLOT);
+  float* scale_s = bias_s + ST_BIAS_MAX;
+  const int ntile = p.tiles_m * p.tiles_n, total = ntile * p.G;
+  const int nk = (p.K + FBK - 1) / FBK;
+  const int mine = (total - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int iters = mine * nk;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
+  const int r = lane & 31, h = lane >> 5;
+
+  // bias / DropPath scales -> LDS, before any DMA is in flight
+  if (p.bias)
+    for (int e = threadIdx.x; e < p.G * p.N; e += 256) {
+      const int g = e / p.N, j = e - g * p.N;
+      bias_s[e] = p.bias[(long)g * p.sbias + j];
+    }
+  const int nscale = p.rscale ? (int)(((long)p.G * p.M + p.rows_per_sample - 1) / p.rows_per_sample) : 0;
+  for (int e = threadIdx.x; e < nscale; e += 256) scale_s[e] = p.rscale[e];
+  __syncthreads();
+
+  struct Tile { int g, i0, j0; };
+  auto tile_of = [&](int q) {
+    const int lin = xcd_tile((int)blockIdx.x + q * (int)gridDim.x, total);
+    const int t = lin % ntile, g = lin / ntile;
+    const int tm = t / p.tiles_n;
+    return Tile{g, tm * 64, (t - tm * p.tiles_n) * 64};
+  };
+
+  auto stage = [&](int it, char* buf) {
+    const int q = it / nk, kt = it - q * nk;
+    const Tile tl = tile_of(q);
+    const int k0 = kt * FBK;
+    const E* Ag = reinterpret_cast<const E*>(p.A) + goff(p, tl.g, p.sA, p.sAh);
+    const E* Bg = reinterpret_cast<const E*>(p.B) + goff(p, tl.g, p.sB, p.sBh);
+    if constexpr (TA) {
+      stage_r<64>(make_rsrc(Ag), buf, p.lda, tl.i0, p.M, k0, p.K, w, lane);
+    } else if (k0 < p.K1) {
+      stage_k<64>(make_rsrc(Ag), buf, p.lda, tl.i0, p.M, k0, p.K1, w, lane);
+    } else {
+      const E* A2g = reinterpret_cast<const E*>(p.A2) + (long)tl.g * p.sA2;
+      stage_k<64>(make_rsrc(A2g), buf, p.lda2, tl.i0, p.M, k0 - p.K1, p.K - p.K1, w, lane);
+    }
+    if constexpr (TB) stage_r<64>(make_rsrc(Bg), buf + TILE, p.ldb, tl.j0, p.N, k0, p.K, w, lane);
+    else stage_k<64>(make_rsrc(Bg), buf + TILE, p.ldb, tl.j0, p.N, k0, p.K, w, lane);
+    if constexpr (HR) {
+      // the residual tile (rows i0.., columns j0..) as a k-contiguous image, every slot (the
+      // DMA count per slot is a compile-time constant): past the tile's last k-step it is the
+      // real tile, otherwise out-of-range (zero-filled, no traffic)
+      const E* Rg = reinterpret_cast<const E*>(p.R) + goff(p, tl.g, p.sC, p.sCh);
+      stage_k<64>(make_rsrc(Rg), buf + 2 * TILE, p.ldc, tl.i0, kt == nk - 1 ? p.M : 0, tl.j0, p.N, w, lane);
+    }
+  };
+
+  f32x16 acc = zero16();
+  auto compute = [&](const char* buf) {
+#pragma unroll
+    for (int s = 0; s < FBK / 16; ++s) {
+      frag8<E> fa, fb;
+      if constexpr (TA) fa = frag_r<E, 64>(buf, wm * 32, s, lane);
+      else fa = frag_k<E>(buf, wm * 32, s, lane);
+      if constexpr (TB) fb = frag_r<E, 64>(buf + TILE, wn * 32, s, lane);
+      else fb = frag_k<E>(buf + TILE, wn * 32, s, lane);
+      acc = MF<E>::mma(fb, fa, acc);
+    }
+  };
+
+  // lane (r, h) holds C(i = r, j = 8 g4 + 4 h + 0..3) of its 32 x 32 sub-tile.  Every wave
+  // issues exactly 4 buffer stores per tile (lanes outside the problem store to an
+  // out-of-range offset, which the buffer unit drops), so the counted waits below know how
+  // many stores are younger than the ring's DMAs.
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  auto epilogue = [&](int q, const char* buf) {
+    const Tile tl = tile_of(q);
+    const int il = wm * 32 + r, i = tl.i0 + il;
+    const bool row_ok = i < p.M;
+    float sc = 1.f;
+    if (p.rscale && row_ok) sc = scale_s[((long)tl.g * p.M + i) / p.rows_per_sample];
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<E*>(p.C) + goff(p, tl.g, p.sC, p.sCh), 0, 0x7ffffff0, 0x00020000);
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int jl = wn * 32 + 8 * g4 + 4 * h, j = tl.j0 + jl;
+      const bool ok = row_ok && j < p.N;
+      float v[4] = {acc[4 * g4], acc[4 * g4 + 1], acc[4 * g4 + 2], acc[4 * g4 + 3]};
+      if (p.bias) {
+        const float* bp = bias_s + tl.g * p.N + (ok ? j : 0);
+        v[0] += bp[0]; v[1] += bp[1]; v[2] += bp[2]; v[3] += bp[3];
+      }
+      if (p.act) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = act_fwd(v[e], p.act);
+      }
+      if constexpr (HR) {
+        const int pos = (jl >> 3) ^ ((il >> 1) & 7);
+        const uint2 rv = *reinterpret_cast<const uint2*>(buf + 2 * TILE + il * 128 + pos * 16 + 8 * h);
+        const cmx_f2 r0 = unpack2<E>(rv.x), r1 = unpack2<E>(rv.y);
+        v[0] = r0.x + sc * v[0]; v[1] = r0.y + sc * v[1]; v[2] = r1.x + sc * v[2]; v[3] = r1.y + sc * v[3];
+      }
+      const int off = ok ? (int)(((long)i * p.ldc + j) * 2) : OOB;
+      u32x2 d = {pack2<E>(v[0], v[1]), pack2<E>(v[2], v[3])};
+      __builtin_amdgcn_raw_buffer_store_b64(d, rc, off, 0, 0);
+    }
+  };
+
+  // counted waits: all but the `keep` youngest ring slots landed, plus `st` younger stores
+  auto wait_keep = [](int keep, bool st) {
+    if (st) {
+      if (NS > 3 && keep >= 3) vm_wait<3 * PER + 4>();
+      else if (NS > 2 && keep == 2) vm_wait<2 * PER + 4>();
+      else if (keep >= 1) vm_wait<PER + 4>();
+      else vm_wait<4>();
+    } else {
+      if (NS > 3 && keep >= 3) vm_wait<3 * PER>();
+      else if (NS > 2 && keep == 2) vm_wait<2 * PER>();
+      else if (keep >= 1) vm_wait<PER>();
+      else vm_wait<0>();
+    }
+  };
+
+  const int pro = min(NS - 1, iters);
+#pragma unroll
+  for (int q = 0; q < NS - 1; ++q)
+    if (q < pro) stage(q, smem + q * SLOT);
+  wait_keep(pro - 1, false);
+  raw_barrier();
+  int cur = 0;
+  for (int it = 0; it < iters; ++it) {
+    const int nxt = cur == 0 ? NS - 1 : cur - 1;
+    if (it + NS - 1 < iters) stage(it + NS - 1, smem + nxt * SLOT);
+    compute(smem + cur * SLOT);
+    const int q = it / nk;
+    const bool last = it - q * nk == nk - 1;
+    if (last) {
+      epilogue(q, smem + cur * SLOT);
+      acc = zero16();
+    }
+    const int ahead = min(NS - 1, iters - 1 - it);
+    wait_keep(ahead - 1, last);
+    raw_barrier();
+    cur = cur + 1 == NS ? 0 : cur + 1;
+  }
+  vm_wait<0>();
+}
+
 // ============================================================================ grouped launch
 // Many independent problems in ONE launch (the weight gradients of a whole backward segment,
 // which nothing reads before the optimizer): record r owns blocks [blk0, blk0 + nblk) of the
@@ -1009,6 +1183,66 @@ void launch_fast(const GemmArgs& a, int bm, int bn, int G, int nsplit, int tA, i
   else launch_fast_t<bf16>(a, bm, bn, G, nsplit, tA, tB, s);
 }
 
+// one block per CU (queried once)
+int cu_count() {
+  static const int n = [] {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                               hipSuccess)
+      c = 0;
+    return c > 0 ? c : 256;
+  }();
+  return n;
+}
+
+// Stream-kernel policy (CMX_GEMM_STREAM = the least number of 64 x 64 tiles that takes the
+// persistent kernel, 0 = off; CMX_GEMM_STREAM_NS / _NSR = ring depth without / with a residual
+// image; CMX_GEMM_STREAM_BPC = resident blocks per CU the grid is sized for)
+template <typename E>
+bool launch_stream_t(const GemmArgs& a, int tA, int tB, hipStream_t s) {
+  static int& ns = cmx_knob("GEMM_STREAM_NS", 3);
+  static int& nsr = cmx_knob("GEMM_STREAM_NSR", 2);
+  static int& bpc = cmx_knob("GEMM_STREAM_BPC", 2);
+  const long total = (long)a.tiles_m * a.tiles_n * a.G;
+  long grid = (long)cu_count() * (bpc > 0 ? bpc : 1);
+  if (grid >= total) grid = total;
+  else grid = grid / 8 * 8;
+  const bool hr = a.R != nullptr;
+  const int depth = hr ? nsr : ns;
+#define CMX_STREAM_LAUNCH(NS, HR)                                                                                 \
+  do {                                                                                                            \
+    if (!tA && !tB) hipLaunchKernelGGL((gemm_stream_kernel<false, false, NS, HR, E>), dim3(grid), dim3(256), 0, s, a); \
+    else if (!tA && tB) hipLaunchKernelGGL((gemm_stream_kernel<false, true, NS, HR, E>), dim3(grid), dim3(256), 0, s, a); \
+    else return false;                                                                                            \
+  } while (0)
+  if (hr) {
+    if (depth >= 3) CMX_STREAM_LAUNCH(3, true);
+    else CMX_STREAM_LAUNCH(2, true);
+  } else {
+    if (depth >= 4) CMX_STREAM_LAUNCH(4, false);
+    else if (depth == 3) CMX_STREAM_LAUNCH(3, false);
+    else CMX_STREAM_LAUNCH(2, false);
+  }
+#undef CMX_STREAM_LAUNCH
+  return true;
+}
+
+// the problems the stream kernel takes: 16-bit, one split, plain row-major 16-bit store with
+// the bias / activation / DropPath-residual epilogue, 64 x 64 tiles, enough of them
+bool stream_ok(const GemmArgs& a, int bm, int bn, int splitk, int tA, int dtype) {
+  static int& min_tiles = cmx_knob("GEMM_STREAM", 0);
+  if (min_tiles <= 0 || bm != 64 || bn != 64 || splitk != 1 || tA || a.out_mode != 0 || a.ones_col || a.nup ||
+      a.scatter || a.conv)
+    return false;
+  if ((long)a.tiles_m * a.tiles_n * a.G < min_tiles) return false;
+  if (a.N % 4 || a.ldc % 4 || a.sC % 4 || a.sCh % 4 || ((uintptr_t)a.C & 7)) return false;
+  if ((long)a.M * a.ldc >= (1L << 30) - 64) return false;                      // 31-bit byte offsets
+  if (a.bias && (long)a.G * a.N > ST_BIAS_MAX) return false;
+  if (a.rscale && ((long)a.G * a.M + a.rows_per_sample - 1) / a.rows_per_sample > ST_SCALE_MAX) return false;
+  if (a.R && (a.N % 8 || a.ldc % 8 || a.sC % 8 || ((uintptr_t)a.R & 15))) return false;
+  return dtype == 1 || dtype == 2;
+}
+
 template <typename T, int BM, int BN, bool EXT>
 void launch_generic_x(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream_t s) {
   dim3 grid(a.tiles_m * a.tiles_n, G, nsplit);
@@ -1212,7 +1446,10 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
     int bm, bn;
     plan_tiles(G, M, nb, K, &bm, &bn);
     a.tiles_m = cdiv(M, bm); a.tiles_n = cdiv(nb, bn);
-    launch_fast(a, bm, bn, G, splitk, transA, transB, dtype, s);
+    const bool streamed = stream_ok(a, bm, bn, splitk, transA, dtype) &&
+                          (dtype == 2 ? launch_stream_t<f16>(a, transA, transB, s)
+                                      : launch_stream_t<bf16>(a, transA, transB, s));
+    if (!streamed) launch_fast(a, bm, bn, G, splitk, transA, transB, dtype, s);
   } else {
     // tile shape: the output's narrow side gets 64 (stage-1 C = 64 outputs, 64-row wgrads)
     const bool m64 = M <= 64, n64 = N <= 64;

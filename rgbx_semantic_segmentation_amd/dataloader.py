@@ -155,12 +155,9 @@ class GPUAugmentLoader:
 
     def __iter__(self):
         for items in self.loader:
-            samples = []
-            for it in items:
-                s = tuple(torch.from_numpy(np.ascontiguousarray(it[k])) for k in ("data", "label", "modal_x"))
-                if torch.cuda.is_available():
-                    s = tuple(t.pin_memory() for t in s)
-                samples.append(s)
+            # host arrays go straight into TrainPre.batch's reused pinned staging buffer: one
+            # host-to-device copy and one launch per augmentation stage for the whole minibatch
+            samples = [tuple(it[k] for k in ("data", "label", "modal_x")) for it in items]
             rgb, gt, x = self.pre.batch(samples)
             yield dict(data=rgb, label=gt, modal_x=x, fn=[it["fn"] for it in items], n=items[0]["n"])
 

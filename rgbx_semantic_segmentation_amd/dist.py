@@ -73,7 +73,11 @@ class BucketedGradSync:
         from . import deferred
         if sid in self.launched or sid not in self.ranges:
             return
-        deferred.flush()
+        # a stage-boundary flush may go to the weight-gradient side stream (CMX_WGRAD_SIDE);
+        # the all-reduce then waits for it as well as for the backward so far
+        last = sid == max(self.ranges)
+        side = deferred.WGRAD_SIDE and not last
+        deferred.flush(side=side)
         a, b = self.ranges[sid]
         main = torch.cuda.current_stream() if self.store.grad.is_cuda else None
         if main is None:                         # CPU tensors (gloo tests): blocking, in order
@@ -82,6 +86,8 @@ class BucketedGradSync:
             if self.side is None:
                 self.side = torch.cuda.Stream(device=main.device)
             self.side.wait_stream(main)
+            if side:
+                self.side.wait_stream(deferred.side_stream(main.device))
             with torch.cuda.stream(self.side):
                 self._reduce(self.store.grad[a:b])
             self.works.append(self.side)

@@ -16,6 +16,7 @@ from typing import List, Optional
 import torch
 import torch.nn as nn
 
+from ... import deferred
 from ... import functions as F
 from ... import streams
 from ..net_utils import (FeatureRectifyModule, FeatureFusionModule, ImprovedFeatureRectifyModule,
@@ -47,6 +48,11 @@ def drop_path_probs(depths: List[int], rate: float):
             out.append((p, list(p)))
         cur += d
     return out
+
+
+def _side_flush_hook(grad):
+    deferred.flush(side=True)
+    return None
 
 
 class DWConv(nn.Module):                          # dual_segformer.py:19-33
@@ -177,6 +183,10 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
                 # the gradient of this stage's input exists once the backward has passed the
                 # stage (segment 3 - s): its gradients can be all-reduced while stages < s run
                 x.register_hook(sync.segment_hook(3 - s))
+            elif deferred.WGRAD_SIDE and s > 0 and x.requires_grad and x.is_cuda:
+                # the weight gradients of everything above this stage run on the side stream
+                # beside the input-gradient chain of stages < s (deferred.flush(side=True))
+                x.register_hook(_side_flush_hook)
             x, Ho, Wo = F.conv(store, pe.proj, x, G, G * B, Hc, Wc, Cin, pe.stride, pe.pad, nchw=(s == 0))
             x = F.layernorm(store, pe.norm, x, G)
             Hc, Wc, Cin = Ho, Wo, self.embed_dims[s]

@@ -89,6 +89,38 @@ def test_train_pre_pipeline(dev, seed, h, w, H, W):
     assert np.array_equal(x_g.cpu().numpy(), x_o)
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_train_pre_batch_bit_exact(dev, seed):
+    """TrainPre.batch (one cmx_aug_batch launch per stage for the whole minibatch, pinned
+    staging) vs oracle.train_pre sample by sample with the same draws: bit-exact.  Mixed source
+    sizes, host numpy and device samples in one batch, and three batches in a row so both
+    staging buffers are reused."""
+    from rgbx_semantic_segmentation_amd.augment import TrainPre, draw_params
+    H, W = 48, 64
+    pre = TrainPre(MEAN, STD, 40, H, W, SCALES, 255, rng=random.Random(seed))
+    shadow = random.Random(seed)                       # replays the batch's draws in order
+    rng = np.random.default_rng(200 + seed)
+    for it in range(3):
+        shapes = [(57, 75), (48, 64), (40, 90), (61, 61)][: 2 + it]
+        samples, host = [], []
+        for j, (h, w) in enumerate(shapes):
+            rgb, x = _img(rng, h, w), _img(rng, h, w)
+            gt = _img(rng, h, w, 0)
+            gt[:3, :4] = 255
+            host.append((rgb, gt, x))
+            if j % 2:
+                samples.append(tuple(torch.from_numpy(a).cuda() for a in (rgb, gt, x)))
+            else:
+                samples.append((rgb, gt, x[:, :, ::-1].copy()[:, :, ::-1]))   # non-contiguous-safe copy path
+        r_g, g_g, x_g = pre.batch(samples)
+        for b, (rgb, gt, x) in enumerate(host):
+            prm = draw_params(rgb.shape[0], rgb.shape[1], SCALES, shadow)
+            r_o, g_o, x_o = A.train_pre(rgb, gt, x, prm, 40, H, W, MEAN, STD)
+            assert np.array_equal(g_g[b].cpu().numpy(), g_o), (it, b)
+            assert np.array_equal(r_g[b].cpu().numpy(), r_o), (it, b)
+            assert np.array_equal(x_g[b].cpu().numpy(), x_o), (it, b)
+
+
 def test_train_pre_batch_and_loader(dev, tmp_path):
     """get_train_loader(engine, RGBXDataset, config) on PNG files: device batches of the
     reference's dict shape, label values in [0, K-1] or the cutout background."""

@@ -31,13 +31,18 @@ def test_train_loop_and_resume(dev, tmp_path, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_segment_allreduce_sees_final_gradients(dev):
+@pytest.mark.parametrize("wgrad_side", [False, True])
+def test_segment_allreduce_sees_final_gradients(dev, monkeypatch, wgrad_side):
     """The overlapped gradient exchange (dist.BucketedGradSync) must reduce each segment only
     after every gradient in it is final.  World-size-1 rehearsal: the "all-reduce" doubles its
     segment on the side stream; any gradient written after its segment was launched stays
-    undoubled and shows up against 2x the gradients of a plain backward."""
+    undoubled and shows up against 2x the gradients of a plain backward.  wgrad_side: the
+    segment's weight gradients are themselves on the weight-gradient side stream
+    (CMX_WGRAD_SIDE), which the all-reduce must also wait for."""
+    from rgbx_semantic_segmentation_amd import deferred
     from rgbx_semantic_segmentation_amd.dist import BucketedGradSync
     from rgbx_semantic_segmentation_amd.models.builder import EncoderDecoder
+    monkeypatch.setattr(deferred, "WGRAD_SIDE", wgrad_side)
 
     class Doubling(BucketedGradSync):
         def _world(self):
@@ -69,6 +74,52 @@ def test_segment_allreduce_sees_final_gradients(dev):
     torch.cuda.synchronize()
     bad = (model.store.grad - 2 * ref).abs() > 1e-6 * (1 + ref.abs())
     assert not bad.any(), f"{int(bad.sum())} gradient elements were reduced before they were final"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
+def test_wgrad_side_stream_matches_single_stream(dev, monkeypatch, dtype):
+    """CMX_WGRAD_SIDE: the weight gradients of the stages above each stage boundary run as
+    grouped launches on a side stream beside the input-gradient chain below it.  Every problem
+    keeps its own tile / split choice, so the gradients must equal the single-stream backward's
+    bit for bit, eagerly and replayed from a HIP graph."""
+    from rgbx_semantic_segmentation_amd import deferred
+    from rgbx_semantic_segmentation_amd.models.builder import EncoderDecoder
+    torch.manual_seed(0)
+    model = EncoderDecoder(dict(backbone="mit_b0", num_classes=9, compute_dtype=dtype,
+                                decoder_embed_dim=256)).to(dev)
+    model.eval()
+    g = torch.Generator().manual_seed(4)
+    rgb = torch.randn(2, 3, 64, 96, generator=g).to(dev)
+    x = torch.randn(2, 3, 64, 96, generator=g).to(dev)
+    lab = torch.randint(0, 9, (2, 64, 96), generator=g).to(dev)
+    monkeypatch.setattr(deferred, "WGRAD_SIDE", False)
+    model(rgb, x, lab).backward()
+    torch.cuda.synchronize()
+    ref = model.store.grad.clone()
+    monkeypatch.setattr(deferred, "WGRAD_SIDE", True)
+    model.store.grad.zero_()
+    model(rgb, x, lab).backward()
+    assert not deferred._side_used, "the end-of-backward flush did not join the side stream"
+    torch.cuda.synchronize()
+    assert torch.equal(model.store.grad, ref), float((model.store.grad - ref).abs().max())
+    # the same inside a HIP graph (fork / join as graph edges)
+    deferred.reserve()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        model(rgb, x, lab).backward()
+    torch.cuda.current_stream().wait_stream(s)
+    import gc
+    gc.collect()
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+        model(rgb, x, lab).backward()
+    model.store.grad.zero_()
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(model.store.grad, ref), float((model.store.grad - ref).abs().max())
 
 
 @pytest.mark.gpu
