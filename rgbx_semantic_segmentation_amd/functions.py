@@ -46,6 +46,42 @@ def _fwd_gemm(x, W, b, y, act="none", res=None, rscale=None, rps=1, x2=None):
     return y
 
 
+# CMX_LN_FUSE: the norm that follows a residual GEMM (proj -> norm2, fc2 -> next norm1 / the
+# stage norm) computed in that GEMM's epilogue (cmx_gemm_ln) on the streams of these widths:
+# "1" = 64 and 128 channels, "64" = 64 only, "0" (default) = every norm its own launch
+_LN_FUSE_ENV = os.environ.get("CMX_LN_FUSE", "0")
+LN_FUSE = {"0": (), "1": (64, 128), "64": (64,), "128": (128,)}.get(_LN_FUSE_ENV, ())
+
+
+class LNStash:
+    """Forward side channel from a residual GEMM to the LayerNorm that consumes its output:
+    the GEMM's epilogue computed (y, mean, rstd) = LN(x) for ``gamma`` / ``beta`` / ``eps``;
+    the norm (layernorm_res(..., pre=stash)) takes them instead of launching, after checking
+    they were made from the same tensor."""
+    __slots__ = ("gamma", "beta", "eps", "src", "y", "mean", "rstd")
+
+    def __init__(self, gamma, beta, eps):
+        self.gamma, self.beta, self.eps = gamma, beta, eps
+        self.src = self.y = self.mean = self.rstd = None
+
+    def take(self, x, gamma, beta, eps):
+        if (self.src is None or self.src.data_ptr() != x.data_ptr() or self.src.shape != x.shape
+                or gamma.data_ptr() != self.gamma.data_ptr() or beta.data_ptr() != self.beta.data_ptr()
+                or eps != self.eps):
+            return None
+        out = (self.y, self.mean, self.rstd)
+        self.src = self.y = self.mean = self.rstd = None
+        return out
+
+
+def ln_stash(store, mod, G):
+    """An LNStash for norm ``mod`` when the LN fusion is on for its width, else None."""
+    if mod.weight.shape[-1] not in LN_FUSE:
+        return None
+    return LNStash(store.w(mod.weight, compute=False).view(G, -1), store.w(mod.bias, compute=False).view(G, -1),
+                   mod.eps)
+
+
 class GLinear(Function):
     """y[g] = act(x1[g] @ W[g][:, :k1]^T (+ x2[g] @ W[g][:, k1:]^T) + b[g]), optionally
     y = res + rscale[sample] * (...)  (nn.Linear / 1x1 Conv2d; the two-input form replaces
@@ -54,12 +90,21 @@ class GLinear(Function):
     x + drop_path(proj/fc2(...)), dual_segformer.py:168-169)."""
 
     @staticmethod
-    def forward(ctx, W, Wg, b, bg, anchor, act, res, rscale, rps, x1, x2, tap=None):
+    def forward(ctx, W, Wg, b, bg, anchor, act, res, rscale, rps, x1, x2, tap=None, ln=None):
         G, N, Ktot = W.shape
         M = x1.shape[1]
         assert x1.shape[-1] + (x2.shape[-1] if x2 is not None else 0) == Ktot, (x1.shape, W.shape)
         y = torch.empty(G, M, N, dtype=x1.dtype, device=x1.device)
-        _fwd_gemm(x1, W, b, y, act=act, res=res, rscale=rscale, rps=rps, x2=x2)
+        if ln is not None and K.gemm_ln_ok(x1, y):
+            # the consumer norm's forward in this GEMM's epilogue (LNStash)
+            ly = torch.empty_like(y)
+            mean = torch.empty(G * M, dtype=torch.float32, device=y.device)
+            rstd = torch.empty(G * M, dtype=torch.float32, device=y.device)
+            K.gemm_ln(x1, W, y, ly, ln.gamma, ln.beta, mean, rstd, ln.eps, bias=b, residual=res, rscale=rscale,
+                      rows_per_sample=rps, act=act, A2=x2)
+            ln.src, ln.y, ln.mean, ln.rstd = y, ly, mean, rstd
+        else:
+            _fwd_gemm(x1, W, b, y, act=act, res=res, rscale=rscale, rps=rps, x2=x2)
         ctx.save_for_backward(W, x1, x2, y if act == "relu" else None)
         ctx.meta = (Wg, bg, act, res is not None, rscale, rps, tap)
         return y
@@ -89,12 +134,13 @@ class GLinear(Function):
         _wgrad_into(dz, x1, Wg[:, :, :k1], bg)
         if x2 is not None:
             _wgrad_into(dz, x2, Wg[:, :, k1:])
-        return (None, None, None, None, None, None, dres, None, None, dx1, dx2, None)
+        return (None, None, None, None, None, None, dres, None, None, dx1, dx2, None, None)
 
 
-def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1, tap=None):
+def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1, tap=None, ln=None):
     """Grouped linear using parameter ``wp`` (and bias ``bp``) of the store; x2 = second
-    input segment (cat-free), res/rscale/rps = fused DropPath residual (rps = rows per sample)."""
+    input segment (cat-free), res/rscale/rps = fused DropPath residual (rps = rows per sample);
+    ln = LNStash of the norm that consumes the output (its forward then runs in the epilogue)."""
     W = store.w(wp)
     Wg = store.g(wp)
     G = W.shape[0]
@@ -104,7 +150,7 @@ def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1
     if bp is not None:
         b = store.w(bp, compute=False).view(G, -1)
         bg = store.g(bp).view(G, -1)
-    return GLinear.apply(W, Wg, b, bg, wp, act, res, rscale, rps, x1, x2, tap)
+    return GLinear.apply(W, Wg, b, bg, wp, act, res, rscale, rps, x1, x2, tap, ln)
 
 
 # ---------------------------------------------------------------------------- LayerNorm
@@ -133,8 +179,12 @@ class LayerNormResF(Function):
     scale[sample] * dx for the producer of x (GradTap)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, gg, bg, eps, G, scale, rps, tap, anchor):
-        y, mean, rstd = K.layernorm_fwd(x, gamma, beta, eps, G=G)
+    def forward(ctx, x, gamma, beta, gg, bg, eps, G, scale, rps, tap, anchor, pre=None):
+        got = pre.take(x, gamma, beta, eps) if pre is not None else None
+        if got is not None:
+            y, mean, rstd = got                      # computed by the producing GEMM's epilogue
+        else:
+            y, mean, rstd = K.layernorm_fwd(x, gamma, beta, eps, G=G)
         ctx.save_for_backward(x, gamma, mean, rstd)
         ctx.meta = (gg, bg, G, scale, rps, tap)
         ctx.set_materialize_grads(False)     # unused outputs arrive as None, not zero-filled tensors
@@ -165,16 +215,17 @@ class LayerNormResF(Function):
             deferred.reduce(ws, gg, bg, G, nb, nb * 2 * C, 2 * C, 1, 2 * C, C, gg.stride(0), 0, bg.stride(0), 0)
         if dxs is not None:
             tap.put(dxs)
-        return dx, None, None, None, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None, None, None, None
 
 
-def layernorm_res(store, mod, x, G, scale=None, rps=1, tap=None):
-    """(LN(x), LN(x) for a second consumer, x) with the fused backward (LayerNormResF)."""
+def layernorm_res(store, mod, x, G, scale=None, rps=1, tap=None, pre=None):
+    """(LN(x), LN(x) for a second consumer, x) with the fused backward (LayerNormResF).
+    pre: the LNStash the producing GEMM filled (forward already computed), or None."""
     gamma = store.w(mod.weight, compute=False).view(G, -1)
     beta = store.w(mod.bias, compute=False).view(G, -1)
     gg = store.g(mod.weight).view(G, -1)
     bg = store.g(mod.bias).view(G, -1)
-    return LayerNormResF.apply(x, gamma, beta, gg, bg, mod.eps, G, scale, rps, tap, mod.weight)
+    return LayerNormResF.apply(x, gamma, beta, gg, bg, mod.eps, G, scale, rps, tap, mod.weight, pre)
 
 
 class LayerNormF(Function):
@@ -802,17 +853,27 @@ def pair_embed(store, ce, o):
 
 
 # ---------------------------------------------------------------------------- FRM
+# CMX_FRM_CHANNEL=1: ChannelWeights as the one-launch grid-barrier kernels (cmx_frm_channel_*).
+# Off by default: inside the step they cost 80-190 us per launch (r03_h census: 1.0 ms per step
+# for the eight launches, against ~0.3 ms for the multi-launch path) -- a grid barrier needs
+# every one of its 256 blocks resident, and beside the FFM side stream's kernels the resident
+# blocks spin until the rest get a CU.
+FRM_ONE_LAUNCH = os.environ.get("CMX_FRM_CHANNEL", "0") == "1"
+
+
 class FRMF(Function):
     """FeatureRectifyModule (net_utils.py:124-152) on x (2, B, N, C).
 
-    Forward (3 launches): ChannelWeights (:11-30) -- avg || max pooling and the two-layer channel
-    MLP -- as ONE grid-barrier kernel (cmx_frm_channel_fwd), the SpatialWeights 2C -> C 1x1 conv
-    as a cat-free GEMM, and ONE kernel for SpatialWeights' C -> 2 conv + sigmoid fused with the
-    rectification.
-    Backward (3 launches + 2 deferred wgrads): one kernel for the rectification + spatial-head
-    backward (dx direct path, dh, dcw / dw2 partials), one G = 2 dgrad GEMM adding both modality
-    slices of the 2C -> C conv into dx, and the channel branch backward as ONE grid-barrier kernel
-    (cmx_frm_channel_bwd: dcw slab sum, W2 pass, W1 pass, pooling gradient into dx)."""
+    Forward (6 launches): avg || max pooling (partial + final), the two-layer channel MLP
+    (ChannelWeights, :16-30), the SpatialWeights 2C -> C 1x1 conv as a cat-free GEMM, and ONE
+    kernel for SpatialWeights' C -> 2 conv + sigmoid fused with the rectification.
+    Backward (7 launches): one kernel for the rectification + spatial-head backward (dx direct
+    path, dh, dcw / dw2 partials), one G = 2 dgrad GEMM adding both modality slices of the 2C -> C
+    conv into dx, the dcw partial sum, the channel MLP backward as one pass over each weight
+    matrix (dz formed from the producer's partial slices, dW / db written, dx left as partial
+    slices), and the pooling backward summing those slices itself.
+    With CMX_FRM_CHANNEL=1 the channel branch is ONE grid-barrier kernel per direction
+    (cmx_frm_channel_fwd / _bwd) instead."""
 
     @staticmethod
     def forward(ctx, x, prm, anchor):
@@ -823,10 +884,17 @@ class FRMF(Function):
         argmax = torch.empty(B, 2 * C, dtype=torch.int32, device=x.device)
         y1 = torch.empty(B, 4 * C, dtype=torch.float32, device=x.device)
         cw = torch.empty(B, 2 * C, dtype=torch.float32, device=x.device)
-        # ChannelWeights (net_utils.py:11-30): avg || max pool + both MLP GEMVs, one launch
-        ws = K._ws(K.query("cmx_frm_channel_fwd_workspace", B, N, C), x.device)
-        K.call("cmx_frm_channel_fwd", K.ptr(x), K.ptr(W1), K.ptr(b1), K.ptr(W2), K.ptr(b2), K.ptr(pooled),
-               K.ptr(argmax), K.ptr(y1), K.ptr(cw), K.ptr(ws), B, N, C, dt, K.stream())
+        # ChannelWeights (net_utils.py:11-30): avg || max pool + both MLP GEMVs
+        if FRM_ONE_LAUNCH:
+            ws = K._ws(K.query("cmx_frm_channel_fwd_workspace", B, N, C), x.device)
+            K.call("cmx_frm_channel_fwd", K.ptr(x), K.ptr(W1), K.ptr(b1), K.ptr(W2), K.ptr(b2), K.ptr(pooled),
+                   K.ptr(argmax), K.ptr(y1), K.ptr(cw), K.ptr(ws), B, N, C, dt, K.stream())
+        else:
+            ws = K._ws(K.query("cmx_frm_pool_workspace", B, N, C), x.device)
+            K.call("cmx_frm_pool_fwd", K.ptr(x), K.ptr(pooled), K.ptr(argmax), K.ptr(ws), B, N, C, dt, K.stream())
+            K.call("cmx_small_linear_fwd", K.ptr(pooled), K.ptr(W1), K.ptr(b1), K.ptr(y1), B, 4 * C, 4 * C, 2,
+                   K.stream())
+            K.call("cmx_small_linear_fwd", K.ptr(y1), K.ptr(W2), K.ptr(b2), K.ptr(cw), B, 4 * C, 2 * C, 3, K.stream())
         # h = cat(x1, x2) W0^T + b0 (SpatialWeights' first 1x1 conv, net_utils.py:72-73), cat-free
         h = torch.empty(1, B * N, C, dtype=x.dtype, device=x.device)
         K.gemm(x[0].view(1, B * N, C), W0[None], h, bias=b0[None], A2=x[1].view(1, B * N, C))
@@ -867,12 +935,25 @@ class FRMF(Function):
         K.gemm(dh[None].expand(2, B * N, C), Wd.transpose(1, 2), dx2, residual=dx2)
         _wgrad_into(dh[None], x[0].view(1, B * N, C), gW0[None, :, :C], gb0.view(1, C))
         _wgrad_into(dh[None], x[1].view(1, B * N, C), gW0[None, :, C:])
-        # channel MLP + pooling backward in one launch: dcw partial slabs (B, nb, 2C) -> W2 pass ->
-        # W1 pass -> pooling gradient added into dx
-        cws = K._ws(K.query("cmx_frm_channel_bwd_workspace", B, C), x.device)
-        K.call("cmx_frm_channel_bwd", K.ptr(ws), nb, K.ptr(cw), K.ptr(y1), K.ptr(pooled), K.ptr(argmax), K.ptr(W1),
-               K.ptr(W2), K.ptr(gW1), K.ptr(gb1), K.ptr(gW2), K.ptr(gb2), K.ptr(dx), K.ptr(cws), B, N, C, dt,
-               K.stream())
+        if FRM_ONE_LAUNCH:
+            # channel MLP + pooling backward in one launch: dcw partial slabs (B, nb, 2C) -> W2 pass ->
+            # W1 pass -> pooling gradient added into dx
+            cws = K._ws(K.query("cmx_frm_channel_bwd_workspace", B, C), x.device)
+            K.call("cmx_frm_channel_bwd", K.ptr(ws), nb, K.ptr(cw), K.ptr(y1), K.ptr(pooled), K.ptr(argmax),
+                   K.ptr(W1), K.ptr(W2), K.ptr(gW1), K.ptr(gb1), K.ptr(gW2), K.ptr(gb2), K.ptr(dx), K.ptr(cws), B, N,
+                   C, dt, K.stream())
+            return dx, None, None
+        # channel MLP backward: dcw partial slabs (B, nb, 2C) -> W2 pass -> W1 pass -> pooling
+        ns = K.query("cmx_small_linear_nslice")
+        dcw = torch.empty(B, 2 * C, dtype=torch.float32, device=x.device)      # sum of the nb partial slabs
+        K.call("cmx_partials_sum", K.ptr(ws), K.ptr(dcw), B, nb, 2 * C, 0, 1.0, K.stream())
+        dy1p = torch.empty(ns, B, 4 * C, dtype=torch.float32, device=x.device)
+        K.call("cmx_small_linear_bwd", K.ptr(dcw), 1, 0, 2 * C, K.ptr(cw), K.ptr(y1), K.ptr(W2), K.ptr(dy1p),
+               K.ptr(gW2), K.ptr(gb2), B, 4 * C, 2 * C, 3, 0, K.stream())
+        dpp = torch.empty(ns, B, 4 * C, dtype=torch.float32, device=x.device)
+        K.call("cmx_small_linear_bwd", K.ptr(dy1p), ns, B * 4 * C, 4 * C, K.ptr(y1), K.ptr(pooled), K.ptr(W1),
+               K.ptr(dpp), K.ptr(gW1), K.ptr(gb1), B, 4 * C, 4 * C, 2, 0, K.stream())
+        K.call("cmx_frm_pool_bwd", K.ptr(dpp), ns, B * 4 * C, K.ptr(argmax), K.ptr(dx), B, N, C, dt, K.stream())
         return dx, None, None
 
 

@@ -133,18 +133,20 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
                 rows.append((1.0 - self.dp[s][0][i], 1.0 - self.dp[s][1][i]))
         return rows
 
-    def run_block(self, store, blk: Block, x, B, H, W, s_attn, s_mlp, prev=(None, None)):
+    def run_block(self, store, blk: Block, x, B, H, W, s_attn, s_mlp, prev=(None, None, None), next_norm=None):
         """One Block (dual_segformer.py:166-180) for both streams.  ``prev`` = (DropPath scale,
-        GradTap) of the residual branch that produced ``x`` (the previous block's fc2): norm1's
-        backward writes that branch's scaled gradient.  Returns (x_out, (s_mlp, tap)) for the
-        next consumer of x_out."""
+        GradTap, LNStash) of the residual branch that produced ``x`` (the previous block's fc2):
+        norm1's backward writes that branch's scaled gradient, and its forward was computed by
+        that GEMM's epilogue when the stash holds it.  ``next_norm`` = the norm that consumes
+        x_out (the next block's norm1 or the stage norm): fc2's epilogue computes it.  Returns
+        (x_out, (s_mlp, tap, stash)) for the next consumer of x_out."""
         G, M, C = x.shape
         N = H * W
         a = blk.attn
         # norm1 also passes x through for the attention residual: its backward sums both gradients
         # (q and the SR path read norm1's output through separate handles: the norm's backward
         # sums their gradients on load)
-        h, h2, xr = F.layernorm_res(store, blk.norm1, x, G, scale=prev[0], rps=N, tap=prev[1])
+        h, h2, xr = F.layernorm_res(store, blk.norm1, x, G, scale=prev[0], rps=N, tap=prev[1], pre=prev[2])
         q = F.glinear(store, a.q.weight, a.q.bias, h)
         if a.sr_ratio > 1:
             R = a.sr_ratio
@@ -157,13 +159,15 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
         o = F.SRAttentionF.apply(q, kv, G * B, N, Nk, a.num_heads, C // a.num_heads)
         # x + drop_path(proj(o)): residual and DropPath scale fused into the proj GEMM epilogue
         tap_a = F.GradTap() if s_attn is not None else None
-        x = F.glinear(store, a.proj.weight, a.proj.bias, o, res=xr, rscale=s_attn, rps=N, tap=tap_a)
-        h, _, xr = F.layernorm_res(store, blk.norm2, x, G, scale=s_attn, rps=N, tap=tap_a)
+        st2 = F.ln_stash(store, blk.norm2, G)
+        x = F.glinear(store, a.proj.weight, a.proj.bias, o, res=xr, rscale=s_attn, rps=N, tap=tap_a, ln=st2)
+        h, _, xr = F.layernorm_res(store, blk.norm2, x, G, scale=s_attn, rps=N, tap=tap_a, pre=st2)
         f = F.glinear(store, blk.mlp.fc1.weight, blk.mlp.fc1.bias, h)
         f = F.dwconv(store, blk.mlp.dwconv.dwconv, f, G * B, B, H, W, "gelu")
         tap_m = F.GradTap() if s_mlp is not None else None
-        x = F.glinear(store, blk.mlp.fc2.weight, blk.mlp.fc2.bias, f, res=xr, rscale=s_mlp, rps=N, tap=tap_m)
-        return x, (s_mlp, tap_m)
+        stn = F.ln_stash(store, next_norm, G) if next_norm is not None else None
+        x = F.glinear(store, blk.mlp.fc2.weight, blk.mlp.fc2.bias, f, res=xr, rscale=s_mlp, rps=N, tap=tap_m, ln=stn)
+        return x, (s_mlp, tap_m, stn)
 
     def run(self, store, images, B, H, W, training, dp_scales: Optional[torch.Tensor], bn_group=None):
         """images: (2*B, 3, H, W) fp32 NCHW (RGB batch then X batch).
@@ -190,16 +194,18 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
             x, Ho, Wo = F.conv(store, pe.proj, x, G, G * B, Hc, Wc, Cin, pe.stride, pe.pad, nchw=(s == 0))
             x = F.layernorm(store, pe.norm, x, G)
             Hc, Wc, Cin = Ho, Wo, self.embed_dims[s]
-            prev = (None, None)
-            for i, blk in enumerate(getattr(self, f"block{s + 1}")):
+            prev = (None, None, None)
+            blocks = getattr(self, f"block{s + 1}")
+            snorm = getattr(self, f"norm{s + 1}")
+            for i, blk in enumerate(blocks):
                 sa = sm = None
                 if dp_scales is not None:
                     sa, sm = dp_scales[bi, 0], dp_scales[bi, 1]
-                x, prev = self.run_block(store, blk, x, B, Hc, Wc, sa, sm, prev)
+                nxt = blocks[i + 1].norm1 if i + 1 < len(blocks) else snorm
+                x, prev = self.run_block(store, blk, x, B, Hc, Wc, sa, sm, prev, next_norm=nxt)
                 bi += 1
             # stage norm: its backward also writes the last block's DropPath-scaled gradient
-            x, _, _ = F.layernorm_res(store, getattr(self, f"norm{s + 1}"), x, G, scale=prev[0], rps=Hc * Wc,
-                                      tap=prev[1])
+            x, _, _ = F.layernorm_res(store, snorm, x, G, scale=prev[0], rps=Hc * Wc, tap=prev[1], pre=prev[2])
             C = self.embed_dims[s]
             fr = self.FRMs[s]
             if isinstance(fr, ImprovedFeatureRectifyModule):

@@ -310,3 +310,48 @@ def test_gemm_stream_epilogues(stream_on, dtype, act, res, nsr):
     Kn.gemm(x1, W, C, bias=bias[:, :1].expand(G, 128).contiguous(), A2=x2)
     ref = torch.bmm(torch.cat([x1, x2], -1).float(), W.float().transpose(1, 2)) + bias[:, :1, None]
     assert rel(C, ref) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("G,M,N,K", [(2, 38400, 64, 64), (2, 38400, 64, 256), (2, 9600, 128, 128), (2, 9600, 128, 512),
+                                     (2, 1001, 64, 96), (1, 700, 128, 320)])
+@pytest.mark.parametrize("res", [False, True])
+def test_gemm_ln_epilogue(dev, dtype, G, M, N, K, res):
+    """cmx_gemm_ln: the residual GEMM's output C and LayerNorm(C) (the Block's next norm,
+    dual_segformer.py:166-169) from one launch, against torch's layer_norm of the STORED C
+    (the norm reads the 16-bit rows in the unfused path too); per-row mean / rstd against
+    the same.  Shapes: stage-1 / stage-2 proj and fc2 (one- and k-group tiles), ragged rows."""
+    from rgbx_semantic_segmentation_amd import kernels as Kn
+    torch.manual_seed(9)
+    rps = M // 2 if M % 2 == 0 else M
+    A = torch.randn(G, M, K, device="cuda").to(dtype)
+    B = (torch.randn(G, N, K, device="cuda") / K ** 0.5).to(dtype)
+    bias = torch.randn(G, N, device="cuda")
+    R = torch.randn(G, M, N, device="cuda").to(dtype) if res else None
+    s = torch.rand(G * M // rps, device="cuda") * 1.5 if res else None
+    gamma = torch.randn(G, N, device="cuda")
+    beta = torch.randn(G, N, device="cuda")
+    C = torch.empty(G, M, N, device="cuda", dtype=dtype)
+    Y = torch.empty_like(C)
+    mean = torch.empty(G * M, device="cuda")
+    rstd = torch.empty(G * M, device="cuda")
+    Kn.gemm_ln(A, B, C, Y, gamma, beta, mean, rstd, 1e-6, bias=bias, residual=R, rscale=s, rows_per_sample=rps)
+    C2 = torch.empty_like(C)
+    Kn.gemm(A, B, C2, bias=bias, residual=R, rscale=s, rows_per_sample=rps)
+    # the plain call may split K (few tiles): same values within one 16-bit rounding
+    assert ((C.float() - C2.float()).abs() <= C2.float().abs() * 2 ** -7 + 1e-3).all()
+    ref = ref_epi(torch.bmm(A.float(), B.float().transpose(1, 2)), bias, "none", R, s, rps)
+    assert rel(C, ref) < 1e-2
+    Cf = C.float()
+    for g in range(G):
+        yr = F.layer_norm(Cf[g], (N,), gamma[g], beta[g], 1e-6)
+        assert (Y[g].float() - yr).abs().max().item() < 3e-2 * max(1.0, yr.abs().max().item() / 8)
+        mu = Cf[g].mean(-1)
+        rs = torch.rsqrt(Cf[g].var(-1, unbiased=False) + 1e-6)
+        assert torch.allclose(mean[g * M:(g + 1) * M], mu, atol=1e-5, rtol=1e-5)
+        assert torch.allclose(rstd[g * M:(g + 1) * M], rs, atol=1e-4, rtol=1e-4)
+    # the unfused norm kernel on the stored rows gives the same statistics
+    y2, m2, r2 = Kn.layernorm_fwd(C, gamma, beta, 1e-6, G=G)
+    assert torch.allclose(m2.view(-1), mean, atol=1e-6, rtol=1e-6)
+    assert torch.allclose(r2.view(-1), rstd, atol=1e-5, rtol=1e-5)
+    assert ((Y.float() - y2.float()).abs() <= 2 ** -7 * y2.float().abs() + 1e-3).all()

@@ -176,3 +176,36 @@ def test_grad_scaler_matches_torch_grad_scaler(dev):
               f"adamw steps {opt.step_t.item():g}, max(|dp| - 1e-6|p|) {worst:.2e}")
         assert worst <= 1e-8, (it, kind, worst)
     assert sc.get_scale() == 2.0 ** 10 and float(opt.step_t.item()) == 5.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+def test_ln_fusion_matches_unfused(dev, monkeypatch, dtype):
+    """CMX_LN_FUSE: the norm after each residual GEMM on the 64 / 128-channel stages (norm2 after
+    proj, the next norm1 / stage norm after fc2) is computed in that GEMM's epilogue.  Same
+    statistics over the same stored rows as the LayerNorm kernel, so the step's loss, logits
+    and every gradient match the unfused step (within 16-bit output rounding of the norm)."""
+    from rgbx_semantic_segmentation_amd import functions as F
+    from rgbx_semantic_segmentation_amd.models.builder import EncoderDecoder
+    torch.manual_seed(0)
+    model = EncoderDecoder(dict(backbone="mit_b2", num_classes=9, compute_dtype=dtype,
+                                decoder_embed_dim=256)).to(dev)
+    model.eval()
+    g = torch.Generator().manual_seed(5)
+    rgb = torch.randn(2, 3, 96, 128, generator=g).to(dev)
+    x = torch.randn(2, 3, 96, 128, generator=g).to(dev)
+    lab = torch.randint(0, 9, (2, 96, 128), generator=g).to(dev)
+    res = {}
+    for fuse in (False, True):
+        monkeypatch.setattr(F, "LN_FUSE", (64, 128) if fuse else ())
+        with torch.no_grad():
+            logits = model(rgb, x).float()
+        loss = model(rgb, x, lab)
+        loss.backward()
+        torch.cuda.synchronize()
+        res[fuse] = (logits, loss.item(), model.store.grad.clone())
+    (l0, s0, g0), (l1, s1, g1) = res[False], res[True]
+    assert abs(s0 - s1) <= 2e-3 * abs(s0), (s0, s1)
+    assert ((l0 - l1).abs().max() / l0.abs().max()).item() < 2e-2
+    err = ((g0 - g1).abs().max() / g0.abs().max()).item()
+    assert err < 5e-2, err
