@@ -102,6 +102,9 @@ int cmx_dwconv3x3_bwd(const void* da, const void* h, const float* w, const float
  *      stored (Cout, kh, kw, Cin)); the NCHW variant takes the fp32 input image. */
 int cmx_im2col_nhwc(const void* x, void* cols, int NI, int H, int W, int C, int KH, int KW, int stride, int pad, int Ho, int Wo, int64_t ldc, int dtype, hipStream_t stream);
 int cmx_im2col_nchw_f32(const float* x, void* cols, int NI, int C, int H, int W, int KH, int KW, int stride, int pad, int Ho, int Wo, int64_t ldc, int dtype, hipStream_t stream);
+/* the same over two image batches: images n < nsplit from x, the rest from x2 (the RGB and X
+ * inputs of EncoderDecoder.forward without the concat, builder.py:240-253) */
+int cmx_im2col_nchw2_f32(const float* x, const float* x2, int nsplit, void* cols, int NI, int C, int H, int W, int KH, int KW, int stride, int pad, int Ho, int Wo, int64_t ldc, int dtype, hipStream_t stream);
 int cmx_col2im_nhwc(const void* cols, void* dx, int NI, int H, int W, int C, int KH, int KW, int stride, int pad, int Ho, int Wo, int64_t ldc, int dtype, hipStream_t stream);
 
 /* ---- FFM cross attention (CrossAttention.forward, net_utils.py:199-214):

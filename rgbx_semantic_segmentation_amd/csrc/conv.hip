@@ -54,7 +54,8 @@ __global__ void zero_pad_cols_kernel(T* __restrict__ cols, long rows, int K, lon
 template <typename T>
 __global__ __launch_bounds__(256) void im2col_nchw_kernel(const float* __restrict__ x, T* __restrict__ cols, int NI,
                                                           int C, int H, int W, int KH, int KW, int stride, int pad,
-                                                          int Ho, int Wo, long ldc) {
+                                                          int Ho, int Wo, long ldc, const float* __restrict__ x2,
+                                                          int nsplit) {
   const int K = C * KH * KW;
   const int cpr = (int)(ldc / 8);
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
@@ -71,7 +72,8 @@ __global__ __launch_bounds__(256) void im2col_nchw_kernel(const float* __restric
     float t = 0.f;
     if (k0 + j < K) {
       const int iy = oy * stride - pad + kh, ix = ox * stride - pad + kw;
-      if (iy >= 0 && iy < H && ix >= 0 && ix < W) t = x[(((long)n * C + c) * H + iy) * W + ix];
+      if (iy >= 0 && iy < H && ix >= 0 && ix < W)
+        t = n < nsplit ? x[(((long)n * C + c) * H + iy) * W + ix] : x2[(((long)(n - nsplit) * C + c) * H + iy) * W + ix];
     }
     v[j] = t;
     if (++kw == KW) {
@@ -144,8 +146,19 @@ int cmx_im2col_nhwc(const void* x, void* cols, int NI, int H, int W, int C, int 
   return cmx_check_launch("im2col_nhwc");
 }
 
+int cmx_im2col_nchw2_f32(const float* x, const float* x2, int nsplit, void* cols, int NI, int C, int H, int W, int KH,
+                         int KW, int stride, int pad, int Ho, int Wo, int64_t ldc, int dtype, hipStream_t s);
+
 int cmx_im2col_nchw_f32(const float* x, void* cols, int NI, int C, int H, int W, int KH, int KW, int stride,
                         int pad, int Ho, int Wo, int64_t ldc, int dtype, hipStream_t s) {
+  return cmx_im2col_nchw2_f32(x, x, NI, cols, NI, C, H, W, KH, KW, stride, pad, Ho, Wo, ldc, dtype, s);
+}
+
+// images n < nsplit from x, the rest from x2 (the RGB and X batches of EncoderDecoder.forward,
+// builder.py:240-253, without concatenating them first)
+int cmx_im2col_nchw2_f32(const float* x, const float* x2, int nsplit, void* cols, int NI, int C, int H, int W, int KH,
+                         int KW, int stride, int pad, int Ho, int Wo, int64_t ldc, int dtype, hipStream_t s) {
+  CMX_REQUIRE(x && x2 && nsplit >= 0 && nsplit <= NI, CMX_ERR_ARG, "im2col_nchw2: nsplit %d of %d", nsplit, NI);
   CMX_REQUIRE(ldc >= (long)KH * KW * C && ldc % 8 == 0, CMX_ERR_SHAPE, "im2col_nchw: ldc %ld (>= K, multiple of 8)",
               (long)ldc);
   CMX_REQUIRE(Ho == (H + 2 * pad - KH) / stride + 1 && Wo == (W + 2 * pad - KW) / stride + 1, CMX_ERR_SHAPE,
@@ -153,7 +166,7 @@ int cmx_im2col_nchw_f32(const float* x, void* cols, int NI, int C, int H, int W,
   CMX_DISPATCH(dtype, T, {
     hipLaunchKernelGGL(im2col_nchw_kernel<T>, dim3((unsigned)(((long)NI * Ho * Wo * (ldc / 8) + 255) / 256)), dim3(256),
                        0, s, x,
-                       (T*)cols, NI, C, H, W, KH, KW, stride, pad, Ho, Wo, (long)ldc);
+                       (T*)cols, NI, C, H, W, KH, KW, stride, pad, Ho, Wo, (long)ldc, x2, nsplit);
   });
   return cmx_check_launch("im2col_nchw");
 }

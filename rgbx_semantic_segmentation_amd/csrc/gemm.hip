@@ -228,10 +228,12 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
     int bm, bn;
     plan_tiles(G, M, nb, K, &bm, &bn);
     a.tiles_m = cdiv(M, bm); a.tiles_n = cdiv(nb, bn);
-    const bool streamed = stream_ok(a, bm, bn, splitk, transA, dtype) &&
-                          (dtype == 2 ? launch_stream_t<f16>(a, transA, transB, s)
-                                      : launch_stream_t<bf16>(a, transA, transB, s));
-    if (!streamed) launch_fast(a, bm, bn, G, splitk, transA, transB, dtype, s);
+    bool done = reg_ok(a, splitk, transA, dtype) &&
+                (dtype == 2 ? launch_reg_t<f16>(a, transB, s) : launch_reg_t<bf16>(a, transB, s));
+    if (!done)
+      done = stream_ok(a, bm, bn, splitk, transA, dtype) &&
+             (dtype == 2 ? launch_stream_t<f16>(a, transA, transB, s) : launch_stream_t<bf16>(a, transA, transB, s));
+    if (!done) launch_fast(a, bm, bn, G, splitk, transA, transB, dtype, s);
   } else {
     // tile shape: the output's narrow side gets 64 (stage-1 C = 64 outputs, 64-row wgrads)
     const bool m64 = M <= 64, n64 = N <= 64;

@@ -791,6 +791,138 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(const GemmArgs p) {
   vm_wait<0>();
 }
 
+// ============================================================================ register-streamed GEMM
+// The many-row, short-k GEMMs of stages 1-2 and the decoder (M 9600-76800 rows, K <= 512, the
+// weight slice small enough for LDS): the block stages its (BN x K) weight slice in LDS once
+// (LDS-DMA), then each of its 4 waves walks 32-row strips of A on its own -- A fragments
+// loaded straight from HBM into registers (16 B per lane, the MFMA operand layout: row r, 8
+// consecutive k), the next k-chunk / strip prefetched while this one is multiplied, the
+// epilogue stored from the accumulators.  No LDS image of A or C and no barrier after the
+// weight staging, so a CU keeps ~8 independent load streams in flight instead of a few
+// lock-stepped DMA -> MFMA -> epilogue chains (the 64 x 64 tile kernel's latency bound).
+// The residual tile and DropPath scale of a strip are loaded at the strip's start, before its
+// k-chunk prefetches, so the epilogue's wait on them never waits for a younger prefetch.
+template <bool TB, int BN, int NK, typename E>
+__global__ __launch_bounds__(256, 4) void gemm_reg_kernel(const GemmArgs p) {
+  constexpr int NT = BN / 32, IMG = BN * 64 * 2;
+  __shared__ __attribute__((aligned(1024))) char smem[NK * IMG + BN * 4];
+  float* bias_s = reinterpret_cast<float*>(smem + NK * IMG);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  const int g = blockIdx.z, n0 = blockIdx.y * BN;
+  const E* Bg = reinterpret_cast<const E*>(p.B) + goff(p, g, p.sB, p.sBh);
+  const i32x4 rB = make_rsrc(Bg);
+#pragma unroll
+  for (int kc = 0; kc < NK; ++kc) {
+    if constexpr (TB) stage_r<BN>(rB, smem + kc * IMG, p.ldb, n0, p.N, kc * 64, p.K, w, lane);
+    else stage_k<BN>(rB, smem + kc * IMG, p.ldb, n0, p.N, kc * 64, p.K, w, lane);
+  }
+  for (int e = threadIdx.x; e < BN; e += 256)
+    bias_s[e] = (p.bias && n0 + e < p.N) ? p.bias[(long)g * p.sbias + n0 + e] : 0.f;
+  vm_wait<0>();
+  __syncthreads();
+
+  const E* Ag = reinterpret_cast<const E*>(p.A) + goff(p, g, p.sA, p.sAh);
+  const E* A2g = p.A2 ? reinterpret_cast<const E*>(p.A2) + (long)g * p.sA2 : Ag;
+  const E* Rg = p.R ? reinterpret_cast<const E*>(p.R) + goff(p, g, p.sC, p.sCh) : nullptr;
+  E* Cg = reinterpret_cast<E*>(p.C) + goff(p, g, p.sC, p.sCh);
+  const int nstrip = (p.M + 31) / 32;
+  const int nwv = gridDim.x * 4;
+  int t = blockIdx.x * 4 + w;
+  if (t >= nstrip) return;                       // waves are independent from here on
+
+  // A chunk kc of strip t: 4 x 16 B buffer loads per lane (row t*32 + r, k = 64 kc + 16 s + 8 h;
+  // rows past M / k past K read as zeros through the out-of-range offset).  32-bit offsets on
+  // a resource in SGPRs: no 64-bit address per load held in VGPRs.  A 64-deep chunk lies in
+  // one of the two A segments (K1 % 64 == 0), so the segment choice is wave-uniform.
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(const_cast<E*>(Ag), 0, 0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rA2 = __builtin_amdgcn_make_buffer_rsrc(const_cast<E*>(A2g), 0, 0x7ffffff0, 0x00020000);
+  auto load_a = [&](int tt, int kc, uint4* fa) {
+    const int i = tt * 32 + r;
+    const bool first = kc * 64 < p.K1;
+    const int k0 = first ? kc * 64 : kc * 64 - p.K1;
+    const int kend = first ? p.K1 : p.K - p.K1;
+    const int rowoff = (int)((long)i * (first ? p.lda : p.lda2) * 2);
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const int k = k0 + 16 * s4 + 8 * h;
+      const int off = (i < p.M && k < kend) ? rowoff + k * 2 : OOB;
+      fa[s4] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(first ? rA : rA2, off, 0, 0));
+    }
+  };
+
+  // double buffer indexed by compile-time k-chunk parity (a runtime index would put the
+  // arrays in scratch); an odd chunk count leaves the next strip's chunk 0 in buffer 1, moved
+  // down at the strip's end
+  uint4 abuf[2][4];
+  load_a(t, 0, abuf[0]);
+  for (; t < nstrip; t += nwv) {
+    // (a compiler-level memory barrier: keeps the weight fragments' LDS reads inside the strip
+    // loop -- hoisted out of it they would hold NK x 32 VGPRs live and spill)
+    asm volatile("" ::: "memory");
+    const int i = t * 32 + r;
+    const bool row_ok = i < p.M;
+    // residual + DropPath scale of this strip, ahead of the strip's prefetches
+    uint2 rv[NT][4];
+    float sc = 1.f;
+    if (Rg) {
+      const E* rr = Rg + (long)min(i, p.M - 1) * p.ldc + n0;
+#pragma unroll
+      for (int b = 0; b < NT; ++b)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int jl = 32 * b + 8 * g4 + 4 * h;
+          rv[b][g4] = n0 + jl < p.N ? *reinterpret_cast<const uint2*>(rr + jl) : make_uint2(0, 0);
+        }
+      if (p.rscale) sc = p.rscale[((long)g * p.M + min(i, p.M - 1)) / p.rows_per_sample];
+    }
+    f32x16 acc[NT];
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[b] = zero16();
+#pragma unroll
+    for (int kc = 0; kc < NK; ++kc) {
+      // prefetch: the next chunk of this strip, else chunk 0 of this wave's next strip
+      if (kc + 1 < NK) load_a(t, kc + 1, abuf[(kc + 1) & 1]);
+      else if (t + nwv < nstrip) load_a(t + nwv, 0, abuf[(kc + 1) & 1]);
+      const char* img = smem + kc * IMG;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const frag8<E> fa = frag_bits<E>(abuf[kc & 1][s4]);
+#pragma unroll
+        for (int b = 0; b < NT; ++b) {
+          frag8<E> fb;
+          if constexpr (TB) fb = frag_r<E, BN>(img, 32 * b, s4, lane);
+          else fb = frag_k<E>(img, 32 * b, s4, lane);
+          acc[b] = MF<E>::mma(fb, fa, acc[b]);
+        }
+      }
+    }
+    if constexpr (NK & 1) {
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) abuf[0][s4] = abuf[1][s4];
+    }
+    if (!row_ok) continue;
+    E* crow = Cg + (long)i * p.ldc + n0;
+#pragma unroll
+    for (int b = 0; b < NT; ++b)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int jl = 32 * b + 8 * g4 + 4 * h;
+        if (n0 + jl >= p.N) continue;
+        float v[4] = {acc[b][4 * g4] + bias_s[jl], acc[b][4 * g4 + 1] + bias_s[jl + 1],
+                      acc[b][4 * g4 + 2] + bias_s[jl + 2], acc[b][4 * g4 + 3] + bias_s[jl + 3]};
+        if (p.act) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = act_fwd(v[e], p.act);
+        }
+        if (Rg) {
+          const cmx_f2 r0 = unpack2<E>(rv[b][g4].x), r1 = unpack2<E>(rv[b][g4].y);
+          v[0] = r0.x + sc * v[0]; v[1] = r0.y + sc * v[1]; v[2] = r1.x + sc * v[2]; v[3] = r1.y + sc * v[3];
+        }
+        *reinterpret_cast<uint2*>(crow + jl) = make_uint2(pack2<E>(v[0], v[1]), pack2<E>(v[2], v[3]));
+      }
+  }
+}
+
 // ============================================================================ grouped launch
 // Many independent problems in ONE launch (the weight gradients of a whole backward segment,
 // which nothing reads before the optimizer): record r owns blocks [blk0, blk0 + nblk) of the
@@ -1210,6 +1342,45 @@ inline bool stream_ok(const GemmArgs& a, int bm, int bn, int splitk, int tA, int
   return dtype == 1 || dtype == 2;
 }
 
+// Register-streamed GEMM policy (CMX_GEMM_REG = the least M that takes it, 0 = off): the
+// forward / dgrad layouts (A k-contiguous), one split, plain 16-bit store with bias /
+// activation / DropPath residual, K <= 512 with the (BN x K) weight slice in LDS
+template <typename E>
+bool launch_reg_t(const GemmArgs& a, int tB, hipStream_t s) {
+  static int& bpc = cmx_knob("GEMM_REG_BPC", 4);
+  const int nk = (a.K + 63) / 64;
+  const int bn = 64;                             // 32 x 64 per wave: ~100 VGPRs, 4 waves / SIMD
+  const int nsl = (a.N + bn - 1) / bn;
+  const long strips = (a.M + 31) / 32;
+  long gx = ((long)cu_count() * (bpc > 0 ? bpc : 1) + (long)nsl * a.G - 1) / ((long)nsl * a.G);
+  gx = (gx + 7) / 8 * 8;                       // slices / groups of one row walker share an XCD
+  if (gx > (strips + 3) / 4) gx = (strips + 3) / 4;
+  const dim3 grid((unsigned)gx, nsl, a.G);
+#define CMX_REG_LAUNCH(TBV, BNV, NKV) \
+  hipLaunchKernelGGL((gemm_reg_kernel<TBV, BNV, NKV, E>), grid, dim3(256), 0, s, a)
+#define CMX_REG_NK(TBV, BNV)                    \
+  do {                                          \
+    if (nk == 1) CMX_REG_LAUNCH(TBV, BNV, 1);   \
+    else if (nk == 2) CMX_REG_LAUNCH(TBV, BNV, 2); \
+    else CMX_REG_LAUNCH(TBV, BNV, 4);           \
+  } while (0)
+  if (nk > 4) return false;
+  if (tB) CMX_REG_NK(true, 64); else CMX_REG_NK(false, 64);
+#undef CMX_REG_NK
+#undef CMX_REG_LAUNCH
+  return true;
+}
+
+inline bool reg_ok(const GemmArgs& a, int splitk, int tA, int dtype) {
+  static int& min_m = cmx_knob("GEMM_REG", 0);
+  if (min_m <= 0 || a.M < min_m || tA || splitk != 1 || a.out_mode != 0 || a.ones_col || a.nup || a.scatter ||
+      a.conv || a.lnY || a.gh != 1)
+    return false;
+  if (a.K > 256 || a.K % 8 || a.N < 32 || a.N % 4 || a.ldc % 4 || a.sC % 4 || ((uintptr_t)a.C & 7)) return false;
+  if (a.R && ((uintptr_t)a.R & 7)) return false;
+  return dtype == 1 || dtype == 2;
+}
+
 template <typename T, int BM, int BN, bool EXT>
 void launch_generic_x(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream_t s) {
   dim3 grid(a.tiles_m * a.tiles_n, G, nsplit);
@@ -1320,7 +1491,9 @@ inline int auto_split(int G, int M, int N, int K, int ones_col) {
   extern template void gemmk::launch_generic<T, BM, BN>(const GemmArgs&, int, int, int, int, hipStream_t);
 #define CMX_GEMM_FAST_INST(E)                                                                         \
   template void gemmk::launch_fast_t<E>(const GemmArgs&, int, int, int, int, int, int, hipStream_t); \
-  template bool gemmk::launch_stream_t<E>(const GemmArgs&, int, int, hipStream_t);
+  template bool gemmk::launch_stream_t<E>(const GemmArgs&, int, int, hipStream_t);                    \
+  template bool gemmk::launch_reg_t<E>(const GemmArgs&, int, hipStream_t);
 #define CMX_GEMM_FAST_EXTERN(E)                                                                              \
   extern template void gemmk::launch_fast_t<E>(const GemmArgs&, int, int, int, int, int, int, hipStream_t); \
-  extern template bool gemmk::launch_stream_t<E>(const GemmArgs&, int, int, hipStream_t);
+  extern template bool gemmk::launch_stream_t<E>(const GemmArgs&, int, int, hipStream_t);                    \
+  extern template bool gemmk::launch_reg_t<E>(const GemmArgs&, int, hipStream_t);

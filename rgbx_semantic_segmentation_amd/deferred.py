@@ -43,6 +43,10 @@ from . import _lib
 from ._lib import LIB, call, query, ptr, stream
 
 ENABLED = os.environ.get("CMX_DEFER", "1") == "1"
+# CMX_GROUPED_SORT=1: the grouped launch's problems in decreasing per-block work (k-tiles per
+# block x tile area), so the longest blocks are dispatched first and the short ones fill the
+# tail (longest-processing-time order; a problem's tiles stay contiguous for the XCD map)
+GROUPED_SORT = os.environ.get("CMX_GROUPED_SORT", "0") == "1"
 WGRAD_SIDE = os.environ.get("CMX_WGRAD_SIDE", "0") == "1"
 _side: dict = {}                 # device index -> side stream of the stage-boundary flushes
 _side_used: set = set()          # device indices with side work not yet joined
@@ -302,21 +306,29 @@ def _issue() -> None:
         sizes = [query("cmx_gemm_workspace", G, M, N, s) if s > 1 else 0 for (G, M, N, K, hb), s in zip(dims, splits)]
         arena = torch.empty(max(1, sum((z + 255) // 256 * 64 for z in sizes)), dtype=torch.float32, device=device)
         nrec = len(dims)
+        order = list(range(nrec))
+        if GROUPED_SORT:
+            def _cost(i):
+                G, M, N, K, hb = dims[i]
+                nb = N - 1 if hb else N
+                kt = -(-(-(-K // 64)) // splits[i])
+                return kt * (64 if M <= 64 else 128) * (64 if nb <= 64 else 128)
+            order.sort(key=lambda i: -_cost(i))
         table = _table(nrec * _GREC)
         base = table.data_ptr()
         blk, off = 0, 0
-        for i in range(nrec):
+        for pos, i in enumerate(order):
             s, sz = splits[i], sizes[i]
             ws = arena.data_ptr() + off if s > 1 else 0
             if i < len(gemms):
                 A, B, Wg, bg, G, M, N, K, lda, ldb, ldc, sA, sB, sC, sdb = gemms[i]
-                nb = LIB.cmx_gemm_group_pack(base + i * _GREC, ptr(A), ptr(B), ptr(Wg), ptr(bg), ws, G, M, N, K, lda,
+                nb = LIB.cmx_gemm_group_pack(base + pos * _GREC, ptr(A), ptr(B), ptr(Wg), ptr(bg), ws, G, M, N, K, lda,
                                              ldb, ldc, sA, sB, sC, sdb, 1, 1, 1, int(bg is not None), s, blk)
                 dst = Wg.data_ptr()
             else:
                 (dy, x, Wg, bg, G, NIg, H, W, C, KH, KW, st, pad, Ho, Wo, Nout, tap, sdy, sx, sC, sdb) = \
                     convs[i - len(gemms)]
-                nb = LIB.cmx_gemm_group_pack_conv_wgrad(base + i * _GREC, ptr(dy), ptr(x), ptr(Wg), ptr(bg), ws, G, NIg,
+                nb = LIB.cmx_gemm_group_pack_conv_wgrad(base + pos * _GREC, ptr(dy), ptr(x), ptr(Wg), ptr(bg), ws, G, NIg,
                                                         H, W, C, KH, KW, st, pad, Ho, Wo, Nout, tap, sdy, sx, sC, sdb, s,
                                                         blk)
                 M, N, ldc = Nout, C + (1 if bg is not None else 0), KH * KW * C

@@ -577,9 +577,11 @@ class ConvF(Function):
     """Conv2d as im2col + grouped GEMM on NHWC (OverlapPatchEmbed.proj, Attention.sr)."""
 
     @staticmethod
-    def forward(ctx, x, W, Wg, b, bg, geom, anchor):
-        # geom: (G, NI, H, Wd, C, KH, KW, stride, pad, Ho, Wo, nchw)
+    def forward(ctx, x, W, Wg, b, bg, geom, anchor, x2=None):
+        # geom: (G, NI, H, Wd, C, KH, KW, stride, pad, Ho, Wo, nchw); x2: the second image batch
+        # of an NCHW input given as two tensors (x holds the first NI - len(x2) images)
         G, NI, H, Wd, C, KH, KW, st, pad, Ho, Wo, nchw = geom
+        ctx.x2 = x2
         Kp = W.shape[-1]
         if IMPLICIT_CONV and not nchw and x.dtype in (torch.bfloat16, torch.float16) and C % 64 == 0 \
                 and x.is_contiguous():
@@ -602,8 +604,13 @@ class ConvF(Function):
         ctx.implicit = False
         cols = torch.empty(G, NI // G * Ho * Wo, Kp, dtype=W.dtype, device=W.device)
         if nchw:
-            K.call("cmx_im2col_nchw_f32", K.ptr(x), K.ptr(cols), NI, C, H, Wd, KH, KW, st, pad, Ho, Wo, Kp,
-                   K.dtype_code(cols), K.stream())
+            x2 = getattr(ctx, "x2", None)
+            if x2 is not None:          # (rgb, modal_x) as two batches: no concatenated copy
+                K.call("cmx_im2col_nchw2_f32", K.ptr(x), K.ptr(x2), NI - x2.shape[0], K.ptr(cols), NI, C, H, Wd, KH,
+                       KW, st, pad, Ho, Wo, Kp, K.dtype_code(cols), K.stream())
+            else:
+                K.call("cmx_im2col_nchw_f32", K.ptr(x), K.ptr(cols), NI, C, H, Wd, KH, KW, st, pad, Ho, Wo, Kp,
+                       K.dtype_code(cols), K.stream())
         else:
             K.call("cmx_im2col_nhwc", K.ptr(x), K.ptr(cols), NI, H, Wd, C, KH, KW, st, pad, Ho, Wo, Kp,
                    K.dtype_code(cols), K.stream())
@@ -642,10 +649,10 @@ class ConvF(Function):
             K.call("cmx_col2im_nhwc", K.ptr(dcols), K.ptr(dx), NI, H, Wd, C, KH, KW, st, pad, Ho, Wo, W.shape[-1],
                    K.dtype_code(dx), K.stream())
             dx = dx.view(ctx.xshape)
-        return dx, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None
 
 
-def conv(store, mod, x, G, NI, H, W, C, stride, pad, nchw=False):
+def conv(store, mod, x, G, NI, H, W, C, stride, pad, nchw=False, x2=None):
     KH, KW = mod.kernel_size
     Ho = (H + 2 * pad - KH) // stride + 1
     Wo = (W + 2 * pad - KW) // stride + 1
@@ -656,7 +663,7 @@ def conv(store, mod, x, G, NI, H, W, C, stride, pad, nchw=False):
     b = store.w(mod.bias, compute=False).view(G, -1) if mod.bias is not None else None
     bg = store.g(mod.bias).view(G, -1) if mod.bias is not None else None
     geom = (G, NI, H, W, C, KH, KW, stride, pad, Ho, Wo, nchw)
-    return ConvF.apply(x, Wt, Wgt, b, bg, geom, mod.weight), Ho, Wo
+    return ConvF.apply(x, Wt, Wgt, b, bg, geom, mod.weight, x2), Ho, Wo
 
 
 # ---------------------------------------------------------------------------- FFM cross attention

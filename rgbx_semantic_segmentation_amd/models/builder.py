@@ -213,7 +213,9 @@ class EncoderDecoder(nn.Module):
         dev = self.store.device
         if self.training and torch.is_grad_enabled() and not torch.cuda.is_current_stream_capturing():
             self.store.ensure_grads()
-        images = torch.cat([rgb, modal_x], 0).to(device=dev, dtype=torch.float32).contiguous()
+        rgb = rgb.to(device=dev, dtype=torch.float32).contiguous()
+        modal_x = modal_x.to(device=dev, dtype=torch.float32).contiguous()
+        images = (rgb, modal_x)            # the stage-1 im2col reads both batches (no concat)
         self._nbt_bumped = False
         dp, d2 = self._stochastic(B, dev)
         group = self.process_group if (self.sync_bn and self.training) else None

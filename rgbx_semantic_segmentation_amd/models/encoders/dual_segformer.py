@@ -147,15 +147,28 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
         # (q and the SR path read norm1's output through separate handles: the norm's backward
         # sums their gradients on load)
         h, h2, xr = F.layernorm_res(store, blk.norm1, x, G, scale=prev[0], rps=N, tap=prev[1], pre=prev[2])
-        q = F.glinear(store, a.q.weight, a.q.bias, h)
-        if a.sr_ratio > 1:
-            R = a.sr_ratio
-            xs, Hk, Wk = F.conv(store, a.sr, h2, G, G * B, H, W, C, R, 0)
-            xs = F.layernorm(store, a.norm, xs, G)
-            Nk = Hk * Wk
+
+        def kv_path():
+            if a.sr_ratio > 1:
+                xs, Hk, Wk = F.conv(store, a.sr, h2, G, G * B, H, W, C, a.sr_ratio, 0)
+                xs = F.layernorm(store, a.norm, xs, G)
+                return F.glinear(store, a.kv.weight, a.kv.bias, xs), Hk * Wk
+            return F.glinear(store, a.kv.weight, a.kv.bias, h2), N
+
+        side = streams.sr_stream(x.device) if (streams.SR_SIDE and x.is_cuda) else None
+        if side is not None:
+            # the key/value path beside the q Linear (joined before the attention core)
+            main = torch.cuda.current_stream()
+            side.wait_stream(main)
+            h2.record_stream(side)
+            with torch.cuda.stream(side):
+                kv, Nk = kv_path()
+            q = F.glinear(store, a.q.weight, a.q.bias, h)
+            main.wait_stream(side)
+            kv.record_stream(main)
         else:
-            xs, Nk = h2, N
-        kv = F.glinear(store, a.kv.weight, a.kv.bias, xs)
+            q = F.glinear(store, a.q.weight, a.q.bias, h)
+            kv, Nk = kv_path()
         o = F.SRAttentionF.apply(q, kv, G * B, N, Nk, a.num_heads, C // a.num_heads)
         # x + drop_path(proj(o)): residual and DropPath scale fused into the proj GEMM epilogue
         tap_a = F.GradTap() if s_attn is not None else None
@@ -170,16 +183,21 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
         return x, (s_mlp, tap_m, stn)
 
     def run(self, store, images, B, H, W, training, dp_scales: Optional[torch.Tensor], bn_group=None):
-        """images: (2*B, 3, H, W) fp32 NCHW (RGB batch then X batch).
+        """images: (2*B, 3, H, W) fp32 NCHW (RGB batch then X batch), or the pair of (B, 3, H, W)
+        batches (rgb, modal_x) read by the stage-1 im2col in place.
         dp_scales: (n_blocks_total, 2, 2*? ) per-block (attn, mlp) per-sample scales or None.
         Returns the 4 fused maps [(B*N_s, C_s) tokens] and their grids."""
         G = 2
-        x = images
+        x2 = None
+        if isinstance(images, (tuple, list)):
+            x, x2 = images
+        else:
+            x = images
         outs, grids = [], []
         bi = 0
         Hc, Wc, Cin = H, W, 3
         sync = getattr(self, "grad_sync", None)     # dist.BucketedGradSync (data parallel) or None
-        main = torch.cuda.current_stream() if images.is_cuda else None
+        main = torch.cuda.current_stream() if x.is_cuda else None
         side = streams.ffm_stream(main.device) if (main is not None and streams.FFM_SIDE) else None
         for s in range(4):
             pe = getattr(self, f"patch_embed{s + 1}")
@@ -191,7 +209,8 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
                 # the weight gradients of everything above this stage run on the side stream
                 # beside the input-gradient chain of stages < s (deferred.flush(side=True))
                 x.register_hook(_side_flush_hook)
-            x, Ho, Wo = F.conv(store, pe.proj, x, G, G * B, Hc, Wc, Cin, pe.stride, pe.pad, nchw=(s == 0))
+            x, Ho, Wo = F.conv(store, pe.proj, x, G, G * B, Hc, Wc, Cin, pe.stride, pe.pad, nchw=(s == 0),
+                               x2=x2 if s == 0 else None)
             x = F.layernorm(store, pe.norm, x, G)
             Hc, Wc, Cin = Ho, Wo, self.embed_dims[s]
             prev = (None, None, None)

@@ -16,7 +16,19 @@ import os
 import torch
 
 FFM_SIDE = os.environ.get("CMX_FFM_STREAM", "1") == "1"
+# CMX_SR_STREAM=1: each Attention's key/value path (SR conv -> norm -> kv Linear,
+# dual_segformer.py:114-124) on a second side stream beside the q Linear (:111), forward and
+# (autograd follows the forward's streams) backward
+SR_SIDE = os.environ.get("CMX_SR_STREAM", "0") == "1"
 _ffm: dict = {}
+_sr: dict = {}
+
+
+def sr_stream(device) -> torch.cuda.Stream:
+    idx = torch.device(device).index
+    if idx not in _sr:
+        _sr[idx] = torch.cuda.Stream(device=device)
+    return _sr[idx]
 
 
 def ffm_stream(device) -> torch.cuda.Stream:

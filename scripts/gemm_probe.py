@@ -15,7 +15,9 @@ from rgbx_semantic_segmentation_amd import kernels as K  # noqa: E402
 from scripts.gemm_sweep import timeit  # noqa: E402
 
 SHAPES = [(2, 38400, 256, 64, 0), (2, 38400, 64, 64, 1), (2, 38400, 64, 256, 0), (2, 9600, 128, 128, 1),
-          (2, 9600, 512, 128, 0), (2, 2400, 320, 320, 1), (2, 2400, 1280, 320, 0), (2, 600, 512, 512, 1)]
+          (2, 9600, 512, 128, 0), (2, 2400, 320, 320, 1), (2, 2400, 1280, 320, 0), (2, 600, 512, 512, 1),
+          (2, 38400, 64, 256, 1), (2, 38400, 256, 64, 1), (2, 9600, 128, 512, 0), (2, 9600, 512, 128, 1),
+          (1, 38400, 512, 64, 0), (2, 2400, 320, 1280, 0)]
 
 
 def operands(G, M, N, Kd, tB):

@@ -355,3 +355,67 @@ def test_gemm_ln_epilogue(dev, dtype, G, M, N, K, res):
     assert torch.allclose(m2.view(-1), mean, atol=1e-6, rtol=1e-6)
     assert torch.allclose(r2.view(-1), rstd, atol=1e-5, rtol=1e-5)
     assert ((Y.float() - y2.float()).abs() <= 2 ** -7 * y2.float().abs() + 1e-3).all()
+
+
+@pytest.fixture
+def reg_on(dev):
+    """Route eligible problems to the register-streamed kernel (CMX_GEMM_REG = least M)."""
+    from rgbx_semantic_segmentation_amd import kernels as Kn
+    old = Kn.tune_get("GEMM_REG")
+    Kn.tune("GEMM_REG", 1)
+    yield Kn
+    Kn.tune("GEMM_REG", old if old >= 0 else 0)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("G,M,N,K", [(2, 38400, 256, 64), (2, 38400, 64, 256), (2, 9600, 512, 128), (2, 9600, 128, 512),
+                                     (1, 38400, 512, 64), (2, 1001, 200, 192), (1, 777, 40, 152), (2, 4800, 320, 320)])
+@pytest.mark.parametrize("tB", [0, 1])
+def test_gemm_reg_kernel(reg_on, dtype, G, M, N, K, tB):
+    """Register-streamed kernel (weight slice in LDS, A strips straight to registers, no
+    barriers after staging) against torch and against the tile kernel, for ragged M / N / K,
+    both weight layouts, one to eight 64-deep k-chunks and 64- / 128-wide weight slices."""
+    Kn = reg_on
+    if tB and N % 8:
+        pytest.skip("transposed weight needs N % 8 == 0")
+    torch.manual_seed(10)
+    A = torch.randn(G, M, K, device="cuda").to(dtype)
+    B = torch.randn(G, N, K, device="cuda").to(dtype)
+    Bv = B.transpose(1, 2).contiguous().transpose(1, 2) if tB else B
+    C = torch.full((G, M, N), 3.0, device="cuda", dtype=dtype)
+    Kn.gemm(A, Bv, C)
+    ref = torch.bmm(A.float(), B.float().transpose(1, 2))
+    assert rel(C, ref) < 1e-2
+    Kn.tune("GEMM_REG", 0)
+    C2 = torch.empty_like(C)
+    Kn.gemm(A, Bv, C2)
+    Kn.tune("GEMM_REG", 1)
+    assert ((C.float() - C2.float()).abs() <= C2.float().abs() * 2 ** -7 + 1e-2).all()
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("act", ["none", "gelu"])
+@pytest.mark.parametrize("res", [False, True])
+def test_gemm_reg_epilogues(reg_on, dtype, act, res):
+    """Register-streamed kernel epilogue: bias + activation + DropPath-scaled residual on a
+    stage-1 fc2-shaped problem with ragged rows, and the two-segment (cat-free) A."""
+    Kn = reg_on
+    torch.manual_seed(11)
+    G, M, N, K, rps = 2, 4 * 1999, 64, 256, 1999
+    A = torch.randn(G, M, K, device="cuda").to(dtype)
+    B = torch.randn(G, N, K, device="cuda").to(dtype) * (1.0 / K ** 0.5)
+    bias = torch.randn(G, N, device="cuda")
+    R = torch.randn(G, M, N, device="cuda").to(dtype) if res else None
+    s = torch.tensor([0.0, 1.25, 1.25, 0.0, 1.0, 1.25, 0.0, 1.25], device="cuda") if res else None
+    C = torch.empty(G, M, N, device="cuda", dtype=dtype)
+    Kn.gemm(A, B, C, bias=bias, residual=R, rscale=s, rows_per_sample=rps, act=act)
+    ref = ref_epi(torch.bmm(A.float(), B.float().transpose(1, 2)), bias, act, R, s, rps)
+    assert rel(C, ref) < 1e-2
+    x1 = torch.randn(G, 9600, 64, device="cuda").to(dtype)
+    x2 = torch.randn(G, 9600, 128, device="cuda").to(dtype)
+    W = torch.randn(G, 128, 192, device="cuda").to(dtype)
+    C = torch.empty(G, 9600, 128, device="cuda", dtype=dtype)
+    b2 = torch.randn(G, 128, device="cuda")
+    Kn.gemm(x1, W, C, bias=b2, A2=x2)
+    ref = torch.bmm(torch.cat([x1, x2], -1).float(), W.float().transpose(1, 2)) + b2[:, None, :]
+    assert rel(C, ref) < 1e-2
