@@ -947,6 +947,8 @@ __global__ __launch_bounds__(64 * SQW) void sra_dkv_small(const E* __restrict__ 
 }
 
 int pick_qw(int N, int heads, int Bt) {
+  static int& force = cmx_knob("SRA_QW", 0);     // 1 / 2: query sub-tiles per wave (A/B), 0 = auto
+  if (force == 1 || force == 2) return force;
   const long wg2 = (long)cdiv(N, 64 * NWAVE) * heads * Bt;   // workgroups at 2 sub-tiles per wave
   return wg2 >= 512 ? 2 : 1;
 }
@@ -958,6 +960,8 @@ int pick_qw(int N, int heads, int Bt) {
 // workgroups at stage 2 (152 -> 304) were slower, 13.8 -> 16.4 us forward).  Every workgroup
 // stages the (b, head)'s K / V (L2-resident after the first): only L2 -> LDS traffic.
 int pick_nw(int N, int heads, int Bt, int qw) {
+  static int& force = cmx_knob("SRA_NW", 0);     // 2 / 4 / 8 waves per workgroup (A/B), 0 = auto
+  if (force == 2 || force == 4 || force == 8) return qw == 2 && force == 2 ? 4 : force;
   if (qw == 2 || (long)cdiv(N, 32 * NWAVE) * heads * Bt >= 128) return NWAVE;
   return 2;
 }
@@ -994,7 +998,8 @@ void sra_fwd_fast_launch_t(const void* q, const void* k, const void* v, void* o,
 #define CMX_SRA_FWD(QW_, NW_)                                                                                       \
   hipLaunchKernelGGL((sra_fwd_fast<E, QW_, NW_>), grid, dim3(64 * NW_), 0, s, (const E*)q, (const E*)k,         \
                      (const E*)v, (E*)o, lse, N, Nk, nkp, heads, qs, kvs, os, sl2)
-  if (qw == 2) CMX_SRA_FWD(2, 8);
+  if (qw == 2 && nw == 4) CMX_SRA_FWD(2, 4);
+  else if (qw == 2) CMX_SRA_FWD(2, 8);
   else if (nw == 8) CMX_SRA_FWD(1, 8);
   else if (nw == 4) CMX_SRA_FWD(1, 4);
   else if (nw == 2) CMX_SRA_FWD(1, 2);
@@ -1014,7 +1019,8 @@ void sra_dq_fast_launch_t(const void* q, const void* k, const void* v, const voi
   hipLaunchKernelGGL((sra_dq_fast<E, QW_, NW_>), grid, dim3(64 * NW_), 0, s, (const E*)q, (const E*)k,          \
                      (const E*)v, (const E*)o, (const E*)dout, lse, Dws, (E*)dq, N, Nk, nkp, heads, qs,  \
                      kvs, os, dos, dqs, sl2, scale)
-  if (qw == 2) CMX_SRA_DQ(2, 8);
+  if (qw == 2 && nw == 4) CMX_SRA_DQ(2, 4);
+  else if (qw == 2) CMX_SRA_DQ(2, 8);
   else if (nw == 8) CMX_SRA_DQ(1, 8);
   else if (nw == 4) CMX_SRA_DQ(1, 4);
   else if (nw == 2) CMX_SRA_DQ(1, 2);

@@ -30,7 +30,7 @@ def main():
     agg = {}
     for src, key in ((f, "FETCH_SIZE_kb"), (w, "WRITE_SIZE_kb")):
         for (kname, _), v in src.items():
-            short = kname.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0].split("<")[0]
+            short = kname.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0].split("<")[0].split("::")[-1]
             if wanted and not any(s in kname for s in wanted):
                 continue
             a = agg.setdefault(short, {"launches_fetch": 0, "launches_write": 0, "FETCH_SIZE_kb": 0.0, "WRITE_SIZE_kb": 0.0})
