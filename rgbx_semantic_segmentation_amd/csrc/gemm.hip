@@ -207,18 +207,12 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
   a.kt_per_split = (nk + splitk - 1) / splitk;
   splitk = (nk + a.kt_per_split - 1) / a.kt_per_split;      // no empty splits
   a.nsplit = splitk;
-  // CMX_GEMM_DIRECT=1: register epilogue for plain 16-bit outputs (A/B switch, default off)
-  static int& direct_env = cmx_knob("GEMM_DIRECT", 0);
-  a.direct = direct_env && fast && splitk == 1 && out_mode == 0 && !ones_col && !a.nup && !a.scatter && nb % 4 == 0 &&
-             ldc % 4 == 0 && sC % 4 == 0 && ((uintptr_t)C & 7) == 0 && (!R || ((uintptr_t)R & 7) == 0) &&
-             (!bias || (sbias % 4 == 0 && ((uintptr_t)bias & 15) == 0));
   if (ln) {
     // whole rows per tile: 64 x 64 (N = 64) or 64 x 128 (N = 128) on the 16-bit LDS-image path
     CMX_REQUIRE(fast && splitk == 1 && out_mode == 0 && !ones_col && !a.nup && !a.scatter && gh == 1 &&
                 (N == 64 || N == 128) && ln->y && ln->gamma && ln->beta && ln->mean && ln->rstd &&
                 ((uintptr_t)ln->y & 15) == 0 && a.cvec, CMX_ERR_ARG,
                 "gemm_ln: needs the 16-bit path, N = 64 or 128, one split, a plain 16-B aligned store (N=%d)", N);
-    a.direct = 0;
     a.lnY = ln->y; a.lnG = ln->gamma; a.lnB = ln->beta; a.lnMean = ln->mean; a.lnRstd = ln->rstd; a.lnEps = ln->eps;
     a.tiles_m = cdiv(M, 64); a.tiles_n = 1;
     launch_fast(a, 64, N, G, 1, transA, transB, dtype, s);

@@ -34,10 +34,6 @@ struct GemmArgs {
   // the plain stride g * sX
   int gh;
   long sAh, sBh, sCh;
-  // direct = 1: the 16-bit fast path stores its tile straight from the accumulators (4 columns
-  // = 8 B per lane and register group) instead of through the fp32 LDS image (set by the host
-  // for plain-layout 16-bit outputs without split-K, k-groups or upsample / scatter epilogues)
-  int direct;
   // LayerNorm of the stored rows (cmx_gemm_ln): the tile spans whole rows (N == BN); lnY (C's
   // layout) = LN(C) over the N columns with per-group gamma / beta (G, N), per-row mean / rstd
   // (G * M) -- the next Block norm on the residual stream computed in the producing GEMM's
@@ -334,7 +330,7 @@ constexpr int gemm_smem_bytes() {
 // One output tile (of one split / group) of problem p.  `lin` = the block's linear index
 // within the problem, in (split, group, tile) order; smem = gemm_smem_bytes<BM, BN, NS>().
 // E = the 16-bit storage type (bf16 or f16: v_mfma_f32_32x32x16_bf16 / _f16, same tiles and rate)
-template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1, typename E = bf16>
+template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1, typename E = bf16, bool LN = false>
 __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin, char* smem) {
   constexpr int A_BYTES = BM * FBK * 2, STAGE = (BM + BN) * FBK * 2, SLOT = KW * STAGE;
   constexpr int TM = BM / 64, TN = BN / 64;
@@ -498,49 +494,6 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
     cur = cur + 1 == NS ? 0 : cur + 1;
   }
 
-  if (KW == 1 && p.direct) {
-    // direct epilogue: lane (r, h) holds C(i = r, j = accrow(q, h)) of each 32 x 32 sub-tile;
-    // registers 4 g4 .. 4 g4 + 3 are the 4 consecutive columns 8 g4 + 4 h + (0..3)
-    const int r = lane & 31, h = lane >> 5;
-    if (do_db && h == 0) {
-#pragma unroll
-      for (int a = 0; a < TM; ++a) {
-        const int i = i0 + wm * (BM / 2) + a * 32 + r;
-        if (i < p.M) dbias_store(p, g, i, accd[a][0]);
-      }
-    }
-#pragma unroll
-    for (int a = 0; a < TM; ++a) {
-      const int i = i0 + wm * (BM / 2) + a * 32 + r;
-      if (i >= p.M) continue;
-      const float sc = (p.R && p.rscale) ? p.rscale[((long)g * p.M + i) / p.rows_per_sample] : 1.f;
-#pragma unroll
-      for (int b = 0; b < TN; ++b)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int j = j0 + wn * (BN / 2) + b * 32 + 8 * g4 + 4 * h;
-          if (j >= nreal) continue;
-          float v[4] = {acc[a][b][4 * g4], acc[a][b][4 * g4 + 1], acc[a][b][4 * g4 + 2], acc[a][b][4 * g4 + 3]};
-          if (p.bias) {
-            const float4 bv = *reinterpret_cast<const float4*>(p.bias + (long)g * p.sbias + j);
-            v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
-          }
-          if (p.act) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = act_fwd(v[e], p.act);
-          }
-          const long off = goff(p, g, p.sC, p.sCh) + (long)i * p.ldc + j;
-          if (p.R) {
-            const uint2 rv = *reinterpret_cast<const uint2*>(reinterpret_cast<const E*>(p.R) + off);
-            const cmx_f2 r0 = unpack2<E>(rv.x), r1 = unpack2<E>(rv.y);
-            v[0] = r0.x + sc * v[0]; v[1] = r0.y + sc * v[1]; v[2] = r1.x + sc * v[2]; v[3] = r1.y + sc * v[3];
-          }
-          *reinterpret_cast<uint2*>(reinterpret_cast<E*>(p.C) + off) = make_uint2(pack2<E>(v[0], v[1]), pack2<E>(v[2], v[3]));
-        }
-    }
-    return;
-  }
-
   // epilogue through LDS.  acc[a][b] holds C^T (B fragment fed as the MFMA's A operand), so
   // lane (r, h) register q is C(i = r, j = accrow(q, h)) of its 32x32 sub-tile and registers
   // 4g..4g+3 are 4 consecutive j: one ds_write_b128 each into a row-major fp32 tile (pitch
@@ -604,17 +557,22 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
       }
     } else {
       epi_store8<E>(p, g, i, j, nv, v);
-      if (p.lnY) ln_row8<E, TPR>(p, g, i, j, v);
+      if constexpr (LN) ln_row8<E, TPR>(p, g, i, j, v);
     }
   }
 }
 
 // 1-D grid over (split, group, tile); each XCD gets a contiguous run of that order, i.e.
 // neighbouring tiles of one (split, group): they share A row panels and the B k-slice in L2
-template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1, typename E = bf16>
-__global__ __launch_bounds__(256 * KW, KW == 4 ? 1 : 2) void gemm_bf16_kernel(const GemmArgs p) {
+// LN: the LayerNorm epilogue of cmx_gemm_ln (a separate instantiation: the norm's registers
+// would otherwise count against every GEMM's occupancy)
+// (64 x 64 two-stage blocks take 32 KB of LDS: five fit a CU when the kernel stays within 96
+// VGPRs, which the launch bound asks of the register allocator -- at 97 only four are resident)
+template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1, typename E = bf16, bool LN = false>
+__global__ __launch_bounds__(256 * KW, (BM == 64 && BN == 64 && NS == 2 && KW == 1 && !LN) ? 5 : (KW == 4 ? 1 : 2))
+void gemm_bf16_kernel(const GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[gemm_smem_bytes<BM, BN, NS, KW>()];
-  gemm_bf16_body<BM, BN, TA, TB, NS, KW, E>(p, xcd_tile(blockIdx.x, p.tiles_m * p.tiles_n * p.G * p.nsplit), smem);
+  gemm_bf16_body<BM, BN, TA, TB, NS, KW, E, LN>(p, xcd_tile(blockIdx.x, p.tiles_m * p.tiles_n * p.G * p.nsplit), smem);
 }
 
 // ============================================================================ stream kernel
@@ -1218,6 +1176,13 @@ void launch_reduce(const GemmArgs& a, int G, long groups, hipStream_t s) {
 template <int BM, int BN, int NS, int KW = 1, typename E = bf16>
 void launch_bf16(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream_t s) {
   dim3 grid(a.tiles_m * a.tiles_n * G * nsplit);
+  if constexpr (BM == 64) {
+    if (a.lnY) {                                 // cmx_gemm_ln: forward / dgrad layouts only
+      if (tB) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, false, true, NS, KW, E, true>), grid, dim3(256 * KW), 0, s, a);
+      else hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, false, false, NS, KW, E, true>), grid, dim3(256 * KW), 0, s, a);
+      return;
+    }
+  }
 #define CMX_GEMM_LAUNCH(TA, TB) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, TA, TB, NS, KW, E>), grid, dim3(256 * KW), 0, s, a)
   if (!tA && !tB) CMX_GEMM_LAUNCH(false, false);
   else if (!tA && tB) CMX_GEMM_LAUNCH(false, true);
