@@ -39,6 +39,7 @@ int bn_nblk(long M) {
 }
 
 constexpr int UNR = 4;            // rows per lane with loads in flight together
+constexpr int UNRB = 2;           // ... in bn_bwd_reduce_kernel (four operands per row)
 constexpr int BN_MAXC = 2048;     // LDS coefficient staging limit of the elementwise passes
 
 template <typename T, int TPR>
@@ -217,6 +218,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x, 
 }
 
 // partials (nblk, 2, C) doubles of sum g and sum g*xhat
+// (two rows per lane in flight, not UNR = 4: with the residual and Dropout2d operands the
+// four-row form held 256 VGPRs -- one wave per SIMD)
 template <typename T, int TPR>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                             const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -245,10 +248,10 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
       sh[j] = beta[c0 + j] - mu[j] * sc[j];
     }
     const long stride = (long)gridDim.x * RS;
-    for (long m = (long)blockIdx.x * RS + slot; m < M; m += UNR * stride) {
-      float xv[UNR][V], d[UNR][V], r[UNR][V], ds[UNR][V];
+    for (long m = (long)blockIdx.x * RS + slot; m < M; m += UNRB * stride) {
+      float xv[UNRB][V], d[UNRB][V], r[UNRB][V], ds[UNRB][V];
 #pragma unroll
-      for (int u = 0; u < UNR; ++u) {
+      for (int u = 0; u < UNRB; ++u) {
         const long mu_ = m + u * stride;
         if (mu_ < M) {
           const long e = mu_ * C + c0;
@@ -262,7 +265,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
         }
       }
 #pragma unroll
-      for (int u = 0; u < UNR; ++u)
+      for (int u = 0; u < UNRB; ++u)
 #pragma unroll
         for (int j = 0; j < V; ++j) {
           const float pre = xv[u][j] * sc[j] + sh[j] + (res ? r[u][j] : 0.f);
