@@ -35,8 +35,9 @@ const char* cmx_last_error(void);
 /* pinned host -> device copy of a packed record table on `stream` (see grouped launches) */
 int cmx_upload(void* dst, const void* src, size_t nbytes, hipStream_t stream);
 /* launch-policy knobs (GEMM_TILES, GEMM_SMALLK, GEMM_T128, GEMM_KW, GEMM_NS64, GEMM_SPLITKW,
- * GEMM_DIRECT, GEMM_DEEP, GEMM_STREAM, GEMM_STREAM_NS, GEMM_STREAM_NSR, GEMM_STREAM_BPC, SRA_SMALL_N,
- * SRA_DKV_DIRECT, GROUPED_KT, GROUPED_CHUNK, GROUPED_NS): initialised from the
+ * GEMM_DEEP, GEMM_STREAM, GEMM_STREAM_NS, GEMM_STREAM_NSR, GEMM_STREAM_BPC, GEMM_REG,
+ * GEMM_REG_BPC, SRA_SMALL_N, SRA_DKV_DIRECT, SRA_QW, SRA_NW, GROUPED_KT, GROUPED_CHUNK,
+ * GROUPED_NS): initialised from the
  * CMX_<NAME> environment variable, changed in-process by cmx_tune for interleaved A/B runs;
  * a knob set before the first launch that reads it keeps the set value.  tune_get: -1 if unset. */
 int cmx_tune(const char* name, int value);
