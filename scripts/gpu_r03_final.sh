@@ -27,3 +27,7 @@ timeout -k 10 300 python -u bench.py --backbone mit_b0 --height 240 --width 320 
 timeout -k 10 300 python -u bench.py --backbone mit_b4 --height 480 --width 640 --batch 4 --classes 9 --steps 10 --warmup 3 \
   --no-cpu-baseline > gpurun_out/bench_c4_$TAG.json 2>&1 || exit $?
 grep -h -o '"value": [0-9.]*' gpurun_out/bench_c1_$TAG.json gpurun_out/bench_c4_$TAG.json
+timeout -k 10 300 python -u bench.py --backbone mit_b5 --height 1024 --width 1024 --batch 1 --classes 19 \
+  --dtype float16 --loss-scaling --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/bench_c5_fp16_$TAG.json \
+  2> gpurun_out/bench_c5_fp16_$TAG.err || exit $?
+grep -h -o '"value": [0-9.]*' gpurun_out/bench_c5_fp16_$TAG.json
