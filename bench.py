@@ -255,10 +255,13 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         run_one()
+    t_enq = time.perf_counter() - t0              # host time to enqueue the K replays
     torch.cuda.synchronize()
     if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    print(f"[bench] host enqueue {t_enq / args.steps * 1e3:.3f} ms/step of {elapsed / args.steps * 1e3:.3f}",
+          file=sys.stderr)
     if use_dist:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

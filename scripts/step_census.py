@@ -12,6 +12,18 @@ rows = c.execute("select start, end, name from kernels order by start").fetchall
 idx = [i for i, r in enumerate(rows) if r[2].replace("void ", "").startswith("adamw")]
 seg = rows[idx[-2] + 1:idx[-1] + 1]
 print(f"launches/step {len(seg)}  wall {(seg[-1][1] - seg[0][0]) / 1e3:.0f} us  busy {sum(r[1] - r[0] for r in seg) / 1e3:.0f} us")
+# idle time between one step's AdamW and the next step's first kernel (the replay boundary), and
+# the largest idle gaps inside the step
+prev = rows[idx[-2]]
+print(f"boundary gap {(seg[0][0] - prev[1]) / 1e3:.1f} us after {prev[2][:40]}; first kernels: "
+      + ", ".join(re.sub(r"\(.*", "", r[2].replace("void ", ""))[:30] for r in seg[:3]))
+gaps, end = [], seg[0][1]
+for s_, e_, n_ in seg[1:]:
+    if s_ > end:
+        gaps.append(((s_ - end) / 1e3, re.sub(r"\(.*", "", n_.replace("void ", ""))[:50]))
+    end = max(end, e_)
+print(f"idle inside the step {sum(g for g, _ in gaps):.0f} us over {len(gaps)} gaps; largest: "
+      + "; ".join(f"{g:.1f} us before {n}" for g, n in sorted(gaps, reverse=True)[:6]))
 cat = collections.defaultdict(lambda: [0, 0.0])
 for s, e, n in seg:
     k = re.sub(r"\(.*", "", n.replace("void ", "").replace("(anonymous namespace)::", ""))
