@@ -194,6 +194,7 @@ __device__ __forceinline__ float act_grad_from_out(float y, int act) {
 //   db[n]    (+)= sum_m dz[m][n]                                          (column block 0)
 constexpr int NSLICE = 16;
 constexpr int SLICE_MAX = 256;                  // rows per slice: Nout <= 16 * 256 = 4096
+constexpr int LBR = 8;                          // weight rows per lane with loads in flight together
 __global__ __launch_bounds__(256) void linear_bwd_kernel(const float* __restrict__ dyp, int nsl, long ss, long sm,
                                                          const float* __restrict__ y, const float* __restrict__ x,
                                                          const float* __restrict__ w, float* __restrict__ dxp,
@@ -238,21 +239,33 @@ __global__ __launch_bounds__(256) void linear_bwd_kernel(const float* __restrict
     xk[m] = (m < M && k < K) ? x[(long)m * K + k] : 0.f;
   }
   if (k < K) {
-#pragma unroll 4
-    for (int r = ty; r < rows; r += 4) {
-      const int n = n0 + r;
-      const float wv = w[(long)n * K + k];
-      float g = 0.f;
+    // LBR rows' weights (and old dW) loaded together before any is used: the pass streams W and
+    // dW once, and with one 4-B load per lane in flight its rate was latency-bound (bytes in
+    // flight / latency); same accumulation order as row-at-a-time
+    for (int r0 = ty; r0 < rows; r0 += 4 * LBR) {
+      float wv[LBR], dwo[LBR];
 #pragma unroll
-      for (int m = 0; m < MMAX; ++m) {
-        if (m < M) {
-          const float dz = dzs[m][r];
-          acc[m] += dz * wv;
-          g += dz * xk[m];
+      for (int u = 0; u < LBR; ++u) {
+        const int r = r0 + 4 * u;
+        wv[u] = r < rows ? w[(long)(n0 + r) * K + k] : 0.f;
+        dwo[u] = accumulate && r < rows ? dw[(long)(n0 + r) * K + k] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < LBR; ++u) {
+        const int r = r0 + 4 * u;
+        if (r < rows) {
+          float g = 0.f;
+#pragma unroll
+          for (int m = 0; m < MMAX; ++m) {
+            if (m < M) {
+              const float dz = dzs[m][r];
+              acc[m] += dz * wv[u];
+              g += dz * xk[m];
+            }
+          }
+          dw[(long)(n0 + r) * K + k] = accumulate ? dwo[u] + g : g;
         }
       }
-      float* d = dw + (long)n * K + k;
-      *d = accumulate ? *d + g : g;
     }
   }
   if (!dxp) return;
