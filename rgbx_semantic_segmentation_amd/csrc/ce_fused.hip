@@ -131,8 +131,9 @@ __device__ __forceinline__ void footprint(int y0, int n, float scale, int in, in
   Yb = bb;
 }
 
+constexpr int CE_BWD_NT = 256;
 template <typename T>
-__global__ __launch_bounds__(256) void ce_bwd_fused(const T* __restrict__ logits, const int64_t* __restrict__ label,
+__global__ __launch_bounds__(CE_BWD_NT) void ce_bwd_fused(const T* __restrict__ logits, const int64_t* __restrict__ label,
                                                     const float* __restrict__ dloss, const float* __restrict__ stats,
                                                     T* __restrict__ dlogits, int h, int w, int H, int W, int K,
                                                     int ignore, int tiles_x, int tiles_y) {
@@ -157,11 +158,11 @@ __global__ __launch_bounds__(256) void ce_bwd_fused(const T* __restrict__ logits
   const T* base = logits + (long)b * h * w * K;
   // all global loads first (logits tile + halo, the labels of the thread's footprint pixels),
   // then the LDS stores: one memory latency per block instead of one per 256 items
-  constexpr int NL = (LP * KF + 255) / 256, NPX = (RY * RX + 255) / 256;
+  constexpr int NL = (LP * KF + CE_BWD_NT - 1) / CE_BWD_NT, NPX = (RY * RX + CE_BWD_NT - 1) / CE_BWD_NT;
   float v[NL];
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
-    const int e = threadIdx.x + i * 256;
+    const int e = threadIdx.x + i * CE_BWD_NT;
     const int k = e % K, px = e / K;                  // coalesced global reads along k
     const int yy = y0 - 1 + px / LW, xx = x0 - 1 + px % LW;
     v[i] = (e < LP * K && yy >= 0 && yy < h && xx >= 0 && xx < w) ? to_f32(base[((long)yy * w + xx) * K + k]) : 0.f;
@@ -169,15 +170,15 @@ __global__ __launch_bounds__(256) void ce_bwd_fused(const T* __restrict__ logits
   long labs[NPX];
 #pragma unroll
   for (int i = 0; i < NPX; ++i) {
-    const int pi = threadIdx.x + i * 256;
+    const int pi = threadIdx.x + i * CE_BWD_NT;
     labs[i] = pi < np ? label[((long)b * H + Ya + pi / rx) * W + Xa + pi % rx] : (long)ignore;
   }
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
-    const int e = threadIdx.x + i * 256;
+    const int e = threadIdx.x + i * CE_BWD_NT;
     if (e < LP * K) lg[(e % K) * LP + e / K] = v[i];
   }
-  for (int e = threadIdx.x; e < TY * RY + TX * RX; e += 256) {
+  for (int e = threadIdx.x; e < TY * RY + TX * RX; e += CE_BWD_NT) {
     const bool isy = e < TY * RY;
     const int q = isy ? e : e - TY * RY;
     const int R = isy ? RY : RX;
@@ -197,7 +198,7 @@ __global__ __launch_bounds__(256) void ce_bwd_fused(const T* __restrict__ logits
   // phase A: g for every footprint pixel (one pixel per lane)
 #pragma unroll
   for (int i = 0; i < NPX; ++i) {
-    const int pi = threadIdx.x + i * 256;
+    const int pi = threadIdx.x + i * CE_BWD_NT;
     if (pi >= np) break;
     const int Y = Ya + pi / rx, X = Xa + pi % rx;
     const long lab = labs[i];
@@ -234,33 +235,47 @@ __global__ __launch_bounds__(256) void ce_bwd_fused(const T* __restrict__ logits
       if (k < K) g[k * RY * RX + pi] = from_f32<T>(z[k] * inv - (k == lab ? gs : 0.f));
   }
   __syncthreads();
-  // phase B: x-adjoint t1[k][row][xl] = sum_X wx[xl][X] g[k][row][X]
-  for (int e = threadIdx.x; e < K * ry * nx; e += 256) {
-    const int xl = e % nx, row = (e / nx) % ry, k = e / (nx * ry);
+  // phase B: x-adjoint t1[k][row][xl] = sum_X wx[xl][X] g[k][row][X].  The item index runs over
+  // the compile-time box (KF, RY, TX) -- constant divisors -- and skips what the tile lacks; the
+  // 8 taps are unchecked when they lie inside the footprint (every column but the image borders')
+  for (int e = threadIdx.x; e < KF * RY * TX; e += CE_BWD_NT) {
+    const int xl = e % TX, row = (e / TX) % RY, k = e / (TX * RY);
+    if (k >= K || row >= ry || xl >= nx) continue;
     const T* gr = g + k * RY * RX + row * rx;
     const float* wr = wx + xl * RX;
     // exact x4 (align_corners=False): low-res column x takes full-res X in [4x - 2, 4x + 6)
     // only (the borders' clamped taps included); the other footprint weights are zero
     const int jb = 4 * (x0 + xl) - 2 - Xa;
     float acc = 0.f;
+    if (jb >= 0 && jb + 8 <= rx) {
 #pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      const int j = jb + jj;
-      acc += (j >= 0 && j < rx) ? wr[j] * to_f32(gr[j]) : 0.f;
+      for (int jj = 0; jj < 8; ++jj) acc += wr[jb + jj] * to_f32(gr[jb + jj]);
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int j = jb + jj;
+        acc += (j >= 0 && j < rx) ? wr[j] * to_f32(gr[j]) : 0.f;
+      }
     }
     t1[(row * TX + xl) * KP + k] = acc;
   }
   __syncthreads();
   // phase C: y-adjoint, write the tile (k fastest: coalesced along the NHWC row)
-  for (int e = threadIdx.x; e < ny * nx * K; e += 256) {
-    const int k = e % K, xl = (e / K) % nx, yl = e / (K * nx);
+  for (int e = threadIdx.x; e < TY * TX * KF; e += CE_BWD_NT) {
+    const int k = e % KF, xl = (e / KF) % TX, yl = e / (KF * TX);
+    if (k >= K || xl >= nx || yl >= ny) continue;
     const float* wr = wy + yl * RY;
     const int jb = 4 * (y0 + yl) - 2 - Ya;              // rows [4y - 2, 4y + 6), as above
     float acc = 0.f;
+    if (jb >= 0 && jb + 8 <= ry) {
 #pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      const int j = jb + jj;
-      acc += (j >= 0 && j < ry) ? wr[j] * t1[(j * TX + xl) * KP + k] : 0.f;
+      for (int jj = 0; jj < 8; ++jj) acc += wr[jb + jj] * t1[((jb + jj) * TX + xl) * KP + k];
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int j = jb + jj;
+        acc += (j >= 0 && j < ry) ? wr[j] * t1[(j * TX + xl) * KP + k] : 0.f;
+      }
     }
     dlogits[((long)b * h * w + (long)(y0 + yl) * w + x0 + xl) * K + k] = from_f32<T>(acc);
   }
@@ -297,7 +312,7 @@ int cmx_upsample_ce_bwd(const void* logits, const int64_t* label, const float* d
               "upsample_ce_bwd: needs K <= %d and an exact x4 upsampling (K=%d, %dx%d -> %dx%d)", KF, K, h, w, H, W);
   const int tx = (w + TX - 1) / TX, ty = (h + TY - 1) / TY;
   CMX_DISPATCH(dtype, T, {
-    hipLaunchKernelGGL(ce_bwd_fused<T>, dim3(B * tx * ty), dim3(256), 0, s, (const T*)logits, label, dloss, stats,
+    hipLaunchKernelGGL(ce_bwd_fused<T>, dim3(B * tx * ty), dim3(CE_BWD_NT), 0, s, (const T*)logits, label, dloss, stats,
                        (T*)dlogits, h, w, H, W, K, ignore_index, tx, ty);
   });
   return cmx_check_launch("upsample_ce_bwd");
