@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void ce_fwd_tiled(const T* __restrict__ logits
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
     const int e = threadIdx.x + i * 256;
-    if (e < LRF * LRF * K) lg[(e / K) * KF + e % K] = v[i];
+    if (e < LRF * LRF * K) lg[(e % K) * (LRF * LRF) + e / K] = v[i];   // class-major (see the backward)
   }
   __syncthreads();
   float ls = 0.f, lc = 0.f;
@@ -72,17 +72,22 @@ __global__ __launch_bounds__(256) void ce_fwd_tiled(const T* __restrict__ logits
       float wy0, wy1, wx0, wx1;
       src_idx(Y, sh, h, y0, y1, wy0, wy1);
       src_idx(X, sw, w, x0, x1, wx0, wx1);
-      const float* pa = lg + ((y0 - ly0) * LRF + (x0 - lx0)) * KF;
-      const float* pb = lg + ((y0 - ly0) * LRF + (x1 - lx0)) * KF;
-      const float* pc = lg + ((y1 - ly0) * LRF + (x0 - lx0)) * KF;
-      const float* pd = lg + ((y1 - ly0) * LRF + (x1 - lx0)) * KF;
+      // class-major image [k][px] (49 pixels per class): the lanes of a wave read at most 10
+      // distinct words per class, on distinct banks (a pixel-major [px][k] image put the wave's
+      // low-res pixels 40 words apart: 1.7 bank conflicts per LDS read)
+      constexpr int LP = LRF * LRF;
+      const float* pa = lg + (y0 - ly0) * LRF + (x0 - lx0);
+      const float* pb = lg + (y0 - ly0) * LRF + (x1 - lx0);
+      const float* pc = lg + (y1 - ly0) * LRF + (x0 - lx0);
+      const float* pd = lg + (y1 - ly0) * LRF + (x1 - lx0);
       // compile-time trip counts predicated on k < K: the LDS reads of all classes are in
       // flight together and z stays in registers (a runtime-bound loop waits on each read)
       float z[KF];
       float m = -INFINITY, zl = 0.f;
 #pragma unroll
       for (int k = 0; k < KF; ++k) {
-        z[k] = k < K ? wy0 * (wx0 * pa[k] + wx1 * pb[k]) + wy1 * (wx0 * pc[k] + wx1 * pd[k]) : -INFINITY;
+        z[k] = k < K ? wy0 * (wx0 * pa[k * LP] + wx1 * pb[k * LP]) + wy1 * (wx0 * pc[k * LP] + wx1 * pd[k * LP])
+                     : -INFINITY;
         m = fmaxf(m, z[k]);
         if (k == lab) zl = z[k];
       }
@@ -131,7 +136,9 @@ __device__ __forceinline__ void footprint(int y0, int n, float scale, int in, in
   Yb = bb;
 }
 
-constexpr int CE_BWD_NT = 256;
+// eight waves per workgroup: the 400 footprint pixels of phase A take one pass, and 3 resident
+// workgroups (LDS-bound) give six waves per SIMD to hide the LDS / exp latency
+constexpr int CE_BWD_NT = 512;
 template <typename T>
 __global__ __launch_bounds__(CE_BWD_NT) void ce_bwd_fused(const T* __restrict__ logits, const int64_t* __restrict__ label,
                                                     const float* __restrict__ dloss, const float* __restrict__ stats,
