@@ -5,6 +5,13 @@ the decoder BN) + fused AdamW, i.e. train.py:185-207 for one batch.  The whole s
 captured once into a HIP graph (torch.cuda.CUDAGraph) and replayed; the WarmUpPolyLR
 update is written into the optimizer's device LR scalar between replays.
 
+Protocol: 2 eager steps, capture, W warm-up replays, a settle phase (windows of 10 replays
+until >= 1 s of device time and two window medians within 2 %, at most 4 s; CMX_BENCH_SETTLE_S
+/ _MAX_S), then EXACTLY K timed replays between barrier + synchronize.  The line carries the
+per-replay device times (HIP events between replays: min / median / max of warm-up and timed
+window, the settle window medians) and the sysfs sclk / mclk / power sampled over the timed
+window, so a slow box shows itself in the record.
+
 Usage:  python bench.py [--gpus N --steps K --warmup W]   (N>1: one rank per GPU via
         torch.distributed.run; rank 0 prints ONE JSON line).
 """
@@ -98,6 +105,82 @@ def cpu_baseline(args):
             "config1": {"workload": "CMX-B0 train step 240x320 bs=1 K=9 (BASELINE.json configs[0])",
                         "value": round(1.0 / sec0, 4), "unit": "images/s", "sample": f"2 warm-up + 10 timed steps, "
                                                                                      f"{sec0 * 1e3:.1f} ms/step"}}
+
+
+def device_sysfs(dev_index: int):
+    """The amdgpu sysfs directory of the HIP device (matched by PCI domain:bus:device), or None."""
+    try:
+        p = torch.cuda.get_device_properties(dev_index)
+        path = f"/sys/bus/pci/devices/{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        return path if os.path.exists(os.path.join(path, "pp_dpm_sclk")) else None
+    except Exception:
+        return None
+
+
+def read_clocks(sysfs):
+    """Current (sclk MHz, mclk MHz, power W) from amdgpu sysfs; None for what cannot be read."""
+    def cur(name):
+        try:
+            for line in open(os.path.join(sysfs, name)):
+                if line.rstrip().endswith("*"):
+                    return int(line.split(":")[1].strip().split("M")[0])
+        except (OSError, ValueError, IndexError, TypeError):
+            pass
+        return None
+
+    def power():
+        try:
+            import glob
+            for h in glob.glob(os.path.join(sysfs, "hwmon", "hwmon*")):
+                for n in ("power1_average", "power1_input"):
+                    f = os.path.join(h, n)
+                    if os.path.exists(f):
+                        return round(int(open(f).read()) / 1e6, 1)
+        except (OSError, ValueError, TypeError):
+            pass
+        return None
+    if sysfs is None:
+        return None, None, None
+    return cur("pp_dpm_sclk"), cur("pp_dpm_mclk"), power()
+
+
+class ClockSampler:
+    """Samples sclk / mclk / power from sysfs on a host thread while the timed window runs
+    (the replays are asynchronous, so the host thread costs the device nothing)."""
+
+    def __init__(self, sysfs, period_s: float = 0.02):
+        import threading
+        self.sysfs, self.period, self.samples = sysfs, period_s, []
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        while not self._stop.is_set():
+            self.samples.append(read_clocks(self.sysfs))
+            self._stop.wait(self.period)
+
+    def __enter__(self):
+        if self.sysfs is not None:
+            self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        if self._t.is_alive():
+            self._t.join()
+
+    def summary(self):
+        def stat(i):
+            v = sorted(s[i] for s in self.samples if s[i] is not None)
+            return None if not v else {"min": v[0], "median": v[len(v) // 2], "max": v[-1]}
+        return {"samples": len(self.samples), "sclk_mhz": stat(0), "mclk_mhz": stat(1), "power_w": stat(2)}
+
+
+def replay_stats(ms):
+    v = sorted(ms)
+    if not v:
+        return None
+    return {"n": len(v), "min": round(v[0], 4), "median": round(v[len(v) // 2], 4), "max": round(v[-1], 4)}
 
 
 def free_port() -> int:
@@ -247,21 +330,71 @@ def main():
         else:
             step()
 
-    for _ in range(args.warmup):
-        run_one()
+    def replays(n):
+        """n steps with a HIP event between consecutive ones (on the stream the graph replays
+        on); returns the per-step device times in ms once the caller has synchronised."""
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
+        evs[0].record()
+        for i in range(n):
+            run_one()
+            evs[i + 1].record()
+        return lambda: [evs[i].elapsed_time(evs[i + 1]) for i in range(n)]
+
+    sysfs = device_sysfs(local)
+    clk_idle = read_clocks(sysfs)
+    warm_ms = replays(args.warmup)
+    torch.cuda.synchronize()
+    warm_ms = warm_ms()
+    # settle (SURVEY.md §8(d): warm-up bounded by a stabilised replay time): after the W
+    # warm-up steps, replay in windows of 10 until >= settle_s of device time has passed and
+    # two consecutive window medians agree within 2 % (at most settle_max_s).  Every rank
+    # takes the same decision (the replays hold collectives at N > 1).
+    settle_s = float(os.environ.get("CMX_BENCH_SETTLE_S", "1.0"))
+    settle_max_s = max(settle_s, float(os.environ.get("CMX_BENCH_SETTLE_MAX_S", "4.0")))
+    settle_med, settle_n, settle_t = [], 0, 0.0
+    while settle_s > 0:
+        w = replays(10)
+        torch.cuda.synchronize()
+        w = sorted(w())
+        settle_n, settle_t = settle_n + 10, settle_t + sum(w) / 1e3
+        settle_med.append(w[5])
+        done = settle_t >= settle_max_s or (settle_t >= settle_s and len(settle_med) >= 2
+                                            and abs(settle_med[-1] - settle_med[-2]) <= 0.02 * settle_med[-2])
+        if use_dist:
+            flag = torch.tensor([0 if done else 1], device=dev, dtype=torch.int32)
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+            done = int(flag.item()) == 0
+        if done:
+            break
     if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run_one()
-    t_enq = time.perf_counter() - t0              # host time to enqueue the K replays
-    torch.cuda.synchronize()
-    if use_dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    with ClockSampler(sysfs) as clocks:
+        t0 = time.perf_counter()
+        timed_ms = replays(args.steps)
+        t_enq = time.perf_counter() - t0              # host time to enqueue the K replays
+        torch.cuda.synchronize()
+        if use_dist:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+    timed_ms = timed_ms()
     print(f"[bench] host enqueue {t_enq / args.steps * 1e3:.3f} ms/step of {elapsed / args.steps * 1e3:.3f}",
           file=sys.stderr)
+    trace_n = int(os.environ.get("CMX_BENCH_TRACE", "0"))
+    if trace_n > 0:
+        # diagnostic: the per-replay device-time series of warm-up, timed window and trace_n
+        # more replays, with the clocks sampled beside them
+        with ClockSampler(sysfs, 0.05) as tclk:
+            extra = replays(trace_n)
+            torch.cuda.synchronize()
+        extra = extra()
+        print("[bench-trace] idle clocks " + json.dumps(clk_idle), file=sys.stderr)
+        print("[bench-trace] warmup " + json.dumps([round(v, 3) for v in warm_ms]), file=sys.stderr)
+        print("[bench-trace] timed " + json.dumps([round(v, 3) for v in timed_ms]), file=sys.stderr)
+        for i in range(0, trace_n, 50):
+            print(f"[bench-trace] extra[{i}:] " + json.dumps([round(v, 3) for v in extra[i:i + 50]]), file=sys.stderr)
+        print("[bench-trace] extra clocks " + json.dumps(tclk.summary()), file=sys.stderr)
+        print("[bench-trace] extra clock series " + json.dumps(tclk.samples[::5]), file=sys.stderr)
     if use_dist:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -309,6 +442,11 @@ def main():
                                    "peak_tflops": PEAK_BF16_TFLOPS, "frac": round(step_frac, 5)},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "replay_ms": {"warmup": replay_stats(warm_ms), "timed": replay_stats(timed_ms),
+                          "settle": {"replays": settle_n, "device_s": round(settle_t, 3),
+                                     "window_medians": [round(v, 3) for v in settle_med]}},
+            "clocks": {"idle": dict(zip(("sclk_mhz", "mclk_mhz", "power_w"), clk_idle)),
+                       "timed": clocks.summary()},
         }
         print(json.dumps(out))
     if use_dist:

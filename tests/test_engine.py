@@ -120,3 +120,16 @@ def test_builder_selects_improved_fusion_modules():
     mixed = EncoderDecoder(dict(backbone="mit_b0", num_classes=9, feature_fusion_module="IFFM"))
     assert isinstance(mixed.backbone.FRMs[0], N.FeatureRectifyModule)
     assert isinstance(mixed.backbone.FFMs[0], N.ImprovedFeatureFusionModule)
+
+
+def test_train_fp16_always_loss_scaled():
+    """fp16 storage without --use-mixed-precision must still run the GradScaler
+    (the reference only trains fp16 under autocast + GradScaler, train.py:185-198)."""
+    import train
+    p = train.build_parser()
+    assert train.resolve_precision(p.parse_args([])) == ("bfloat16", False)
+    assert train.resolve_precision(p.parse_args(["--use-mixed-precision"])) == ("float16", True)
+    assert train.resolve_precision(p.parse_args(["--compute-dtype", "float16"])) == ("float16", True)
+    assert train.resolve_precision(p.parse_args(["--compute-dtype", "float32"])) == ("float32", False)
+    assert train.resolve_precision(p.parse_args(["--compute-dtype", "bfloat16",
+                                                 "--use-mixed-precision"])) == ("bfloat16", True)

@@ -69,6 +69,14 @@ def build_parser():
     return p
 
 
+def resolve_precision(args):
+    """(compute dtype, dynamic loss scaling on?).  The reference runs fp16 only under autocast
+    with a GradScaler (train.py:185-198), so fp16 storage always turns loss scaling on, as in
+    bench.py: fp16 training without it would let gradient under/overflow go undetected."""
+    dtype = args.compute_dtype or ("float16" if args.use_mixed_precision else "bfloat16")
+    return dtype, bool(args.use_mixed_precision or dtype == "float16")
+
+
 def main(argv=None):
     parser = build_parser()
     with Engine(custom_parser=parser, argv=argv) as engine:
@@ -108,7 +116,7 @@ def main(argv=None):
         from rgbx_semantic_segmentation_amd import dist as cdist
 
         norm = torch.nn.SyncBatchNorm if engine.distributed else torch.nn.BatchNorm2d
-        dtype = args.compute_dtype or ("float16" if args.use_mixed_precision else "bfloat16")
+        dtype, loss_scaling = resolve_precision(args)
         cfg = dict(backbone=args.backbone, num_classes=args.num_classes, compute_dtype=dtype,
                    decoder_embed_dim=512)
         model = EncoderDecoder(cfg, norm_layer=norm).to(dev)
@@ -124,7 +132,7 @@ def main(argv=None):
         total_iteration = args.nepochs * args.niters_per_epoch
         lr_policy = WarmUpPolyLR(args.lr, args.lr_power, total_iteration, args.niters_per_epoch * args.warm_up_epoch)
 
-        scaler = GradScaler(enabled=args.use_mixed_precision, device=dev)
+        scaler = GradScaler(enabled=loss_scaling, device=dev)
         engine.register_state(dataloader=train_loader, model=model, optimizer=optimizer)
         if engine.continue_state_object:
             engine.restore_checkpoint()
