@@ -252,6 +252,7 @@ def main():
     from rgbx_semantic_segmentation_amd.data import make_batch
     from rgbx_semantic_segmentation_amd.utils.lr_policy import WarmUpPolyLR
     from rgbx_semantic_segmentation_amd.flops import train_flops_per_image
+    from rgbx_semantic_segmentation_amd.floor import floor_table
     from rgbx_semantic_segmentation_amd import dist as cdist
 
     torch.manual_seed(12345)
@@ -405,6 +406,13 @@ def main():
     fl_img = train_flops_per_image(backbone=args.backbone, H=args.height, W=args.width, K=args.classes)
     step_frac = (ips / world) * fl_img / (PEAK_BF16_TFLOPS * 1e12)
 
+    # the step's roofline floor: sum over kernel families of max(FLOP / MFMA peak, bytes / HBM)
+    # of the work as executed (floor.py); frac = floor / measured per-rank step time
+    frows, ftot = floor_table(backbone=args.backbone, H=args.height, W=args.width, B=args.batch, K=args.classes,
+                              n_params=float(model.store.flat.numel()))
+    step_floor = {"floor_us": round(ftot, 1), "frac": round(ftot / (ms * 1e3), 4),
+                  "families_us": {f: round(us, 1) for f, _, _, us, _ in frows}}
+
     # every rank runs the roofline step (its SyncBN collectives need all ranks); rank 0 reports.
     # No optimizer step follows it, so the gradient all-reduce hooks are detached first.
     from rgbx_semantic_segmentation_amd.roofline import measure_dominant
@@ -440,6 +448,7 @@ def main():
             "step_mfma_roofline": {"train_gflop_per_image": round(fl_img / 1e9, 3),
                                    "achieved_tflops": round((ips / world) * fl_img / 1e12, 2),
                                    "peak_tflops": PEAK_BF16_TFLOPS, "frac": round(step_frac, 5)},
+            "step_floor": step_floor,
             "roofline": roof,
             "cpu_baseline": cpu,
             "replay_ms": {"warmup": replay_stats(warm_ms), "timed": replay_stats(timed_ms),

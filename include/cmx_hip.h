@@ -34,10 +34,8 @@ int cmx_abi_version(void);
 const char* cmx_last_error(void);
 /* pinned host -> device copy of a packed record table on `stream` (see grouped launches) */
 int cmx_upload(void* dst, const void* src, size_t nbytes, hipStream_t stream);
-/* launch-policy knobs (GEMM_TILES, GEMM_SMALLK, GEMM_T128, GEMM_KW, GEMM_NS64, GEMM_SPLITKW,
- * GEMM_DEEP, GEMM_STREAM, GEMM_STREAM_NS, GEMM_STREAM_NSR, GEMM_STREAM_BPC, GEMM_REG,
- * GEMM_REG_BPC, SRA_SMALL_N, SRA_DKV_DIRECT, SRA_QW, SRA_NW, GROUPED_KT, GROUPED_CHUNK,
- * GROUPED_NS): initialised from the
+/* launch-policy knobs (GEMM_TILES, GEMM_SMALLK, GEMM_T128, GEMM_KW, GEMM_SPLITKW, SRA_SMALL_N,
+ * SRA_DKV_DIRECT, SRA_QW, SRA_NW, GROUPED_KT, GROUPED_CHUNK): initialised from the
  * CMX_<NAME> environment variable, changed in-process by cmx_tune for interleaved A/B runs;
  * a knob set before the first launch that reads it keeps the set value.  tune_get: -1 if unset. */
 int cmx_tune(const char* name, int value);
@@ -199,11 +197,6 @@ int cmx_upsample_ce_bwd(const void* logits, const int64_t* label, const float* d
  * reducer applies the epilogue); splitk <= 0: the library's choice, cmx_gemm_splitk(). */
 size_t cmx_gemm_workspace(int G, int M, int N, int splitk);
 int cmx_gemm_splitk(int G, int M, int N, int K, int ones_col, int dtype);
-/* cmx_gemm (no split, plain 16-bit store, N = 64 or 128 so one tile spans whole rows) whose
- * epilogue also writes ln_y = LayerNorm(C) over the N columns (gamma / beta (G, N), eps) and
- * the per-row mean / rstd (G * M): Block.norm1 / norm2 (dual_segformer.py:166-169) and the stage
- * norm computed by the residual GEMM (proj / fc2) that produces their input.  ln_y has C's layout. */
-int cmx_gemm_ln(const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R, const float* rscale, int G, int M, int N, int K, int K1, int64_t lda, int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias, int rows_per_sample, int transA, int transB, int act, void* ln_y, const float* gamma, const float* beta, float* mean, float* rstd, float eps, int dtype, hipStream_t stream);
 int cmx_gemm(const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R, const float* rscale, float* dbias, float* workspace, int G, int M, int N, int K, int K1, int64_t lda, int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias, int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode, int ones_col, int splitk, int dtype, hipStream_t stream);
 /* cmx_gemm_h2: cmx_gemm (no A2 / bias / residual / epilogue extras) over a two-level batch of G = Go * gh
  *      problems: problem g reads / writes at (g / gh) * sX + (g % gh) * sXh -- the per-head k^T v,

@@ -135,21 +135,12 @@ struct UpSpec {
   int h[3], w[3], n, oH, oW;
 };
 
-// LayerNorm epilogue of cmx_gemm_ln (null: none)
-struct LnSpec {
-  void* y;
-  const float *gamma, *beta;
-  float *mean, *rstd;
-  float eps;
-};
-
 int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R,
               const float* rscale, float* dbias, float* workspace, int G, int M, int N, int K, int K1, int64_t lda,
               int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias,
               int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode, int ones_col, int splitk,
               int dtype, hipStream_t s, const UpSpec* up, int scR = 0, int scH = 0, int scW = 0, int scC = 0,
-              int scHo = 0, int scWo = 0, int gh = 1, int64_t sAh = 0, int64_t sBh = 0, int64_t sCh = 0,
-              const LnSpec* ln = nullptr) {
+              int scHo = 0, int scWo = 0, int gh = 1, int64_t sAh = 0, int64_t sBh = 0, int64_t sCh = 0) {
   CMX_REQUIRE(G > 0 && M > 0 && N > 0 && K > 0, CMX_ERR_SHAPE, "gemm: empty problem G=%d M=%d N=%d K=%d", G, M, N, K);
   CMX_REQUIRE(dtype >= 0 && dtype <= 2, CMX_ERR_DTYPE, "gemm: unsupported dtype %d", dtype);
   CMX_REQUIRE(out_mode >= 0 && out_mode <= 2 && act >= 0 && act <= 3, CMX_ERR_ARG, "gemm: out_mode/act");
@@ -207,27 +198,11 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
   a.kt_per_split = (nk + splitk - 1) / splitk;
   splitk = (nk + a.kt_per_split - 1) / a.kt_per_split;      // no empty splits
   a.nsplit = splitk;
-  if (ln) {
-    // whole rows per tile: 64 x 64 (N = 64) or 64 x 128 (N = 128) on the 16-bit LDS-image path
-    CMX_REQUIRE(fast && splitk == 1 && out_mode == 0 && !ones_col && !a.nup && !a.scatter && gh == 1 &&
-                (N == 64 || N == 128) && ln->y && ln->gamma && ln->beta && ln->mean && ln->rstd &&
-                ((uintptr_t)ln->y & 15) == 0 && a.cvec, CMX_ERR_ARG,
-                "gemm_ln: needs the 16-bit path, N = 64 or 128, one split, a plain 16-B aligned store (N=%d)", N);
-    a.lnY = ln->y; a.lnG = ln->gamma; a.lnB = ln->beta; a.lnMean = ln->mean; a.lnRstd = ln->rstd; a.lnEps = ln->eps;
-    a.tiles_m = cdiv(M, 64); a.tiles_n = 1;
-    launch_fast(a, 64, N, G, 1, transA, transB, dtype, s);
-    return cmx_check_launch("gemm_ln");
-  }
   if (fast) {
     int bm, bn;
     plan_tiles(G, M, nb, K, &bm, &bn);
     a.tiles_m = cdiv(M, bm); a.tiles_n = cdiv(nb, bn);
-    bool done = reg_ok(a, splitk, transA, dtype) &&
-                (dtype == 2 ? launch_reg_t<f16>(a, transB, s) : launch_reg_t<bf16>(a, transB, s));
-    if (!done)
-      done = stream_ok(a, bm, bn, splitk, transA, dtype) &&
-             (dtype == 2 ? launch_stream_t<f16>(a, transA, transB, s) : launch_stream_t<bf16>(a, transA, transB, s));
-    if (!done) launch_fast(a, bm, bn, G, splitk, transA, transB, dtype, s);
+    launch_fast(a, bm, bn, G, splitk, transA, transB, dtype, s);
   } else {
     // tile shape: the output's narrow side gets 64 (stage-1 C = 64 outputs, 64-row wgrads)
     const bool m64 = M <= 64, n64 = N <= 64;
@@ -268,18 +243,6 @@ int cmx_gemm(const void* A, const void* A2, const void* B, void* C, const float*
              int dtype, hipStream_t s) {
   return gemm_impl(A, A2, B, C, bias, R, rscale, dbias, workspace, G, M, N, K, K1, lda, lda2, ldb, ldc, sA, sA2, sB,
                    sC, sbias, sdb, rows_per_sample, transA, transB, act, out_mode, ones_col, splitk, dtype, s, nullptr);
-}
-
-// cmx_gemm + the LayerNorm of the stored rows in the epilogue (see include/cmx_hip.h)
-int cmx_gemm_ln(const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R,
-                const float* rscale, int G, int M, int N, int K, int K1, int64_t lda, int64_t lda2, int64_t ldb,
-                int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias, int rows_per_sample,
-                int transA, int transB, int act, void* ln_y, const float* gamma, const float* beta, float* mean,
-                float* rstd, float eps, int dtype, hipStream_t s) {
-  const LnSpec ln{ln_y, gamma, beta, mean, rstd, eps};
-  return gemm_impl(A, A2, B, C, bias, R, rscale, nullptr, nullptr, G, M, N, K, K1, lda, lda2, ldb, ldc, sA, sA2, sB,
-                   sC, sbias, 0, rows_per_sample, transA, transB, act, 0, 0, 1, dtype, s, nullptr, 0, 0, 0, 0, 0, 0, 1,
-                   0, 0, 0, &ln);
 }
 
 // dx of a non-overlapping patchify conv (stride == kernel == R, pad 0: Attention.sr,
@@ -465,20 +428,9 @@ int cmx_gemm_grouped(const void* recs, int nrec, int total_blocks, int dtype, hi
   // (scripts/grouped_chunk_sweep.sh); PMC HBM bytes per launch 3.13 GB at 16-tile runs,
   // 2.48 GB at 64 (contiguous: 2.43 GB), so 64 keeps the L2 reuse of neighbouring tiles
   static int& chunk = cmx_knob("GROUPED_CHUNK", 64);
-  static int& ns = cmx_knob("GROUPED_NS", 2);
   const GroupRec* rr = (const GroupRec*)recs;
-#define CMX_GROUPED_LAUNCH(E, NS) \
-  hipLaunchKernelGGL((gemm_grouped_kernel<E, NS>), dim3(total_blocks), dim3(256), 0, s, rr, nrec, chunk)
-  if (dtype == 2) {
-    if (ns >= 4) CMX_GROUPED_LAUNCH(f16, 4);
-    else if (ns == 3) CMX_GROUPED_LAUNCH(f16, 3);
-    else CMX_GROUPED_LAUNCH(f16, 2);
-  } else {
-    if (ns >= 4) CMX_GROUPED_LAUNCH(bf16, 4);
-    else if (ns == 3) CMX_GROUPED_LAUNCH(bf16, 3);
-    else CMX_GROUPED_LAUNCH(bf16, 2);
-  }
-#undef CMX_GROUPED_LAUNCH
+  if (dtype == 2) hipLaunchKernelGGL((gemm_grouped_kernel<f16>), dim3(total_blocks), dim3(256), 0, s, rr, nrec, chunk);
+  else hipLaunchKernelGGL((gemm_grouped_kernel<bf16>), dim3(total_blocks), dim3(256), 0, s, rr, nrec, chunk);
   return cmx_check_launch("gemm_grouped");
 }
 

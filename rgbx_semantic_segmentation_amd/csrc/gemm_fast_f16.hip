@@ -1,4 +1,4 @@
-// f16 instantiations of the 16-bit GEMM launchers (LDS-DMA tile kernel, stream kernel); see gemm_kernels.h
+// f16 instantiations of the 16-bit GEMM launchers (LDS-DMA tile kernels); see gemm_kernels.h
 #include "gemm_kernels.h"
 using gemmk::GemmArgs;
 CMX_GEMM_FAST_INST(f16)

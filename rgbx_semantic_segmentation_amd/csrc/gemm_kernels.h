@@ -1,6 +1,6 @@
 // gemm_kernels.h -- device code and launchers of the MFMA GEMM family (see gemm.hip for the
 // design notes).  Split out so the template instantiations compile in parallel translation
-// units: gemm_fast_bf16.hip / gemm_fast_f16.hip (the 16-bit LDS-DMA and stream kernels),
+// units: gemm_fast_bf16.hip / gemm_fast_f16.hip (the 16-bit LDS-DMA tile kernels),
 // gemm_generic_*.hip (the register-staged path per element type), gemm.hip (entry points,
 // grouped launches).  Launchers instantiated elsewhere are declared `extern template` in the
 // TUs that call them (GEMM_EXTERN_LAUNCHERS below).
@@ -34,14 +34,6 @@ struct GemmArgs {
   // the plain stride g * sX
   int gh;
   long sAh, sBh, sCh;
-  // LayerNorm of the stored rows (cmx_gemm_ln): the tile spans whole rows (N == BN); lnY (C's
-  // layout) = LN(C) over the N columns with per-group gamma / beta (G, N), per-row mean / rstd
-  // (G * M) -- the next Block norm on the residual stream computed in the producing GEMM's
-  // epilogue instead of a separate launch re-reading the rows
-  void* lnY;
-  const float *lnG, *lnB;
-  float *lnMean, *lnRstd;
-  float lnEps;
 };
 
 // block id -> tile id, giving each of the 8 XCDs (hardware deals block b to XCD b % 8) a
@@ -211,36 +203,6 @@ __device__ __forceinline__ float* slab_db(const GemmArgs& p, int G, int g, int z
   return p.ws + (long)G * p.nsplit * p.M * Nr + ((long)g * p.nsplit + z) * p.M;
 }
 
-// LayerNorm of row i from the TPR threads that hold its 8-column groups (consecutive lanes):
-// statistics over the STORED (16-bit rounded) values, in the order ln_fwd_kernel sums them
-// (8 values per lane, then a TPR-lane butterfly), so the fused and unfused norms agree
-template <typename E, int TPR>
-__device__ __forceinline__ void ln_row8(const GemmArgs& p, int g, int i, int j, const float* v) {
-  float xb[8], s = 0.f;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    xb[e] = to_f32(from_f32<E>(v[e]));
-    s += xb[e];
-  }
-  s = group_sum(s, TPR);
-  const float mu = s / p.N;
-  float q = 0.f;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) { const float d = xb[e] - mu; q += d * d; }
-  q = group_sum(q, TPR);
-  const float rstd = rsqrtf(q / p.N + p.lnEps);
-  const float* gg = p.lnG + (long)g * p.N + j;
-  const float* bb = p.lnB + (long)g * p.N + j;
-  float o[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) o[e] = (xb[e] - mu) * rstd * gg[e] + bb[e];
-  store_vec<E>(reinterpret_cast<E*>(p.lnY) + goff(p, g, p.sC, p.sCh) + (long)i * p.ldc + j, o);
-  if ((threadIdx.x % TPR) == 0) {
-    p.lnMean[(long)g * p.M + i] = mu;
-    p.lnRstd[(long)g * p.M + i] = rstd;
-  }
-}
-
 // ============================================================================ bf16 fast path
 constexpr int FBK = 64;                         // k per pipeline stage
 // swizzle of the transposed image [64][ROWS]: 16-B chunk position of chunk c in k-row kk
@@ -330,7 +292,7 @@ constexpr int gemm_smem_bytes() {
 // One output tile (of one split / group) of problem p.  `lin` = the block's linear index
 // within the problem, in (split, group, tile) order; smem = gemm_smem_bytes<BM, BN, NS>().
 // E = the 16-bit storage type (bf16 or f16: v_mfma_f32_32x32x16_bf16 / _f16, same tiles and rate)
-template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1, typename E = bf16, bool LN = false>
+template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1, typename E = bf16>
 __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin, char* smem) {
   constexpr int A_BYTES = BM * FBK * 2, STAGE = (BM + BN) * FBK * 2, SLOT = KW * STAGE;
   constexpr int TM = BM / 64, TN = BN / 64;
@@ -557,328 +519,19 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
       }
     } else {
       epi_store8<E>(p, g, i, j, nv, v);
-      if constexpr (LN) ln_row8<E, TPR>(p, g, i, j, v);
     }
   }
 }
 
 // 1-D grid over (split, group, tile); each XCD gets a contiguous run of that order, i.e.
 // neighbouring tiles of one (split, group): they share A row panels and the B k-slice in L2
-// LN: the LayerNorm epilogue of cmx_gemm_ln (a separate instantiation: the norm's registers
-// would otherwise count against every GEMM's occupancy)
 // (64 x 64 two-stage blocks take 32 KB of LDS: five fit a CU when the kernel stays within 96
 // VGPRs, which the launch bound asks of the register allocator -- at 97 only four are resident)
-template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1, typename E = bf16, bool LN = false>
-__global__ __launch_bounds__(256 * KW, (BM == 64 && BN == 64 && NS == 2 && KW == 1 && !LN) ? 5 : (KW == 4 ? 1 : 2))
+template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1, typename E = bf16>
+__global__ __launch_bounds__(256 * KW, (BM == 64 && BN == 64 && NS == 2 && KW == 1) ? 5 : (KW == 4 ? 1 : 2))
 void gemm_bf16_kernel(const GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[gemm_smem_bytes<BM, BN, NS, KW>()];
-  gemm_bf16_body<BM, BN, TA, TB, NS, KW, E, LN>(p, xcd_tile(blockIdx.x, p.tiles_m * p.tiles_n * p.G * p.nsplit), smem);
-}
-
-// ============================================================================ stream kernel
-// Persistent 64 x 64 tiles for the many-tile, short-k problems of stages 1-2 and the decoder
-// (M 9600-76800 tokens, K 64-512: a handful of k-tiles per output tile).  One block per tile
-// runs DMA -> MFMA -> epilogue as one latency chain, every block of a launch in the same phase,
-// so HBM idles while the tiles are multiplied and stored.  Here a block walks the tiles
-// t = b, b + grid, ... (XCD-aware order: block b's virtual ids stay on its XCD) and the NS-deep
-// LDS-DMA ring runs straight across tile boundaries: the next tiles' operands are in flight
-// while a tile's epilogue stores leave from the accumulators (no LDS image).  The epilogue
-// reads nothing from global memory between DMAs (a younger global load could only be waited
-// for together with every older DMA -- vmcnt counts in issue order): the residual tile rides
-// the ring as a third image, bias and DropPath scales are staged into LDS once per block, and
-// the barriers are raw s_barrier (a __syncthreads fence would drain the ring).
-constexpr int ST_BIAS_MAX = 2048;      // G * N bias floats staged per block
-constexpr int ST_SCALE_MAX = 256;      // DropPath scales (G * M / rows_per_sample)
-
-template <int NS, bool HR>
-constexpr int stream_smem_bytes() {
-  return NS * (HR ? 3 : 2) * 64 * FBK * 2 + (ST_BIAS_MAX + ST_SCALE_MAX) * 4;
-}
-
-__device__ __forceinline__ void raw_barrier() {
-  __builtin_amdgcn_s_waitcnt((15) | (3 << 14) | (7 << 4) | (0 << 8));   // lgkmcnt(0) only
-  __builtin_amdgcn_s_barrier();
-}
-
-template <bool TA, bool TB, int NS, bool HR, typename E>
-__global__ __launch_bounds__(256, 2) void gemm_stream_kernel(const GemmArgs p) {
-  constexpr int TILE = 64 * FBK * 2;                  // one 64 x 64 16-bit image
-  constexpr int SLOT = (HR ? 3 : 2) * TILE;
-  constexpr int PER = HR ? 6 : 4;                      // DMA instructions per wave per ring slot
-  __shared__ __attribute__((aligned(1024))) char smem[stream_smem_bytes<NS, HR>()];
-  float* bias_s = reinterpret_cast<float*>(smem + NS * SLOT);
-  float* scale_s = bias_s + ST_BIAS_MAX;
-  const int ntile = p.tiles_m * p.tiles_n, total = ntile * p.G;
-  const int nk = (p.K + FBK - 1) / FBK;
-  const int mine = (total - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
-  const int iters = mine * nk;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
-  const int r = lane & 31, h = lane >> 5;
-
-  // bias / DropPath scales -> LDS, before any DMA is in flight
-  if (p.bias)
-    for (int e = threadIdx.x; e < p.G * p.N; e += 256) {
-      const int g = e / p.N, j = e - g * p.N;
-      bias_s[e] = p.bias[(long)g * p.sbias + j];
-    }
-  const int nscale = p.rscale ? (int)(((long)p.G * p.M + p.rows_per_sample - 1) / p.rows_per_sample) : 0;
-  for (int e = threadIdx.x; e < nscale; e += 256) scale_s[e] = p.rscale[e];
-  __syncthreads();
-
-  struct Tile { int g, i0, j0; };
-  auto tile_of = [&](int q) {
-    const int lin = xcd_tile((int)blockIdx.x + q * (int)gridDim.x, total);
-    const int t = lin % ntile, g = lin / ntile;
-    const int tm = t / p.tiles_n;
-    return Tile{g, tm * 64, (t - tm * p.tiles_n) * 64};
-  };
-
-  auto stage = [&](int it, char* buf) {
-    const int q = it / nk, kt = it - q * nk;
-    const Tile tl = tile_of(q);
-    const int k0 = kt * FBK;
-    const E* Ag = reinterpret_cast<const E*>(p.A) + goff(p, tl.g, p.sA, p.sAh);
-    const E* Bg = reinterpret_cast<const E*>(p.B) + goff(p, tl.g, p.sB, p.sBh);
-    if constexpr (TA) {
-      stage_r<64>(make_rsrc(Ag), buf, p.lda, tl.i0, p.M, k0, p.K, w, lane);
-    } else if (k0 < p.K1) {
-      stage_k<64>(make_rsrc(Ag), buf, p.lda, tl.i0, p.M, k0, p.K1, w, lane);
-    } else {
-      const E* A2g = reinterpret_cast<const E*>(p.A2) + (long)tl.g * p.sA2;
-      stage_k<64>(make_rsrc(A2g), buf, p.lda2, tl.i0, p.M, k0 - p.K1, p.K - p.K1, w, lane);
-    }
-    if constexpr (TB) stage_r<64>(make_rsrc(Bg), buf + TILE, p.ldb, tl.j0, p.N, k0, p.K, w, lane);
-    else stage_k<64>(make_rsrc(Bg), buf + TILE, p.ldb, tl.j0, p.N, k0, p.K, w, lane);
-    if constexpr (HR) {
-      // the residual tile (rows i0.., columns j0..) as a k-contiguous image, every slot (the
-      // DMA count per slot is a compile-time constant): past the tile's last k-step it is the
-      // real tile, otherwise out-of-range (zero-filled, no traffic)
-      const E* Rg = reinterpret_cast<const E*>(p.R) + goff(p, tl.g, p.sC, p.sCh);
-      stage_k<64>(make_rsrc(Rg), buf + 2 * TILE, p.ldc, tl.i0, kt == nk - 1 ? p.M : 0, tl.j0, p.N, w, lane);
-    }
-  };
-
-  f32x16 acc = zero16();
-  auto compute = [&](const char* buf) {
-#pragma unroll
-    for (int s = 0; s < FBK / 16; ++s) {
-      frag8<E> fa, fb;
-      if constexpr (TA) fa = frag_r<E, 64>(buf, wm * 32, s, lane);
-      else fa = frag_k<E>(buf, wm * 32, s, lane);
-      if constexpr (TB) fb = frag_r<E, 64>(buf + TILE, wn * 32, s, lane);
-      else fb = frag_k<E>(buf + TILE, wn * 32, s, lane);
-      acc = MF<E>::mma(fb, fa, acc);
-    }
-  };
-
-  // lane (r, h) holds C(i = r, j = 8 g4 + 4 h + 0..3) of its 32 x 32 sub-tile.  Every wave
-  // issues exactly 4 buffer stores per tile (lanes outside the problem store to an
-  // out-of-range offset, which the buffer unit drops), so the counted waits below know how
-  // many stores are younger than the ring's DMAs.
-  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-  auto epilogue = [&](int q, const char* buf) {
-    const Tile tl = tile_of(q);
-    const int il = wm * 32 + r, i = tl.i0 + il;
-    const bool row_ok = i < p.M;
-    float sc = 1.f;
-    if (p.rscale && row_ok) sc = scale_s[((long)tl.g * p.M + i) / p.rows_per_sample];
-    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<E*>(p.C) + goff(p, tl.g, p.sC, p.sCh), 0, 0x7ffffff0, 0x00020000);
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const int jl = wn * 32 + 8 * g4 + 4 * h, j = tl.j0 + jl;
-      const bool ok = row_ok && j < p.N;
-      float v[4] = {acc[4 * g4], acc[4 * g4 + 1], acc[4 * g4 + 2], acc[4 * g4 + 3]};
-      if (p.bias) {
-        const float* bp = bias_s + tl.g * p.N + (ok ? j : 0);
-        v[0] += bp[0]; v[1] += bp[1]; v[2] += bp[2]; v[3] += bp[3];
-      }
-      if (p.act) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = act_fwd(v[e], p.act);
-      }
-      if constexpr (HR) {
-        const int pos = (jl >> 3) ^ ((il >> 1) & 7);
-        const uint2 rv = *reinterpret_cast<const uint2*>(buf + 2 * TILE + il * 128 + pos * 16 + 8 * h);
-        const cmx_f2 r0 = unpack2<E>(rv.x), r1 = unpack2<E>(rv.y);
-        v[0] = r0.x + sc * v[0]; v[1] = r0.y + sc * v[1]; v[2] = r1.x + sc * v[2]; v[3] = r1.y + sc * v[3];
-      }
-      const int off = ok ? (int)(((long)i * p.ldc + j) * 2) : OOB;
-      u32x2 d = {pack2<E>(v[0], v[1]), pack2<E>(v[2], v[3])};
-      __builtin_amdgcn_raw_buffer_store_b64(d, rc, off, 0, 0);
-    }
-  };
-
-  // counted waits: all but the `keep` youngest ring slots landed, plus `st` younger stores
-  auto wait_keep = [](int keep, bool st) {
-    if (st) {
-      if (NS > 3 && keep >= 3) vm_wait<3 * PER + 4>();
-      else if (NS > 2 && keep == 2) vm_wait<2 * PER + 4>();
-      else if (keep >= 1) vm_wait<PER + 4>();
-      else vm_wait<4>();
-    } else {
-      if (NS > 3 && keep >= 3) vm_wait<3 * PER>();
-      else if (NS > 2 && keep == 2) vm_wait<2 * PER>();
-      else if (keep >= 1) vm_wait<PER>();
-      else vm_wait<0>();
-    }
-  };
-
-  const int pro = min(NS - 1, iters);
-#pragma unroll
-  for (int q = 0; q < NS - 1; ++q)
-    if (q < pro) stage(q, smem + q * SLOT);
-  wait_keep(pro - 1, false);
-  raw_barrier();
-  int cur = 0;
-  for (int it = 0; it < iters; ++it) {
-    const int nxt = cur == 0 ? NS - 1 : cur - 1;
-    if (it + NS - 1 < iters) stage(it + NS - 1, smem + nxt * SLOT);
-    compute(smem + cur * SLOT);
-    const int q = it / nk;
-    const bool last = it - q * nk == nk - 1;
-    if (last) {
-      epilogue(q, smem + cur * SLOT);
-      acc = zero16();
-    }
-    const int ahead = min(NS - 1, iters - 1 - it);
-    wait_keep(ahead - 1, last);
-    raw_barrier();
-    cur = cur + 1 == NS ? 0 : cur + 1;
-  }
-  vm_wait<0>();
-}
-
-// ============================================================================ register-streamed GEMM
-// The many-row, short-k GEMMs of stages 1-2 and the decoder (M 9600-76800 rows, K <= 512, the
-// weight slice small enough for LDS): the block stages its (BN x K) weight slice in LDS once
-// (LDS-DMA), then each of its 4 waves walks 32-row strips of A on its own -- A fragments
-// loaded straight from HBM into registers (16 B per lane, the MFMA operand layout: row r, 8
-// consecutive k), the next k-chunk / strip prefetched while this one is multiplied, the
-// epilogue stored from the accumulators.  No LDS image of A or C and no barrier after the
-// weight staging, so a CU keeps ~8 independent load streams in flight instead of a few
-// lock-stepped DMA -> MFMA -> epilogue chains (the 64 x 64 tile kernel's latency bound).
-// The residual tile and DropPath scale of a strip are loaded at the strip's start, before its
-// k-chunk prefetches, so the epilogue's wait on them never waits for a younger prefetch.
-template <bool TB, int BN, int NK, typename E>
-__global__ __launch_bounds__(256, 4) void gemm_reg_kernel(const GemmArgs p) {
-  constexpr int NT = BN / 32, IMG = BN * 64 * 2;
-  __shared__ __attribute__((aligned(1024))) char smem[NK * IMG + BN * 4];
-  float* bias_s = reinterpret_cast<float*>(smem + NK * IMG);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
-  const int g = blockIdx.z, n0 = blockIdx.y * BN;
-  const E* Bg = reinterpret_cast<const E*>(p.B) + goff(p, g, p.sB, p.sBh);
-  const i32x4 rB = make_rsrc(Bg);
-#pragma unroll
-  for (int kc = 0; kc < NK; ++kc) {
-    if constexpr (TB) stage_r<BN>(rB, smem + kc * IMG, p.ldb, n0, p.N, kc * 64, p.K, w, lane);
-    else stage_k<BN>(rB, smem + kc * IMG, p.ldb, n0, p.N, kc * 64, p.K, w, lane);
-  }
-  for (int e = threadIdx.x; e < BN; e += 256)
-    bias_s[e] = (p.bias && n0 + e < p.N) ? p.bias[(long)g * p.sbias + n0 + e] : 0.f;
-  vm_wait<0>();
-  __syncthreads();
-
-  const E* Ag = reinterpret_cast<const E*>(p.A) + goff(p, g, p.sA, p.sAh);
-  const E* A2g = p.A2 ? reinterpret_cast<const E*>(p.A2) + (long)g * p.sA2 : Ag;
-  const E* Rg = p.R ? reinterpret_cast<const E*>(p.R) + goff(p, g, p.sC, p.sCh) : nullptr;
-  E* Cg = reinterpret_cast<E*>(p.C) + goff(p, g, p.sC, p.sCh);
-  const int nstrip = (p.M + 31) / 32;
-  const int nwv = gridDim.x * 4;
-  int t = blockIdx.x * 4 + w;
-  if (t >= nstrip) return;                       // waves are independent from here on
-
-  // A chunk kc of strip t: 4 x 16 B buffer loads per lane (row t*32 + r, k = 64 kc + 16 s + 8 h;
-  // rows past M / k past K read as zeros through the out-of-range offset).  32-bit offsets on
-  // a resource in SGPRs: no 64-bit address per load held in VGPRs.  A 64-deep chunk lies in
-  // one of the two A segments (K1 % 64 == 0), so the segment choice is wave-uniform.
-  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(const_cast<E*>(Ag), 0, 0x7ffffff0, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rA2 = __builtin_amdgcn_make_buffer_rsrc(const_cast<E*>(A2g), 0, 0x7ffffff0, 0x00020000);
-  auto load_a = [&](int tt, int kc, uint4* fa) {
-    const int i = tt * 32 + r;
-    const bool first = kc * 64 < p.K1;
-    const int k0 = first ? kc * 64 : kc * 64 - p.K1;
-    const int kend = first ? p.K1 : p.K - p.K1;
-    const int rowoff = (int)((long)i * (first ? p.lda : p.lda2) * 2);
-#pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
-      const int k = k0 + 16 * s4 + 8 * h;
-      const int off = (i < p.M && k < kend) ? rowoff + k * 2 : OOB;
-      fa[s4] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(first ? rA : rA2, off, 0, 0));
-    }
-  };
-
-  // double buffer indexed by compile-time k-chunk parity (a runtime index would put the
-  // arrays in scratch); an odd chunk count leaves the next strip's chunk 0 in buffer 1, moved
-  // down at the strip's end
-  uint4 abuf[2][4];
-  load_a(t, 0, abuf[0]);
-  for (; t < nstrip; t += nwv) {
-    // (a compiler-level memory barrier: keeps the weight fragments' LDS reads inside the strip
-    // loop -- hoisted out of it they would hold NK x 32 VGPRs live and spill)
-    asm volatile("" ::: "memory");
-    const int i = t * 32 + r;
-    const bool row_ok = i < p.M;
-    // residual + DropPath scale of this strip, ahead of the strip's prefetches
-    uint2 rv[NT][4];
-    float sc = 1.f;
-    if (Rg) {
-      const E* rr = Rg + (long)min(i, p.M - 1) * p.ldc + n0;
-#pragma unroll
-      for (int b = 0; b < NT; ++b)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int jl = 32 * b + 8 * g4 + 4 * h;
-          rv[b][g4] = n0 + jl < p.N ? *reinterpret_cast<const uint2*>(rr + jl) : make_uint2(0, 0);
-        }
-      if (p.rscale) sc = p.rscale[((long)g * p.M + min(i, p.M - 1)) / p.rows_per_sample];
-    }
-    f32x16 acc[NT];
-#pragma unroll
-    for (int b = 0; b < NT; ++b) acc[b] = zero16();
-#pragma unroll
-    for (int kc = 0; kc < NK; ++kc) {
-      // prefetch: the next chunk of this strip, else chunk 0 of this wave's next strip
-      if (kc + 1 < NK) load_a(t, kc + 1, abuf[(kc + 1) & 1]);
-      else if (t + nwv < nstrip) load_a(t + nwv, 0, abuf[(kc + 1) & 1]);
-      const char* img = smem + kc * IMG;
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const frag8<E> fa = frag_bits<E>(abuf[kc & 1][s4]);
-#pragma unroll
-        for (int b = 0; b < NT; ++b) {
-          frag8<E> fb;
-          if constexpr (TB) fb = frag_r<E, BN>(img, 32 * b, s4, lane);
-          else fb = frag_k<E>(img, 32 * b, s4, lane);
-          acc[b] = MF<E>::mma(fb, fa, acc[b]);
-        }
-      }
-    }
-    if constexpr (NK & 1) {
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) abuf[0][s4] = abuf[1][s4];
-    }
-    if (!row_ok) continue;
-    E* crow = Cg + (long)i * p.ldc + n0;
-#pragma unroll
-    for (int b = 0; b < NT; ++b)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int jl = 32 * b + 8 * g4 + 4 * h;
-        if (n0 + jl >= p.N) continue;
-        float v[4] = {acc[b][4 * g4] + bias_s[jl], acc[b][4 * g4 + 1] + bias_s[jl + 1],
-                      acc[b][4 * g4 + 2] + bias_s[jl + 2], acc[b][4 * g4 + 3] + bias_s[jl + 3]};
-        if (p.act) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = act_fwd(v[e], p.act);
-        }
-        if (Rg) {
-          const cmx_f2 r0 = unpack2<E>(rv[b][g4].x), r1 = unpack2<E>(rv[b][g4].y);
-          v[0] = r0.x + sc * v[0]; v[1] = r0.y + sc * v[1]; v[2] = r1.x + sc * v[2]; v[3] = r1.y + sc * v[3];
-        }
-        *reinterpret_cast<uint2*>(crow + jl) = make_uint2(pack2<E>(v[0], v[1]), pack2<E>(v[2], v[3]));
-      }
-  }
+  gemm_bf16_body<BM, BN, TA, TB, NS, KW, E>(p, xcd_tile(blockIdx.x, p.tiles_m * p.tiles_n * p.G * p.nsplit), smem);
 }
 
 // ============================================================================ grouped launch
@@ -904,10 +557,10 @@ __device__ __forceinline__ int xcd_chunk_tile(int b, int nt, int ch) {
   return ((j / ch) * 8 + x) * ch + j % ch;
 }
 
-// NS = DMA ring depth: 2 (two blocks per CU) or 3 / 4 (one block per CU, 96 / 128 KB of LDS:
-// more k-tiles in flight per CU; CMX_GROUPED_NS)
+// (two-stage DMA ring, two blocks per CU: deeper rings at one block per CU measured 2-17 %
+// slower on the B2 step, round 3)
 template <typename E, int NS = 2>
-__global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_grouped_kernel(const GroupRec* __restrict__ recs, int nrec,
+__global__ __launch_bounds__(256, 2) void gemm_grouped_kernel(const GroupRec* __restrict__ recs, int nrec,
                                                                              int chunk) {
   __shared__ __attribute__((aligned(1024))) char smem[gemm_smem_bytes<128, 128, NS>()];
   const int lin = chunk > 0 ? xcd_chunk_tile(blockIdx.x, gridDim.x, chunk) : xcd_tile(blockIdx.x, gridDim.x);
@@ -1176,13 +829,6 @@ void launch_reduce(const GemmArgs& a, int G, long groups, hipStream_t s) {
 template <int BM, int BN, int NS, int KW = 1, typename E = bf16>
 void launch_bf16(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream_t s) {
   dim3 grid(a.tiles_m * a.tiles_n * G * nsplit);
-  if constexpr (BM == 64) {
-    if (a.lnY) {                                 // cmx_gemm_ln: forward / dgrad layouts only
-      if (tB) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, false, true, NS, KW, E, true>), grid, dim3(256 * KW), 0, s, a);
-      else hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, false, false, NS, KW, E, true>), grid, dim3(256 * KW), 0, s, a);
-      return;
-    }
-  }
 #define CMX_GEMM_LAUNCH(TA, TB) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, TA, TB, NS, KW, E>), grid, dim3(256 * KW), 0, s, a)
   if (!tA && !tB) CMX_GEMM_LAUNCH(false, false);
   else if (!tA && tB) CMX_GEMM_LAUNCH(false, true);
@@ -1194,9 +840,6 @@ void launch_bf16(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream
 template <int BM, int BN, typename E = bf16>
 void launch_bf16_ns(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream_t s) {
   const long blocks = (long)a.tiles_m * a.tiles_n * G * nsplit;
-  // a 64 x 64 stage is only 16 KB, so a 4-deep ring (64 KB) would still leave two blocks per
-  // CU; measured: no gain (2.82 vs 2.95 ms of GEMM per step), so off by default (CMX_GEMM_NS64=4)
-  static int& ns64 = cmx_knob("GEMM_NS64", 2);
   // k-group blocks for 64 x 64 tiles without split-K or bias column (CMX_GEMM_KW = the largest
   // group count allowed, default 2; 1 = off).  Measured (scripts/gemm_sweep.py, G2 M600 N512):
   // K 2048 20.1 -> 11.9 us, K 512 7.5 -> 5.8 us at KW = 2; grids above 512 blocks and one-slot
@@ -1217,20 +860,7 @@ void launch_bf16_ns(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStr
       return;
     }
   }
-  // deep rings for short-k 64 x 64 problems (CMX_GEMM_DEEP = the deepest ring, 0 = off): ring
-  // depth min(k-tiles + 1, DEEP), so every k-tile of a block is in flight at once -- a block of
-  // 2-5 k-tiles behind a 2-deep ring waits one DMA round trip per k-tile
-  static int& deep = cmx_knob("GEMM_DEEP", 0);
-  if constexpr (BM == 64 && BN == 64) {
-    if (deep >= 3 && blocks > 256) {
-      const int nk64 = (a.K + FBK - 1) / FBK;
-      const int want = nk64 + 1 < deep ? nk64 + 1 : deep;
-      if (want >= 6) { launch_bf16<64, 64, 6, 1, E>(a, G, nsplit, tA, tB, s); return; }
-      if (want >= 4) { launch_bf16<64, 64, 4, 1, E>(a, G, nsplit, tA, tB, s); return; }
-      if (want == 3) { launch_bf16<64, 64, 3, 1, E>(a, G, nsplit, tA, tB, s); return; }
-    }
-  }
-  if (blocks <= 256 || (BM == 64 && BN == 64 && ns64 == 4)) launch_bf16<BM, BN, 4, 1, E>(a, G, nsplit, tA, tB, s);
+  if (blocks <= 256) launch_bf16<BM, BN, 4, 1, E>(a, G, nsplit, tA, tB, s);
   else launch_bf16<BM, BN, 2, 1, E>(a, G, nsplit, tA, tB, s);
 }
 
@@ -1257,93 +887,6 @@ inline int cu_count() {
     return c > 0 ? c : 256;
   }();
   return n;
-}
-
-// Stream-kernel policy (CMX_GEMM_STREAM = the least number of 64 x 64 tiles that takes the
-// persistent kernel, 0 = off; CMX_GEMM_STREAM_NS / _NSR = ring depth without / with a residual
-// image; CMX_GEMM_STREAM_BPC = resident blocks per CU the grid is sized for)
-template <typename E>
-bool launch_stream_t(const GemmArgs& a, int tA, int tB, hipStream_t s) {
-  static int& ns = cmx_knob("GEMM_STREAM_NS", 3);
-  static int& nsr = cmx_knob("GEMM_STREAM_NSR", 2);
-  static int& bpc = cmx_knob("GEMM_STREAM_BPC", 2);
-  const long total = (long)a.tiles_m * a.tiles_n * a.G;
-  long grid = (long)cu_count() * (bpc > 0 ? bpc : 1);
-  if (grid >= total) grid = total;
-  else grid = grid / 8 * 8;
-  const bool hr = a.R != nullptr;
-  const int depth = hr ? nsr : ns;
-#define CMX_STREAM_LAUNCH(NS, HR)                                                                                 \
-  do {                                                                                                            \
-    if (!tA && !tB) hipLaunchKernelGGL((gemm_stream_kernel<false, false, NS, HR, E>), dim3(grid), dim3(256), 0, s, a); \
-    else if (!tA && tB) hipLaunchKernelGGL((gemm_stream_kernel<false, true, NS, HR, E>), dim3(grid), dim3(256), 0, s, a); \
-    else return false;                                                                                            \
-  } while (0)
-  if (hr) {
-    if (depth >= 3) CMX_STREAM_LAUNCH(3, true);
-    else CMX_STREAM_LAUNCH(2, true);
-  } else {
-    if (depth >= 4) CMX_STREAM_LAUNCH(4, false);
-    else if (depth == 3) CMX_STREAM_LAUNCH(3, false);
-    else CMX_STREAM_LAUNCH(2, false);
-  }
-#undef CMX_STREAM_LAUNCH
-  return true;
-}
-
-// the problems the stream kernel takes: 16-bit, one split, plain row-major 16-bit store with
-// the bias / activation / DropPath-residual epilogue, 64 x 64 tiles, enough of them
-inline bool stream_ok(const GemmArgs& a, int bm, int bn, int splitk, int tA, int dtype) {
-  static int& min_tiles = cmx_knob("GEMM_STREAM", 0);
-  if (min_tiles <= 0 || bm != 64 || bn != 64 || splitk != 1 || tA || a.out_mode != 0 || a.ones_col || a.nup ||
-      a.scatter || a.conv)
-    return false;
-  if ((long)a.tiles_m * a.tiles_n * a.G < min_tiles) return false;
-  if (a.N % 4 || a.ldc % 4 || a.sC % 4 || a.sCh % 4 || ((uintptr_t)a.C & 7)) return false;
-  if ((long)a.M * a.ldc >= (1L << 30) - 64) return false;                      // 31-bit byte offsets
-  if (a.bias && (long)a.G * a.N > ST_BIAS_MAX) return false;
-  if (a.rscale && ((long)a.G * a.M + a.rows_per_sample - 1) / a.rows_per_sample > ST_SCALE_MAX) return false;
-  if (a.R && (a.N % 8 || a.ldc % 8 || a.sC % 8 || ((uintptr_t)a.R & 15))) return false;
-  return dtype == 1 || dtype == 2;
-}
-
-// Register-streamed GEMM policy (CMX_GEMM_REG = the least M that takes it, 0 = off): the
-// forward / dgrad layouts (A k-contiguous), one split, plain 16-bit store with bias /
-// activation / DropPath residual, K <= 512 with the (BN x K) weight slice in LDS
-template <typename E>
-bool launch_reg_t(const GemmArgs& a, int tB, hipStream_t s) {
-  static int& bpc = cmx_knob("GEMM_REG_BPC", 4);
-  const int nk = (a.K + 63) / 64;
-  const int bn = 64;                             // 32 x 64 per wave: ~100 VGPRs, 4 waves / SIMD
-  const int nsl = (a.N + bn - 1) / bn;
-  const long strips = (a.M + 31) / 32;
-  long gx = ((long)cu_count() * (bpc > 0 ? bpc : 1) + (long)nsl * a.G - 1) / ((long)nsl * a.G);
-  gx = (gx + 7) / 8 * 8;                       // slices / groups of one row walker share an XCD
-  if (gx > (strips + 3) / 4) gx = (strips + 3) / 4;
-  const dim3 grid((unsigned)gx, nsl, a.G);
-#define CMX_REG_LAUNCH(TBV, BNV, NKV) \
-  hipLaunchKernelGGL((gemm_reg_kernel<TBV, BNV, NKV, E>), grid, dim3(256), 0, s, a)
-#define CMX_REG_NK(TBV, BNV)                    \
-  do {                                          \
-    if (nk == 1) CMX_REG_LAUNCH(TBV, BNV, 1);   \
-    else if (nk == 2) CMX_REG_LAUNCH(TBV, BNV, 2); \
-    else CMX_REG_LAUNCH(TBV, BNV, 4);           \
-  } while (0)
-  if (nk > 4) return false;
-  if (tB) CMX_REG_NK(true, 64); else CMX_REG_NK(false, 64);
-#undef CMX_REG_NK
-#undef CMX_REG_LAUNCH
-  return true;
-}
-
-inline bool reg_ok(const GemmArgs& a, int splitk, int tA, int dtype) {
-  static int& min_m = cmx_knob("GEMM_REG", 0);
-  if (min_m <= 0 || a.M < min_m || tA || splitk != 1 || a.out_mode != 0 || a.ones_col || a.nup || a.scatter ||
-      a.conv || a.lnY || a.gh != 1)
-    return false;
-  if (a.K > 256 || a.K % 8 || a.N < 32 || a.N % 4 || a.ldc % 4 || a.sC % 4 || ((uintptr_t)a.C & 7)) return false;
-  if (a.R && ((uintptr_t)a.R & 7)) return false;
-  return dtype == 1 || dtype == 2;
 }
 
 template <typename T, int BM, int BN, bool EXT>
@@ -1455,10 +998,6 @@ inline int auto_split(int G, int M, int N, int K, int ones_col) {
 #define CMX_GEMM_GENERIC_EXTERN(T, BM, BN) \
   extern template void gemmk::launch_generic<T, BM, BN>(const GemmArgs&, int, int, int, int, hipStream_t);
 #define CMX_GEMM_FAST_INST(E)                                                                         \
-  template void gemmk::launch_fast_t<E>(const GemmArgs&, int, int, int, int, int, int, hipStream_t); \
-  template bool gemmk::launch_stream_t<E>(const GemmArgs&, int, int, hipStream_t);                    \
-  template bool gemmk::launch_reg_t<E>(const GemmArgs&, int, hipStream_t);
+  template void gemmk::launch_fast_t<E>(const GemmArgs&, int, int, int, int, int, int, hipStream_t);
 #define CMX_GEMM_FAST_EXTERN(E)                                                                              \
-  extern template void gemmk::launch_fast_t<E>(const GemmArgs&, int, int, int, int, int, int, hipStream_t); \
-  extern template bool gemmk::launch_stream_t<E>(const GemmArgs&, int, int, hipStream_t);                    \
-  extern template bool gemmk::launch_reg_t<E>(const GemmArgs&, int, hipStream_t);
+  extern template void gemmk::launch_fast_t<E>(const GemmArgs&, int, int, int, int, int, int, hipStream_t);

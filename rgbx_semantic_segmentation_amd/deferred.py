@@ -24,12 +24,6 @@ table must outlive the graph (every replay re-reads it): it is kept for the proc
 Outside a capture it is released once an event recorded after the copy has completed.
 
 ``CMX_DEFER=0`` runs every weight gradient immediately instead (A/B switch for measurements).
-
-``CMX_WGRAD_SIDE=1``: the flushes at stage boundaries (``flush(side=True)``, from the encoder's
-stage-input hooks) issue their grouped launches on a side stream that forks from the backward
-at that point, so the weight gradients of the decoder / stages 4..2 run beside the input-gradient
-chain of the stages below; the end-of-backward flush joins it (``join_side``) before anything
-after the backward -- the optimizer, the gradient all-reduce -- can read a gradient.
 """
 from __future__ import annotations
 
@@ -43,30 +37,6 @@ from . import _lib
 from ._lib import LIB, call, query, ptr, stream
 
 ENABLED = os.environ.get("CMX_DEFER", "1") == "1"
-# CMX_GROUPED_SORT=1: the grouped launch's problems in decreasing per-block work (k-tiles per
-# block x tile area), so the longest blocks are dispatched first and the short ones fill the
-# tail (longest-processing-time order; a problem's tiles stay contiguous for the XCD map)
-GROUPED_SORT = os.environ.get("CMX_GROUPED_SORT", "0") == "1"
-WGRAD_SIDE = os.environ.get("CMX_WGRAD_SIDE", "0") == "1"
-_side: dict = {}                 # device index -> side stream of the stage-boundary flushes
-_side_used: set = set()          # device indices with side work not yet joined
-
-
-def side_stream(device) -> torch.cuda.Stream:
-    idx = torch.device(device).index
-    if idx not in _side:
-        _side[idx] = torch.cuda.Stream(device=device)
-    return _side[idx]
-
-
-def join_side() -> None:
-    """Order the current stream after every side-stream flush issued so far."""
-    if not _side_used:
-        return
-    cur = torch.cuda.current_stream()
-    for idx in list(_side_used):
-        cur.wait_stream(_side[idx])
-    _side_used.clear()
 
 _GREC = query("cmx_gemm_group_record_size")
 _RREC = query("cmx_reduce_record_size")
@@ -262,26 +232,12 @@ def _upload(table: torch.Tensor, nbytes: int, device) -> torch.Tensor:
     return dev
 
 
-def flush(side: bool = False) -> None:
-    """Issue the queued weight-gradient GEMMs (one launch) and reductions (one launch).
-    side=True (a stage-boundary flush): on the side stream, forked from the current stream
-    here; otherwise on the current stream, after joining any earlier side-stream flush."""
-    q = _q
-    pending_work = bool(q.gemms or q.convs or q.reds)
-    if side:
-        if pending_work:
-            cur = torch.cuda.current_stream()
-            ss = side_stream(cur.device)
-            ss.wait_stream(cur)
-            q.streams[cur.cuda_stream] = cur      # _issue records the operands' use on ss
-            _side_used.add(cur.device.index)
-            with torch.cuda.stream(ss):
-                _issue()
-        return
-    q.armed = False
-    if pending_work:
+def flush() -> None:
+    """Issue the queued weight-gradient GEMMs (one launch) and reductions (one launch) on the
+    current stream."""
+    _q.armed = False
+    if _q.gemms or _q.convs or _q.reds:
         _issue()
-    join_side()
 
 
 def _issue() -> None:
@@ -307,13 +263,6 @@ def _issue() -> None:
         arena = torch.empty(max(1, sum((z + 255) // 256 * 64 for z in sizes)), dtype=torch.float32, device=device)
         nrec = len(dims)
         order = list(range(nrec))
-        if GROUPED_SORT:
-            def _cost(i):
-                G, M, N, K, hb = dims[i]
-                nb = N - 1 if hb else N
-                kt = -(-(-(-K // 64)) // splits[i])
-                return kt * (64 if M <= 64 else 128) * (64 if nb <= 64 else 128)
-            order.sort(key=lambda i: -_cost(i))
         table = _table(nrec * _GREC)
         base = table.data_ptr()
         blk, off = 0, 0

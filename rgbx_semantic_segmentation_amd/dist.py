@@ -48,8 +48,8 @@ class BucketedGradSync:
         # CMX_DP_OVERLAP=0: one blocking all-reduce per segment at optimizer time (no overlap)
         self.overlap = (os.environ.get("CMX_DP_OVERLAP", "1") == "1") if overlap is None else overlap
         # gradient payload on the wire: "fp32" (SUM all-reduce of the fp32 gradients, DDP's
-        # semantics) or "bf16" (reduce-scatter + all-gather of bf16 gradients: half the bytes
-        # over xGMI; the sum is rounded to bf16 along the ring)
+        # semantics) or "bf16" (fp32 reduce-scatter + bf16 all-gather: 6 instead of 8 bytes per
+        # element over xGMI; one rounding of the fp32 sum to bf16)
         self.payload = (payload or os.environ.get("CMX_DP_PAYLOAD", "fp32")).lower()
         if self.payload not in ("fp32", "bf16"):
             raise ValueError(f"gradient payload {self.payload!r}: fp32 or bf16")
@@ -73,11 +73,7 @@ class BucketedGradSync:
         from . import deferred
         if sid in self.launched or sid not in self.ranges:
             return
-        # a stage-boundary flush may go to the weight-gradient side stream (CMX_WGRAD_SIDE);
-        # the all-reduce then waits for it as well as for the backward so far
-        last = sid == max(self.ranges)
-        side = deferred.WGRAD_SIDE and not last
-        deferred.flush(side=side)
+        deferred.flush()
         a, b = self.ranges[sid]
         main = torch.cuda.current_stream() if self.store.grad.is_cuda else None
         if main is None:                         # CPU tensors (gloo tests): blocking, in order
@@ -86,8 +82,6 @@ class BucketedGradSync:
             if self.side is None:
                 self.side = torch.cuda.Stream(device=main.device)
             self.side.wait_stream(main)
-            if side:
-                self.side.wait_stream(deferred.side_stream(main.device))
             with torch.cuda.stream(self.side):
                 self._reduce(self.store.grad[a:b])
             self.works.append(self.side)
@@ -107,30 +101,34 @@ class BucketedGradSync:
                 self._reduce_bf16(part)
 
     def _reduce_bf16(self, t: torch.Tensor) -> None:
-        """SUM over ranks of fp32 ``t`` in place with a bf16 payload: a reduce-scatter of the
-        bf16 gradients (each rank ends with the sum of its shard) and an all-gather of the summed
-        shards (2 + 2 bytes per element on the wire vs 4 + 4 for an fp32 ring all-reduce).  The
-        sum is formed by the collective's bf16 reduction (RCCL: P - 1 roundings to bf16 along the
-        ring).  Both collectives are safe inside a HIP-graph capture; an all-to-all + local fp32
-        sum was not (RCCL all_to_all_single inside a capture crashed at capture end or hung at
-        exit even at world size 1: scripts/rccl_capture_probe.py, gpurun_out r03_b).  On the GPU
-        the casts are HIP kernels (cmx_cast_f32_bf16 / cmx_cast_bf16_f32); the CPU branch is the
-        gloo rehearsal of the same protocol."""
+        """SUM over ranks of fp32 ``t`` in place with a bf16 return leg: a reduce-scatter of the
+        fp32 gradients (each rank ends with the fp32 sum of its shard, accumulated in fp32 along
+        the ring), one rounding of that sum to bf16, and an all-gather of the bf16 shards (4 + 2
+        bytes per element on the wire vs 4 + 4 for an fp32 ring all-reduce; every rank, the
+        shard's owner too, takes the gathered bf16 value, so the ranks stay bit-identical).
+        Both collectives are safe inside a HIP-graph capture; an all-to-all was not (RCCL
+        all_to_all_single inside a capture crashed at capture end or hung at exit even at world
+        size 1: scripts/rccl_capture_probe.py).  On the GPU the casts are HIP
+        kernels (cmx_cast_f32_bf16 / cmx_cast_bf16_f32); the CPU branch is the gloo rehearsal."""
         P = self.world
         n = t.numel()
         shard = -(-n // (8 * P)) * 8                 # per-rank shard, a multiple of 8 elements
-        send = torch.zeros(P * shard, dtype=torch.bfloat16, device=t.device)
-        mine = torch.empty(shard, dtype=torch.bfloat16, device=t.device)
-        out = torch.empty_like(send)
-        aligned = t.is_cuda and n % 8 == 0
-        if aligned:
-            from . import _lib
-            _lib.call("cmx_cast_f32_bf16", _lib.ptr(t), _lib.ptr(send), n, _lib.stream())
+        if n == P * shard:
+            send = t
         else:
+            send = torch.zeros(P * shard, dtype=torch.float32, device=t.device)
             send[:n].copy_(t)
+        mine = torch.empty(shard, dtype=torch.float32, device=t.device)
         dist.reduce_scatter_tensor(mine, send, op=dist.ReduceOp.SUM, group=self.group)
-        dist.all_gather_into_tensor(out, mine, group=self.group)
-        if aligned:
+        mine16 = torch.empty(shard, dtype=torch.bfloat16, device=t.device)
+        out = torch.empty(P * shard, dtype=torch.bfloat16, device=t.device)
+        if t.is_cuda:
+            from . import _lib
+            _lib.call("cmx_cast_f32_bf16", _lib.ptr(mine), _lib.ptr(mine16), shard, _lib.stream())
+        else:
+            mine16.copy_(mine)
+        dist.all_gather_into_tensor(out, mine16, group=self.group)
+        if t.is_cuda and n % 8 == 0:
             _lib.call("cmx_cast_bf16_f32", _lib.ptr(out), _lib.ptr(t), n, _lib.stream())
         else:
             t.copy_(out[:n])
@@ -161,6 +159,40 @@ class BucketedGradSync:
             torch.cuda.current_stream().wait_stream(self.side)
         self.works, self.launched = [], set()
         return 1.0 / self.world
+
+
+def flatten_bn_buffers(model, device=None):
+    """Every BatchNorm's running_mean / running_var as views of ONE contiguous fp32 tensor
+    (returned; None without BatchNorms), so DDP's per-forward buffer broadcast is one
+    collective.  state_dict keys and shapes are unchanged; in-place updates of the running
+    statistics (the BN kernels, load_state_dict) land in the flat tensor."""
+    bns = [m for m in model.modules() if isinstance(m, torch.nn.modules.batchnorm._BatchNorm)
+           and m.running_mean is not None]
+    if not bns:
+        return None
+    parts = []
+    for m in bns:
+        parts += [m.running_mean, m.running_var]
+    dev = torch.device(device) if device is not None else parts[0].device
+    flat = torch.cat([p.detach().to(device=dev, dtype=torch.float32).reshape(-1) for p in parts])
+    off = 0
+    for m in bns:
+        for k in ("running_mean", "running_var"):
+            n = m._buffers[k].numel()
+            m._buffers[k] = flat[off:off + n].view(m._buffers[k].shape)
+            off += n
+    return flat
+
+
+@torch.no_grad()
+def broadcast_buffers(flat, group=None, src: int = 0):
+    """DDP's per-forward buffer sync (DistributedDataParallel(broadcast_buffers=True), the
+    default the reference uses, train.py:145-146): every rank's BatchNorm running statistics
+    are replaced by rank ``src``'s at the start of each training forward -- one broadcast of the
+    flat buffer (flatten_bn_buffers).  num_batches_tracked is not sent: every rank increments
+    it in lockstep, so it is equal already."""
+    if flat is not None:
+        dist.broadcast(flat, src=src, group=group)
 
 
 @torch.no_grad()

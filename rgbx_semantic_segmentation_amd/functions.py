@@ -46,42 +46,6 @@ def _fwd_gemm(x, W, b, y, act="none", res=None, rscale=None, rps=1, x2=None):
     return y
 
 
-# CMX_LN_FUSE: the norm that follows a residual GEMM (proj -> norm2, fc2 -> next norm1 / the
-# stage norm) computed in that GEMM's epilogue (cmx_gemm_ln) on the streams of these widths:
-# "1" = 64 and 128 channels, "64" = 64 only, "0" (default) = every norm its own launch
-_LN_FUSE_ENV = os.environ.get("CMX_LN_FUSE", "0")
-LN_FUSE = {"0": (), "1": (64, 128), "64": (64,), "128": (128,)}.get(_LN_FUSE_ENV, ())
-
-
-class LNStash:
-    """Forward side channel from a residual GEMM to the LayerNorm that consumes its output:
-    the GEMM's epilogue computed (y, mean, rstd) = LN(x) for ``gamma`` / ``beta`` / ``eps``;
-    the norm (layernorm_res(..., pre=stash)) takes them instead of launching, after checking
-    they were made from the same tensor."""
-    __slots__ = ("gamma", "beta", "eps", "src", "y", "mean", "rstd")
-
-    def __init__(self, gamma, beta, eps):
-        self.gamma, self.beta, self.eps = gamma, beta, eps
-        self.src = self.y = self.mean = self.rstd = None
-
-    def take(self, x, gamma, beta, eps):
-        if (self.src is None or self.src.data_ptr() != x.data_ptr() or self.src.shape != x.shape
-                or gamma.data_ptr() != self.gamma.data_ptr() or beta.data_ptr() != self.beta.data_ptr()
-                or eps != self.eps):
-            return None
-        out = (self.y, self.mean, self.rstd)
-        self.src = self.y = self.mean = self.rstd = None
-        return out
-
-
-def ln_stash(store, mod, G):
-    """An LNStash for norm ``mod`` when the LN fusion is on for its width, else None."""
-    if mod.weight.shape[-1] not in LN_FUSE:
-        return None
-    return LNStash(store.w(mod.weight, compute=False).view(G, -1), store.w(mod.bias, compute=False).view(G, -1),
-                   mod.eps)
-
-
 class GLinear(Function):
     """y[g] = act(x1[g] @ W[g][:, :k1]^T (+ x2[g] @ W[g][:, k1:]^T) + b[g]), optionally
     y = res + rscale[sample] * (...)  (nn.Linear / 1x1 Conv2d; the two-input form replaces
@@ -90,21 +54,12 @@ class GLinear(Function):
     x + drop_path(proj/fc2(...)), dual_segformer.py:168-169)."""
 
     @staticmethod
-    def forward(ctx, W, Wg, b, bg, anchor, act, res, rscale, rps, x1, x2, tap=None, ln=None):
+    def forward(ctx, W, Wg, b, bg, anchor, act, res, rscale, rps, x1, x2, tap=None):
         G, N, Ktot = W.shape
         M = x1.shape[1]
         assert x1.shape[-1] + (x2.shape[-1] if x2 is not None else 0) == Ktot, (x1.shape, W.shape)
         y = torch.empty(G, M, N, dtype=x1.dtype, device=x1.device)
-        if ln is not None and K.gemm_ln_ok(x1, y):
-            # the consumer norm's forward in this GEMM's epilogue (LNStash)
-            ly = torch.empty_like(y)
-            mean = torch.empty(G * M, dtype=torch.float32, device=y.device)
-            rstd = torch.empty(G * M, dtype=torch.float32, device=y.device)
-            K.gemm_ln(x1, W, y, ly, ln.gamma, ln.beta, mean, rstd, ln.eps, bias=b, residual=res, rscale=rscale,
-                      rows_per_sample=rps, act=act, A2=x2)
-            ln.src, ln.y, ln.mean, ln.rstd = y, ly, mean, rstd
-        else:
-            _fwd_gemm(x1, W, b, y, act=act, res=res, rscale=rscale, rps=rps, x2=x2)
+        _fwd_gemm(x1, W, b, y, act=act, res=res, rscale=rscale, rps=rps, x2=x2)
         ctx.save_for_backward(W, x1, x2, y if act == "relu" else None)
         ctx.meta = (Wg, bg, act, res is not None, rscale, rps, tap)
         return y
@@ -134,13 +89,12 @@ class GLinear(Function):
         _wgrad_into(dz, x1, Wg[:, :, :k1], bg)
         if x2 is not None:
             _wgrad_into(dz, x2, Wg[:, :, k1:])
-        return (None, None, None, None, None, None, dres, None, None, dx1, dx2, None, None)
+        return (None, None, None, None, None, None, dres, None, None, dx1, dx2, None)
 
 
-def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1, tap=None, ln=None):
+def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1, tap=None):
     """Grouped linear using parameter ``wp`` (and bias ``bp``) of the store; x2 = second
-    input segment (cat-free), res/rscale/rps = fused DropPath residual (rps = rows per sample);
-    ln = LNStash of the norm that consumes the output (its forward then runs in the epilogue)."""
+    input segment (cat-free), res/rscale/rps = fused DropPath residual (rps = rows per sample)."""
     W = store.w(wp)
     Wg = store.g(wp)
     G = W.shape[0]
@@ -150,7 +104,7 @@ def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1
     if bp is not None:
         b = store.w(bp, compute=False).view(G, -1)
         bg = store.g(bp).view(G, -1)
-    return GLinear.apply(W, Wg, b, bg, wp, act, res, rscale, rps, x1, x2, tap, ln)
+    return GLinear.apply(W, Wg, b, bg, wp, act, res, rscale, rps, x1, x2, tap)
 
 
 # ---------------------------------------------------------------------------- LayerNorm
@@ -179,12 +133,8 @@ class LayerNormResF(Function):
     scale[sample] * dx for the producer of x (GradTap)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, gg, bg, eps, G, scale, rps, tap, anchor, pre=None):
-        got = pre.take(x, gamma, beta, eps) if pre is not None else None
-        if got is not None:
-            y, mean, rstd = got                      # computed by the producing GEMM's epilogue
-        else:
-            y, mean, rstd = K.layernorm_fwd(x, gamma, beta, eps, G=G)
+    def forward(ctx, x, gamma, beta, gg, bg, eps, G, scale, rps, tap, anchor):
+        y, mean, rstd = K.layernorm_fwd(x, gamma, beta, eps, G=G)
         ctx.save_for_backward(x, gamma, mean, rstd)
         ctx.meta = (gg, bg, G, scale, rps, tap)
         ctx.set_materialize_grads(False)     # unused outputs arrive as None, not zero-filled tensors
@@ -215,17 +165,16 @@ class LayerNormResF(Function):
             deferred.reduce(ws, gg, bg, G, nb, nb * 2 * C, 2 * C, 1, 2 * C, C, gg.stride(0), 0, bg.stride(0), 0)
         if dxs is not None:
             tap.put(dxs)
-        return dx, None, None, None, None, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None, None, None
 
 
-def layernorm_res(store, mod, x, G, scale=None, rps=1, tap=None, pre=None):
-    """(LN(x), LN(x) for a second consumer, x) with the fused backward (LayerNormResF).
-    pre: the LNStash the producing GEMM filled (forward already computed), or None."""
+def layernorm_res(store, mod, x, G, scale=None, rps=1, tap=None):
+    """(LN(x), LN(x) for a second consumer, x) with the fused backward (LayerNormResF)."""
     gamma = store.w(mod.weight, compute=False).view(G, -1)
     beta = store.w(mod.bias, compute=False).view(G, -1)
     gg = store.g(mod.weight).view(G, -1)
     bg = store.g(mod.bias).view(G, -1)
-    return LayerNormResF.apply(x, gamma, beta, gg, bg, mod.eps, G, scale, rps, tap, mod.weight, pre)
+    return LayerNormResF.apply(x, gamma, beta, gg, bg, mod.eps, G, scale, rps, tap, mod.weight)
 
 
 class LayerNormF(Function):

@@ -161,37 +161,6 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, bias: torch.Tensor |
     return C
 
 
-def gemm_ln_ok(A: torch.Tensor, C: torch.Tensor) -> bool:
-    """cmx_gemm_ln's shape rule: 16-bit, whole 64- or 128-column rows, 16-B aligned row-major C."""
-    N = C.shape[-1]
-    return (A.dtype in (torch.bfloat16, torch.float16) and N in (64, 128) and C.is_contiguous()
-            and C.data_ptr() % 16 == 0 and A.is_cuda)
-
-
-def gemm_ln(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, ln_y: torch.Tensor, gamma: torch.Tensor,
-            beta: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, eps: float, bias: torch.Tensor | None = None,
-            residual: torch.Tensor | None = None, rscale: torch.Tensor | None = None, rows_per_sample: int = 1,
-            act: str = "none", A2: torch.Tensor | None = None) -> torch.Tensor:
-    """gemm(...) whose epilogue also writes ln_y = LayerNorm(C) (gamma / beta (G, N) fp32) and the
-    per-row mean / rstd (G * M fp32) (cmx_gemm_ln)."""
-    G, M, K1 = A.shape
-    Kd = K1 + (A2.shape[2] if A2 is not None else 0)
-    N = B.shape[1]
-    assert B.shape == (G, N, Kd) and C.shape == (G, M, N) and ln_y.shape == C.shape and ln_y.stride() == C.stride()
-    assert gamma.shape == (G, N) and beta.shape == (G, N) and gamma.is_contiguous() and beta.is_contiguous()
-    assert mean.numel() == G * M and rstd.numel() == G * M
-    tA, lda, sA = _operand(A, "A")
-    lda2, sA2 = (_operand(A2, "A2")[1:] if A2 is not None else (0, 0))
-    tB, ldb, sB = _operand(B, "B")
-    sbias = (bias.stride(0) if bias.dim() == 2 else 0) if bias is not None else 0
-    if residual is not None:
-        assert residual.shape == C.shape and residual.stride() == C.stride() and residual.dtype == C.dtype
-    call("cmx_gemm_ln", ptr(A), ptr(A2), ptr(B), ptr(C), ptr(bias), ptr(residual), ptr(rscale), G, M, N, Kd, K1,
-         lda, lda2, ldb, C.stride(1), sA, sA2, sB, C.stride(0), sbias, int(rows_per_sample), tA, tB, ACT[act],
-         ptr(ln_y), ptr(gamma), ptr(beta), ptr(mean), ptr(rstd), float(eps), dtype_code(A), stream())
-    return C
-
-
 def gemm_h2(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, out_mode: int = 0, splitk: int = 0) -> torch.Tensor:
     """C[o, h] = A[o, h] @ B[o, h]^T over a two-level batch of logical 4-D views A (Go, gh, M, K),
     B (Go, gh, N, K), C (Go, gh, M, N) (cmx_gemm_h2): e.g. per-head products whose heads are

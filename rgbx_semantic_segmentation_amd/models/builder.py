@@ -105,6 +105,10 @@ class EncoderDecoder(nn.Module):
                               "bf16": torch.bfloat16, "float16": torch.float16, "fp16": torch.float16}[str(dt)]
         self.sync_bn = norm_layer is nn.SyncBatchNorm
         self.process_group = None
+        # DDP's default (train.py:145-146): the BatchNorm running statistics of rank 0 are
+        # broadcast at the start of every training forward when a process group is set
+        self.broadcast_buffers = True
+        self._bnbuf = None
         self.store: Optional[ParamStore] = None
         self.forced_masks = None
         self.init_weights(cfg, pretrained=_get(cfg, "pretrained_model", None))
@@ -153,6 +157,9 @@ class EncoderDecoder(nn.Module):
                 m._buffers["num_batches_tracked"] = cnt[i]
                 m._nbt_shared = True
             self._nbt = cnt
+        if self._bnbuf is None:      # running statistics as views of one tensor: one broadcast per forward
+            from .. import dist as cdist
+            self._bnbuf = cdist.flatten_bn_buffers(self, device)
         return self
 
     def cuda(self, device=None):
@@ -217,6 +224,12 @@ class EncoderDecoder(nn.Module):
         modal_x = modal_x.to(device=dev, dtype=torch.float32).contiguous()
         images = (rgb, modal_x)            # the stage-1 im2col reads both batches (no concat)
         self._nbt_bumped = False
+        pg = self.process_group
+        if self.training and self.broadcast_buffers and pg is not None and self._bnbuf is not None:
+            import torch.distributed as tdist
+            if tdist.get_world_size(pg) > 1:
+                from .. import dist as cdist
+                cdist.broadcast_buffers(self._bnbuf, pg)
         dp, d2 = self._stochastic(B, dev)
         group = self.process_group if (self.sync_bn and self.training) else None
         if self.training and getattr(self, "_nbt", None) is not None and not self._nbt_bumped:

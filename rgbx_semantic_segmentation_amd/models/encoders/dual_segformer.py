@@ -16,7 +16,6 @@ from typing import List, Optional
 import torch
 import torch.nn as nn
 
-from ... import deferred
 from ... import functions as F
 from ... import streams
 from ..net_utils import (FeatureRectifyModule, FeatureFusionModule, ImprovedFeatureRectifyModule,
@@ -48,11 +47,6 @@ def drop_path_probs(depths: List[int], rate: float):
             out.append((p, list(p)))
         cur += d
     return out
-
-
-def _side_flush_hook(grad):
-    deferred.flush(side=True)
-    return None
 
 
 class DWConv(nn.Module):                          # dual_segformer.py:19-33
@@ -133,20 +127,18 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
                 rows.append((1.0 - self.dp[s][0][i], 1.0 - self.dp[s][1][i]))
         return rows
 
-    def run_block(self, store, blk: Block, x, B, H, W, s_attn, s_mlp, prev=(None, None, None), next_norm=None):
+    def run_block(self, store, blk: Block, x, B, H, W, s_attn, s_mlp, prev=(None, None)):
         """One Block (dual_segformer.py:166-180) for both streams.  ``prev`` = (DropPath scale,
-        GradTap, LNStash) of the residual branch that produced ``x`` (the previous block's fc2):
-        norm1's backward writes that branch's scaled gradient, and its forward was computed by
-        that GEMM's epilogue when the stash holds it.  ``next_norm`` = the norm that consumes
-        x_out (the next block's norm1 or the stage norm): fc2's epilogue computes it.  Returns
-        (x_out, (s_mlp, tap, stash)) for the next consumer of x_out."""
+        GradTap) of the residual branch that produced ``x`` (the previous block's fc2): norm1's
+        backward writes that branch's scaled gradient.  Returns (x_out, (s_mlp, tap)) for the
+        next consumer of x_out."""
         G, M, C = x.shape
         N = H * W
         a = blk.attn
         # norm1 also passes x through for the attention residual: its backward sums both gradients
         # (q and the SR path read norm1's output through separate handles: the norm's backward
         # sums their gradients on load)
-        h, h2, xr = F.layernorm_res(store, blk.norm1, x, G, scale=prev[0], rps=N, tap=prev[1], pre=prev[2])
+        h, h2, xr = F.layernorm_res(store, blk.norm1, x, G, scale=prev[0], rps=N, tap=prev[1])
 
         def kv_path():
             if a.sr_ratio > 1:
@@ -155,32 +147,18 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
                 return F.glinear(store, a.kv.weight, a.kv.bias, xs), Hk * Wk
             return F.glinear(store, a.kv.weight, a.kv.bias, h2), N
 
-        side = streams.sr_stream(x.device) if (streams.SR_SIDE and x.is_cuda) else None
-        if side is not None:
-            # the key/value path beside the q Linear (joined before the attention core)
-            main = torch.cuda.current_stream()
-            side.wait_stream(main)
-            h2.record_stream(side)
-            with torch.cuda.stream(side):
-                kv, Nk = kv_path()
-            q = F.glinear(store, a.q.weight, a.q.bias, h)
-            main.wait_stream(side)
-            kv.record_stream(main)
-        else:
-            q = F.glinear(store, a.q.weight, a.q.bias, h)
-            kv, Nk = kv_path()
+        q = F.glinear(store, a.q.weight, a.q.bias, h)
+        kv, Nk = kv_path()
         o = F.SRAttentionF.apply(q, kv, G * B, N, Nk, a.num_heads, C // a.num_heads)
         # x + drop_path(proj(o)): residual and DropPath scale fused into the proj GEMM epilogue
         tap_a = F.GradTap() if s_attn is not None else None
-        st2 = F.ln_stash(store, blk.norm2, G)
-        x = F.glinear(store, a.proj.weight, a.proj.bias, o, res=xr, rscale=s_attn, rps=N, tap=tap_a, ln=st2)
-        h, _, xr = F.layernorm_res(store, blk.norm2, x, G, scale=s_attn, rps=N, tap=tap_a, pre=st2)
+        x = F.glinear(store, a.proj.weight, a.proj.bias, o, res=xr, rscale=s_attn, rps=N, tap=tap_a)
+        h, _, xr = F.layernorm_res(store, blk.norm2, x, G, scale=s_attn, rps=N, tap=tap_a)
         f = F.glinear(store, blk.mlp.fc1.weight, blk.mlp.fc1.bias, h)
         f = F.dwconv(store, blk.mlp.dwconv.dwconv, f, G * B, B, H, W, "gelu")
         tap_m = F.GradTap() if s_mlp is not None else None
-        stn = F.ln_stash(store, next_norm, G) if next_norm is not None else None
-        x = F.glinear(store, blk.mlp.fc2.weight, blk.mlp.fc2.bias, f, res=xr, rscale=s_mlp, rps=N, tap=tap_m, ln=stn)
-        return x, (s_mlp, tap_m, stn)
+        x = F.glinear(store, blk.mlp.fc2.weight, blk.mlp.fc2.bias, f, res=xr, rscale=s_mlp, rps=N, tap=tap_m)
+        return x, (s_mlp, tap_m)
 
     def run(self, store, images, B, H, W, training, dp_scales: Optional[torch.Tensor], bn_group=None):
         """images: (2*B, 3, H, W) fp32 NCHW (RGB batch then X batch), or the pair of (B, 3, H, W)
@@ -205,26 +183,21 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
                 # the gradient of this stage's input exists once the backward has passed the
                 # stage (segment 3 - s): its gradients can be all-reduced while stages < s run
                 x.register_hook(sync.segment_hook(3 - s))
-            elif deferred.WGRAD_SIDE and s > 0 and x.requires_grad and x.is_cuda:
-                # the weight gradients of everything above this stage run on the side stream
-                # beside the input-gradient chain of stages < s (deferred.flush(side=True))
-                x.register_hook(_side_flush_hook)
             x, Ho, Wo = F.conv(store, pe.proj, x, G, G * B, Hc, Wc, Cin, pe.stride, pe.pad, nchw=(s == 0),
                                x2=x2 if s == 0 else None)
             x = F.layernorm(store, pe.norm, x, G)
             Hc, Wc, Cin = Ho, Wo, self.embed_dims[s]
-            prev = (None, None, None)
+            prev = (None, None)
             blocks = getattr(self, f"block{s + 1}")
             snorm = getattr(self, f"norm{s + 1}")
             for i, blk in enumerate(blocks):
                 sa = sm = None
                 if dp_scales is not None:
                     sa, sm = dp_scales[bi, 0], dp_scales[bi, 1]
-                nxt = blocks[i + 1].norm1 if i + 1 < len(blocks) else snorm
-                x, prev = self.run_block(store, blk, x, B, Hc, Wc, sa, sm, prev, next_norm=nxt)
+                x, prev = self.run_block(store, blk, x, B, Hc, Wc, sa, sm, prev)
                 bi += 1
             # stage norm: its backward also writes the last block's DropPath-scaled gradient
-            x, _, _ = F.layernorm_res(store, snorm, x, G, scale=prev[0], rps=Hc * Wc, tap=prev[1], pre=prev[2])
+            x, _, _ = F.layernorm_res(store, snorm, x, G, scale=prev[0], rps=Hc * Wc, tap=prev[1])
             C = self.embed_dims[s]
             fr = self.FRMs[s]
             if isinstance(fr, ImprovedFeatureRectifyModule):

@@ -5,9 +5,10 @@ its own stream beside stage s + 1 of the encoder (its backward then runs there t
 the encoder's backward); inside the step's HIP graph the fork / join are graph edges.
 ``CMX_FFM_STREAM=0`` keeps everything on the current stream (A/B switch for measurements).
 
-(A second side stream for the weight-gradient GEMMs was measured and removed: the ~230
-fork / join edges per step cost more than the overlap won, and the weight gradients now
-run as one deferred grouped launch per segment, deferred.py.)
+(Measured and removed: a side stream for the weight-gradient GEMMs -- the fork / join edges
+cost more than the overlap won, and the weight gradients run as one deferred grouped launch,
+deferred.py -- and one for each Attention's key/value path beside the q Linear, -5 % per
+step in round 3.)
 """
 from __future__ import annotations
 
@@ -16,19 +17,7 @@ import os
 import torch
 
 FFM_SIDE = os.environ.get("CMX_FFM_STREAM", "1") == "1"
-# CMX_SR_STREAM=1: each Attention's key/value path (SR conv -> norm -> kv Linear,
-# dual_segformer.py:114-124) on a second side stream beside the q Linear (:111), forward and
-# (autograd follows the forward's streams) backward
-SR_SIDE = os.environ.get("CMX_SR_STREAM", "0") == "1"
 _ffm: dict = {}
-_sr: dict = {}
-
-
-def sr_stream(device) -> torch.cuda.Stream:
-    idx = torch.device(device).index
-    if idx not in _sr:
-        _sr[idx] = torch.cuda.Stream(device=device)
-    return _sr[idx]
 
 
 def ffm_stream(device) -> torch.cuda.Stream:

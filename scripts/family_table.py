@@ -33,36 +33,19 @@ def stage_shapes():
 
 
 def work():
-    """Per-step algorithmic work by family: {family: (flop, bytes)}."""
-    imgs = B * G                              # image-streams per step (both modalities)
-    gemm_mac = sra_flop = 0.0
-    dw_elems = ln_rows_c = 0.0
-    for st in stage_shapes():
-        N, C, Nk, R = st["N"], st["C"], st["Nk"], st["R"]
-        pe = N * C * st["cin"] * st["k"] ** 2
-        blk = N * C * C + 2 * Nk * C * C + N * C * C + 8 * N * C * C + (Nk * R * R * C * C if R > 1 else 0)
-        gemm_mac += imgs * (pe + st["depth"] * blk)
-        gemm_mac += B * (2 * N * C * C + 24 * C * C + 17 * N * C * C)          # FRM + FFM 1x1s (per image pair)
-        sra_flop += imgs * st["depth"] * 4 * N * Nk * C * 3.5                   # fwd + bwd (2.5x fwd)
-        dw_elems += imgs * st["depth"] * N * 4 * C
-        # norms: norm1, norm2 per block (+ attention norm on Nk rows), patch-embed norm, stage norm
-        ln_rows_c += imgs * (st["depth"] * (2 * N + (Nk if R > 1 else 0)) + 2 * N) * C
-    N1 = stage_shapes()[0]["N"]
-    gemm_mac += B * (sum(s["N"] * s["C"] * E for s in stage_shapes()) + N1 * 4 * E * E + N1 * E * K)
-    # forward + dgrad of every GEMM (the weight gradients are the grouped launch's)
-    gemm_flop = 2 * 2 * gemm_mac
-    wgrad_flop = 2 * gemm_mac
-    return {
-        "GEMM fwd+dgrad (tile / k-group / split-K)": (gemm_flop, None),
-        "grouped wgrad GEMM + grouped reduce": (wgrad_flop, 2.079e9),
-        "SRA attention (fwd, dQ, dK/dV, reduce)": (sra_flop, None),
-        # fwd: read h, write out + act'(z) = 6 B; bwd: read da, act', h, write dh = 8 B per element
-        "DWConv 3x3 + GELU (fwd_save, bwd_saved)": (None, dw_elems * (3 + 4) * BF),
-        # fwd: read x, write y (4 B); bwd: read dy (+dy2), x, write dx (+dxs) ~ 5 tensors (10 B)
-        "LayerNorm (fwd, bwd)": (None, ln_rows_c * (2 + 5) * BF),
-        # 66.58 M params x (p, g, m, v read 16 B + p, m, v write 12 B + 16-bit shadow 2 B)
-        "AdamW": (None, 66.58e6 * 30),
-    }
+    """Per-step algorithmic work by family: {family: (flop, bytes)}, from the as-executed model
+    of rgbx_semantic_segmentation_amd/floor.py (the same count as the bench line's step floor
+    and the roofline object: executed FLOPs, e.g. 211.2 GFLOP for the grouped weight gradients
+    after the decoder commute)."""
+    sys.path.insert(0, __file__.rsplit("/scripts/", 1)[0])
+    from rgbx_semantic_segmentation_amd.floor import step_work
+    w = step_work(backbone="mit_b2", H=H, W=W, B=B, K=K, E=E, n_params=66.58e6)
+    names = {"gemm": "GEMM fwd+dgrad (tile / k-group / split-K)", "wgrad": "grouped wgrad GEMM + grouped reduce",
+             "sra": "SRA attention (fwd, dQ, dK/dV, reduce)", "dwconv": "DWConv 3x3 + GELU (fwd_save, bwd_saved)",
+             "layernorm": "LayerNorm (fwd, bwd)", "adamw": "AdamW", "batchnorm": "BatchNorm (stats, fold, apply, bwd)",
+             "frm": "FRM (pool, channel MLP, combine)", "ffm": "FFM context / cross attention",
+             "ce": "upsample + CE", "bilinear": "bilinear (decoder fuse adjoint)", "im2col": "im2col / col2im"}
+    return {names[k]: (v[0] or None, v[1] or None) for k, v in w.items()}
 
 
 FAMILIES = [
@@ -109,7 +92,9 @@ def main():
             fam["other"][1] += us
     wk = work()
     out = []
-    hdr = ["family", "launches", "us/step", "share", "alg. GFLOP", "TFLOP/s", "of MFMA", "alg. GB", "TB/s", "of HBM"]
+    hdr = ["family", "launches", "us/step", "share", "alg. GFLOP", "TFLOP/s", "of MFMA", "alg. GB", "TB/s", "of HBM",
+           "floor us", "x floor"]
+    floor_total = 0.0
     out.append(hdr)
     for fname, (n, us) in sorted(fam.items(), key=lambda kv: -kv[1][1]):
         if n == 0:
@@ -126,16 +111,24 @@ def main():
             row += [f"{byts / 1e9:.2f}", f"{tb:.2f}", f"{tb / HBM_TBS:.1%}"]
         else:
             row += ["-", "-", "-"]
+        fl = max((flop or 0) / (MFMA_TF * 1e6), (byts or 0) / (HBM_TBS * 1e6))
+        floor_total += fl
+        row += [f"{fl:.0f}" if fl else "-", f"{us / fl:.1f}" if fl else "-"]
         out.append(row)
     print(f"# {path}: {head}  (kernel time summed {total:.0f} us over {launches:.0f} launches)")
+    wall = float(re.search(r"wall (\d+)", head).group(1)) if re.search(r"wall (\d+)", head) else total
+    foot = (f"step floor (sum over families of max(FLOP / {MFMA_TF} TFLOP/s, bytes / {HBM_TBS} TB/s), "
+            f"rgbx_semantic_segmentation_amd/floor.py): {floor_total:.0f} us = {floor_total / wall:.3f} of the {wall:.0f} us step")
     if md:
         print("| " + " | ".join(out[0]) + " |")
         print("|" + "---|" * len(out[0]))
         for r in out[1:]:
             print("| " + " | ".join(r) + " |")
+        print("\n" + foot)
     else:
         for r in out:
             print(f"{r[0]:44s} " + " ".join(f"{c:>10s}" for c in r[1:]))
+        print(foot)
 
 
 if __name__ == "__main__":

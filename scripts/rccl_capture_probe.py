@@ -1,6 +1,8 @@
 """Which RCCL collectives survive HIP-graph capture at world size 1 (one case per process:
 a crash ends only that case).  Usage: python scripts/rccl_capture_probe.py CASE
-CASE in {a2a_eager, ag_eager, rs_eager, ag_graph, rs_graph, a2a_graph}."""
+CASE in {a2a, ag, rs, rs32, ar, bc}_{eager, graph}: all_to_all_single / all_gather (bf16) /
+reduce_scatter (bf16, fp32) / all_reduce (fp32, the default gradient payload and SyncBN) /
+broadcast (fp32, the per-forward BatchNorm buffer sync)."""
 import os
 import sys
 
@@ -14,17 +16,26 @@ def main(case):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    print(f"torch {torch.__version__} hip {torch.version.hip} rccl {torch.cuda.nccl.version()}", flush=True)
     n = 1 << 16
-    src = torch.randn(n, device=dev).to(torch.bfloat16)
+    fp32 = case.split("_")[0] in ("rs32", "ar", "bc")
+    src = torch.randn(n, device=dev).to(torch.float32 if fp32 else torch.bfloat16)
     out = torch.empty_like(src)
 
     def op():
-        if case.startswith("a2a"):
+        kind = case.split("_")[0]
+        if kind == "a2a":
             dist.all_to_all_single(out, src)
-        elif case.startswith("ag"):
+        elif kind == "ag":
             dist.all_gather_into_tensor(out, src)
-        else:
+        elif kind in ("rs", "rs32"):
             dist.reduce_scatter_tensor(out, src)
+        elif kind == "ar":
+            out.copy_(src)
+            dist.all_reduce(out)
+        else:
+            out.copy_(src)
+            dist.broadcast(out, src=0)
 
     op()
     torch.cuda.synchronize()

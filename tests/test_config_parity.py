@@ -194,6 +194,16 @@ def test_bf16_train_step_vs_fp64_oracle(dev, case):
             eb, ebe = err(b, b64), err(dict(emu.named_buffers())[n], b64)
             rows.append((n, eb, ebe))
             _check(n, eb, max(ebe, 1e-7), bad)
+    import os
+    if os.environ.get("CMX_PARITY_DUMP"):
+        # the GPU step's CM-FRM / FFM gradients and loss for an off-box look at where they
+        # round (scripts/parity_frm_probe.py reruns the oracle variants on the same seeds)
+        import numpy as np
+        out = os.environ.get("CMX_PARITY_OUT", os.path.join("gpurun_out", "parity"))
+        os.makedirs(out, exist_ok=True)
+        keep = {n: p.grad.detach().float().cpu().numpy() for n, p in model.named_parameters()
+                if (".FRMs." in "." + n or ".FFMs." in "." + n) and p.grad.numel() <= 3_000_000}
+        np.savez_compressed(os.path.join(out, f"{case}_grads.npz"), loss=np.float64(loss.item()), **keep)
     ratios = sorted((e / max(ee, 1e-30), n) for n, e, ee in rows)
     print(f"\n{case}: loss scale {S:g}; cpu oracle {t_cpu:.1f} s; loss gpu {loss.item():.6f} fp64 {loss64.item():.6f}; "
           f"logits e_gpu {e_l:.3e} e_emu {e_le:.3e}; {len(rows)} tensors, gpu/emu error ratio "

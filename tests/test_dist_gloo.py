@@ -126,7 +126,7 @@ def _worker_store(rank, world, port, payload, q):
             den = ddp[n].abs().max().clamp_min(1e-12)
             worst = max(worst, ((got - ddp[n]).abs().max() / den).item())
             worst_glob = max(worst_glob, ((ref.get_parameter(n).grad - ddp[n]).abs().max() / den).item())
-        tol = 1e-6 if payload == "fp32" else 8e-3           # bf16: payload + ring-sum roundings
+        tol = 1e-6 if payload == "fp32" else 4e-3           # bf16: ONE rounding of the fp32 sum (<= 2^-8 rel.)
         q.put((rank, worst <= tol, worst_glob > 1e-3, worst, worst_glob))
     finally:
         dist.destroy_process_group()
@@ -157,3 +157,60 @@ def test_chunk_is_16B_aligned_for_fractional_mb(monkeypatch):
     for mb, payload in ((0.05, "bf16"), (0.05, "fp32"), (0.3, "bf16"), (25, "fp32")):
         s = cdist.BucketedGradSync(_Store(), None, payload=payload, chunk_mb=mb)
         assert s.chunk % 64 == 0, (mb, payload, s.chunk)
+
+
+def _worker_buffers(rank, world, port, q):
+    """DDP's per-forward buffer broadcast (broadcast_buffers=True, train.py:145-146) on the
+    flat BatchNorm buffer: after a local training step every rank's running statistics
+    differ; the broadcast at the next forward makes them rank 0's, through the module views."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rgbx_semantic_segmentation_amd.dist import broadcast_buffers, flatten_bn_buffers
+        torch.manual_seed(1)
+        m = torch.nn.Sequential(torch.nn.Conv2d(3, 4, 1), torch.nn.BatchNorm2d(4), torch.nn.ReLU(),
+                                torch.nn.BatchNorm2d(4))
+        flat = flatten_bn_buffers(m)
+        ok = flat is not None and flat.numel() == 16 and m[1].running_mean.data_ptr() == flat.data_ptr()
+        torch.manual_seed(100 + rank)               # a per-rank batch: local statistics drift apart
+        m.train()
+        m(torch.randn(2, 3, 5, 5))
+        mine = flat.clone()
+        allv = [torch.empty_like(flat) for _ in range(world)]
+        dist.all_gather(allv, mine)
+        ok = ok and not torch.equal(allv[0], allv[1])
+        broadcast_buffers(flat)
+        ok = ok and torch.equal(flat, allv[0]) and torch.equal(m[3].running_var, allv[0][12:16])
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bn_buffer_broadcast_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31500 + (os.getpid() % 1000)
+    procs = [ctx.Process(target=_worker_buffers, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[1] for r in res), res
+
+
+def test_model_bn_buffers_are_one_flat_tensor():
+    """EncoderDecoder's BatchNorm running statistics (FFM channel-embed BNs + the decoder's
+    linear_fuse BN) flatten into one tensor with the state_dict keys / shapes unchanged."""
+    from rgbx_semantic_segmentation_amd.models.builder import EncoderDecoder
+    from rgbx_semantic_segmentation_amd.dist import flatten_bn_buffers
+    m = EncoderDecoder(dict(backbone="mit_b0", num_classes=9, decoder_embed_dim=256))
+    before = {k: v.clone() for k, v in m.state_dict().items() if "running" in k}
+    flat = flatten_bn_buffers(m)
+    after = {k: v for k, v in m.state_dict().items() if "running" in k}
+    assert set(before) == set(after) and len(before) >= 4
+    assert flat.numel() == sum(v.numel() for v in before.values())
+    for k in before:
+        assert torch.equal(before[k], after[k])
+    flat.fill_(3.0)
+    assert all(float(v.min()) == 3.0 for k, v in m.state_dict().items() if "running" in k)

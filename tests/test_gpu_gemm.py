@@ -230,192 +230,3 @@ def test_gemm_h2_per_head(dev, dtype, GB, heads, N, D):
     ref = kh.float() @ ctxT.float().transpose(2, 3)
     assert rel(out, ref) < (1e-5 if dtype == torch.float32 else 1e-2), rel(out, ref)
     assert not wide[..., :C].abs().any()                                     # the other half untouched
-
-
-@pytest.fixture
-def stream_on(dev):
-    """Route every eligible 64 x 64 problem to the persistent stream kernel (CMX_GEMM_STREAM)."""
-    from rgbx_semantic_segmentation_amd import kernels as Kn
-    old = Kn.tune_get("GEMM_STREAM")
-    Kn.tune("GEMM_STREAM", 1)
-    yield Kn
-    Kn.tune("GEMM_STREAM", old if old >= 0 else 0)
-
-
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("G,M,N,K", [(2, 38400, 256, 64), (2, 38400, 64, 256), (2, 9600, 128, 128),
-                                     (1, 777, 40, 64), (2, 3001, 200, 192), (1, 130, 64, 24)])
-@pytest.mark.parametrize("tB", [0, 1])
-@pytest.mark.parametrize("ns", [2, 3, 4])
-def test_gemm_stream_kernel(stream_on, dtype, G, M, N, K, tB, ns):
-    """The persistent stream kernel (tiles walked per block, the LDS-DMA ring running across
-    tile boundaries, register epilogue through masked buffer stores) against torch, for ragged
-    M / N / K, both B layouts and every ring depth; the same fp32 accumulation order as the
-    per-tile kernel, so the two agree bit for bit."""
-    Kn = stream_on
-    torch.manual_seed(7)
-    A = torch.randn(G, M, K, device="cuda").to(dtype)
-    B = torch.randn(G, N, K, device="cuda").to(dtype)
-    Bv = B.transpose(1, 2).contiguous().transpose(1, 2) if tB else B
-    C = torch.full((G, M, N), 7.0, device="cuda", dtype=dtype)
-    Kn.tune("GEMM_STREAM_NS", ns)
-    try:
-        Kn.gemm(A, Bv, C)
-    finally:
-        Kn.tune("GEMM_STREAM_NS", 3)
-    ref = torch.bmm(A.float(), B.float().transpose(1, 2))
-    assert rel(C, ref) < 1e-2
-    Kn.tune("GEMM_STREAM", 0)
-    C2 = torch.empty_like(C)
-    Kn.gemm(A, Bv, C2)
-    Kn.tune("GEMM_STREAM", 1)
-    assert torch.equal(C, C2)
-
-
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("act", ["none", "gelu", "relu"])
-@pytest.mark.parametrize("res", [False, True])
-@pytest.mark.parametrize("nsr", [2, 3])
-def test_gemm_stream_epilogues(stream_on, dtype, act, res, nsr):
-    """Stream kernel epilogue: bias + activation + DropPath-scaled residual (the residual tile
-    rides the DMA ring), on a proj / fc2-shaped problem (stage-1 tokens, C = 64) with ragged
-    rows and per-sample scales, and the two-segment A (cat-free Linear) with a bias."""
-    Kn = stream_on
-    torch.manual_seed(8)
-    G, M, N, K, rps = 2, 4 * 1999, 64, 256, 1999
-    A = torch.randn(G, M, K, device="cuda").to(dtype)
-    B = torch.randn(G, N, K, device="cuda").to(dtype) * (1.0 / K ** 0.5)
-    bias = torch.randn(G, N, device="cuda")
-    R = torch.randn(G, M, N, device="cuda").to(dtype) if res else None
-    s = torch.tensor([0.0, 1.25, 1.25, 0.0, 1.0, 1.25, 0.0, 1.25], device="cuda") if res else None
-    C = torch.empty(G, M, N, device="cuda", dtype=dtype)
-    Kn.tune("GEMM_STREAM_NSR", nsr)
-    try:
-        Kn.gemm(A, B, C, bias=bias, residual=R, rscale=s, rows_per_sample=rps, act=act)
-    finally:
-        Kn.tune("GEMM_STREAM_NSR", 2)
-    ref = ref_epi(torch.bmm(A.float(), B.float().transpose(1, 2)), bias, act, R, s, rps)
-    assert rel(C, ref) < 1e-2
-    Kn.tune("GEMM_STREAM", 0)
-    C2 = torch.empty_like(C)
-    Kn.gemm(A, B, C2, bias=bias, residual=R, rscale=s, rows_per_sample=rps, act=act)
-    Kn.tune("GEMM_STREAM", 1)
-    # same accumulation; the epilogue's float ops may contract differently: within 1 ulp
-    assert ((C.float() - C2.float()).abs() <= C2.float().abs() * 2 ** -7 + 1e-6).all()
-    # two-segment A: Linear on cat(x1, x2) without the cat
-    x1 = torch.randn(G, 9600, 64, device="cuda").to(dtype)
-    x2 = torch.randn(G, 9600, 128, device="cuda").to(dtype)
-    W = torch.randn(G, 128, 192, device="cuda").to(dtype)
-    C = torch.empty(G, 9600, 128, device="cuda", dtype=dtype)
-    Kn.gemm(x1, W, C, bias=bias[:, :1].expand(G, 128).contiguous(), A2=x2)
-    ref = torch.bmm(torch.cat([x1, x2], -1).float(), W.float().transpose(1, 2)) + bias[:, :1, None]
-    assert rel(C, ref) < 1e-2
-
-
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("G,M,N,K", [(2, 38400, 64, 64), (2, 38400, 64, 256), (2, 9600, 128, 128), (2, 9600, 128, 512),
-                                     (2, 1001, 64, 96), (1, 700, 128, 320)])
-@pytest.mark.parametrize("res", [False, True])
-def test_gemm_ln_epilogue(dev, dtype, G, M, N, K, res):
-    """cmx_gemm_ln: the residual GEMM's output C and LayerNorm(C) (the Block's next norm,
-    dual_segformer.py:166-169) from one launch, against torch's layer_norm of the STORED C
-    (the norm reads the 16-bit rows in the unfused path too); per-row mean / rstd against
-    the same.  Shapes: stage-1 / stage-2 proj and fc2 (one- and k-group tiles), ragged rows."""
-    from rgbx_semantic_segmentation_amd import kernels as Kn
-    torch.manual_seed(9)
-    rps = M // 2 if M % 2 == 0 else M
-    A = torch.randn(G, M, K, device="cuda").to(dtype)
-    B = (torch.randn(G, N, K, device="cuda") / K ** 0.5).to(dtype)
-    bias = torch.randn(G, N, device="cuda")
-    R = torch.randn(G, M, N, device="cuda").to(dtype) if res else None
-    s = torch.rand(G * M // rps, device="cuda") * 1.5 if res else None
-    gamma = torch.randn(G, N, device="cuda")
-    beta = torch.randn(G, N, device="cuda")
-    C = torch.empty(G, M, N, device="cuda", dtype=dtype)
-    Y = torch.empty_like(C)
-    mean = torch.empty(G * M, device="cuda")
-    rstd = torch.empty(G * M, device="cuda")
-    Kn.gemm_ln(A, B, C, Y, gamma, beta, mean, rstd, 1e-6, bias=bias, residual=R, rscale=s, rows_per_sample=rps)
-    C2 = torch.empty_like(C)
-    Kn.gemm(A, B, C2, bias=bias, residual=R, rscale=s, rows_per_sample=rps)
-    # the plain call may split K (few tiles): same values within one 16-bit rounding
-    assert ((C.float() - C2.float()).abs() <= C2.float().abs() * 2 ** -7 + 1e-3).all()
-    ref = ref_epi(torch.bmm(A.float(), B.float().transpose(1, 2)), bias, "none", R, s, rps)
-    assert rel(C, ref) < 1e-2
-    Cf = C.float()
-    for g in range(G):
-        yr = F.layer_norm(Cf[g], (N,), gamma[g], beta[g], 1e-6)
-        assert (Y[g].float() - yr).abs().max().item() < 3e-2 * max(1.0, yr.abs().max().item() / 8)
-        mu = Cf[g].mean(-1)
-        rs = torch.rsqrt(Cf[g].var(-1, unbiased=False) + 1e-6)
-        assert torch.allclose(mean[g * M:(g + 1) * M], mu, atol=1e-5, rtol=1e-5)
-        assert torch.allclose(rstd[g * M:(g + 1) * M], rs, atol=1e-4, rtol=1e-4)
-    # the unfused norm kernel on the stored rows gives the same statistics
-    y2, m2, r2 = Kn.layernorm_fwd(C, gamma, beta, 1e-6, G=G)
-    assert torch.allclose(m2.view(-1), mean, atol=1e-6, rtol=1e-6)
-    assert torch.allclose(r2.view(-1), rstd, atol=1e-5, rtol=1e-5)
-    assert ((Y.float() - y2.float()).abs() <= 2 ** -7 * y2.float().abs() + 1e-3).all()
-
-
-@pytest.fixture
-def reg_on(dev):
-    """Route eligible problems to the register-streamed kernel (CMX_GEMM_REG = least M)."""
-    from rgbx_semantic_segmentation_amd import kernels as Kn
-    old = Kn.tune_get("GEMM_REG")
-    Kn.tune("GEMM_REG", 1)
-    yield Kn
-    Kn.tune("GEMM_REG", old if old >= 0 else 0)
-
-
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("G,M,N,K", [(2, 38400, 256, 64), (2, 38400, 64, 256), (2, 9600, 512, 128), (2, 9600, 128, 512),
-                                     (1, 38400, 512, 64), (2, 1001, 200, 192), (1, 777, 40, 152), (2, 4800, 320, 320)])
-@pytest.mark.parametrize("tB", [0, 1])
-def test_gemm_reg_kernel(reg_on, dtype, G, M, N, K, tB):
-    """Register-streamed kernel (weight slice in LDS, A strips straight to registers, no
-    barriers after staging) against torch and against the tile kernel, for ragged M / N / K,
-    both weight layouts, one to eight 64-deep k-chunks and 64- / 128-wide weight slices."""
-    Kn = reg_on
-    if tB and N % 8:
-        pytest.skip("transposed weight needs N % 8 == 0")
-    torch.manual_seed(10)
-    A = torch.randn(G, M, K, device="cuda").to(dtype)
-    B = torch.randn(G, N, K, device="cuda").to(dtype)
-    Bv = B.transpose(1, 2).contiguous().transpose(1, 2) if tB else B
-    C = torch.full((G, M, N), 3.0, device="cuda", dtype=dtype)
-    Kn.gemm(A, Bv, C)
-    ref = torch.bmm(A.float(), B.float().transpose(1, 2))
-    assert rel(C, ref) < 1e-2
-    Kn.tune("GEMM_REG", 0)
-    C2 = torch.empty_like(C)
-    Kn.gemm(A, Bv, C2)
-    Kn.tune("GEMM_REG", 1)
-    assert ((C.float() - C2.float()).abs() <= C2.float().abs() * 2 ** -7 + 1e-2).all()
-
-
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("act", ["none", "gelu"])
-@pytest.mark.parametrize("res", [False, True])
-def test_gemm_reg_epilogues(reg_on, dtype, act, res):
-    """Register-streamed kernel epilogue: bias + activation + DropPath-scaled residual on a
-    stage-1 fc2-shaped problem with ragged rows, and the two-segment (cat-free) A."""
-    Kn = reg_on
-    torch.manual_seed(11)
-    G, M, N, K, rps = 2, 4 * 1999, 64, 256, 1999
-    A = torch.randn(G, M, K, device="cuda").to(dtype)
-    B = torch.randn(G, N, K, device="cuda").to(dtype) * (1.0 / K ** 0.5)
-    bias = torch.randn(G, N, device="cuda")
-    R = torch.randn(G, M, N, device="cuda").to(dtype) if res else None
-    s = torch.tensor([0.0, 1.25, 1.25, 0.0, 1.0, 1.25, 0.0, 1.25], device="cuda") if res else None
-    C = torch.empty(G, M, N, device="cuda", dtype=dtype)
-    Kn.gemm(A, B, C, bias=bias, residual=R, rscale=s, rows_per_sample=rps, act=act)
-    ref = ref_epi(torch.bmm(A.float(), B.float().transpose(1, 2)), bias, act, R, s, rps)
-    assert rel(C, ref) < 1e-2
-    x1 = torch.randn(G, 9600, 64, device="cuda").to(dtype)
-    x2 = torch.randn(G, 9600, 128, device="cuda").to(dtype)
-    W = torch.randn(G, 128, 192, device="cuda").to(dtype)
-    C = torch.empty(G, 9600, 128, device="cuda", dtype=dtype)
-    b2 = torch.randn(G, 128, device="cuda")
-    Kn.gemm(x1, W, C, bias=b2, A2=x2)
-    ref = torch.bmm(torch.cat([x1, x2], -1).float(), W.float().transpose(1, 2)) + b2[:, None, :]
-    assert rel(C, ref) < 1e-2
