@@ -18,3 +18,7 @@ db=$(ls gpurun_out/sq_$TAG/*.db gpurun_out/sq_$TAG/*/*.db 2>/dev/null | head -1)
 python3 scripts/sq_summary.py $db > gpurun_out/sq_summary_$TAG.txt 2>&1
 rm -rf gpurun_out/sq_$TAG
 head -50 gpurun_out/sq_summary_$TAG.txt
+CMX_PARITY_DUMP=1 timeout -k 10 600 python -u -m pytest tests/test_config_parity.py -m gpu -x -q --timeout 580 \
+  --timeout-method thread -k "config2_b2_480x640_bs2" > gpurun_out/parity_dump_$TAG.log 2>&1
+rc=$?; tail -3 gpurun_out/parity_dump_$TAG.log; [ $rc -le 1 ] || exit $rc
+ls -la gpurun_out/parity/
