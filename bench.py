@@ -367,6 +367,14 @@ def main():
             done = int(flag.item()) == 0
         if done:
             break
+    # the host's own cost of one replay (enqueue of every node), with the device queue empty:
+    # if it approaches the device time per step, the step turns host-bound
+    host_enq = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        h0 = time.perf_counter()
+        run_one()
+        host_enq.append((time.perf_counter() - h0) * 1e3)
     if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -453,7 +461,8 @@ def main():
             "cpu_baseline": cpu,
             "replay_ms": {"warmup": replay_stats(warm_ms), "timed": replay_stats(timed_ms),
                           "settle": {"replays": settle_n, "device_s": round(settle_t, 3),
-                                     "window_medians": [round(v, 3) for v in settle_med]}},
+                                     "window_medians": [round(v, 3) for v in settle_med]},
+                          "host_enqueue_idle_queue": sorted(round(v, 3) for v in host_enq)},
             "clocks": {"idle": dict(zip(("sclk_mhz", "mclk_mhz", "power_w"), clk_idle)),
                        "timed": clocks.summary()},
         }

@@ -17,7 +17,10 @@ import re
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcmx_hip.so")
+# CMX_LIB_VARIANT=name loads libcmx_hip_<name>.so (an A/B build of the same sources with other
+# compile-time options, csrc/Makefile VARIANT=); default: libcmx_hip.so
+_VARIANT = os.environ.get("CMX_LIB_VARIANT", "")
+LIB_PATH = os.path.join(_HERE, f"libcmx_hip_{_VARIANT}.so" if _VARIANT else "libcmx_hip.so")
 HEADER_PATHS = [os.path.join(_HERE, "..", "include", "cmx_hip.h"), os.path.join(_HERE, "cmx_hip.h")]
 
 

@@ -15,33 +15,33 @@
 // (IFRM's lambdas, which the reference's optimizer never sees): left untouched.  Optionally emits the bf16 weight shadow for
 // the next step's GEMMs and scales the gradient (1/world_size after a SUM all-reduce).
 // HBM-bound: 16 B read (p,g,m,v) + 12 B written (p,m,v) [+2 B shadow] per parameter.
+// The step count is read at every block's start as t_prev and used as t = t_prev + 1; the LAST
+// block to finish (arrival ticket) stores t, after every block has read t_prev -- the increment
+// needs no launch of its own.  One AdamW launch in flight per device at a time (the ticket is
+// a device global that the last block resets).
 #include "cmx_common.h"
+
+__device__ unsigned int g_adamw_ticket = 0;
 
 // S = the weight shadow's 16-bit type (bf16 or f16, the compute dtype's GEMM operand)
 template <typename S>
 __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                              float* __restrict__ v, S* __restrict__ shadow, const uint8_t* __restrict__ decay64,
-                             long n, const float* __restrict__ lr_ptr, const float* __restrict__ step_ptr, double b1d,
+                             long n, const float* __restrict__ lr_ptr, float* __restrict__ step_ptr, double b1d,
                              double b2d, float eps, double wd, float gscale, const float* __restrict__ loss_scale,
                              const float* __restrict__ found_inf) {
   // GradScaler semantics (train.py:185-198): a step whose gradients held inf / nan is skipped
   if (found_inf && *found_inf != 0.f) return;
   if (loss_scale) gscale /= *loss_scale;                       // unscale
   const double lr = *lr_ptr;
-  const double t = *step_ptr;
+  const double t = (double)*step_ptr + 1.0;
   const float step_size = (float)(lr / (1.0 - pow(b1d, t)));
   const float bc2s = (float)sqrt(1.0 - pow(b2d, t));
   const float omb1 = (float)(1.0 - b1d), b2 = (float)b2d, omb2 = (float)(1.0 - b2d);
   const float decf = (float)(1.0 - lr * wd);
   const long nv = n / 4;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)nv; i += gridDim.x * blockDim.x) {
-    const long e = i * 4;
-    float4 pp = *reinterpret_cast<float4*>(p + e);
-    float4 gg = *reinterpret_cast<const float4*>(g + e);
-    float4 mm = *reinterpret_cast<float4*>(m + e);
-    float4 vv = *reinterpret_cast<float4*>(v + e);
-    const uint8_t flag = decay64[e >> 6];              // 0: no decay, 1: decay, 2: frozen
-    if (flag == 2) continue;
+  auto update = [&](const long e, float4 pp, const float4 gg, float4 mm, float4 vv, const uint8_t flag) {
+    if (flag == 2) return;                             // 0: no decay, 1: decay, 2: frozen
     const float dec = flag ? decf : 1.f;
     float pa[4] = {pp.x, pp.y, pp.z, pp.w}, ga[4] = {gg.x, gg.y, gg.z, gg.w};
     float ma[4] = {mm.x, mm.y, mm.z, mm.w}, va[4] = {vv.x, vv.y, vv.z, vv.w};
@@ -57,16 +57,37 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
     *reinterpret_cast<float4*>(p + e) = make_float4(pa[0], pa[1], pa[2], pa[3]);
     *reinterpret_cast<float4*>(m + e) = make_float4(ma[0], ma[1], ma[2], ma[3]);
     *reinterpret_cast<float4*>(v + e) = make_float4(va[0], va[1], va[2], va[3]);
-    if (shadow) {
-      uint32_t a = pack2<S>(pa[0], pa[1]);
-      uint32_t b = pack2<S>(pa[2], pa[3]);
-      *reinterpret_cast<uint2*>(shadow + e) = make_uint2(a, b);
+    if (shadow) *reinterpret_cast<uint2*>(shadow + e) = make_uint2(pack2<S>(pa[0], pa[1]), pack2<S>(pa[2], pa[3]));
+  };
+  // two float4 groups per thread per iteration: eight 16-B loads in flight before any update
+  const long stride = (long)gridDim.x * blockDim.x;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + stride < nv; i += 2 * stride) {
+    const long e0 = i * 4, e1 = (i + stride) * 4;
+    const float4 p0 = *reinterpret_cast<const float4*>(p + e0), p1 = *reinterpret_cast<const float4*>(p + e1);
+    const float4 g0 = *reinterpret_cast<const float4*>(g + e0), g1 = *reinterpret_cast<const float4*>(g + e1);
+    const float4 m0 = *reinterpret_cast<const float4*>(m + e0), m1 = *reinterpret_cast<const float4*>(m + e1);
+    const float4 v0 = *reinterpret_cast<const float4*>(v + e0), v1 = *reinterpret_cast<const float4*>(v + e1);
+    const uint8_t f0 = decay64[e0 >> 6], f1 = decay64[e1 >> 6];
+    update(e0, p0, g0, m0, v0, f0);
+    update(e1, p1, g1, m1, v1, f1);
+  }
+  if (i < nv) {
+    const long e = i * 4;
+    update(e, *reinterpret_cast<const float4*>(p + e), *reinterpret_cast<const float4*>(g + e),
+           *reinterpret_cast<const float4*>(m + e), *reinterpret_cast<const float4*>(v + e), decay64[e >> 6]);
+  }
+  // the step count: the last block to arrive stores t (every block read t_prev at its start)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // relaxed: every thread of this block consumed t_prev before the barrier above (an
+    // acquire / release here would write back and invalidate the L2 once per block)
+    const unsigned prev = __hip_atomic_fetch_add(&g_adamw_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {
+      __hip_atomic_store(&g_adamw_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *step_ptr = (float)t;
     }
   }
-}
-
-__global__ void step_incr_kernel(float* step, const float* found_inf) {
-  if (!(found_inf && *found_inf != 0.f)) *step += 1.f;
 }
 
 // found_inf[0] = 1 if any of g[0, n) is inf / nan (left untouched otherwise; reset by the
@@ -99,7 +120,8 @@ __global__ void loss_scale_update_kernel(float* scale, int* tracker, float* foun
 
 extern "C" {
 
-// n must be a multiple of 64; step_ptr is incremented by this call before use (torch order)
+// n must be a multiple of 64; the step count at step_ptr is incremented by this call and the
+// incremented value used (torch order); a step skipped for found_inf leaves it unchanged
 int cmx_adamw_step(float* p, const float* g, float* m, float* v, void* shadow, int shadow_dtype, const uint8_t* decay64,
                    int64_t n, const float* lr_ptr, float* step_ptr, double beta1, double beta2, float eps,
                    double weight_decay, float grad_scale, hipStream_t s) {
@@ -113,9 +135,8 @@ int cmx_adamw_step_scaled(float* p, const float* g, float* m, float* v, void* sh
                           const float* found_inf, hipStream_t s) {
   CMX_REQUIRE(n % 64 == 0, CMX_ERR_SHAPE, "adamw: n must be a multiple of 64");
   CMX_REQUIRE(!shadow || shadow_dtype == 1 || shadow_dtype == 2, CMX_ERR_DTYPE, "adamw: shadow dtype %d", shadow_dtype);
-  hipLaunchKernelGGL(step_incr_kernel, dim3(1), dim3(1), 0, s, step_ptr, found_inf);
   long blocks = (n / 4 + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
+  if (blocks > 2048) blocks = 2048;            // 2048 arrivals on the step ticket per launch
   if (shadow_dtype == 2)
     hipLaunchKernelGGL(adamw_kernel<f16>, dim3((unsigned)blocks), dim3(256), 0, s, p, g, m, v, (f16*)shadow, decay64,
                        (long)n, lr_ptr, step_ptr, beta1, beta2, eps, weight_decay, grad_scale, loss_scale, found_inf);

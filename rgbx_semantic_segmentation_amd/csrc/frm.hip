@@ -463,6 +463,7 @@ __global__ __launch_bounds__(256) void combine_bwd_kernel(const T* __restrict__ 
 }
 
 // ------------------------------------------------------------------------ pooling (backward)
+constexpr int PB_SL = 16;                       // partial slices of dpooled (small_linear_bwd's NSLICE)
 // dx[g][b][n][c] += dpooled_avg[b][gC+c] / N + (n == argmax[b][gC+c]) * dpooled_max[b][2C+gC+c];
 // dpooled arrives as partial slices dp[b][k] = sum_s part[s*ss + b*sm + k].
 template <typename T, int TPR>
@@ -474,12 +475,18 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const float* __restrict__
   const int gb = blockIdx.y, g = gb / B, b = gb % B;
   const int lane = threadIdx.x % TPR, slot = threadIdx.x / TPR;
   const int nch = C / V;
-  // the block's 2C dpooled values, each summed over the nsl partial slices, once per block
+  // the block's 2C dpooled values, each summed over the nsl (<= PB_SL) partial slices, once per
+  // block: every slice's load issued before the sum (a runtime-bounded serial loop waited one
+  // L2 round trip per slice: 18 us per launch at stages 3 / 4)
   for (int e = threadIdx.x; e < 2 * C; e += 256) {
     const int k = e < C ? g * C + e : 2 * C + g * C + (e - C);
     const float* p = part + b * sm + k;
+    float v[PB_SL];
+#pragma unroll
+    for (int q = 0; q < PB_SL; ++q) v[q] = q < nsl ? p[q * ss] : 0.f;
     float t = 0.f;
-    for (int q = 0; q < nsl; ++q) t += p[q * ss];
+#pragma unroll
+    for (int q = 0; q < PB_SL; ++q) t += v[q];
     sdp[e] = e < C ? t / N : t;
   }
   __syncthreads();
@@ -570,7 +577,8 @@ int cmx_frm_pool_fwd(const void* x, float* pooled, int* argmax, float* workspace
 int cmx_frm_pool_bwd(const float* dpooled_part, int nslice, int64_t slice_stride, const int* argmax, void* dx, int B,
                      int N, int C, int dtype, hipStream_t s) {
   const int V = dtype == 0 ? 4 : 8;
-  CMX_REQUIRE(C % V == 0 && C / V <= MAXCH * 64 && C <= 1024 && nslice > 0, CMX_ERR_SHAPE, "frm_pool_bwd: C=%d", C);
+  CMX_REQUIRE(C % V == 0 && C / V <= MAXCH * 64 && C <= 1024 && nslice > 0 && nslice <= PB_SL, CMX_ERR_SHAPE,
+              "frm_pool_bwd: C=%d nslice=%d", C, nslice);
   const int tpr = row_lanes(C, V);
   const int rpb = 256 / tpr;
   long nb = (N + rpb - 1) / rpb;

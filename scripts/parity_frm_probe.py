@@ -24,18 +24,6 @@ from oracle import bf16_emul  # noqa: E402
 import test_config_parity as T  # noqa: E402
 
 
-class _FakeGPU:
-    """Stand-in for the GPU model in T._masks (only the attributes it reads)."""
-
-    def __init__(self, ref):
-        class BB:
-            pass
-        self.backbone = BB()
-        self.backbone.depths = ref.backbone.depths
-        self.decode_head = ref.decode_head
-        self.forced_masks = None
-
-
 def build(case):
     backbone, H, W, B, K, dtype = T.CONFIGS[case]
     torch.manual_seed(0)
@@ -69,13 +57,23 @@ def main(path):
     ref, (backbone, H, W, B, K) = build(case)
     variants = {}
     ref64 = copy.deepcopy(ref).double()
-    fake = _FakeGPU(ref)
+    from rgbx_semantic_segmentation_amd.models.builder import EncoderDecoder
+    fake = EncoderDecoder(dict(backbone=backbone, num_classes=K, decoder_embed_dim=512))   # masks only (CPU)
     models = {"fp64": ref64}
     models["base"] = bf16_emul.emulate_storage(copy.deepcopy(ref), torch.bfloat16)
-    T._masks(fake, list(models.values()), B, n_calls=2)
+    T._masks(fake, list(models.values()), B, n_calls=2)      # (re-drawn identically per call: fixed seed)
     rgb, x, lab = T._inputs(B, H, W, K)
     g64 = grads(ref64, rgb, x, lab, torch.float64)
     variants["base"] = grads(models["base"], rgb, x, lab, torch.float32)
+    # the same emulation with other fp32 summation orders (CPU thread counts): how much do these
+    # gradients move when only the order of fp32 accumulation changes?
+    nt = torch.get_num_threads()
+    for t in (1, 3):
+        torch.set_num_threads(t)
+        em = bf16_emul.emulate_storage(copy.deepcopy(ref), torch.bfloat16)
+        T._masks(fake, [em], B, n_calls=2)
+        variants[f"threads{t}"] = grads(em, rgb, x, lab, torch.float32)
+    torch.set_num_threads(nt)
     names = [n for n in gpu.files if n != "loss"]
     gmax = max(v.abs().max().item() for v in g64.values())
     print(f"{case}: GPU loss {float(gpu['loss']):.6f}")
