@@ -34,6 +34,20 @@ pytestmark = pytest.mark.gpu
 
 RATIO = 4.0
 OUTLIER_RATIO = 12.0
+# CM-FRM / FFM tensors of the bf16 cases: at most 2x the emulated error,
+# outliers up to 4x for at most 4 % of them (6 of 148 at B2), with two documented adjustments:
+#  * ChannelWeights' first Linear (FRMs.s.channel_weights.mlp.0): hidden units whose fp64
+#    pre-activation lies within 2^-7 of the layer's typical magnitude in some sample are
+#    excluded from the row comparison -- their ReLU decision is decided by rounding, and a flip
+#    moves the whole gradient row (round 4: every FRM outlier row was such a unit, e.g. stage 2
+#    unit 81 with z = -0.00038, whose fp64 row is exactly zero);
+#  * SpatialWeights' biases (a sum over all B*H*W pixels with heavy cancellation): the yardstick
+#    is at least 2^-8 x sum|per-pixel terms| / max|gradient|, the error bf16 inputs alone allow.
+RATIO_FUSION = 2.0
+OUTLIER_FUSION = 4.0
+FUSION_OUTLIER_SHARE = 0.04
+ZBAND = 2.0 ** -7
+BF16_EPS = 2.0 ** -8
 
 CONFIGS = {
     # name: (backbone, H, W, batch, classes, dtype)   BASELINE.json configs[0..4] (configs[2] is
@@ -87,7 +101,7 @@ def _inputs(B, H, W, K, seed=3):
     return make_batch(B, H, W, K, seed=seed)
 
 
-def _record(case, loss, loss64, rows, bad, grad_bad):
+def _record(case, loss, loss64, rows, bad, grad_bad, notes=None):
     """The per-tensor margins on record: {case}.json under $CMX_PARITY_OUT (default
     gpurun_out/parity, copied into profiles/ after a GPU run) with e_gpu, e_emu and their
     ratio for every compared tensor."""
@@ -95,13 +109,57 @@ def _record(case, loss, loss64, rows, bad, grad_bad):
     import os
     out = os.environ.get("CMX_PARITY_OUT", os.path.join("gpurun_out", "parity"))
     os.makedirs(out, exist_ok=True)
-    tab = [{"tensor": n, "e_gpu": e, "e_emu": ee, "ratio": e / max(ee, 1e-30)} for n, e, ee in rows]
+    notes = notes or {}
+    tab = [dict({"tensor": n, "e_gpu": e, "e_emu": ee, "ratio": e / max(ee, 1e-30)},
+                **({"note": notes[n]} if n in notes else {})) for n, e, ee in rows]
     rs = sorted(t["ratio"] for t in tab)
     with open(os.path.join(out, f"{case}.json"), "w") as f:
         json.dump({"case": case, "ratio_bound": RATIO, "outlier_ratio_bound": OUTLIER_RATIO,
+                   "fusion_ratio_bound": RATIO_FUSION, "fusion_outlier_ratio_bound": OUTLIER_FUSION,
                    "loss_gpu": loss, "loss_fp64": loss64, "n_tensors": len(tab),
                    "ratio_median": rs[len(rs) // 2], "ratio_max": rs[-1],
                    "n_over_bound": len(bad) + len(grad_bad), "tensors": tab}, f, indent=1)
+
+
+def _fusion_probes(ref64):
+    """fp64 hooks on every CM-FRM: the channel MLP's first-layer pre-activation z (B, 4C) of
+    the last forward, and the gradients of the spatial head's two 1x1 conv outputs (their bias
+    gradients are the sums of these over the pixels)."""
+    probes = {}
+    for s, frm in enumerate(ref64.backbone.FRMs):
+        if not hasattr(frm, "channel_weights"):
+            continue
+
+        def zhook(m, a, o, s=s):
+            probes[("z", s)] = o.detach()
+        frm.channel_weights.mlp[0].register_forward_hook(zhook)
+        for i in (0, 2):
+            def ghook(m, a, o, s=s, i=i):
+                if o.requires_grad:
+                    o.register_hook(lambda g, s=s, i=i: probes.__setitem__((f"dsw{i}", s), g.detach()))
+            frm.spatial_weights.mlp[i].register_forward_hook(ghook)
+    return probes
+
+
+def _fusion_adjust(n, gpu_g, emu_g, g64, den, probes):
+    """(e_gpu, e_emu, note) for the two adjusted CM-FRM cases (see RATIO_FUSION), else None."""
+    import re
+    m = re.match(r"backbone\.FRMs\.(\d+)\.channel_weights\.mlp\.0\.(weight|bias)$", n)
+    if m and ("z", int(m.group(1))) in probes:
+        z = probes[("z", int(m.group(1)))]
+        keep = (z.abs() > ZBAND * z.abs().median()).all(0)
+        if bool(keep.any()):
+            eg = (gpu_g - g64)[keep].abs().max().item() / den
+            ee = (emu_g - g64)[keep].abs().max().item() / den
+            return eg, ee, f"{int((~keep).sum())} ReLU-band units excluded"
+    m = re.match(r"backbone\.FRMs\.(\d+)\.spatial_weights\.mlp\.(0|2)\.bias$", n)
+    if m and (f"dsw{m.group(2)}", int(m.group(1))) in probes:
+        t = probes[(f"dsw{m.group(2)}", int(m.group(1)))]
+        allow = BF16_EPS * t.abs().sum((0, 2, 3)).max().item() / max(g64.abs().max().item(), 1e-300)
+        eg = (gpu_g - g64).abs().max().item() / den
+        ee = (emu_g - g64).abs().max().item() / den
+        return eg, max(ee, allow), f"cancellation allowance {allow:.3g}"
+    return None
 
 
 def _check(name, e_gpu, e_emu, bad, ratio=RATIO):
@@ -132,6 +190,7 @@ def test_bf16_train_step_vs_fp64_oracle(dev, case):
     model.load_state_dict(ref.state_dict(), strict=True)
     emu = emulate_storage(copy.deepcopy(ref), h16)
     ref64 = ref.double()
+    probes = _fusion_probes(ref64) if h16 == torch.bfloat16 else {}
     for m in (ref64, emu, model):
         m.train()
     _masks(model, [ref64, emu], B, n_calls=2)
@@ -179,15 +238,25 @@ def test_bf16_train_step_vs_fp64_oracle(dev, case):
     p64 = dict(ref64.named_parameters())
     pem = dict(emu.named_parameters())
     gmax = max(p.grad.abs().max().item() for p in ref64.parameters())
-    grad_bad = []
+    grad_bad, fusion_bad, notes = [], [], {}
+    n_fusion = 0
     for n, p in model.named_parameters():
         g64 = p64[n].grad
         assert g64 is not None and p.grad is not None, n
         den = max(g64.abs().max().item(), 1e-6 * gmax)
-        eg = (p.grad.detach().double().cpu() - g64).abs().max().item() / den
+        gg = p.grad.detach().double().cpu()
+        eg = (gg - g64).abs().max().item() / den
         ee = (pem[n].grad.double() - g64).abs().max().item() / den
+        fusion = h16 == torch.bfloat16 and (".FRMs." in n or ".FFMs." in n)
+        if fusion:
+            adj = _fusion_adjust(n, gg, pem[n].grad.double(), g64, den, probes)
+            if adj is not None:
+                eg, ee, notes[n] = adj
+            n_fusion += 1
+            _check(n, eg, ee, fusion_bad, ratio=RATIO_FUSION)
+        else:
+            _check(n, eg, ee, grad_bad)
         rows.append((n, eg, ee))
-        _check(n, eg, ee, grad_bad)
     for n, b in model.named_buffers():
         if "running" in n:
             b64 = dict(ref64.named_buffers())[n]
@@ -209,7 +278,9 @@ def test_bf16_train_step_vs_fp64_oracle(dev, case):
           f"logits e_gpu {e_l:.3e} e_emu {e_le:.3e}; {len(rows)} tensors, gpu/emu error ratio "
           f"median {ratios[len(ratios) // 2][0]:.2f}, max {ratios[-1][0]:.2f} ({ratios[-1][1]})")
     print("worst ratios:", [(round(r, 2), n) for r, n in ratios[-8:]])
-    _record(case, loss.item(), loss64.item(), rows, bad, grad_bad)
+    _record(case, loss.item(), loss64.item(), rows, bad, grad_bad + fusion_bad, notes)
     n_allowed = max(2, len(rows) // 100)
     assert not bad, bad
     assert len(grad_bad) <= n_allowed and all(b[0] <= OUTLIER_RATIO for b in grad_bad), grad_bad[:10]
+    n_fusion_allowed = max(2, int(FUSION_OUTLIER_SHARE * n_fusion))
+    assert len(fusion_bad) <= n_fusion_allowed and all(b[0] <= OUTLIER_FUSION for b in fusion_bad), fusion_bad
