@@ -140,11 +140,6 @@ int cmx_small_linear_bwd(const float* dy_part, int dy_nslice, int64_t dy_slice_s
  * accumulated); the pooling gradient is ADDED into dx.  B <= 8, C % 16 == 0, C <= 512.  One launch
  * of each direction at a time per device.  barrier_timeouts: count of polls that gave up (0 = every
  * grid was co-resident; synchronous, for tests). */
-size_t cmx_frm_channel_fwd_workspace(int B, int N, int C);
-int cmx_frm_channel_fwd(const void* x, const float* w1, const float* b1, const float* w2, const float* b2, float* pooled, int* argmax, float* y1, float* cw, float* workspace, int B, int N, int C, int dtype, hipStream_t stream);
-size_t cmx_frm_channel_bwd_workspace(int B, int C);
-int cmx_frm_channel_bwd(const float* dcw_part, int nslab, const float* cw, const float* y1, const float* pooled, const int* argmax, const float* w1, const float* w2, float* dw1, float* db1, float* dw2, float* db2, void* dx, float* workspace, int B, int N, int C, int dtype, hipStream_t stream);
-int cmx_frm_barrier_timeouts(void);
 int cmx_frm_combine_fwd(const void* x, const float* cw, const void* h, const float* w2, const float* b2, float* sw, void* out, int B, int N, int C, int dtype, hipStream_t stream);
 /* backward: dx direct path (2,B,N,C), dh (B*N, C); workspace = dcw partials (B, nblk, 2C) followed by the
  * [dw2 (2C) | db2 (2)] partials (B*nblk, 2C+2); nblk = cmx_frm_combine_bwd_nblk(N, C, dtype) */
@@ -198,6 +193,14 @@ int cmx_upsample_ce_bwd(const void* logits, const int64_t* label, const float* d
 size_t cmx_gemm_workspace(int G, int M, int N, int splitk);
 int cmx_gemm_splitk(int G, int M, int N, int K, int ones_col, int dtype);
 int cmx_gemm(const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R, const float* rscale, float* dbias, float* workspace, int G, int M, int N, int K, int K1, int64_t lda, int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias, int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode, int ones_col, int splitk, int dtype, hipStream_t stream);
+/* ---- independent GEMMs in ONE launch: Attention.q beside Attention.kv (dual_segformer.py:114-121, forward and
+ *      dgrad) and the decoder's linear_c1..c4 (MLPDecoder.py:66-73).  cmx_gemm_plan takes cmx_gemm's arguments
+ *      and fills a plan (host memory of cmx_gemm_plan_size() bytes) instead of launching: > 0 = block count,
+ *      0 = not eligible (16-bit 64 x 64-tile problems without split-K / bias-gradient column only; the caller
+ *      runs cmx_gemm), < 0 = invalid.  cmx_gemm_multi launches n <= 4 plans of one dtype and B layout. */
+size_t cmx_gemm_plan_size(void);
+int cmx_gemm_plan(void* plan, const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R, const float* rscale, float* dbias, float* workspace, int G, int M, int N, int K, int K1, int64_t lda, int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias, int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode, int ones_col, int splitk, int dtype);
+int cmx_gemm_multi(const void* plans, int n, hipStream_t stream);
 /* cmx_gemm_h2: cmx_gemm (no A2 / bias / residual / epilogue extras) over a two-level batch of G = Go * gh
  *      problems: problem g reads / writes at (g / gh) * sX + (g % gh) * sXh -- the per-head k^T v,
  *      u @ ctx and their backward products of the FFM cross attention (net_utils.py:206-212), one
@@ -222,6 +225,16 @@ int cmx_gemm_grouped(const void* recs, int nrec, int total_blocks, int dtype, hi
  *      grouped-GEMM record per tap whose B operand gathers x at that tap (dW row pitch KH*KW*C). */
 int cmx_conv_implicit_fwd(const void* x, const void* Wt, void* y, const float* bias, float* workspace, int G, int NIg, int H, int Wd, int C, int KH, int KW, int stride, int pad, int Ho, int Wo, int N, int64_t sx, int64_t sW, int64_t sy, int64_t sbias, int splitk, int dtype, hipStream_t stream);
 int cmx_gemm_group_pack_conv_wgrad(void* rec, const void* dy, const void* x, float* dW, float* dbias, float* workspace, int G, int NIg, int H, int Wd, int C, int KH, int KW, int stride, int pad, int Ho, int Wo, int N, int tap, int64_t sdy, int64_t sx, int64_t sdW, int64_t sdb, int splitk, int blk0);
+/* ---- stage-1 OverlapPatchEmbed.proj (Conv2d 3 -> N, k7 s4 p3, dual_segformer.py:196-197 / :219) straight from
+ *      the fp32 NCHW input batches, no im2col columns: img0 feeds group 0 (RGB), img1 group 1 (the X modality;
+ *      image_encoder forward, dual_segformer.py:347-350).  Wt = the 16-bit (G, N, Kp) weight shadow, columns in
+ *      the reference's (c, kh, kw) flatten order, Kp = 152 (147 zero-padded); y (G, B*Ho*Wo, N) NHWC 16-bit.
+ *      cmx_pe1_conv_wgrad writes one fp32 partial slab (N, Kp + 1) per workgroup into ws (G, nblk, N, Kp + 1),
+ *      nblk = cmx_pe1_conv_wgrad_nblk(B, Ho, Wo); column Kp is the bias gradient.  The caller sums the slabs
+ *      (cmx_reduce_pack with csplit = Kp). */
+int cmx_pe1_conv_fwd(const float* img0, const float* img1, const void* Wt, const float* bias, void* y, int G, int B, int C, int H, int W, int KH, int KW, int stride, int pad, int Ho, int Wo, int N, int Kp, int64_t sW, int64_t sbias, int64_t sy, int dtype, hipStream_t stream);
+int cmx_pe1_conv_wgrad_nblk(int B, int Ho, int Wo);
+int cmx_pe1_conv_wgrad(const void* dy, const float* img0, const float* img1, float* ws, int G, int B, int C, int H, int W, int KH, int KW, int stride, int pad, int Ho, int Wo, int N, int Kp, int64_t sdy, int dtype, hipStream_t stream);
 size_t cmx_reduce_record_size(void);
 int cmx_reduce_pack(void* rec, const float* src, float* dst, float* dst2, int G, int nblk, int64_t sg, int64_t sb, int rows, int cols, int csplit, int64_t dg, int ldd, int64_t dg2, int ldd2, int accumulate, int blk0);
 int cmx_reduce_grouped(const void* recs, int nrec, int total_blocks, hipStream_t stream);

@@ -127,6 +127,42 @@ __device__ __forceinline__ void store_vec(T* p, const float* in) {
   }
 }
 
+// ---------------------------------------------------------------- in-kernel partial folds
+// A kernel whose blocks each produce a partial result can fold the partials in the LAST block
+// to arrive instead of a second launch.  The 8 XCDs have separate L2s, so the partials are
+// written with agent-scope stores (global_store ... sc1: through to the device-coherent level)
+// and read back with agent-scope loads (sc1: not served from a stale L2 line); each block
+// drains its stores (s_waitcnt 0) before taking a ticket with a relaxed device atomic.  No
+// release / acquire fence: at agent scope those write back / invalidate the whole L2 per block
+// (AdamW measured 891 us with one per block).  The ticket counter is reset by the last block,
+// so a graph replay or the next launch finds it at zero; a ticket array is owned by one kernel
+// family and its launches are stream-ordered.
+__device__ __forceinline__ void st_agent(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_agent(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld_agent(const int* p) {
+  return __hip_atomic_load(const_cast<int*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// true in every thread of the block that arrives last of `total` blocks sharing `ticket`
+__device__ __forceinline__ bool last_arrival(unsigned* ticket, unsigned total) {
+  __shared__ int s_last;
+  __builtin_amdgcn_s_waitcnt(0);                // this thread's partial stores have completed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == total - 1;
+    if (prev == total - 1) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return s_last != 0;
+}
+
 // ---------------------------------------------------------------- reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -29,101 +29,95 @@ inline int row_lanes(int C, int V) {
 }
 
 // ------------------------------------------------------------------------ pooling (forward)
-// partial avg / max / argmax over a chunk of tokens of one (group, image): blockIdx = (chunk,
-// g*B + b).  16-B loads, rows spread over the block's row slots, the slots combined in LDS
-// (max ties -> the lowest token index, as a sequential scan).
-template <typename T, int TPR>
-__global__ __launch_bounds__(256) void pool_partial_kernel(const T* __restrict__ x, float* __restrict__ psum,
-                                                           float* __restrict__ pmax, int* __restrict__ pidx, int B,
-                                                           int N, int C, int chunk) {
-  constexpr int V = VecT<T>::N, RPB = 256 / TPR;
-  __shared__ float rs[RPB][MAXCH * TPR * V];
-  __shared__ float rm[RPB][MAXCH * TPR * V];
-  __shared__ int ri[RPB][MAXCH * TPR * V];
-  const int gb = blockIdx.y, c_ = blockIdx.x;
-  const int lane = threadIdx.x % TPR, slot = threadIdx.x / TPR;
-  const int nch = C / V;
-  const int n0 = c_ * chunk, n1 = min(N, n0 + chunk);
-  float sm[MAXCH][V], mx[MAXCH][V];
-  int ix[MAXCH][V];
+// ONE launch: block (z, cg, gb) reduces token chunk z of the 32-channel group cg of one (group,
+// image) gb to a partial [sum | max | argmax]; the last block of (cg, gb) to arrive folds the
+// nz partials into pooled / argmax (last_arrival, cmx_common.h).  Lanes per token row = 32 / V
+// (4 for 16-bit storage, 8 for fp32), one 16-B vector each; the row slots combine in LDS with
+// 8 threads per channel and a lane shuffle.  Max ties -> the lowest token index (the sequential
+// scan PyTorch's CPU max does), whatever order the slots / chunks combine in.
+constexpr int PG = 32;                          // channels per block
+constexpr int PZ_MAX = 32;                      // token chunks per (channel group, image): the fold
+                                                // reads PG * nz * 3 values, <= 12 per thread
+constexpr int POOL_TICKETS = 4096;
+__device__ unsigned g_pool_ticket[POOL_TICKETS];
+
+__device__ __forceinline__ void maxidx_merge(float& m, int& mi, float v, int i) {
+  if (v > m || (v == m && i < mi)) { m = v; mi = i; }
+}
+// combine (s, m, mi) over the 8 consecutive lanes of a channel, fixed order (deterministic)
+__device__ __forceinline__ void group8_merge(float& s, float& m, int& mi) {
 #pragma unroll
-  for (int k = 0; k < MAXCH; ++k)
-#pragma unroll
-    for (int j = 0; j < V; ++j) { sm[k][j] = 0.f; mx[k][j] = -INFINITY; ix[k][j] = 0x7fffffff; }
-  const T* base = x + (long)gb * N * C;
-#pragma unroll 2
-  for (int n = n0 + slot; n < n1; n += RPB) {
-#pragma unroll
-    for (int k = 0; k < MAXCH; ++k) {
-      const int ch = lane + k * TPR;
-      if (ch >= nch) continue;
-      float v[V];
-      load_vec<T>(base + (long)n * C + ch * V, v);
-#pragma unroll
-      for (int j = 0; j < V; ++j) {
-        sm[k][j] += v[j];
-        if (v[j] > mx[k][j]) { mx[k][j] = v[j]; ix[k][j] = n; }
-      }
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < MAXCH; ++k)
-#pragma unroll
-    for (int j = 0; j < V; ++j) {
-      const int c = (lane + k * TPR) * V + j;
-      if (c < C) { rs[slot][c] = sm[k][j]; rm[slot][c] = mx[k][j]; ri[slot][c] = ix[k][j]; }
-    }
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float s = 0.f, m = -INFINITY;
-    int mi = 0x7fffffff;
-    for (int q = 0; q < RPB; ++q) {
-      s += rs[q][c];
-      const float v = rm[q][c];
-      const int i = ri[q][c];
-      if (v > m || (v == m && i < mi)) { m = v; mi = i; }
-    }
-    const long o = ((long)gb * gridDim.x + c_) * C + c;
-    psum[o] = s; pmax[o] = m; pidx[o] = mi;
+  for (int o = 1; o < 8; o <<= 1) {
+    const float s2 = __shfl_xor(s, o, 64), m2 = __shfl_xor(m, o, 64);
+    const int i2 = __shfl_xor(mi, o, 64);
+    s += s2;
+    maxidx_merge(m, mi, m2, i2);
   }
 }
 
-// block = 16 channels x 16 chunk slices of one (group, image); the slices meet in LDS.  Max ties
-// resolve to the lowest token index, as the sequential scan over chunks would.  (A 64-channel x
-// 4-slice block walked its 128 chunk partials as a 32-step chain of dependent L2 loads: 12 us.)
-constexpr int PF_CH = 16, PF_SL = 16;
-__global__ __launch_bounds__(256) void pool_final_kernel(const float* __restrict__ psum, const float* __restrict__ pmax,
-                                                         const int* __restrict__ pidx, float* __restrict__ pooled,
-                                                         int* __restrict__ argmax, int B, int N, int C, int nchunk) {
-  __shared__ float rs[PF_SL][PF_CH], rm[PF_SL][PF_CH];
-  __shared__ int ri[PF_SL][PF_CH];
-  const int gb = blockIdx.y, cl = threadIdx.x % PF_CH, zl = threadIdx.x / PF_CH;
-  const int c = blockIdx.x * PF_CH + cl;
-  float sm = 0.f, m = -INFINITY;
-  int mi = 0x7fffffff;
-  if (c < C) {
+template <typename T>
+__global__ __launch_bounds__(256) void pool_kernel(const T* __restrict__ x, float* __restrict__ psum,
+                                                   float* __restrict__ pmax, int* __restrict__ pidx,
+                                                   float* __restrict__ pooled, int* __restrict__ argmax, int B,
+                                                   int N, int C, int chunk) {
+  constexpr int V = VecT<T>::N, LPR = PG / V, RPB = 256 / LPR;
+  __shared__ float rs[RPB][PG + 1], rm[RPB][PG + 1];
+  __shared__ int ri[RPB][PG + 1];
+  const int z = blockIdx.x, cg = blockIdx.y, gb = blockIdx.z, nz = gridDim.x, ng = gridDim.y;
+  const int lane = threadIdx.x % LPR, slot = threadIdx.x / LPR;
+  const int n0 = z * chunk, n1 = min(N, n0 + chunk);
+  float sm[V], mx[V];
+  int ix[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) { sm[j] = 0.f; mx[j] = -INFINITY; ix[j] = 0x7fffffff; }
+  const T* base = x + (long)gb * N * C + cg * PG + lane * V;
 #pragma unroll 4
-    for (int k = zl; k < nchunk; k += PF_SL) {
-      const long o = ((long)gb * nchunk + k) * C + c;
-      sm += psum[o];
-      const float v = pmax[o];
-      const int ix = pidx[o];
-      if (v > m || (v == m && ix < mi)) { m = v; mi = ix; }
+  for (int n = n0 + slot; n < n1; n += RPB) {
+    float v[V];
+    load_vec<T>(base + (long)n * C, v);
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      sm[j] += v[j];
+      if (v[j] > mx[j]) { mx[j] = v[j]; ix[j] = n; }
     }
   }
-  rs[zl][cl] = sm; rm[zl][cl] = m; ri[zl][cl] = mi;
+#pragma unroll
+  for (int j = 0; j < V; ++j) { rs[slot][lane * V + j] = sm[j]; rm[slot][lane * V + j] = mx[j]; ri[slot][lane * V + j] = ix[j]; }
   __syncthreads();
-  if (zl > 0 || c >= C) return;
-  for (int q = 1; q < PF_SL; ++q) {
-    sm += rs[q][cl];
-    const float v = rm[q][cl];
-    const int ix = ri[q][cl];
-    if (v > m || (v == m && ix < mi)) { m = v; mi = ix; }
+  // 8 threads per channel: slots q = k, k + 8, ... then the 8-lane merge
+  const int c = threadIdx.x >> 3, k = threadIdx.x & 7;
+  float s = 0.f, m = -INFINITY;
+  int mi = 0x7fffffff;
+  for (int q = k; q < RPB; q += 8) {
+    s += rs[q][c];
+    maxidx_merge(m, mi, rm[q][c], ri[q][c]);
   }
-  const int g = gb / B, b = gb % B;
-  pooled[(long)b * 4 * C + g * C + c] = sm / N;
-  pooled[(long)b * 4 * C + 2 * C + g * C + c] = m;
-  argmax[(long)b * 2 * C + g * C + c] = mi;
+  group8_merge(s, m, mi);
+  const long po = ((long)(gb * ng + cg) * nz + z) * PG + c;
+  if (k == 0) { st_agent(psum + po, s); st_agent(pmax + po, m); st_agent(pidx + po, mi); }
+  if (!last_arrival(&g_pool_ticket[gb * ng + cg], nz)) return;
+  // fold: channel c, chunks z = k, k + 8, k + 16, k + 24 (all loads issued before the merge)
+  const long pb = (long)(gb * ng + cg) * nz * PG + c;
+  float ls[PZ_MAX / 8], lm[PZ_MAX / 8];
+  int li[PZ_MAX / 8];
+#pragma unroll
+  for (int u = 0; u < PZ_MAX / 8; ++u) {
+    const int zz = k + 8 * u;
+    const bool ok = zz < nz;
+    ls[u] = ok ? ld_agent(psum + pb + (long)zz * PG) : 0.f;
+    lm[u] = ok ? ld_agent(pmax + pb + (long)zz * PG) : -INFINITY;
+    li[u] = ok ? ld_agent(pidx + pb + (long)zz * PG) : 0x7fffffff;
+  }
+  s = 0.f; m = -INFINITY; mi = 0x7fffffff;
+#pragma unroll
+  for (int u = 0; u < PZ_MAX / 8; ++u) { s += ls[u]; maxidx_merge(m, mi, lm[u], li[u]); }
+  group8_merge(s, m, mi);
+  if (k == 0) {
+    const int g = gb / B, b = gb % B, ch = cg * PG + c;
+    pooled[(long)b * 4 * C + g * C + ch] = s / N;
+    pooled[(long)b * 4 * C + 2 * C + g * C + ch] = m;
+    argmax[(long)b * 2 * C + g * C + ch] = mi;
+  }
 }
 
 // ------------------------------------------------------------------------ channel MLP
@@ -518,11 +512,14 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const float* __restrict__
   }
 }
 
-int pool_nchunk(int N, int GB) {
-  long nc = (512 + GB - 1) / GB;
-  const long maxc = (N + 15) / 16;
-  if (nc > maxc) nc = maxc;
-  return nc < 1 ? 1 : (int)nc;
+// token chunks per (channel group, image): ~1024 blocks in all, >= 16 tokens each, <= PZ_MAX
+int pool_nchunk(int N, int GB, int C) {
+  const long blocks_per_z = (long)GB * (C / PG);
+  long nz = (1024 + blocks_per_z - 1) / blocks_per_z;
+  const long maxz = (N + 15) / 16;
+  if (nz > maxz) nz = maxz;
+  if (nz > PZ_MAX) nz = PZ_MAX;
+  return nz < 1 ? 1 : (int)nz;
 }
 int combine_nblk(int N, int C, int V) {        // blocks per image of the backward (<= 256: its partials are
   const int rpb = 256 / row_lanes(C, V);       // summed by the channel-MLP backward's prologue)
@@ -550,27 +547,23 @@ unsigned rows_grid(long rows, int rpb) {
 extern "C" {
 
 size_t cmx_frm_pool_workspace(int B, int N, int C) {
-  const int nc = pool_nchunk(N, 2 * B);
-  return (size_t)2 * B * nc * C * 3 * sizeof(float);
+  const int nz = pool_nchunk(N, 2 * B, C > 0 ? C : PG);
+  return (size_t)2 * B * nz * (C > 0 ? C : 0) * 3 * sizeof(float);
 }
 
 int cmx_frm_pool_fwd(const void* x, float* pooled, int* argmax, float* workspace, int B, int N, int C, int dtype,
                      hipStream_t s) {
-  const int V = dtype == 0 ? 4 : 8;
-  CMX_REQUIRE(B > 0 && N > 0 && C > 0 && C % V == 0 && C / V <= MAXCH * 64, CMX_ERR_SHAPE, "frm_pool: B=%d N=%d C=%d",
-              B, N, C);
-  const int nc = pool_nchunk(N, 2 * B);
-  const int chunk = (N + nc - 1) / nc;
+  CMX_REQUIRE(B > 0 && N > 0 && C > 0 && C % PG == 0 && 2L * B * (C / PG) <= POOL_TICKETS, CMX_ERR_SHAPE,
+              "frm_pool: B=%d N=%d C=%d (C %% %d == 0)", B, N, C, PG);
+  const int nz = pool_nchunk(N, 2 * B, C);
+  const int chunk = (N + nz - 1) / nz;
   float* psum = workspace;
-  float* pmax = psum + (size_t)2 * B * nc * C;
-  int* pidx = (int*)(pmax + (size_t)2 * B * nc * C);
-  const int tpr = row_lanes(C, V);
+  float* pmax = psum + (size_t)2 * B * nz * C;
+  int* pidx = (int*)(pmax + (size_t)2 * B * nz * C);
   CMX_DISPATCH(dtype, T, {
-    FRM_TPR_DISPATCH(tpr, TPR, hipLaunchKernelGGL((pool_partial_kernel<T, TPR>), dim3(nc, 2 * B), dim3(256), 0, s,
-                                                  (const T*)x, psum, pmax, pidx, B, N, C, chunk));
+    hipLaunchKernelGGL(pool_kernel<T>, dim3(nz, C / PG, 2 * B), dim3(256), 0, s, (const T*)x, psum, pmax, pidx,
+                       pooled, argmax, B, N, C, chunk);
   });
-  hipLaunchKernelGGL(pool_final_kernel, dim3(cdiv(C, PF_CH), 2 * B), dim3(256), 0, s, psum, pmax, pidx, pooled,
-                     argmax, B, N, C, nc);
   return cmx_check_launch("frm_pool_fwd");
 }
 

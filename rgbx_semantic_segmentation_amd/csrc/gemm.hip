@@ -129,6 +129,12 @@ int cmx_gemm_splitk(int G, int M, int N, int K, int ones_col, int dtype) {
 }  // extern "C"
 
 namespace {
+// a planned problem for cmx_gemm_multi (host memory of cmx_gemm_plan_size() bytes)
+struct GemmPlan {
+  GemmArgs a;
+  int tA, tB, dtype, nblk, nk64, pad;
+};
+
 // upsample-add sources of the epilogue (nup = 0: none)
 struct UpSpec {
   const void* src[3];
@@ -140,7 +146,8 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
               int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias,
               int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode, int ones_col, int splitk,
               int dtype, hipStream_t s, const UpSpec* up, int scR = 0, int scH = 0, int scW = 0, int scC = 0,
-              int scHo = 0, int scWo = 0, int gh = 1, int64_t sAh = 0, int64_t sBh = 0, int64_t sCh = 0) {
+              int scHo = 0, int scWo = 0, int gh = 1, int64_t sAh = 0, int64_t sBh = 0, int64_t sCh = 0,
+              GemmPlan* plan = nullptr) {
   CMX_REQUIRE(G > 0 && M > 0 && N > 0 && K > 0, CMX_ERR_SHAPE, "gemm: empty problem G=%d M=%d N=%d K=%d", G, M, N, K);
   CMX_REQUIRE(dtype >= 0 && dtype <= 2, CMX_ERR_DTYPE, "gemm: unsupported dtype %d", dtype);
   CMX_REQUIRE(out_mode >= 0 && out_mode <= 2 && act >= 0 && act <= 3, CMX_ERR_ARG, "gemm: out_mode/act");
@@ -198,6 +205,20 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
   a.kt_per_split = (nk + splitk - 1) / splitk;
   splitk = (nk + a.kt_per_split - 1) / a.kt_per_split;      // no empty splits
   a.nsplit = splitk;
+  if (plan) {
+    // planning only (cmx_gemm_plan): eligible for a multi launch = the 16-bit path on 64 x 64
+    // tiles, no split-K, no bias-gradient column / upsample / scatter / two-level batch
+    if (!fast || splitk != 1 || ones_col || a.nup || a.scatter || gh != 1 || transA) return 0;
+    int bm, bn;
+    plan_tiles(G, M, nb, K, &bm, &bn);
+    if (bm != 64 || bn != 64) return 0;
+    a.tiles_m = cdiv(M, 64); a.tiles_n = cdiv(nb, 64);
+    memset(plan, 0, sizeof(*plan));
+    plan->a = a; plan->tA = transA; plan->tB = transB; plan->dtype = dtype;
+    plan->nblk = a.tiles_m * a.tiles_n * G;
+    plan->nk64 = (K + FBK - 1) / FBK;
+    return plan->nblk;
+  }
   if (fast) {
     int bm, bn;
     plan_tiles(G, M, nb, K, &bm, &bn);
@@ -243,6 +264,60 @@ int cmx_gemm(const void* A, const void* A2, const void* B, void* C, const float*
              int dtype, hipStream_t s) {
   return gemm_impl(A, A2, B, C, bias, R, rscale, dbias, workspace, G, M, N, K, K1, lda, lda2, ldb, ldc, sA, sA2, sB,
                    sC, sbias, sdb, rows_per_sample, transA, transB, act, out_mode, ones_col, splitk, dtype, s, nullptr);
+}
+
+size_t cmx_gemm_plan_size(void) { return sizeof(GemmPlan); }
+
+// cmx_gemm's arguments, planned instead of launched: > 0 = the problem's block count (eligible
+// for cmx_gemm_multi), 0 = not eligible (run it with cmx_gemm), < 0 = invalid arguments
+int cmx_gemm_plan(void* plan, const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R,
+                  const float* rscale, float* dbias, float* workspace, int G, int M, int N, int K, int K1, int64_t lda,
+                  int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC,
+                  int64_t sbias, int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode,
+                  int ones_col, int splitk, int dtype) {
+  CMX_REQUIRE(plan, CMX_ERR_ARG, "gemm_plan: null plan");
+  return gemm_impl(A, A2, B, C, bias, R, rscale, dbias, workspace, G, M, N, K, K1, lda, lda2, ldb, ldc, sA, sA2, sB,
+                   sC, sbias, sdb, rows_per_sample, transA, transB, act, out_mode, ones_col, splitk, dtype, nullptr,
+                   nullptr, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, reinterpret_cast<GemmPlan*>(plan));
+}
+
+// n <= 4 planned problems (same dtype and B layout) in ONE launch; waves / ring depth chosen for
+// the combined grid as a single problem's launch would be (launch_bf16_ns)
+int cmx_gemm_multi(const void* plans, int n, hipStream_t s) {
+  CMX_REQUIRE(plans && n >= 1 && n <= MULTI_MAX, CMX_ERR_ARG, "gemm_multi: 1..%d problems (got %d)", MULTI_MAX, n);
+  const GemmPlan* pl = reinterpret_cast<const GemmPlan*>(plans);
+  GemmMulti m{};
+  m.n = n;
+  int total = 0, nk64 = 1 << 30;
+  for (int i = 0; i < n; ++i) {
+    CMX_REQUIRE(pl[i].nblk > 0 && pl[i].tA == 0 && pl[i].tB == pl[0].tB && pl[i].dtype == pl[0].dtype &&
+                (pl[i].dtype == 1 || pl[i].dtype == 2), CMX_ERR_ARG, "gemm_multi: plan %d does not match plan 0", i);
+    m.a[i] = pl[i].a;
+    m.blk0[i] = total;
+    total += pl[i].nblk;
+    nk64 = nk64 < pl[i].nk64 ? nk64 : pl[i].nk64;
+  }
+  m.blk0[n] = total;
+  for (int i = n + 1; i <= MULTI_MAX; ++i) m.blk0[i] = total;
+  static int& kwk = cmx_knob("GEMM_KW", 2);
+  const bool kw2 = kwk >= 2 && total <= 512 && nk64 >= 4;
+  if (kw2)
+    for (int i = 0; i < n; ++i) m.a[i].kt_per_split = (m.a[i].K + 2 * FBK - 1) / (2 * FBK);
+  const bool ns4 = total <= 256;
+  const bool tB = pl[0].tB != 0, h = pl[0].dtype == 2;
+#define CMX_MULTI(NS_, KW_, TB_, E_) \
+  hipLaunchKernelGGL((gemm_multi_kernel<NS_, KW_, TB_, E_>), dim3(total), dim3(256 * KW_), 0, s, m)
+#define CMX_MULTI_E(NS_, KW_, TB_) \
+  do { if (h) CMX_MULTI(NS_, KW_, TB_, f16); else CMX_MULTI(NS_, KW_, TB_, bf16); } while (0)
+#define CMX_MULTI_TB(NS_, KW_) do { if (tB) CMX_MULTI_E(NS_, KW_, true); else CMX_MULTI_E(NS_, KW_, false); } while (0)
+  if (kw2 && ns4) CMX_MULTI_TB(4, 2);
+  else if (kw2) CMX_MULTI_TB(2, 2);
+  else if (ns4) CMX_MULTI_TB(4, 1);
+  else CMX_MULTI_TB(2, 1);
+#undef CMX_MULTI_TB
+#undef CMX_MULTI_E
+#undef CMX_MULTI
+  return cmx_check_launch("gemm_multi");
 }
 
 // dx of a non-overlapping patchify conv (stride == kernel == R, pad 0: Attention.sr,

@@ -534,6 +534,30 @@ void gemm_bf16_kernel(const GemmArgs p) {
   gemm_bf16_body<BM, BN, TA, TB, NS, KW, E>(p, xcd_tile(blockIdx.x, p.tiles_m * p.tiles_n * p.G * p.nsplit), smem);
 }
 
+// ============================================================================ multi launch
+// Up to four independent forward / dgrad problems (64 x 64 tiles, no split-K, same B layout) in
+// ONE grid, records passed by value: e.g. Attention.q beside Attention.kv (dual_segformer.py:
+// 114-121; both read norm1's output or its spatial reduction) and the decoder's four
+// linear_c* projections (MLPDecoder.py:66-73).  Block b runs problem i with blk0[i] <= b.
+constexpr int MULTI_MAX = 4;
+struct GemmMulti {
+  GemmArgs a[MULTI_MAX];
+  int blk0[MULTI_MAX + 1];
+  int n;
+};
+
+template <int NS, int KW, bool TB, typename E>
+__global__ __launch_bounds__(256 * KW, (NS == 2 && KW == 1) ? 5 : 2) void gemm_multi_kernel(const GemmMulti m) {
+  __shared__ __attribute__((aligned(1024))) char smem[gemm_smem_bytes<64, 64, NS, KW>()];
+  const int b = blockIdx.x;
+  int i = 0;
+#pragma unroll
+  for (int j = 1; j < MULTI_MAX; ++j)
+    if (j < m.n && b >= m.blk0[j]) i = j;
+  const int nb = m.blk0[i + 1] - m.blk0[i];
+  gemm_bf16_body<64, 64, false, TB, NS, KW, E>(m.a[i], xcd_tile(b - m.blk0[i], nb), smem);
+}
+
 // ============================================================================ grouped launch
 // Many independent problems in ONE launch (the weight gradients of a whole backward segment,
 // which nothing reads before the optimizer): record r owns blocks [blk0, blk0 + nblk) of the

@@ -960,8 +960,9 @@ int pick_qw(int N, int heads, int Bt) {
 // workgroups at stage 2 (152 -> 304) were slower, 13.8 -> 16.4 us forward).  Every workgroup
 // stages the (b, head)'s K / V (L2-resident after the first): only L2 -> LDS traffic.
 int pick_nw(int N, int heads, int Bt, int qw) {
-  static int& force = cmx_knob("SRA_NW", 0);     // 2 / 4 / 8 waves per workgroup (A/B), 0 = auto
+  static int& force = cmx_knob("SRA_NW", 0);     // 2 / 4 / 8 / 10 waves per workgroup (A/B), 0 = auto
   if (force == 2 || force == 4 || force == 8) return qw == 2 && force == 2 ? 4 : force;
+  if (force == 10 && qw == 1) return 10;
   if (qw == 2 || (long)cdiv(N, 32 * NWAVE) * heads * Bt >= 128) return NWAVE;
   return 2;
 }
@@ -1000,6 +1001,7 @@ void sra_fwd_fast_launch_t(const void* q, const void* k, const void* v, void* o,
                      (const E*)v, (E*)o, lse, N, Nk, nkp, heads, qs, kvs, os, sl2)
   if (qw == 2 && nw == 4) CMX_SRA_FWD(2, 4);
   else if (qw == 2) CMX_SRA_FWD(2, 8);
+  else if (nw == 10) CMX_SRA_FWD(1, 10);
   else if (nw == 8) CMX_SRA_FWD(1, 8);
   else if (nw == 4) CMX_SRA_FWD(1, 4);
   else if (nw == 2) CMX_SRA_FWD(1, 2);
@@ -1021,6 +1023,7 @@ void sra_dq_fast_launch_t(const void* q, const void* k, const void* v, const voi
                      kvs, os, dos, dqs, sl2, scale)
   if (qw == 2 && nw == 4) CMX_SRA_DQ(2, 4);
   else if (qw == 2) CMX_SRA_DQ(2, 8);
+  else if (nw == 10) CMX_SRA_DQ(1, 10);
   else if (nw == 8) CMX_SRA_DQ(1, 8);
   else if (nw == 4) CMX_SRA_DQ(1, 4);
   else if (nw == 2) CMX_SRA_DQ(1, 2);

@@ -65,11 +65,13 @@ def step_work(backbone="mit_b2", H=480, W=640, B=2, K=40, E=512, n_params=None):
         N, C = h * w, dims[s]
         M = B * N
         grids.append((h, w, C))
-        # patch embed: stage 1 im2col (fp32 NCHW image -> 16-bit columns) + GEMM; 3x3 s2 implicit conv
+        # patch embed: stage 1 direct conv on the fp32 NCHW images (fwd; wgrad re-reads the
+        # images and dy, one (C, Kp + 1) fp32 result); 3x3 s2 implicit conv
         if s == 0:
             Kp = (cin * k * k + 7) // 8 * 8
-            add("im2col", 0, G * (F32 * B * cin * H * W + A * M * Kp))
-            gemm(M, C, Kp, G, dgrad=False)
+            img = F32 * B * cin * H * W
+            add("pe1", 2 * G * M * C * cin * k * k, G * (img + A * C * Kp + A * M * C))
+            add("pe1", 2 * G * M * C * cin * k * k, G * (img + A * M * C + F32 * C * (Kp + 1)))
         else:
             gemm(M, C, cin * k * k, G)
             add("im2col", 0, G * A * M * cin * k * k * 2)                             # col2im of the dgrad columns

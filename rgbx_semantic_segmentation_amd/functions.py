@@ -107,6 +107,85 @@ def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1
     return GLinear.apply(W, Wg, b, bg, wp, act, res, rscale, rps, x1, x2, tap)
 
 
+# CMX_MULTI_GEMM=0 launches the grouped Linears of GLinearMulti one by one (A/B switch)
+MULTI_GEMM = os.environ.get("CMX_MULTI_GEMM", "1") != "0"
+
+
+def _gemm_group(jobs):
+    """Run independent K.gemm problems (kwargs dicts): the ones eligible for a multi launch
+    (16-bit, 64 x 64 tiles, no split-K) as ONE cmx_gemm_multi grid, the rest one by one."""
+    rest = jobs
+    if MULTI_GEMM and len(jobs) > 1:
+        plans = [K.gemm(**j, plan=True) for j in jobs]
+        ok = [p for p in plans if p is not None]
+        if len(ok) > 1:
+            for i in range(0, len(ok), 4):
+                if len(ok[i:i + 4]) > 1:
+                    K.gemm_multi(ok[i:i + 4])
+                else:
+                    K.gemm(**jobs[plans.index(ok[i])])
+            rest = [j for j, p in zip(jobs, plans) if p is None]
+    for j in rest:
+        K.gemm(**j)
+
+
+class GLinearMulti(Function):
+    """Independent Linears y_i = x_i W_i^T + b_i (G groups each) whose forward GEMMs run as ONE
+    multi launch and whose input gradients as another: Attention.q beside Attention.kv
+    (dual_segformer.py:114-121, both reading norm1's output or its spatial reduction) and the
+    decoder's linear_c1..c4 (MLPDecoder.py:66-73).  Weight gradients are queued as GLinear's."""
+
+    @staticmethod
+    def forward(ctx, spec, *ts):
+        n = len(spec)
+        xs = ts[n:]
+        ys, jobs = [], []
+        for (W, Wg, b, bg), x in zip(spec, xs):
+            y = torch.empty(W.shape[0], x.shape[1], W.shape[1], dtype=x.dtype, device=x.device)
+            jobs.append(dict(A=x, B=W, C=y, bias=b))
+            ys.append(y)
+        _gemm_group(jobs)
+        ctx.spec = spec
+        ctx.save_for_backward(*xs)
+        return tuple(ys)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        xs = ctx.saved_tensors
+        spec = ctx.spec
+        n = len(spec)
+        dxs, jobs = [None] * n, []
+        for i, ((W, Wg, b, bg), x, dy) in enumerate(zip(spec, xs, dys)):
+            if dy is None:
+                continue
+            dy = _c(dy)
+            if ctx.needs_input_grad[1 + n + i]:
+                dxs[i] = torch.empty_like(x)
+                jobs.append(dict(A=dy, B=W.transpose(1, 2), C=dxs[i]))
+            _wgrad_into(dy, x, Wg, bg)
+        _gemm_group(jobs)
+        return (None,) * (1 + n) + tuple(dxs)
+
+
+def glinear_multi(store, specs):
+    """[(weight param, bias param or None, x (G, M_i, K_i))] -> the Linears' outputs (G, M_i, N_i),
+    forward and input gradients each as one multi launch (GLinearMulti)."""
+    spec, anchors, xs = [], [], []
+    for wp, bp, x in specs:
+        W = store.w(wp)
+        G = W.shape[0]
+        W = W.view(G, W.shape[1], -1)
+        Wg = store.g(wp).view(G, W.shape[1], -1)
+        b = bg = None
+        if bp is not None:
+            b = store.w(bp, compute=False).view(G, -1)
+            bg = store.g(bp).view(G, -1)
+        spec.append((W, Wg, b, bg))
+        anchors.append(wp)
+        xs.append(x)
+    return GLinearMulti.apply(tuple(spec), *anchors, *xs)
+
+
 # ---------------------------------------------------------------------------- LayerNorm
 class GradTap:
     """Side channel from a norm's backward to the backward of the residual-branch GEMM that
@@ -522,8 +601,14 @@ def dwconv(store, conv, h, NI, ipg, H, W, act):
 # ---------------------------------------------------------------------------- conv (implicit GEMM / im2col + GEMM)
 # CMX_IMPLICIT_CONV=0 restores the materialised-im2col forward (A/B switch for measurements)
 IMPLICIT_CONV = os.environ.get("CMX_IMPLICIT_CONV", "1") != "0"
+# CMX_PE1_DIRECT=0 restores the stage-1 im2col + GEMM path (A/B switch for measurements)
+PE1_DIRECT = os.environ.get("CMX_PE1_DIRECT", "1") != "0"
+
+
 class ConvF(Function):
-    """Conv2d as im2col + grouped GEMM on NHWC (OverlapPatchEmbed.proj, Attention.sr)."""
+    """Conv2d on NHWC (OverlapPatchEmbed.proj, Attention.sr; dual_segformer.py:196-197, :95-96):
+    implicit GEMM (16-bit, C % 64 == 0), the direct stage-1 conv on the fp32 NCHW images
+    (patch_embed1.hip), else im2col + grouped GEMM."""
 
     @staticmethod
     def forward(ctx, x, W, Wg, b, bg, geom, anchor, x2=None):
@@ -531,6 +616,7 @@ class ConvF(Function):
         # of an NCHW input given as two tensors (x holds the first NI - len(x2) images)
         G, NI, H, Wd, C, KH, KW, st, pad, Ho, Wo, nchw = geom
         ctx.x2 = x2
+        ctx.pe1 = None
         Kp = W.shape[-1]
         if IMPLICIT_CONV and not nchw and x.dtype in (torch.bfloat16, torch.float16) and C % 64 == 0 \
                 and x.is_contiguous():
@@ -551,6 +637,20 @@ class ConvF(Function):
             ctx.implicit = True
             return y
         ctx.implicit = False
+        if nchw and PE1_DIRECT and W.dtype in (torch.bfloat16, torch.float16) and deferred.ENABLED \
+                and b is not None and (C, KH, KW, st, pad) == (3, 7, 7, 4, 3) and W.shape[1] <= 64 \
+                and W.shape[1] % 8 == 0 and x.dtype == torch.float32 and x.is_contiguous() \
+                and (x2 is None or x2.is_contiguous()):
+            # stage 1: direct conv on the fp32 NCHW batches, no im2col columns (patch_embed1.hip)
+            Bg, N = NI // G, W.shape[1]
+            img1 = (x2 if x2 is not None else x[Bg:]) if G == 2 else None
+            y = torch.empty(G, Bg * Ho * Wo, N, dtype=W.dtype, device=W.device)
+            K.call("cmx_pe1_conv_fwd", K.ptr(x), K.ptr(img1), K.ptr(W), K.ptr(b), K.ptr(y), G, Bg, C, H, Wd, KH, KW,
+                   st, pad, Ho, Wo, N, Kp, W.stride(0), b.stride(0), y.stride(0), K.dtype_code(W), K.stream())
+            ctx.pe1 = (x, img1)
+            ctx.save_for_backward(None, W)
+            ctx.meta = (Wg, bg, geom)
+            return y
         cols = torch.empty(G, NI // G * Ho * Wo, Kp, dtype=W.dtype, device=W.device)
         if nchw:
             x2 = getattr(ctx, "x2", None)
@@ -575,6 +675,17 @@ class ConvF(Function):
         Wg, bg, geom = ctx.meta
         G, NI, H, Wd, C, KH, KW, st, pad, Ho, Wo, nchw = geom
         dy = _c(dy)
+        if ctx.pe1 is not None:
+            # per-workgroup (N, Kp + 1) partial slabs [dW | db], summed by the deferred grouped reduce
+            img0, img1 = ctx.pe1
+            Bg, N, Kp = NI // G, W.shape[1], W.shape[-1]
+            nblk = K.query("cmx_pe1_conv_wgrad_nblk", Bg, Ho, Wo)
+            ws = torch.empty(G, nblk, N, Kp + 1, dtype=torch.float32, device=dy.device)
+            K.call("cmx_pe1_conv_wgrad", K.ptr(dy), K.ptr(img0), K.ptr(img1), K.ptr(ws), G, Bg, C, H, Wd, KH, KW, st,
+                   pad, Ho, Wo, N, Kp, dy.stride(0), K.dtype_code(dy), K.stream())
+            deferred.reduce(ws, Wg, bg, G, nblk, nblk * N * (Kp + 1), N * (Kp + 1), N, Kp + 1, Kp, Wg.stride(0),
+                            Wg.stride(1), bg.stride(0), 1)
+            return None, None, None, None, None, None, None, None
         if ctx.implicit:
             x = cols                 # the conv input (no cols were materialised)
             if not deferred.conv_wgrad(dy, x, Wg, bg, (G, NI // G, H, Wd, C, KH, KW, st, pad, Ho, Wo)):
@@ -809,27 +920,20 @@ def pair_embed(store, ce, o):
 
 
 # ---------------------------------------------------------------------------- FRM
-# CMX_FRM_CHANNEL=1: ChannelWeights as the one-launch grid-barrier kernels (cmx_frm_channel_*).
-# Off by default: inside the step they cost 80-190 us per launch (r03_h census: 1.0 ms per step
-# for the eight launches, against ~0.3 ms for the multi-launch path) -- a grid barrier needs
-# every one of its 256 blocks resident, and beside the FFM side stream's kernels the resident
-# blocks spin until the rest get a CU.
-FRM_ONE_LAUNCH = os.environ.get("CMX_FRM_CHANNEL", "0") == "1"
-
-
 class FRMF(Function):
     """FeatureRectifyModule (net_utils.py:124-152) on x (2, B, N, C).
 
-    Forward (6 launches): avg || max pooling (partial + final), the two-layer channel MLP
-    (ChannelWeights, :16-30), the SpatialWeights 2C -> C 1x1 conv as a cat-free GEMM, and ONE
-    kernel for SpatialWeights' C -> 2 conv + sigmoid fused with the rectification.
-    Backward (7 launches): one kernel for the rectification + spatial-head backward (dx direct
+    Forward (5 launches): avg || max pooling as ONE launch (per-chunk partials folded by the
+    last block to arrive, frm.hip pool_kernel), the two-layer channel MLP (ChannelWeights,
+    :16-30), the SpatialWeights 2C -> C 1x1 conv as a cat-free GEMM, and ONE kernel for
+    SpatialWeights' C -> 2 conv + sigmoid fused with the rectification.
+    Backward (5-6 launches): one kernel for the rectification + spatial-head backward (dx direct
     path, dh, dcw / dw2 partials), one G = 2 dgrad GEMM adding both modality slices of the 2C -> C
-    conv into dx, the dcw partial sum, the channel MLP backward as one pass over each weight
-    matrix (dz formed from the producer's partial slices, dW / db written, dx left as partial
-    slices), and the pooling backward summing those slices itself.
-    With CMX_FRM_CHANNEL=1 the channel branch is ONE grid-barrier kernel per direction
-    (cmx_frm_channel_fwd / _bwd) instead."""
+    conv into dx, the channel MLP backward as one pass over each weight matrix (dz formed from
+    the producer's partial slabs, dW / db written, dx left as partial slices; a separate dcw
+    partial sum only where the slabs are too many to re-read per block), and the pooling
+    backward summing those slices itself.
+"""
 
     @staticmethod
     def forward(ctx, x, prm, anchor):
@@ -841,16 +945,10 @@ class FRMF(Function):
         y1 = torch.empty(B, 4 * C, dtype=torch.float32, device=x.device)
         cw = torch.empty(B, 2 * C, dtype=torch.float32, device=x.device)
         # ChannelWeights (net_utils.py:11-30): avg || max pool + both MLP GEMVs
-        if FRM_ONE_LAUNCH:
-            ws = K._ws(K.query("cmx_frm_channel_fwd_workspace", B, N, C), x.device)
-            K.call("cmx_frm_channel_fwd", K.ptr(x), K.ptr(W1), K.ptr(b1), K.ptr(W2), K.ptr(b2), K.ptr(pooled),
-                   K.ptr(argmax), K.ptr(y1), K.ptr(cw), K.ptr(ws), B, N, C, dt, K.stream())
-        else:
-            ws = K._ws(K.query("cmx_frm_pool_workspace", B, N, C), x.device)
-            K.call("cmx_frm_pool_fwd", K.ptr(x), K.ptr(pooled), K.ptr(argmax), K.ptr(ws), B, N, C, dt, K.stream())
-            K.call("cmx_small_linear_fwd", K.ptr(pooled), K.ptr(W1), K.ptr(b1), K.ptr(y1), B, 4 * C, 4 * C, 2,
-                   K.stream())
-            K.call("cmx_small_linear_fwd", K.ptr(y1), K.ptr(W2), K.ptr(b2), K.ptr(cw), B, 4 * C, 2 * C, 3, K.stream())
+        ws = K._ws(K.query("cmx_frm_pool_workspace", B, N, C), x.device)
+        K.call("cmx_frm_pool_fwd", K.ptr(x), K.ptr(pooled), K.ptr(argmax), K.ptr(ws), B, N, C, dt, K.stream())
+        K.call("cmx_small_linear_fwd", K.ptr(pooled), K.ptr(W1), K.ptr(b1), K.ptr(y1), B, 4 * C, 4 * C, 2, K.stream())
+        K.call("cmx_small_linear_fwd", K.ptr(y1), K.ptr(W2), K.ptr(b2), K.ptr(cw), B, 4 * C, 2 * C, 3, K.stream())
         # h = cat(x1, x2) W0^T + b0 (SpatialWeights' first 1x1 conv, net_utils.py:72-73), cat-free
         h = torch.empty(1, B * N, C, dtype=x.dtype, device=x.device)
         K.gemm(x[0].view(1, B * N, C), W0[None], h, bias=b0[None], A2=x[1].view(1, B * N, C))
@@ -891,20 +989,18 @@ class FRMF(Function):
         K.gemm(dh[None].expand(2, B * N, C), Wd.transpose(1, 2), dx2, residual=dx2)
         _wgrad_into(dh[None], x[0].view(1, B * N, C), gW0[None, :, :C], gb0.view(1, C))
         _wgrad_into(dh[None], x[1].view(1, B * N, C), gW0[None, :, C:])
-        if FRM_ONE_LAUNCH:
-            # channel MLP + pooling backward in one launch: dcw partial slabs (B, nb, 2C) -> W2 pass ->
-            # W1 pass -> pooling gradient added into dx
-            cws = K._ws(K.query("cmx_frm_channel_bwd_workspace", B, C), x.device)
-            K.call("cmx_frm_channel_bwd", K.ptr(ws), nb, K.ptr(cw), K.ptr(y1), K.ptr(pooled), K.ptr(argmax),
-                   K.ptr(W1), K.ptr(W2), K.ptr(gW1), K.ptr(gb1), K.ptr(gW2), K.ptr(gb2), K.ptr(dx), K.ptr(cws), B, N,
-                   C, dt, K.stream())
-            return dx, None, None
-        # channel MLP backward: dcw partial slabs (B, nb, 2C) -> W2 pass -> W1 pass -> pooling
+        # channel MLP backward: dcw partial slabs (B, nb, 2C) -> W2 pass -> W1 pass -> pooling.  When
+        # a W2-pass block's share of the slabs is small (B * 2C/16 values x nb slabs <= 8192: stages
+        # 1-2) it sums them itself (slab q of image m at ws[q*2C + m*nb*2C]); otherwise every one
+        # of its column blocks would re-read them and one partial-sum launch is cheaper
         ns = K.query("cmx_small_linear_nslice")
-        dcw = torch.empty(B, 2 * C, dtype=torch.float32, device=x.device)      # sum of the nb partial slabs
-        K.call("cmx_partials_sum", K.ptr(ws), K.ptr(dcw), B, nb, 2 * C, 0, 1.0, K.stream())
         dy1p = torch.empty(ns, B, 4 * C, dtype=torch.float32, device=x.device)
-        K.call("cmx_small_linear_bwd", K.ptr(dcw), 1, 0, 2 * C, K.ptr(cw), K.ptr(y1), K.ptr(W2), K.ptr(dy1p),
+        if B * -(-2 * C // ns) * nb <= 8192:
+            dcw, nsl, ss, sm = ws, nb, 2 * C, nb * 2 * C
+        else:
+            dcw, nsl, ss, sm = torch.empty(B, 2 * C, dtype=torch.float32, device=x.device), 1, 0, 2 * C
+            K.call("cmx_partials_sum", K.ptr(ws), K.ptr(dcw), B, nb, 2 * C, 0, 1.0, K.stream())
+        K.call("cmx_small_linear_bwd", K.ptr(dcw), nsl, ss, sm, K.ptr(cw), K.ptr(y1), K.ptr(W2), K.ptr(dy1p),
                K.ptr(gW2), K.ptr(gb2), B, 4 * C, 2 * C, 3, 0, K.stream())
         dpp = torch.empty(ns, B, 4 * C, dtype=torch.float32, device=x.device)
         K.call("cmx_small_linear_bwd", K.ptr(dy1p), ns, B * 4 * C, 4 * C, K.ptr(y1), K.ptr(pooled), K.ptr(W1),

@@ -6,6 +6,7 @@ Activations are token-major and contiguous unless a stride argument says otherwi
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import torch
 
@@ -121,7 +122,7 @@ def _operand(t: torch.Tensor, name: str):
 def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, bias: torch.Tensor | None = None,
          residual: torch.Tensor | None = None, rscale: torch.Tensor | None = None, rows_per_sample: int = 1,
          act: str = "none", out_mode: int = 0, A2: torch.Tensor | None = None, dbias: torch.Tensor | None = None,
-         splitk: int = 0) -> torch.Tensor:
+         splitk: int = 0, plan: bool = False):
     """C[g] = epi([A[g] | A2[g]] @ B[g]^T) on logical views A (G, M, K1), A2 (G, M, K-K1),
     B (G, N, K), C (G, M, N).
 
@@ -131,7 +132,9 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, bias: torch.Tensor |
     residual has C's layout: C = residual + rscale[(g*M + i) // rows_per_sample] * act(acc + bias).
     dbias (G, M) fp32: also produce sum_k A(i, k) (the bias gradient of a wgrad).
     splitk > 1 splits K over blocks into fp32 slabs reduced with the epilogue applied;
-    0 = the library's choice (cmx_gemm_splitk: fill the chip when the output has few tiles)."""
+    0 = the library's choice (cmx_gemm_splitk: fill the chip when the output has few tiles).
+    plan=True: nothing is launched; returns a GemmPlan for gemm_multi, or None when the problem
+    is not eligible for a multi launch (the caller then runs gemm as usual)."""
     G, M, K1 = A.shape
     Kd = K1 + (A2.shape[2] if A2 is not None else 0)
     N = B.shape[1]
@@ -154,11 +157,40 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, bias: torch.Tensor |
     Nk = N + (1 if dbias is not None else 0)
     if splitk <= 0:
         splitk = query("cmx_gemm_splitk", G, M, Nk, Kd, int(dbias is not None), dtype_code(A))
+    args = (G, M, Nk, Kd, K1, lda, lda2, ldb, C.stride(1), sA, sA2, sB, C.stride(0), sbias, sdb, int(rows_per_sample),
+            tA, tB, ACT[act], int(out_mode), int(dbias is not None), int(splitk), dtype_code(A))
+    if plan:
+        if splitk > 1:
+            return None
+        rec = (ctypes.c_uint8 * _PLAN_BYTES)()
+        nb = query("cmx_gemm_plan", ctypes.addressof(rec), ptr(A), ptr(A2), ptr(B), ptr(C), ptr(bias), ptr(residual),
+                   ptr(rscale), ptr(dbias), 0, *args)
+        if nb < 0:
+            raise _lib.CMXError(f"cmx_gemm_plan failed ({nb}): {_lib.last_error()}")
+        return GemmPlan(rec, (A, A2, B, C, bias, residual, rscale)) if nb > 0 else None
     ws = _ws(query("cmx_gemm_workspace", G, M, Nk, splitk), A.device) if splitk > 1 else None
     call("cmx_gemm", ptr(A), ptr(A2), ptr(B), ptr(C), ptr(bias), ptr(residual), ptr(rscale), ptr(dbias), ptr(ws),
-         G, M, Nk, Kd, K1, lda, lda2, ldb, C.stride(1), sA, sA2, sB, C.stride(0), sbias, sdb, int(rows_per_sample),
-         tA, tB, ACT[act], int(out_mode), int(dbias is not None), int(splitk), dtype_code(A), stream())
+         *args, stream())
     return C
+
+
+_PLAN_BYTES = query("cmx_gemm_plan_size")
+
+
+class GemmPlan:
+    """A planned 64 x 64-tile GEMM (cmx_gemm_plan) and the tensors it reads / writes."""
+
+    def __init__(self, rec, keep):
+        self.rec, self.keep = rec, keep
+
+
+def gemm_multi(plans) -> None:
+    """Launch up to four planned GEMMs (same dtype and B layout) as ONE grid (cmx_gemm_multi)."""
+    n = len(plans)
+    buf = (ctypes.c_uint8 * (_PLAN_BYTES * n))()
+    for i, p in enumerate(plans):
+        ctypes.memmove(ctypes.addressof(buf) + i * _PLAN_BYTES, p.rec, _PLAN_BYTES)
+    call("cmx_gemm_multi", ctypes.addressof(buf), n, stream())
 
 
 def gemm_h2(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, out_mode: int = 0, splitk: int = 0) -> torch.Tensor:

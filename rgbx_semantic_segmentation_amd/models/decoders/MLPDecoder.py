@@ -1,6 +1,6 @@
 """SegFormer all-MLP decode head (reference: models/decoders/MLPDecoder.py:8-81).
 
-Execution on tokens: linear_c{1..4} GEMMs; the upsample + concat + linear_fuse 1x1 conv as
+Execution on tokens: linear_c{1..4} GEMMs (one multi launch, functions.GLinearMulti); the upsample + concat + linear_fuse 1x1 conv as
 functions.DecoderFuseF (the conv applied to each branch at its own resolution and the
 bilinear upsample added in the c1 GEMM's epilogue: the (B, N1, 4E) concat is never formed);
 BatchNorm (SyncBN across ranks when a process group is given) + ReLU + Dropout2d fused into
@@ -40,10 +40,10 @@ class DecoderHead(nn.Module):
     def run(self, store, feats, grids, B, training, dscale=None, group=None):
         E = self.embed_dim
         lin = (self.linear_c1, self.linear_c2, self.linear_c3, self.linear_c4)
-        proj = []
-        for i in range(4):
-            t = F.glinear(store, lin[i].proj.weight, lin[i].proj.bias, feats[i].view(1, -1, feats[i].shape[-1]))
-            proj.append(t.view(B, -1, E))
+        # the four projections as ONE GEMM launch (and their input gradients as another)
+        outs = F.glinear_multi(store, [(lin[i].proj.weight, lin[i].proj.bias, feats[i].view(1, -1, feats[i].shape[-1]))
+                                       for i in range(4)])
+        proj = [t.view(B, -1, E) for t in outs]
         H1, W1 = grids[0]
         M = B * H1 * W1
         conv = self.linear_fuse[0]

@@ -140,15 +140,13 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
         # sums their gradients on load)
         h, h2, xr = F.layernorm_res(store, blk.norm1, x, G, scale=prev[0], rps=N, tap=prev[1])
 
-        def kv_path():
-            if a.sr_ratio > 1:
-                xs, Hk, Wk = F.conv(store, a.sr, h2, G, G * B, H, W, C, a.sr_ratio, 0)
-                xs = F.layernorm(store, a.norm, xs, G)
-                return F.glinear(store, a.kv.weight, a.kv.bias, xs), Hk * Wk
-            return F.glinear(store, a.kv.weight, a.kv.bias, h2), N
-
-        q = F.glinear(store, a.q.weight, a.q.bias, h)
-        kv, Nk = kv_path()
+        if a.sr_ratio > 1:
+            xs, Hk, Wk = F.conv(store, a.sr, h2, G, G * B, H, W, C, a.sr_ratio, 0)
+            xs, Nk = F.layernorm(store, a.norm, xs, G), Hk * Wk
+        else:
+            xs, Nk = h2, N
+        # q and kv as ONE GEMM launch (and their input gradients as another)
+        q, kv = F.glinear_multi(store, [(a.q.weight, a.q.bias, h), (a.kv.weight, a.kv.bias, xs)])
         o = F.SRAttentionF.apply(q, kv, G * B, N, Nk, a.num_heads, C // a.num_heads)
         # x + drop_path(proj(o)): residual and DropPath scale fused into the proj GEMM epilogue
         tap_a = F.GradTap() if s_attn is not None else None

@@ -67,7 +67,19 @@ def sweep():
     print(f"empty fill: {t(lambda: x.fill_(1.0)):.1f} us")
 
 
+def nw_sweep():
+    """SRA_NW / SRA_QW launch-shape A/B, interleaved in one process (cmx_tune)."""
+    from rgbx_semantic_segmentation_amd import _lib
+    for qw, nw in ((0, 0), (1, 8), (1, 10), (1, 4), (2, 8), (1, 2)):
+        _lib.call("cmx_tune", b"SRA_QW", qw)
+        _lib.call("cmx_tune", b"SRA_NW", nw)
+        print(f"--- SRA_QW={qw} SRA_NW={nw}")
+        main()
+
+
 if len(sys.argv) > 1 and sys.argv[1] == "sweep":
     sweep()
+elif len(sys.argv) > 1 and sys.argv[1] == "nw":
+    nw_sweep()
 elif __name__ == "__main__":     # all stages, or `stage S`
     main()

@@ -44,7 +44,8 @@ def work():
              "sra": "SRA attention (fwd, dQ, dK/dV, reduce)", "dwconv": "DWConv 3x3 + GELU (fwd_save, bwd_saved)",
              "layernorm": "LayerNorm (fwd, bwd)", "adamw": "AdamW", "batchnorm": "BatchNorm (stats, fold, apply, bwd)",
              "frm": "FRM (pool, channel MLP, combine)", "ffm": "FFM context / cross attention",
-             "ce": "upsample + CE", "bilinear": "bilinear (decoder fuse adjoint)", "im2col": "im2col / col2im"}
+             "ce": "upsample + CE", "bilinear": "bilinear (decoder fuse adjoint)", "im2col": "im2col / col2im",
+             "pe1": "stage-1 patch embed (direct conv fwd, wgrad)"}
     return {names[k]: (v[0] or None, v[1] or None) for k, v in w.items()}
 
 
@@ -61,6 +62,7 @@ FAMILIES = [
     ("upsample + CE", r"ce_|upsample"),
     ("bilinear (decoder fuse adjoint)", r"bilinear"),
     ("im2col / col2im", r"im2col|col2im"),
+    ("stage-1 patch embed (direct conv fwd, wgrad)", r"pe1_"),
 ]
 
 

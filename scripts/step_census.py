@@ -40,7 +40,7 @@ FAMILIES = [
     ("depthwise 3x3 conv + GELU (MixFFN)", r"^dw2_|^dw_"),
     ("LayerNorm", r"^ln_"),
     ("BatchNorm", r"^bn_"),
-    ("FRM (CM-FRM)", r"^frm_channel|^pool_|^linear_|^combine_|^ifrm"),
+    ("FRM (CM-FRM)", r"^pool_|^linear_|^combine_|^ifrm"),
     ("FFM (cross attention contexts)", r"^ffm_"),
     ("CE loss + upsample", r"^ce_|^upsample_ce"),
     ("bilinear / col2im / im2col / patch", r"^bilinear|^col2im|^im2col|^patch"),

@@ -207,6 +207,87 @@ def test_implicit_conv(dev, Cin, Cout, k, st, pad, H, W, dt):
         assert rel(bg[g], dy[g].float().sum(0)) < 1e-2
 
 
+@pytest.mark.parametrize("case", ["qkv1", "qkv3", "qkv4", "decoder", "mixed"])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_gemm_multi_matches_single(dev, case, dt):
+    """Independent GEMMs as ONE launch (cmx_gemm_plan + cmx_gemm_multi; functions._gemm_group):
+    Attention.q beside .kv at the B2 stage-1 / 3 / 4 shapes (forward with bias, and the dgrads),
+    the decoder's four linear_c products, and a mix with a problem that is not eligible (split-K)
+    and runs on its own.  Each output against torch fp32 on the same operands (1e-2 relative,
+    16-bit output rounding)."""
+    from rgbx_semantic_segmentation_amd import functions as Fn
+    torch.manual_seed(11)
+    shapes = {"qkv1": [(2, 38400, 64, 64), (2, 600, 128, 64)],
+              "qkv3": [(2, 2400, 320, 320), (2, 600, 640, 320)],
+              "qkv4": [(2, 600, 512, 512), (2, 600, 1024, 512)],
+              "decoder": [(1, 38400, 512, 64), (1, 9600, 512, 128), (1, 2400, 512, 320), (1, 600, 512, 512)],
+              "mixed": [(2, 2400, 320, 320), (1, 64, 64, 8192), (2, 600, 128, 64)]}[case]
+    for dgrad in (False, True):
+        jobs, refs = [], []
+        for G, M, N, Kd in shapes:
+            A = torch.randn(G, M, Kd, device=dev).to(dt)
+            W = (torch.randn(G, N, Kd, device=dev) / math.sqrt(Kd)).to(dt)
+            if dgrad:                      # dx (G, M, Kd) = dy (G, M, N) @ W (G, N, Kd)
+                dy = torch.randn(G, M, N, device=dev).to(dt)
+                C = torch.empty(G, M, Kd, device=dev, dtype=dt)
+                jobs.append(dict(A=dy, B=W.transpose(1, 2), C=C))
+                refs.append((C, torch.bmm(dy.float(), W.float())))
+            else:
+                b = torch.randn(G, N, device=dev)
+                C = torch.empty(G, M, N, device=dev, dtype=dt)
+                jobs.append(dict(A=A, B=W, C=C, bias=b))
+                refs.append((C, torch.bmm(A.float(), W.float().transpose(1, 2)) + b[:, None, :]))
+        Fn._gemm_group(jobs)
+        torch.cuda.synchronize()
+        for C, ref in refs:
+            assert rel(C, ref) < 1e-2, (case, dgrad, C.shape, rel(C, ref))
+
+
+@pytest.mark.parametrize("G,B,H,W,N", [(2, 2, 480, 640, 64), (2, 1, 64, 96, 32), (1, 3, 37, 203, 64),
+                                       (2, 2, 4, 4, 64), (2, 1, 100, 260, 48)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_pe1_direct_conv(dev, G, B, H, W, N, dt):
+    """Stage-1 patch embed straight from the fp32 NCHW batches (patch_embed1.hip: Conv2d 3 -> N,
+    k7 s4 p3, dual_segformer.py:196-197) against torch conv2d on the 16-bit-rounded image and
+    weights (fp64 reference: the kernel rounds the patch values to the storage type, accumulates
+    in fp32): output 1e-2 relative (16-bit output rounding); weight / bias gradient from the
+    per-workgroup slabs + grouped reduce 1e-4 relative (fp32 sums of exact 16-bit products).
+    Ragged row tiles (Wo % 64 != 0), a 1 x 1 output grid, G = 1, N = 32 / 48 (B0 / padded)."""
+    from rgbx_semantic_segmentation_amd import deferred
+    from rgbx_semantic_segmentation_amd import kernels as K
+    torch.manual_seed(5)
+    Kp = 152
+    Ho, Wo = (H + 6 - 7) // 4 + 1, (W + 6 - 7) // 4 + 1
+    img = [torch.randn(B, 3, H, W, device=dev) for _ in range(G)]
+    Wt = torch.zeros(G, N, Kp, device=dev, dtype=dt)
+    Wt[:, :, :147] = (torch.randn(G, N, 147, device=dev) / math.sqrt(147)).to(dt)
+    bias = torch.randn(G, N, device=dev)
+    y = torch.full((G, B * Ho * Wo, N), float("nan"), device=dev, dtype=dt)
+    K.call("cmx_pe1_conv_fwd", K.ptr(img[0]), K.ptr(img[-1]) if G == 2 else 0, K.ptr(Wt), K.ptr(bias), K.ptr(y), G, B,
+           3, H, W, 7, 7, 4, 3, Ho, Wo, N, Kp, Wt.stride(0), bias.stride(0), y.stride(0), K.dtype_code(y), K.stream())
+    dy = torch.randn(G, B * Ho * Wo, N, device=dev).to(dt)
+    nblk = K.query("cmx_pe1_conv_wgrad_nblk", B, Ho, Wo)
+    ws = torch.empty(G, nblk, N, Kp + 1, device=dev)
+    K.call("cmx_pe1_conv_wgrad", K.ptr(dy), K.ptr(img[0]), K.ptr(img[-1]) if G == 2 else 0, K.ptr(ws), G, B, 3, H, W,
+           7, 7, 4, 3, Ho, Wo, N, Kp, dy.stride(0), K.dtype_code(dy), K.stream())
+    Wg = torch.full((G, N, Kp), float("nan"), device=dev)
+    bg = torch.full((G, N), float("nan"), device=dev)
+    deferred.reduce(ws, Wg, bg, G, nblk, nblk * N * (Kp + 1), N * (Kp + 1), N, Kp + 1, Kp, Wg.stride(0), Wg.stride(1),
+                    bg.stride(0), 1)
+    deferred.flush()
+    torch.cuda.synchronize()
+    for g in range(G):
+        xr = img[g].to(dt).double()
+        wr = Wt[g, :, :147].double().view(N, 3, 7, 7).requires_grad_(True)
+        ref = F.conv2d(xr, wr, bias[g].double(), stride=4, padding=3)
+        got = y[g].view(B, Ho, Wo, N).permute(0, 3, 1, 2)
+        assert rel(got, ref) < 1e-2, rel(got, ref)
+        ref.backward(dy[g].double().view(B, Ho, Wo, N).permute(0, 3, 1, 2))
+        assert rel(Wg[g, :, :147], wr.grad.reshape(N, 147)) < 1e-4, rel(Wg[g, :, :147], wr.grad.reshape(N, 147))
+        assert Wg[g, :, 147:].abs().max().item() == 0.0          # the padding columns' gradient
+        assert rel(bg[g], dy[g].double().sum(0)) < 1e-4
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("GB,heads,N,D", [(4, 2, 4800, 64), (4, 5, 1200, 64), (2, 8, 300, 64), (4, 1, 333, 32)])
 def test_gemm_h2_per_head(dev, dtype, GB, heads, N, D):

@@ -161,82 +161,43 @@ def test_frm(dev, C, B, H, W, dtype):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("C,B,N", [(64, 2, 19200), (512, 2, 300), (320, 4, 1200)])
-def test_frm_channel_graph_replay(dev, C, B, N):
-    """The one-launch ChannelWeights kernels (grid barriers with self-resetting counters) give the
-    same bits eagerly and on every replay of a captured HIP graph, never time out a barrier, and
-    match the separate pool / small-linear kernels they replace (fp32 sums within 1e-5)."""
+@pytest.mark.parametrize("C,B,N", [(64, 2, 19200), (512, 2, 300), (320, 4, 1200), (32, 1, 7), (160, 3, 4800)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_frm_pool_one_launch(dev, C, B, N, dtype):
+    """ChannelWeights' avg || max pooling (net_utils.py:22-27) as ONE launch: per-chunk partials
+    folded by the last block to arrive (self-resetting arrival tickets).  Against torch on the
+    same values: avg within 1e-6 relative (fp32 sums in another order), max exact, argmax = the
+    FIRST maximal token (values quantised so ties occur); identical bits eagerly and on every
+    replay of a captured graph (the tickets are back at zero after each launch)."""
     from rgbx_semantic_segmentation_amd import kernels as K
-    torch.manual_seed(1)
-    x = torch.randn(2, B, N, C, device=dev).to(torch.bfloat16)
-    W1 = torch.randn(4 * C, 4 * C, device=dev) / (2 * C) ** 0.5
-    b1 = torch.randn(4 * C, device=dev) * 0.1
-    W2 = torch.randn(2 * C, 4 * C, device=dev) / (2 * C) ** 0.5
-    b2 = torch.randn(2 * C, device=dev) * 0.1
-    nslab = 37
-    pcw = torch.randn(B, nslab, 2 * C, device=dev) * 0.05
+    torch.manual_seed(2)
+    x = (torch.randn(2, B, N, C, device=dev) * 4).round().to(dtype)       # few distinct values: ties
     f32 = dict(dtype=torch.float32, device=dev)
-    outs = dict(pooled=torch.empty(B, 4 * C, **f32), argmax=torch.empty(B, 2 * C, dtype=torch.int32, device=dev),
-                y1=torch.empty(B, 4 * C, **f32), cw=torch.empty(B, 2 * C, **f32), gW1=torch.empty_like(W1),
-                gb1=torch.empty_like(b1), gW2=torch.empty_like(W2), gb2=torch.empty_like(b2))
-    dx0 = torch.randn(2, B, N, C, device=dev).to(torch.bfloat16)
-    dx = dx0.clone()
-    wsf = K._ws(K.query("cmx_frm_channel_fwd_workspace", B, N, C), dev)
-    wsb = K._ws(K.query("cmx_frm_channel_bwd_workspace", B, C), dev)
-
-    def run():
-        o = outs
-        dx.copy_(dx0)
-        K.call("cmx_frm_channel_fwd", K.ptr(x), K.ptr(W1), K.ptr(b1), K.ptr(W2), K.ptr(b2), K.ptr(o["pooled"]),
-               K.ptr(o["argmax"]), K.ptr(o["y1"]), K.ptr(o["cw"]), K.ptr(wsf), B, N, C, 1, K.stream())
-        K.call("cmx_frm_channel_bwd", K.ptr(pcw), nslab, K.ptr(o["cw"]), K.ptr(o["y1"]), K.ptr(o["pooled"]),
-               K.ptr(o["argmax"]), K.ptr(W1), K.ptr(W2), K.ptr(o["gW1"]), K.ptr(o["gb1"]), K.ptr(o["gW2"]),
-               K.ptr(o["gb2"]), K.ptr(dx), K.ptr(wsb), B, N, C, 1, K.stream())
-
-    run()
-    torch.cuda.synchronize()
-    eager = {k: v.clone() for k, v in outs.items()}
-    eager["dx"] = dx.clone()
-    # the separate kernels of the same math (pool, small_linear fwd / bwd, pool bwd)
     pooled = torch.empty(B, 4 * C, **f32)
     argmax = torch.empty(B, 2 * C, dtype=torch.int32, device=dev)
     ws = K._ws(K.query("cmx_frm_pool_workspace", B, N, C), dev)
-    K.call("cmx_frm_pool_fwd", K.ptr(x), K.ptr(pooled), K.ptr(argmax), K.ptr(ws), B, N, C, 1, K.stream())
-    y1 = torch.empty(B, 4 * C, **f32)
-    K.call("cmx_small_linear_fwd", K.ptr(pooled), K.ptr(W1), K.ptr(b1), K.ptr(y1), B, 4 * C, 4 * C, 2, K.stream())
-    cw = torch.empty(B, 2 * C, **f32)
-    K.call("cmx_small_linear_fwd", K.ptr(y1), K.ptr(W2), K.ptr(b2), K.ptr(cw), B, 4 * C, 2 * C, 3, K.stream())
-    ns = K.query("cmx_small_linear_nslice")
-    dcw = pcw.sum(1)
-    gW2, gb2, gW1, gb1 = (torch.empty_like(t) for t in (W2, b2, W1, b1))
-    dy1p = torch.empty(ns, B, 4 * C, **f32)
-    K.call("cmx_small_linear_bwd", K.ptr(dcw), 1, 0, 2 * C, K.ptr(cw), K.ptr(y1), K.ptr(W2), K.ptr(dy1p),
-           K.ptr(gW2), K.ptr(gb2), B, 4 * C, 2 * C, 3, 0, K.stream())
-    dpp = torch.empty(ns, B, 4 * C, **f32)
-    K.call("cmx_small_linear_bwd", K.ptr(dy1p), ns, B * 4 * C, 4 * C, K.ptr(y1), K.ptr(pooled), K.ptr(W1),
-           K.ptr(dpp), K.ptr(gW1), K.ptr(gb1), B, 4 * C, 4 * C, 2, 0, K.stream())
-    dxs = dx0.clone()
-    K.call("cmx_frm_pool_bwd", K.ptr(dpp), ns, B * 4 * C, K.ptr(argmax), K.ptr(dxs), B, N, C, 1, K.stream())
+
+    def run():
+        K.call("cmx_frm_pool_fwd", K.ptr(x), K.ptr(pooled), K.ptr(argmax), K.ptr(ws), B, N, C, K.dtype_code(x),
+               K.stream())
+
+    run()
     torch.cuda.synchronize()
-    assert torch.equal(eager["argmax"], argmax)
-    sep = dict(pooled=pooled, y1=y1, cw=cw, gW1=gW1, gb1=gb1, gW2=gW2, gb2=gb2)
-    for k, v in sep.items():
-        assert rel(eager[k], v, 1e-8) < 1e-5, (k, rel(eager[k], v, 1e-8))
-    # dx is bf16 storage: the pooling gradient (fp32 sums in another order) may round one ulp apart
-    d = (eager["dx"].float() - dxs.float()).abs()
-    assert bool((d <= dxs.float().abs() * 2.0 ** -7 + 1e-6).all()), d.max().item()
-    # graph capture + replays: identical bits every time
+    xf = x.float().permute(1, 0, 3, 2).reshape(B, 2 * C, N)                # (B, [x1 | x2] channels, tokens)
+    avg, mx = xf.mean(-1), xf.amax(-1)
+    first = (xf == mx[..., None]).float().argmax(-1).to(torch.int32)      # first maximal token
+    assert rel(pooled[:, :2 * C], avg, 1e-8) < 1e-6
+    assert torch.equal(pooled[:, 2 * C:], mx)
+    assert torch.equal(argmax, first)
+    eager = (pooled.clone(), argmax.clone())
     st = torch.cuda.Stream()
     st.wait_stream(torch.cuda.current_stream())
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=st):
         run()
     for _ in range(3):
-        for v in outs.values():
-            v.zero_()
+        pooled.zero_()
+        argmax.zero_()
         g.replay()
         torch.cuda.synchronize()
-        for k, v in outs.items():
-            assert torch.equal(v, eager[k]), k
-        assert torch.equal(dx, eager["dx"])
-    assert K.query("cmx_frm_barrier_timeouts") == 0
+        assert torch.equal(pooled, eager[0]) and torch.equal(argmax, eager[1])
