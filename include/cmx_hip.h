@@ -232,7 +232,9 @@ int cmx_gemm_group_pack_conv_wgrad(void* rec, const void* dy, const void* x, flo
  *      cmx_pe1_conv_wgrad writes one fp32 partial slab (N, Kp + 1) per workgroup into ws (G, nblk, N, Kp + 1),
  *      nblk = cmx_pe1_conv_wgrad_nblk(B, Ho, Wo); column Kp is the bias gradient.  The caller sums the slabs
  *      (cmx_reduce_pack with csplit = Kp). */
-int cmx_pe1_conv_fwd(const float* img0, const float* img1, const void* Wt, const float* bias, void* y, int G, int B, int C, int H, int W, int KH, int KW, int stride, int pad, int Ho, int Wo, int N, int Kp, int64_t sW, int64_t sbias, int64_t sy, int dtype, hipStream_t stream);
+/*      gamma != NULL: OverlapPatchEmbed.norm (dual_segformer.py:198) fused into the epilogue -- y_ln (same layout as
+ *      y) = LayerNorm of the stored y, mean / rstd (G*B*Ho*Wo) as cmx_layernorm_fwd writes them (N 32 or 64). */
+int cmx_pe1_conv_fwd(const float* img0, const float* img1, const void* Wt, const float* bias, void* y, int G, int B, int C, int H, int W, int KH, int KW, int stride, int pad, int Ho, int Wo, int N, int Kp, int64_t sW, int64_t sbias, int64_t sy, const float* gamma, const float* beta, void* y_ln, float* mean, float* rstd, int64_t sgb, float eps, int dtype, hipStream_t stream);
 int cmx_pe1_conv_wgrad_nblk(int B, int Ho, int Wo);
 int cmx_pe1_conv_wgrad(const void* dy, const float* img0, const float* img1, float* ws, int G, int B, int C, int H, int W, int KH, int KW, int stride, int pad, int Ho, int Wo, int N, int Kp, int64_t sdy, int dtype, hipStream_t stream);
 size_t cmx_reduce_record_size(void);

@@ -77,11 +77,26 @@ __device__ __forceinline__ void build_patches_r(const float* patch, char* img, i
   }
 }
 
+// LN (optional, gamma != nullptr): OverlapPatchEmbed.norm (dual_segformer.py:198,219) on the
+// conv output in the same epilogue -- a row's N <= 64 channels are 8 consecutive lanes' values,
+// so the row statistics are an 8-lane shuffle sum.  The statistics are taken on the stored
+// (16-bit rounded) conv output, in the LayerNorm kernel's order (per-lane sums of 8, then the
+// lane shuffle), so y_ln / mean / rstd are those cmx_layernorm_fwd computes from y.
+struct Pe1Norm {
+  const float* gamma;
+  const float* beta;
+  void* y;
+  float* mean;
+  float* rstd;
+  long sgb;                                     // gamma / beta group stride
+  float eps;
+};
+
 template <typename E>
 __global__ __launch_bounds__(256) void pe1_fwd_kernel(const float* __restrict__ img0, const float* __restrict__ img1,
                                                       const E* __restrict__ Wt, const float* __restrict__ bias,
                                                       E* __restrict__ y, int H, int W, int Ho, int Wo, int N, int Kp,
-                                                      long sW, long sbias, long sy) {
+                                                      long sW, long sbias, long sy, const Pe1Norm ln) {
   __shared__ __attribute__((aligned(1024))) char smem[6 * IMG + PATCH_BYTES];
   char* pimg = smem;                            // 3 patch images
   char* wimg = smem + 3 * IMG;                  // 3 weight images
@@ -119,7 +134,8 @@ __global__ __launch_bounds__(256) void pe1_fwd_kernel(const float* __restrict__ 
   const int jl = (threadIdx.x & 7) * 8;
   if (jl >= N) return;
   const float* bb = bias ? bias + (long)g * sbias + jl : nullptr;
-  E* yrow = y + (long)g * sy + ((long)b * Ho * Wo + (long)oy * Wo + ox0) * N + jl;
+  const long row0 = (long)b * Ho * Wo + (long)oy * Wo + ox0;     // row of the tile's first pixel in group g
+  E* yrow = y + (long)g * sy + row0 * N + jl;
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
     const int il = pass * 32 + (threadIdx.x >> 3);
@@ -133,6 +149,27 @@ __global__ __launch_bounds__(256) void pe1_fwd_kernel(const float* __restrict__ 
       for (int e = 0; e < 8; ++e) v[e] += bb[e];
     }
     store_vec<E>(yrow + (long)il * N, v);
+    if (ln.gamma) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { v[e] = to_f32(from_f32<E>(v[e])); s += v[e]; }
+      s = group_sum(s, N >> 3);
+      const float mu = s / N;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { const float d = v[e] - mu; q += d * d; }
+      q = group_sum(q, N >> 3);
+      const float rstd = rsqrtf(q / N + ln.eps);
+      const float* gm = ln.gamma + (long)g * ln.sgb + jl;
+      const float* bt = ln.beta + (long)g * ln.sgb + jl;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (v[e] - mu) * rstd * gm[e] + bt[e];
+      store_vec<E>(reinterpret_cast<E*>(ln.y) + (long)g * sy + (row0 + il) * N + jl, v);
+      if (jl == 0) {
+        const long grow = (long)g * ((long)gridDim.y * Ho * Wo) + row0 + il;
+        ln.mean[grow] = mu;
+        ln.rstd[grow] = rstd;
+      }
+    }
   }
 }
 
@@ -213,9 +250,14 @@ extern "C" {
 
 int cmx_pe1_conv_fwd(const float* img0, const float* img1, const void* Wt, const float* bias, void* y, int G, int B,
                      int C, int H, int W, int KH, int KW, int stride, int pad, int Ho, int Wo, int N, int Kp, int64_t sW,
-                     int64_t sbias, int64_t sy, int dtype, hipStream_t s) {
+                     int64_t sbias, int64_t sy, const float* gamma, const float* beta, void* y_ln, float* mean,
+                     float* rstd, int64_t sgb, float eps, int dtype, hipStream_t s) {
   const int st = pe1_check(N, Kp, KH, KW, stride, pad, C);
   if (st != CMX_OK) return st;
+  CMX_REQUIRE(!gamma || (beta && y_ln && mean && rstd && (N == 32 || N == 64) && ((uintptr_t)y_ln & 15) == 0),
+              CMX_ERR_ARG, "pe1_conv_fwd: the LayerNorm epilogue needs beta / y_ln / mean / rstd and N 32 or 64 (N=%d)",
+              N);
+  const Pe1Norm ln{gamma, beta, y_ln, mean, rstd, (long)sgb, eps};
   CMX_REQUIRE((dtype == 1 || dtype == 2) && (G == 1 || G == 2) && B > 0 && img0 && (G == 1 || img1), CMX_ERR_ARG,
               "pe1_conv_fwd: 16-bit, G 1 or 2 (dtype %d, G %d)", dtype, G);
   CMX_REQUIRE(Ho == (H + 2 * pad - KH) / stride + 1 && Wo == (W + 2 * pad - KW) / stride + 1, CMX_ERR_SHAPE,
@@ -225,10 +267,10 @@ int cmx_pe1_conv_fwd(const float* img0, const float* img1, const void* Wt, const
   const dim3 grid(Ho * ((Wo + TW - 1) / TW), B, G);
   if (dtype == 2)
     hipLaunchKernelGGL(pe1_fwd_kernel<f16>, grid, dim3(256), 0, s, img0, img1, (const f16*)Wt, bias, (f16*)y, H, W, Ho,
-                       Wo, N, Kp, (long)sW, (long)sbias, (long)sy);
+                       Wo, N, Kp, (long)sW, (long)sbias, (long)sy, ln);
   else
     hipLaunchKernelGGL(pe1_fwd_kernel<bf16>, grid, dim3(256), 0, s, img0, img1, (const bf16*)Wt, bias, (bf16*)y, H, W,
-                       Ho, Wo, N, Kp, (long)sW, (long)sbias, (long)sy);
+                       Ho, Wo, N, Kp, (long)sW, (long)sbias, (long)sy, ln);
   return cmx_check_launch("pe1_conv_fwd");
 }
 

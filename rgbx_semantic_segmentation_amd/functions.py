@@ -646,7 +646,8 @@ class ConvF(Function):
             img1 = (x2 if x2 is not None else x[Bg:]) if G == 2 else None
             y = torch.empty(G, Bg * Ho * Wo, N, dtype=W.dtype, device=W.device)
             K.call("cmx_pe1_conv_fwd", K.ptr(x), K.ptr(img1), K.ptr(W), K.ptr(b), K.ptr(y), G, Bg, C, H, Wd, KH, KW,
-                   st, pad, Ho, Wo, N, Kp, W.stride(0), b.stride(0), y.stride(0), K.dtype_code(W), K.stream())
+                   st, pad, Ho, Wo, N, Kp, W.stride(0), b.stride(0), y.stride(0), 0, 0, 0, 0, 0, 0, 0.0,
+                   K.dtype_code(W), K.stream())
             ctx.pe1 = (x, img1)
             ctx.save_for_backward(None, W)
             ctx.meta = (Wg, bg, geom)
@@ -710,6 +711,78 @@ class ConvF(Function):
                    K.dtype_code(dx), K.stream())
             dx = dx.view(ctx.xshape)
         return dx, None, None, None, None, None, None, None
+
+
+class PatchEmbed1F(Function):
+    """Stage-1 OverlapPatchEmbed (dual_segformer.py:196-198,219): the 7x7 s4 conv straight from
+    the fp32 NCHW batches with its LayerNorm in the same epilogue (cmx_pe1_conv_fwd), so the conv
+    output is written once and never re-read in the forward.  Backward: the LayerNorm backward
+    (dgamma / dbeta partials to the deferred reduce), then the conv's weight gradient as
+    per-workgroup slabs summed by the same reduce (cmx_pe1_conv_wgrad).  The images need no
+    gradient."""
+
+    @staticmethod
+    def forward(ctx, x, x2, W, Wg, b, bg, gamma, beta, gg, gb, eps, geom, anchor):
+        G, NI, H, Wd, C, KH, KW, st, pad, Ho, Wo = geom
+        Bg, N, Kp = NI // G, W.shape[1], W.shape[-1]
+        img1 = (x2 if x2 is not None else x[Bg:]) if G == 2 else None
+        R = Bg * Ho * Wo
+        y = torch.empty(G, R, N, dtype=W.dtype, device=W.device)
+        out = torch.empty_like(y)
+        mean = torch.empty(G * R, dtype=torch.float32, device=W.device)
+        rstd = torch.empty_like(mean)
+        K.call("cmx_pe1_conv_fwd", K.ptr(x), K.ptr(img1), K.ptr(W), K.ptr(b), K.ptr(y), G, Bg, C, H, Wd, KH, KW, st,
+               pad, Ho, Wo, N, Kp, W.stride(0), b.stride(0), y.stride(0), K.ptr(gamma), K.ptr(beta), K.ptr(out),
+               K.ptr(mean), K.ptr(rstd), gamma.stride(0), float(eps), K.dtype_code(W), K.stream())
+        ctx.save_for_backward(y, gamma, mean, rstd)
+        ctx.imgs = (x, img1)
+        ctx.meta = (W.shape, Wg, bg, gg, gb, geom)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        y, gamma, mean, rstd = ctx.saved_tensors
+        img0, img1 = ctx.imgs
+        wshape, Wg, bg, gg, gb, geom = ctx.meta
+        G, NI, H, Wd, C, KH, KW, st, pad, Ho, Wo = geom
+        Bg, N, Kp = NI // G, wshape[1], wshape[-1]
+        dy = _layernorm_bwd_deferred(_c(dout), y, gamma, mean, rstd, G, gg, gb)
+        nblk = K.query("cmx_pe1_conv_wgrad_nblk", Bg, Ho, Wo)
+        ws = torch.empty(G, nblk, N, Kp + 1, dtype=torch.float32, device=dy.device)
+        K.call("cmx_pe1_conv_wgrad", K.ptr(dy), K.ptr(img0), K.ptr(img1), K.ptr(ws), G, Bg, C, H, Wd, KH, KW, st, pad,
+               Ho, Wo, N, Kp, dy.stride(0), K.dtype_code(dy), K.stream())
+        deferred.reduce(ws, Wg, bg, G, nblk, nblk * N * (Kp + 1), N * (Kp + 1), N, Kp + 1, Kp, Wg.stride(0),
+                        Wg.stride(1), bg.stride(0), 1)
+        return (None,) * 13
+
+
+def patch_embed1(store, pe, x, G, NI, H, W, x2=None):
+    """Stage-1 patch embed: conv + LayerNorm (PatchEmbed1F) when eligible (16-bit weights, the
+    deferred weight gradients, N 32 / 64), else conv then layernorm.  Returns (out, Ho, Wo)."""
+    mod = pe.proj
+    KH, KW = mod.kernel_size
+    C = x.shape[1]
+    st, pad = pe.stride, pe.pad
+    Ho, Wo = (H + 2 * pad - KH) // st + 1, (W + 2 * pad - KW) // st + 1
+    Wt = store.w(mod.weight)
+    N = Wt.shape[1]
+    if (PE1_DIRECT and deferred.ENABLED and Wt.dtype in (torch.bfloat16, torch.float16) and mod.bias is not None
+            and (C, KH, KW, st, pad) == (3, 7, 7, 4, 3) and N in (32, 64) and x.dtype == torch.float32
+            and x.is_contiguous() and (x2 is None or x2.is_contiguous())):
+        Wt = Wt.view(G, N, -1)
+        Wg = store.g(mod.weight).view(G, N, -1)
+        b = store.w(mod.bias, compute=False).view(G, -1)
+        bg = store.g(mod.bias).view(G, -1)
+        nm = pe.norm
+        gamma = store.w(nm.weight, compute=False).view(G, -1)
+        beta = store.w(nm.bias, compute=False).view(G, -1)
+        gg = store.g(nm.weight).view(G, -1)
+        gb = store.g(nm.bias).view(G, -1)
+        geom = (G, NI, H, W, C, KH, KW, st, pad, Ho, Wo)
+        out = PatchEmbed1F.apply(x, x2, Wt, Wg, b, bg, gamma, beta, gg, gb, nm.eps, geom, mod.weight)
+        return out, Ho, Wo
+    y, Ho, Wo = conv(store, mod, x, G, NI, H, W, C, st, pad, nchw=True, x2=x2)
+    return layernorm(store, pe.norm, y, G), Ho, Wo
 
 
 def conv(store, mod, x, G, NI, H, W, C, stride, pad, nchw=False, x2=None):
@@ -845,8 +918,9 @@ class CrossPathF(Function):
         da = torch.empty(G, M, 2 * C, dtype=x.dtype, device=x.device)
         dy, du = da[..., :C], da[..., C:]
         # end_proj on cat(y, v): dy into the first half of da, dv apart; the residual passes de
-        _dgrad(de, Wend[:, :, :C], dy)
-        dv = _dgrad(de, Wend[:, :, C:], torch.empty_like(v))
+        dv = torch.empty_like(v)
+        _gemm_group([dict(A=de, B=Wend[:, :, :C].transpose(1, 2), C=dy),        # one launch
+                     dict(A=de, B=Wend[:, :, C:].transpose(1, 2), C=dv)])
         _wgrad_into(de, y, Wgend[:, :, :C], bgend)
         _wgrad_into(de, v, Wgend[:, :, C:])
         # attention: du (second half of da) = dout @ ctx^T per head, then += dkv @ Wkv (kv's dgrad)
@@ -884,9 +958,9 @@ class PairEmbedF(Function):
     def forward(ctx, o, Wres, Wgres, Wce, Wgce, bce, bgce, anchor):
         _, M, C = o.shape
         res = torch.empty(1, M, C, dtype=o.dtype, device=o.device)
-        _fwd_gemm(o[0:1], Wres, None, res, x2=o[1:2])
         t = torch.empty(1, M, Wce.shape[1], dtype=o.dtype, device=o.device)
-        _fwd_gemm(o[0:1], Wce, bce, t, x2=o[1:2])
+        _gemm_group([dict(A=o[0:1], B=Wres, C=res, A2=o[1:2]),                 # one launch
+                     dict(A=o[0:1], B=Wce, C=t, bias=bce, A2=o[1:2])])
         ctx.save_for_backward(o, Wres, Wce)
         ctx.meta = (Wgres, Wgce, bgce)
         return res, t
@@ -1133,11 +1207,12 @@ class DecoderFuseF(Function):
         B, N1, E = e1.shape
         (H1, W1), hw = sizes[0], sizes[1:]        # hw: grids of c2, c3, c4
         W = Wf[0]                                 # (E, 4E): column slots [c4 | c3 | c2 | c1]
-        zs = []
+        zs, jobs = [], []
         for slot, (e, (h, w)) in enumerate(zip((e4, e3, e2), (hw[2], hw[1], hw[0]))):
             z = torch.empty(1, B * h * w, E, dtype=e.dtype, device=e.device)
-            K.gemm(e.reshape(1, B * h * w, E), W[None, :, slot * E:(slot + 1) * E], z)
+            jobs.append(dict(A=e.reshape(1, B * h * w, E), B=W[None, :, slot * E:(slot + 1) * E], C=z))
             zs.append(z)
+        _gemm_group(jobs)                         # the three branch products: one launch
         Z = torch.empty(B * N1, E, dtype=e1.dtype, device=e1.device)
         Wc1 = W[:, 3 * E:]
         K.call("cmx_decoder_fuse_fwd", K.ptr(_c(e1)), Wc1.data_ptr(), K.ptr(Z), K.ptr(bf), K.ptr(zs[0]), K.ptr(zs[1]),
@@ -1154,16 +1229,20 @@ class DecoderFuseF(Function):
         B, N1, E = e1.shape
         (H1, W1), hw = sizes[0], sizes[1:]
         dZ = _c(dZ).view(1, B * N1, E)
-        grads = []
+        grads, jobs = [], []
         for slot, (e, (h, w)) in enumerate(zip((e4, e3, e2), (hw[2], hw[1], hw[0]))):
             dz = _adjoint_to(dZ, B, H1, W1, h, w, E).view(1, B * h * w, E)
             sl = slice(slot * E, (slot + 1) * E)
-            grads.append(_dgrad(dz, Wf[:, :, sl], torch.empty_like(dz)).view(e.shape))
+            g = torch.empty_like(dz)
+            jobs.append(dict(A=dz, B=Wf[:, :, sl].transpose(1, 2), C=g))
+            grads.append(g.view(e.shape))
             _wgrad_into(dz, e.reshape(1, B * h * w, E), Wfg[:, :, sl])
         e1f = e1.reshape(1, B * N1, E)
-        de1 = _dgrad(dZ, Wf[:, :, 3 * E:], torch.empty_like(e1f)).view(e1.shape)
+        de1 = torch.empty_like(e1f)
+        jobs.append(dict(A=dZ, B=Wf[:, :, 3 * E:].transpose(1, 2), C=de1))
         _wgrad_into(dZ, e1f, Wfg[:, :, 3 * E:], bfg)
-        return grads[0], grads[1], grads[2], de1, None, None, None, None, None, None
+        _gemm_group(jobs)                         # the four branches' input gradients: one launch
+        return grads[0], grads[1], grads[2], de1.view(e1.shape), None, None, None, None, None, None
 
 
 # ---------------------------------------------------------------------------- final upsample + CE

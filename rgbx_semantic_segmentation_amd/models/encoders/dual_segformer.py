@@ -181,9 +181,11 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
                 # the gradient of this stage's input exists once the backward has passed the
                 # stage (segment 3 - s): its gradients can be all-reduced while stages < s run
                 x.register_hook(sync.segment_hook(3 - s))
-            x, Ho, Wo = F.conv(store, pe.proj, x, G, G * B, Hc, Wc, Cin, pe.stride, pe.pad, nchw=(s == 0),
-                               x2=x2 if s == 0 else None)
-            x = F.layernorm(store, pe.norm, x, G)
+            if s == 0:      # conv on the NCHW images + LayerNorm in one launch where eligible
+                x, Ho, Wo = F.patch_embed1(store, pe, x, G, G * B, Hc, Wc, x2=x2)
+            else:
+                x, Ho, Wo = F.conv(store, pe.proj, x, G, G * B, Hc, Wc, Cin, pe.stride, pe.pad)
+                x = F.layernorm(store, pe.norm, x, G)
             Hc, Wc, Cin = Ho, Wo, self.embed_dims[s]
             prev = (None, None)
             blocks = getattr(self, f"block{s + 1}")

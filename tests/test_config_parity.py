@@ -37,12 +37,19 @@ OUTLIER_RATIO = 12.0
 # CM-FRM / FFM tensors of the bf16 cases: at most 2x the emulated error,
 # outliers up to 4x for at most 4 % of them (6 of 148 at B2), with two documented adjustments:
 #  * ChannelWeights' first Linear (FRMs.s.channel_weights.mlp.0): hidden units whose fp64
-#    pre-activation lies within 2^-7 of the layer's typical magnitude in some sample are
-#    excluded from the row comparison -- their ReLU decision is decided by rounding, and a flip
-#    moves the whole gradient row (round 4: every FRM outlier row was such a unit, e.g. stage 2
-#    unit 81 with z = -0.00038, whose fp64 row is exactly zero);
-#  * SpatialWeights' biases (a sum over all B*H*W pixels with heavy cancellation): the yardstick
-#    is at least 2^-8 x sum|per-pixel terms| / max|gradient|, the error bf16 inputs alone allow.
+#    pre-activation lies within 2^-7 of the layer's typical magnitude, or within RATIO x the
+#    largest error bf16 storage puts on the layer's pre-activations (emulation, per sample), in
+#    some sample are excluded from the row
+#    comparison -- their ReLU decision is decided by rounding, and a flip moves the whole
+#    gradient row (round 4: every FRM outlier row was such a unit, e.g. stage 2 unit 81 with
+#    z = -0.00038, whose fp64 row is exactly zero);
+#  * SpatialWeights' biases (a sum over all B*H*W pixels with heavy cancellation, e.g. 600 terms
+#    at stage 4 whose sum is ~1/9 of the sum of their magnitudes): the yardstick is at least the
+#    L1 norm of the per-pixel term errors of the bf16-storage emulation, sum|dz_emu - dz_64| /
+#    max|gradient| -- the most any summation order can make of per-term errors of that size --
+#    and at least 2^-8 x sum|per-pixel terms| / max|gradient|, the error bf16 inputs alone allow.
+#    (The emulation's own sum error is one signed realization of those per-term errors; measured
+#    against it, this 2-value tensor moved between 2x and 9.4x with fp32 summation order alone.)
 RATIO_FUSION = 2.0
 OUTLIER_FUSION = 4.0
 FUSION_OUTLIER_SHARE = 0.04
@@ -141,21 +148,30 @@ def _fusion_probes(ref64):
     return probes
 
 
-def _fusion_adjust(n, gpu_g, emu_g, g64, den, probes):
+def _fusion_adjust(n, gpu_g, emu_g, g64, den, probes, probes_emu=None):
     """(e_gpu, e_emu, note) for the two adjusted CM-FRM cases (see RATIO_FUSION), else None."""
     import re
     m = re.match(r"backbone\.FRMs\.(\d+)\.channel_weights\.mlp\.0\.(weight|bias)$", n)
     if m and ("z", int(m.group(1))) in probes:
-        z = probes[("z", int(m.group(1)))]
-        keep = (z.abs() > ZBAND * z.abs().median()).all(0)
+        key = ("z", int(m.group(1)))
+        z = probes[key]
+        band = ZBAND * z.abs().median()
+        if probes_emu and key in probes_emu:         # the pre-activation error bf16 storage allows
+            ez = (probes_emu[key].double() - z).abs().amax(1, keepdim=True)    # per sample, over units
+            band = torch.maximum(band, RATIO * ez)
+        keep = (z.abs() > band).all(0)
         if bool(keep.any()):
             eg = (gpu_g - g64)[keep].abs().max().item() / den
             ee = (emu_g - g64)[keep].abs().max().item() / den
             return eg, ee, f"{int((~keep).sum())} ReLU-band units excluded"
     m = re.match(r"backbone\.FRMs\.(\d+)\.spatial_weights\.mlp\.(0|2)\.bias$", n)
     if m and (f"dsw{m.group(2)}", int(m.group(1))) in probes:
-        t = probes[(f"dsw{m.group(2)}", int(m.group(1)))]
-        allow = BF16_EPS * t.abs().sum((0, 2, 3)).max().item() / max(g64.abs().max().item(), 1e-300)
+        key = (f"dsw{m.group(2)}", int(m.group(1)))
+        t = probes[key]
+        gmax = max(g64.abs().max().item(), 1e-300)
+        allow = BF16_EPS * t.abs().sum((0, 2, 3)).max().item() / gmax
+        if probes_emu and key in probes_emu:
+            allow = max(allow, (probes_emu[key].double() - t).abs().sum((0, 2, 3)).max().item() / gmax)
         eg = (gpu_g - g64).abs().max().item() / den
         ee = (emu_g - g64).abs().max().item() / den
         return eg, max(ee, allow), f"cancellation allowance {allow:.3g}"
@@ -191,6 +207,7 @@ def test_bf16_train_step_vs_fp64_oracle(dev, case):
     emu = emulate_storage(copy.deepcopy(ref), h16)
     ref64 = ref.double()
     probes = _fusion_probes(ref64) if h16 == torch.bfloat16 else {}
+    probes_emu = _fusion_probes(emu) if h16 == torch.bfloat16 else {}
     for m in (ref64, emu, model):
         m.train()
     _masks(model, [ref64, emu], B, n_calls=2)
@@ -249,7 +266,7 @@ def test_bf16_train_step_vs_fp64_oracle(dev, case):
         ee = (pem[n].grad.double() - g64).abs().max().item() / den
         fusion = h16 == torch.bfloat16 and (".FRMs." in n or ".FFMs." in n)
         if fusion:
-            adj = _fusion_adjust(n, gg, pem[n].grad.double(), g64, den, probes)
+            adj = _fusion_adjust(n, gg, pem[n].grad.double(), g64, den, probes, probes_emu)
             if adj is not None:
                 eg, ee, notes[n] = adj
             n_fusion += 1

@@ -252,7 +252,9 @@ def test_pe1_direct_conv(dev, G, B, H, W, N, dt):
     weights (fp64 reference: the kernel rounds the patch values to the storage type, accumulates
     in fp32): output 1e-2 relative (16-bit output rounding); weight / bias gradient from the
     per-workgroup slabs + grouped reduce 1e-4 relative (fp32 sums of exact 16-bit products).
-    Ragged row tiles (Wo % 64 != 0), a 1 x 1 output grid, G = 1, N = 32 / 48 (B0 / padded)."""
+    Ragged row tiles (Wo % 64 != 0), a 1 x 1 output grid, G = 1, N = 32 / 48 (B0 / padded); for
+    N = 32 / 64 the LayerNorm epilogue (OverlapPatchEmbed.norm) against cmx_layernorm_fwd on the
+    same stored conv output, bit for bit."""
     from rgbx_semantic_segmentation_amd import deferred
     from rgbx_semantic_segmentation_amd import kernels as K
     torch.manual_seed(5)
@@ -263,8 +265,21 @@ def test_pe1_direct_conv(dev, G, B, H, W, N, dt):
     Wt[:, :, :147] = (torch.randn(G, N, 147, device=dev) / math.sqrt(147)).to(dt)
     bias = torch.randn(G, N, device=dev)
     y = torch.full((G, B * Ho * Wo, N), float("nan"), device=dev, dtype=dt)
+    fuse_ln = N in (32, 64)
+    gamma = torch.randn(G, N, device=dev) if fuse_ln else None
+    beta = torch.randn(G, N, device=dev) if fuse_ln else None
+    y_ln = torch.empty_like(y) if fuse_ln else None
+    mean = torch.empty(G * B * Ho * Wo, device=dev) if fuse_ln else None
+    rstd = torch.empty_like(mean) if fuse_ln else None
     K.call("cmx_pe1_conv_fwd", K.ptr(img[0]), K.ptr(img[-1]) if G == 2 else 0, K.ptr(Wt), K.ptr(bias), K.ptr(y), G, B,
-           3, H, W, 7, 7, 4, 3, Ho, Wo, N, Kp, Wt.stride(0), bias.stride(0), y.stride(0), K.dtype_code(y), K.stream())
+           3, H, W, 7, 7, 4, 3, Ho, Wo, N, Kp, Wt.stride(0), bias.stride(0), y.stride(0), K.ptr(gamma), K.ptr(beta),
+           K.ptr(y_ln), K.ptr(mean), K.ptr(rstd), N, 1e-5, K.dtype_code(y), K.stream())
+    if fuse_ln:
+        # the fused LayerNorm epilogue (OverlapPatchEmbed.norm) = cmx_layernorm_fwd on the stored y, bit for bit
+        ref_ln, ref_mean, ref_rstd = K.layernorm_fwd(y, gamma, beta, 1e-5, G=G)
+        torch.cuda.synchronize()
+        assert torch.equal(y_ln, ref_ln.view_as(y_ln)), (y_ln.float() - ref_ln.view_as(y_ln).float()).abs().max()
+        assert torch.equal(mean, ref_mean.view(-1)) and torch.equal(rstd, ref_rstd.view(-1))
     dy = torch.randn(G, B * Ho * Wo, N, device=dev).to(dt)
     nblk = K.query("cmx_pe1_conv_wgrad_nblk", B, Ho, Wo)
     ws = torch.empty(G, nblk, N, Kp + 1, device=dev)
