@@ -21,7 +21,14 @@
 // a device global that the last block resets).
 #include "cmx_common.h"
 
+// step-count tickets: a block takes a ticket of its group of ADAMW_GRP consecutive blocks; the
+// last of a group takes one of the top-level ticket; the last of those stores t.  One counter
+// for 65 K blocks serialised 65 K atomics on one address (770 us per launch); spread over 1024
+// group counters they overlap (no more than 64 arrivals per address).
+constexpr int ADAMW_GRP = 64;
+constexpr int ADAMW_NGRP = 4096;
 __device__ unsigned int g_adamw_ticket = 0;
+__device__ unsigned int g_adamw_grp_ticket[ADAMW_NGRP];
 
 // S = the weight shadow's 16-bit type (bf16 or f16, the compute dtype's GEMM operand)
 template <typename S>
@@ -82,10 +89,16 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
   if (threadIdx.x == 0) {
     // relaxed: every thread of this block consumed t_prev before the barrier above (an
     // acquire / release here would write back and invalidate the L2 once per block)
-    const unsigned prev = __hip_atomic_fetch_add(&g_adamw_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1) {
-      __hip_atomic_store(&g_adamw_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *step_ptr = (float)t;
+    const unsigned grp = blockIdx.x / ADAMW_GRP, ngrp = (gridDim.x + ADAMW_GRP - 1) / ADAMW_GRP;
+    const unsigned gsize = min((unsigned)ADAMW_GRP, gridDim.x - grp * ADAMW_GRP);
+    const unsigned pg = __hip_atomic_fetch_add(&g_adamw_grp_ticket[grp], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (pg == gsize - 1) {
+      __hip_atomic_store(&g_adamw_grp_ticket[grp], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned prev = __hip_atomic_fetch_add(&g_adamw_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == ngrp - 1) {
+        __hip_atomic_store(&g_adamw_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *step_ptr = (float)t;
+      }
     }
   }
 }
@@ -135,8 +148,12 @@ int cmx_adamw_step_scaled(float* p, const float* g, float* m, float* v, void* sh
                           const float* found_inf, hipStream_t s) {
   CMX_REQUIRE(n % 64 == 0, CMX_ERR_SHAPE, "adamw: n must be a multiple of 64");
   CMX_REQUIRE(!shadow || shadow_dtype == 1 || shadow_dtype == 2, CMX_ERR_DTYPE, "adamw: shadow dtype %d", shadow_dtype);
+  // CMX_ADAMW_BLOCKS caps the grid (A/B knob; each block takes one relaxed ticket, so the
+  // cap is a scheduling choice, not a correctness one)
+  static int& cap = cmx_knob("ADAMW_BLOCKS", 0);
   long blocks = (n / 4 + 255) / 256;
-  if (blocks > 2048) blocks = 2048;            // 2048 arrivals on the step ticket per launch
+  if (cap > 0 && blocks > cap) blocks = cap;
+  CMX_REQUIRE(blocks <= (long)ADAMW_GRP * ADAMW_NGRP, CMX_ERR_SHAPE, "adamw: %ld blocks exceed the ticket groups", blocks);
   if (shadow_dtype == 2)
     hipLaunchKernelGGL(adamw_kernel<f16>, dim3((unsigned)blocks), dim3(256), 0, s, p, g, m, v, (f16*)shadow, decay64,
                        (long)n, lr_ptr, step_ptr, beta1, beta2, eps, weight_decay, grad_scale, loss_scale, found_inf);

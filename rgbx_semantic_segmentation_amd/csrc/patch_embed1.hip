@@ -24,56 +24,99 @@ constexpr int TW = 64;                          // output pixels per tile
 constexpr int PW = (TW - 1) * PE_S + PE_K;      // 259 input columns per tile row
 constexpr int PWP = 260;                        // LDS pitch of a patch row (floats)
 constexpr int IMG = 64 * 64 * 2;                // one 64 x 64 16-bit operand image (8 KB)
-constexpr int PATCH_BYTES = PE_C * PE_K * PWP * 4;   // 21.8 KB
+constexpr int PROWS = PE_C * PE_K + 1;          // 21 footprint rows + one zero row (columns k >= 147)
+constexpr int KPAD = 192;                       // patch-matrix columns of the three 64-wide k images
+constexpr int PATCH_BYTES = PROWS * PWP * 4 + KPAD * 4;   // footprint (22.9 KB) + column offset table
 
-// the tile's input footprint: rows iy0 .. iy0 + 6, columns ix0 .. ix0 + 258 of the 3 planes
-__device__ __forceinline__ void stage_patch(const float* __restrict__ img, float* patch, int H, int W, int iy0,
-                                            int ix0) {
-  for (int e = threadIdx.x; e < PE_C * PE_K * PW; e += 256) {
+// the tile's input footprint: rows iy0 .. iy0 + 6, columns ix0 .. ix0 + 258 of the 3 planes,
+// PL values per thread (consecutive threads -> consecutive columns: coalesced).  Every load is
+// issued (an out-of-image element reads the plane's first value and is zeroed on the way in),
+// so all PL are in flight together and a thread has exactly PL loads outstanding -- the weight
+// gradient prefetches the next tile's footprint during this tile's MFMAs and waits on
+// vmcnt(PL) for its own DMA (a serial load-then-store loop had one load in flight per thread:
+// ~40 us per tile of latency).
+constexpr int PATCH_N = PE_C * PE_K * PW;       // 5439
+constexpr int PL = (PATCH_N + 255) / 256;       // 22 values per thread
+struct PatchRegs {
+  float v[PL];
+};
+
+__device__ __forceinline__ void load_patch(const float* __restrict__ img, PatchRegs& r, int H, int W, int iy0,
+                                           int ix0) {
+#pragma unroll
+  for (int u = 0; u < PL; ++u) {
+    const int e = threadIdx.x + u * 256;
     const int cr = e / PW, col = e - cr * PW;   // cr = c * 7 + r
-    const int c = cr / PE_K, r = cr - c * PE_K;
-    const int iy = iy0 + r, ix = ix0 + col;
-    patch[cr * PWP + col] = (iy >= 0 && iy < H && ix >= 0 && ix < W) ? img[((long)c * H + iy) * W + ix] : 0.f;
+    const int c = cr / PE_K, kr = cr - c * PE_K;
+    const int iy = iy0 + kr, ix = ix0 + col;
+    const bool in = e < PATCH_N && iy >= 0 && iy < H && ix >= 0 && ix < W;
+    const long off = in ? ((long)c * H + iy) * W + ix : 0;
+    const float v = img[off];
+    r.v[u] = in ? v : 0.f;
+  }
+}
+
+__device__ __forceinline__ void store_patch(float* patch, const PatchRegs& r) {
+#pragma unroll
+  for (int u = 0; u < PL; ++u) {
+    const int e = threadIdx.x + u * 256;
+    if (e < PATCH_N) {
+      const int cr = e / PW, col = e - cr * PW;
+      patch[cr * PWP + col] = r.v[u];
+    }
+  }
+}
+
+// once per workgroup: the zero row, and koff[k] = LDS offset of patch-matrix column k at pixel 0
+// (column k = (c, kh, kw) reads footprint row c*7 + kh at column 4 px + kw; k >= 147 reads the
+// zero row), so a chunk of 8 columns is two table reads and 8 adds -- no index arithmetic.
+// Pixels past the tile's last output column need no masking: their dy rows are zero (weight
+// gradient) or their outputs are not stored (forward), and the footprint there is finite data.
+__device__ __forceinline__ void init_patch_consts(float* patch, int* koff) {
+  for (int i = threadIdx.x; i < PWP; i += 256) patch[(PROWS - 1) * PWP + i] = 0.f;
+  for (int k = threadIdx.x; k < KPAD; k += 256) {
+    int o = (PROWS - 1) * PWP;
+    if (k < PE_KR) {
+      const int c = k / (PE_K * PE_K), rr = k - c * (PE_K * PE_K), kh = rr / PE_K, kw = rr - kh * PE_K;
+      o = (c * PE_K + kh) * PWP + kw;
+    }
+    koff[k] = o;
   }
 }
 
 // 8 patch-matrix entries (pixel px, columns k0 .. k0 + 7) as packed 16-bit values
 template <typename E>
-__device__ __forceinline__ uint4 patch_chunk(const float* patch, int px, int k0, bool live) {
-  float v[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int k = k0 + e;
-    float val = 0.f;
-    if (live && k < PE_KR) {
-      const int c = k / (PE_K * PE_K), rr = k - c * (PE_K * PE_K);
-      const int kh = rr / PE_K, kw = rr - kh * PE_K;
-      val = patch[(c * PE_K + kh) * PWP + px * PE_S + kw];
-    }
-    v[e] = val;
-  }
-  return make_uint4(pack2<E>(v[0], v[1]), pack2<E>(v[2], v[3]), pack2<E>(v[4], v[5]), pack2<E>(v[6], v[7]));
+__device__ __forceinline__ uint4 patch_chunk(const float* patch, const int* koff, int px, int k0) {
+  const int4 o0 = *reinterpret_cast<const int4*>(koff + k0);
+  const int4 o1 = *reinterpret_cast<const int4*>(koff + k0 + 4);
+  const float* pp = patch + px * PE_S;
+  return make_uint4(pack2<E>(pp[o0.x], pp[o0.y]), pack2<E>(pp[o0.z], pp[o0.w]), pack2<E>(pp[o1.x], pp[o1.y]),
+                    pack2<E>(pp[o1.z], pp[o1.w]));
 }
 
 // forward operand: three k-contiguous images [64 px][64 k] (gemm_kernels.h stage_k layout:
 // chunk c of row r at position c ^ ((r >> 1) & 7)), read with frag_k
 template <typename E>
-__device__ __forceinline__ void build_patches_k(const float* patch, char* img, int npx) {
-  for (int it = threadIdx.x; it < TW * 24; it += 256) {
+__device__ __forceinline__ void build_patches_k(const float* patch, const int* koff, char* img) {
+#pragma unroll
+  for (int j = 0; j < TW * 24 / 256; ++j) {
+    const int it = threadIdx.x + j * 256;
     const int px = it / 24, cc = it - px * 24, kc = cc >> 3, c8 = cc & 7;
     *reinterpret_cast<uint4*>(img + kc * IMG + px * 128 + ((c8 ^ ((px >> 1) & 7)) << 4)) =
-        patch_chunk<E>(patch, px, cc * 8, px < npx);
+        patch_chunk<E>(patch, koff, px, cc * 8);
   }
 }
 
 // weight-gradient operand: three pixel-row images [64 px][64 k] in the transposed layout
 // (stage_r: chunk c of k-row px at position c ^ tr_swz<64>(px)), read with frag_r
 template <typename E>
-__device__ __forceinline__ void build_patches_r(const float* patch, char* img, int npx) {
-  for (int it = threadIdx.x; it < TW * 24; it += 256) {
+__device__ __forceinline__ void build_patches_r(const float* patch, const int* koff, char* img) {
+#pragma unroll
+  for (int j = 0; j < TW * 24 / 256; ++j) {
+    const int it = threadIdx.x + j * 256;
     const int px = it / 24, cc = it - px * 24, kc = cc >> 3, c8 = cc & 7;
     *reinterpret_cast<uint4*>(img + kc * IMG + px * 128 + ((c8 ^ tr_swz<64>(px)) << 4)) =
-        patch_chunk<E>(patch, px, cc * 8, px < npx);
+        patch_chunk<E>(patch, koff, px, cc * 8);
   }
 }
 
@@ -101,6 +144,8 @@ __global__ __launch_bounds__(256) void pe1_fwd_kernel(const float* __restrict__ 
   char* pimg = smem;                            // 3 patch images
   char* wimg = smem + 3 * IMG;                  // 3 weight images
   float* patch = reinterpret_cast<float*>(smem + 6 * IMG);
+  int* koff = reinterpret_cast<int*>(patch + PROWS * PWP);
+  init_patch_consts(patch, koff);
   const int g = blockIdx.z, b = blockIdx.y;
   const int tpr = (Wo + TW - 1) / TW;
   const int oy = blockIdx.x / tpr, ox0 = (blockIdx.x - oy * tpr) * TW;
@@ -110,9 +155,13 @@ __global__ __launch_bounds__(256) void pe1_fwd_kernel(const float* __restrict__ 
   const i32x4 rW = make_rsrc(Wt + (long)g * sW);
 #pragma unroll
   for (int kc = 0; kc < 3; ++kc) stage_k<64>(rW, wimg + kc * IMG, Kp, 0, N, kc * 64, Kp, w, lane);
-  stage_patch(img, patch, H, W, oy * PE_S - PE_P, ox0 * PE_S - PE_P);
+  {
+    PatchRegs pr;
+    load_patch(img, pr, H, W, oy * PE_S - PE_P, ox0 * PE_S - PE_P);
+    store_patch(patch, pr);
+  }
   __syncthreads();
-  build_patches_k<E>(patch, pimg, npx);
+  build_patches_k<E>(patch, koff, pimg);
   vm_wait<0>();
   __syncthreads();
   f32x16 acc = zero16();
@@ -184,6 +233,8 @@ __global__ __launch_bounds__(256) void pe1_wgrad_kernel(const E* __restrict__ dy
   char* aimg = smem;                            // dy tile, transposed layout
   char* pimg = smem + IMG;                      // 3 patch images, transposed layout
   float* patch = reinterpret_cast<float*>(smem + 4 * IMG);
+  int* koff = reinterpret_cast<int*>(patch + PROWS * PWP);
+  init_patch_consts(patch, koff);
   const int g = blockIdx.y, nblk = gridDim.x;
   const int tpr = (Wo + TW - 1) / TW, tpi = Ho * tpr, ntile = B * tpi;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
@@ -195,16 +246,37 @@ __global__ __launch_bounds__(256) void pe1_wgrad_kernel(const E* __restrict__ dy
   f32x16 acc[3], accd = zero16();
 #pragma unroll
   for (int kc = 0; kc < 3; ++kc) acc[kc] = zero16();
-  const int t1 = min(ntile, (blockIdx.x + 1) * tpb);
-  for (int t = blockIdx.x * tpb; t < t1; ++t) {
-    const int b = t / tpi, rem = t - b * tpi, oy = rem / tpr, ox0 = (rem - oy * tpr) * TW;
+  const int t0 = blockIdx.x * tpb, t1 = min(ntile, t0 + tpb);
+  auto tile_of = [&](int t, int& b, int& oy, int& ox0) {
+    b = t / tpi;
+    const int rem = t - b * tpi;
+    oy = rem / tpr;
+    ox0 = (rem - oy * tpr) * TW;
+  };
+  PatchRegs pr;                                 // the footprint of the tile being staged next
+  if (t0 < t1) {
+    int b, oy, ox0;
+    tile_of(t0, b, oy, ox0);
+    load_patch(imgs + (long)b * PE_C * H * W, pr, H, W, oy * PE_S - PE_P, ox0 * PE_S - PE_P);
+  }
+  for (int t = t0; t < t1; ++t) {
+    int b, oy, ox0;
+    tile_of(t, b, oy, ox0);
     const int npx = min(TW, Wo - ox0);
     const int m0 = (b * Ho + oy) * Wo + ox0;
+    store_patch(patch, pr);                     // waits for this tile's footprint loads
     stage_r<64>(rdy, aimg, N, 0, N, m0, m0 + npx, w, lane);
-    stage_patch(imgs + (long)b * PE_C * H * W, patch, H, W, oy * PE_S - PE_P, ox0 * PE_S - PE_P);
     __syncthreads();
-    build_patches_r<E>(patch, pimg, npx);
-    vm_wait<0>();
+    if (t + 1 < t1) {                           // next tile's footprint in flight during this one
+      int b2, oy2, ox2;
+      tile_of(t + 1, b2, oy2, ox2);
+      load_patch(imgs + (long)b2 * PE_C * H * W, pr, H, W, oy2 * PE_S - PE_P, ox2 * PE_S - PE_P);
+      build_patches_r<E>(patch, koff, pimg);
+      vm_wait<PL>();                            // the dy DMA (issued before the PL prefetch loads)
+    } else {
+      build_patches_r<E>(patch, koff, pimg);
+      vm_wait<0>();
+    }
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -234,7 +306,7 @@ __global__ __launch_bounds__(256) void pe1_wgrad_kernel(const E* __restrict__ dy
   }
 }
 
-constexpr int PE1_TPB = 8;                      // tiles per weight-gradient workgroup
+constexpr int PE1_TPB = 4;                      // tiles per weight-gradient workgroup (360 at B2 480 x 640: one round, two per CU)
 
 int pe1_check(int N, int Kp, int KH, int KW, int stride, int pad, int C) {
   CMX_REQUIRE(C == PE_C && KH == PE_K && KW == PE_K && stride == PE_S && pad == PE_P, CMX_ERR_SHAPE,

@@ -959,10 +959,27 @@ int pick_qw(int N, int heads, int Bt) {
 // the work over 2.5-4x more CUs (measured: dQ 17.7 -> 14.8 us at stages 3 and 4; 4-wave
 // workgroups at stage 2 (152 -> 304) were slower, 13.8 -> 16.4 us forward).  Every workgroup
 // stages the (b, head)'s K / V (L2-resident after the first): only L2 -> LDS traffic.
+// 10 waves when the 8-wave grid overflows one workgroup per CU and the 10-wave grid does not
+// (stage 1 of B2 480 x 640: 300 -> 240 workgroups; measured fwd 19.6 -> 15.9 us, bwd 69.2 ->
+// 61.6 us; the 44 CUs that ran a second 8-wave workgroup set the launch time.  At stage 2 the
+// 8-wave grid already fits, and 10 waves were slower: 11.7 -> 14.2 us forward)
+int sra_cus() {
+  static const int n = [] {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                               hipSuccess)
+      c = 0;
+    return c > 0 ? c : 256;
+  }();
+  return n;
+}
+
 int pick_nw(int N, int heads, int Bt, int qw) {
   static int& force = cmx_knob("SRA_NW", 0);     // 2 / 4 / 8 / 10 waves per workgroup (A/B), 0 = auto
   if (force == 2 || force == 4 || force == 8) return qw == 2 && force == 2 ? 4 : force;
   if (force == 10 && qw == 1) return 10;
+  if (qw == 1 && (long)cdiv(N, 32 * NWAVE) * heads * Bt > sra_cus() && (long)cdiv(N, 320) * heads * Bt <= sra_cus())
+    return 10;
   if (qw == 2 || (long)cdiv(N, 32 * NWAVE) * heads * Bt >= 128) return NWAVE;
   return 2;
 }
