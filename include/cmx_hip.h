@@ -192,14 +192,14 @@ int cmx_upsample_ce_bwd(const void* logits, const int64_t* label, const float* d
  * reducer applies the epilogue); splitk <= 0: the library's choice, cmx_gemm_splitk(). */
 size_t cmx_gemm_workspace(int G, int M, int N, int splitk);
 int cmx_gemm_splitk(int G, int M, int N, int K, int ones_col, int dtype);
-int cmx_gemm(const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R, const float* rscale, float* dbias, float* workspace, int G, int M, int N, int K, int K1, int64_t lda, int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias, int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode, int ones_col, int splitk, int dtype, hipStream_t stream);
+int cmx_gemm(const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R, const float* rscale, const void* mask, float* dbias, float* workspace, int G, int M, int N, int K, int K1, int64_t lda, int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias, int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode, int ones_col, int splitk, int dtype, hipStream_t stream);
 /* ---- independent GEMMs in ONE launch: Attention.q beside Attention.kv (dual_segformer.py:114-121, forward and
  *      dgrad) and the decoder's linear_c1..c4 (MLPDecoder.py:66-73).  cmx_gemm_plan takes cmx_gemm's arguments
  *      and fills a plan (host memory of cmx_gemm_plan_size() bytes) instead of launching: > 0 = block count,
  *      0 = not eligible (16-bit 64 x 64-tile problems without split-K / bias-gradient column only; the caller
  *      runs cmx_gemm), < 0 = invalid.  cmx_gemm_multi launches n <= 4 plans of one dtype and B layout. */
 size_t cmx_gemm_plan_size(void);
-int cmx_gemm_plan(void* plan, const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R, const float* rscale, float* dbias, float* workspace, int G, int M, int N, int K, int K1, int64_t lda, int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias, int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode, int ones_col, int splitk, int dtype);
+int cmx_gemm_plan(void* plan, const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R, const float* rscale, const void* mask, float* dbias, float* workspace, int G, int M, int N, int K, int K1, int64_t lda, int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias, int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode, int ones_col, int splitk, int dtype);
 int cmx_gemm_multi(const void* plans, int n, hipStream_t stream);
 /* cmx_gemm_h2: cmx_gemm (no A2 / bias / residual / epilogue extras) over a two-level batch of G = Go * gh
  *      problems: problem g reads / writes at (g / gh) * sX + (g % gh) * sXh -- the per-head k^T v,

@@ -147,7 +147,7 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
               int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode, int ones_col, int splitk,
               int dtype, hipStream_t s, const UpSpec* up, int scR = 0, int scH = 0, int scW = 0, int scC = 0,
               int scHo = 0, int scWo = 0, int gh = 1, int64_t sAh = 0, int64_t sBh = 0, int64_t sCh = 0,
-              GemmPlan* plan = nullptr) {
+              GemmPlan* plan = nullptr, const void* mask = nullptr) {
   CMX_REQUIRE(G > 0 && M > 0 && N > 0 && K > 0, CMX_ERR_SHAPE, "gemm: empty problem G=%d M=%d N=%d K=%d", G, M, N, K);
   CMX_REQUIRE(dtype >= 0 && dtype <= 2, CMX_ERR_DTYPE, "gemm: unsupported dtype %d", dtype);
   CMX_REQUIRE(out_mode >= 0 && out_mode <= 2 && act >= 0 && act <= 3, CMX_ERR_ARG, "gemm: out_mode/act");
@@ -173,6 +173,9 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
   a.A = A; a.A2 = A2; a.B = B; a.C = C; a.bias = bias; a.R = R; a.rscale = rscale; a.dbias = dbias; a.ws = workspace;
   a.G = G; a.M = M; a.N = N; a.K = K; a.K1 = K1; a.rows_per_sample = rows_per_sample > 0 ? rows_per_sample : 1;
   a.act = act; a.out_mode = out_mode; a.ones_col = ones_col; a.vec = vec;
+  CMX_REQUIRE(!mask || (out_mode == 0 && !ones_col && (uintptr_t)mask % 16 == 0 && (!R || R != mask)), CMX_ERR_ARG,
+              "gemm: a ReLU mask needs a plain store in C's layout");
+  a.mask = mask;
   // 8-column epilogue groups as aligned vectors: C (and R) rows start on 16-B boundaries
   const long esz = out_mode == 0 ? (dtype != 0 ? 2 : 4) : 4;
   a.cvec = ((uintptr_t)C % 16 == 0) && (ldc * esz) % 16 == 0 && (sC * esz) % 16 == 0 &&
@@ -258,12 +261,13 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
 extern "C" {
 
 int cmx_gemm(const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R,
-             const float* rscale, float* dbias, float* workspace, int G, int M, int N, int K, int K1, int64_t lda,
-             int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias,
-             int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode, int ones_col, int splitk,
-             int dtype, hipStream_t s) {
+             const float* rscale, const void* mask, float* dbias, float* workspace, int G, int M, int N, int K, int K1,
+             int64_t lda, int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC,
+             int64_t sbias, int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode,
+             int ones_col, int splitk, int dtype, hipStream_t s) {
   return gemm_impl(A, A2, B, C, bias, R, rscale, dbias, workspace, G, M, N, K, K1, lda, lda2, ldb, ldc, sA, sA2, sB,
-                   sC, sbias, sdb, rows_per_sample, transA, transB, act, out_mode, ones_col, splitk, dtype, s, nullptr);
+                   sC, sbias, sdb, rows_per_sample, transA, transB, act, out_mode, ones_col, splitk, dtype, s, nullptr,
+                   0, 0, 0, 0, 0, 0, 1, 0, 0, 0, nullptr, mask);
 }
 
 size_t cmx_gemm_plan_size(void) { return sizeof(GemmPlan); }
@@ -271,14 +275,15 @@ size_t cmx_gemm_plan_size(void) { return sizeof(GemmPlan); }
 // cmx_gemm's arguments, planned instead of launched: > 0 = the problem's block count (eligible
 // for cmx_gemm_multi), 0 = not eligible (run it with cmx_gemm), < 0 = invalid arguments
 int cmx_gemm_plan(void* plan, const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R,
-                  const float* rscale, float* dbias, float* workspace, int G, int M, int N, int K, int K1, int64_t lda,
+                  const float* rscale, const void* mask, float* dbias, float* workspace, int G, int M, int N, int K,
+                  int K1, int64_t lda,
                   int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC,
                   int64_t sbias, int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode,
                   int ones_col, int splitk, int dtype) {
   CMX_REQUIRE(plan, CMX_ERR_ARG, "gemm_plan: null plan");
   return gemm_impl(A, A2, B, C, bias, R, rscale, dbias, workspace, G, M, N, K, K1, lda, lda2, ldb, ldc, sA, sA2, sB,
                    sC, sbias, sdb, rows_per_sample, transA, transB, act, out_mode, ones_col, splitk, dtype, nullptr,
-                   nullptr, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, reinterpret_cast<GemmPlan*>(plan));
+                   nullptr, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, reinterpret_cast<GemmPlan*>(plan), mask);
 }
 
 // n <= 4 planned problems (same dtype and B layout) in ONE launch; waves / ring depth chosen for

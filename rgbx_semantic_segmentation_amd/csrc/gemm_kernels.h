@@ -34,6 +34,9 @@ struct GemmArgs {
   // the plain stride g * sX
   int gh;
   long sAh, sBh, sCh;
+  // ReLU-backward mask (NULL: none): after the residual, C(i, j) = 0 where mask(i, j) <= 0; the
+  // mask has C's layout and dtype (the saved ReLU output of the layer whose gradient this is)
+  const void* mask;
 };
 
 // block id -> tile id, giving each of the 8 XCDs (hardware deals block b to XCD b % 8) a
@@ -141,6 +144,7 @@ __device__ __forceinline__ void epi_store(const GemmArgs& p, int g, int i, int j
     const float sc = p.rscale ? p.rscale[((long)g * p.M + i) / p.rows_per_sample] : 1.f;
     v = to_f32(reinterpret_cast<const T*>(p.R)[off]) + sc * v;
   }
+  if (p.mask && !(to_f32(reinterpret_cast<const T*>(p.mask)[off]) > 0.f)) v = 0.f;
   if (p.out_mode == 0) reinterpret_cast<T*>(p.C)[off] = from_f32<T>(v);
   else if (p.out_mode == 1) reinterpret_cast<float*>(p.C)[off] = v;
   else reinterpret_cast<float*>(p.C)[off] += v;
@@ -177,6 +181,13 @@ __device__ __forceinline__ void epi_store8(const GemmArgs& p, int g, int i, int 
     if constexpr (sizeof(T) == 4) load_vec<T>(reinterpret_cast<const T*>(p.R) + off + 4, rv + 4);
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = rv[e] + sc * v[e];
+  }
+  if (p.mask) {
+    float mv[8];
+    load_vec<T>(reinterpret_cast<const T*>(p.mask) + off, mv);
+    if constexpr (sizeof(T) == 4) load_vec<T>(reinterpret_cast<const T*>(p.mask) + off + 4, mv + 4);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = mv[e] > 0.f ? v[e] : 0.f;
   }
   if (p.out_mode == 0) {
     store_vec<T>(reinterpret_cast<T*>(p.C) + off, v);

@@ -919,16 +919,18 @@ class CrossPathF(Function):
         dy, du = da[..., :C], da[..., C:]
         # end_proj on cat(y, v): dy into the first half of da, dv apart; the residual passes de
         dv = torch.empty_like(v)
-        _gemm_group([dict(A=de, B=Wend[:, :, :C].transpose(1, 2), C=dy),        # one launch
+        # dy goes straight into dz's first half: ReLU'(y) applied in the epilogue (mask = y)
+        _gemm_group([dict(A=de, B=Wend[:, :, :C].transpose(1, 2), C=dy, mask=y),    # one launch
                      dict(A=de, B=Wend[:, :, C:].transpose(1, 2), C=dv)])
         _wgrad_into(de, y, Wgend[:, :, :C], bgend)
         _wgrad_into(de, v, Wgend[:, :, C:])
         # attention: du (second half of da) = dout @ ctx^T per head, then += dkv @ Wkv (kv's dgrad)
         dkv = _cross_attn_bwd(dv, u, kv, P, ctxT, B, N, heads, D, du)
-        K.gemm(dkv, Wkv.transpose(1, 2), du, residual=du)
+        # du += dkv @ Wkv, then ReLU'(u) (mask = u): da is dz = relu'(a) * da, no act_bwd pass
+        K.gemm(dkv, Wkv.transpose(1, 2), du, residual=du, mask=u)
         _wgrad_into(dkv, u, Wgkv)
-        # channel_proj + ReLU: dx = relu'(a) * da @ Wcp + de (residual epilogue)
-        dz = K.act_bwd(da, a, "relu")
+        # channel_proj + ReLU: dx = dz @ Wcp + de (residual epilogue)
+        dz = da
         dx = torch.empty_like(x)
         K.gemm(dz, Wcp.transpose(1, 2), dx, residual=de)
         _wgrad_into(dz, x, Wgcp, bgcp)

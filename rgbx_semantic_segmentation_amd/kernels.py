@@ -122,7 +122,7 @@ def _operand(t: torch.Tensor, name: str):
 def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, bias: torch.Tensor | None = None,
          residual: torch.Tensor | None = None, rscale: torch.Tensor | None = None, rows_per_sample: int = 1,
          act: str = "none", out_mode: int = 0, A2: torch.Tensor | None = None, dbias: torch.Tensor | None = None,
-         splitk: int = 0, plan: bool = False):
+         splitk: int = 0, plan: bool = False, mask: torch.Tensor | None = None):
     """C[g] = epi([A[g] | A2[g]] @ B[g]^T) on logical views A (G, M, K1), A2 (G, M, K-K1),
     B (G, N, K), C (G, M, N).
 
@@ -133,6 +133,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, bias: torch.Tensor |
     dbias (G, M) fp32: also produce sum_k A(i, k) (the bias gradient of a wgrad).
     splitk > 1 splits K over blocks into fp32 slabs reduced with the epilogue applied;
     0 = the library's choice (cmx_gemm_splitk: fill the chip when the output has few tiles).
+    mask (C's layout and dtype): C = 0 where mask <= 0, after the residual (a ReLU backward).
     plan=True: nothing is launched; returns a GemmPlan for gemm_multi, or None when the problem
     is not eligible for a multi launch (the caller then runs gemm as usual)."""
     G, M, K1 = A.shape
@@ -154,6 +155,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, bias: torch.Tensor |
         sdb = dbias.stride(0) if dbias.dim() == 2 else 0
     if residual is not None:
         assert residual.shape == C.shape and residual.stride() == C.stride() and residual.dtype == C.dtype
+    if mask is not None:
+        assert mask.shape == C.shape and mask.stride() == C.stride() and mask.dtype == C.dtype and out_mode == 0
     Nk = N + (1 if dbias is not None else 0)
     if splitk <= 0:
         splitk = query("cmx_gemm_splitk", G, M, Nk, Kd, int(dbias is not None), dtype_code(A))
@@ -164,13 +167,13 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, bias: torch.Tensor |
             return None
         rec = (ctypes.c_uint8 * _PLAN_BYTES)()
         nb = query("cmx_gemm_plan", ctypes.addressof(rec), ptr(A), ptr(A2), ptr(B), ptr(C), ptr(bias), ptr(residual),
-                   ptr(rscale), ptr(dbias), 0, *args)
+                   ptr(rscale), ptr(mask), ptr(dbias), 0, *args)
         if nb < 0:
             raise _lib.CMXError(f"cmx_gemm_plan failed ({nb}): {_lib.last_error()}")
-        return GemmPlan(rec, (A, A2, B, C, bias, residual, rscale)) if nb > 0 else None
+        return GemmPlan(rec, (A, A2, B, C, bias, residual, rscale, mask)) if nb > 0 else None
     ws = _ws(query("cmx_gemm_workspace", G, M, Nk, splitk), A.device) if splitk > 1 else None
-    call("cmx_gemm", ptr(A), ptr(A2), ptr(B), ptr(C), ptr(bias), ptr(residual), ptr(rscale), ptr(dbias), ptr(ws),
-         *args, stream())
+    call("cmx_gemm", ptr(A), ptr(A2), ptr(B), ptr(C), ptr(bias), ptr(residual), ptr(rscale), ptr(mask), ptr(dbias),
+         ptr(ws), *args, stream())
     return C
 
 

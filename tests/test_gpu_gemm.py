@@ -73,6 +73,28 @@ def test_gemm_epilogues(dev, dtype, act, res, K):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("K,res", [(96, True), (2048, True), (128, False)])
+def test_gemm_relu_mask_epilogue(dev, dtype, K, res):
+    """ReLU-backward mask epilogue (CrossPath's channel_proj ReLU, net_utils.py:273-274):
+    C = (R + A B^T) * [mask > 0], in place over a column half of a wider buffer (the FFM's
+    [dy | du] gradient), through the tile path and (K = 2048) the split-K reducer."""
+    torch.manual_seed(9)
+    from rgbx_semantic_segmentation_amd import kernels as Kn
+    G, M, N = 2, 600, 96
+    A = torch.randn(G, M, K, device="cuda").to(dtype)
+    B = (torch.randn(G, N, K, device="cuda") / K ** 0.5).to(dtype)
+    buf = torch.randn(G, M, 2 * N, device="cuda").to(dtype)
+    act = torch.relu(torch.randn(G, M, 2 * N, device="cuda")).to(dtype)
+    C, mask = buf[..., N:], act[..., N:]
+    R0 = C.float().clone()
+    Kn.gemm(A, B, C, residual=C if res else None, mask=mask)
+    ref = torch.bmm(A.float(), B.float().transpose(1, 2)) + (R0 if res else 0)
+    ref = ref * (mask.float() > 0)
+    assert rel(C, ref) < (1e-5 if dtype == torch.float32 else 1e-2)
+    assert bool((C.float()[mask.float() <= 0] == 0).all())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_gemm_fp32_out_and_accumulate(dev, dtype):
     torch.manual_seed(2)
     from rgbx_semantic_segmentation_amd import kernels as Kn
