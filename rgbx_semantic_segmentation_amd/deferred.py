@@ -252,6 +252,8 @@ def _issue() -> None:
             cur.wait_stream(st)
             for t in keep:
                 t.record_stream(cur)
+    # the grouped-GEMM records and the reduce records share ONE pinned table and ONE upload
+    gtab = None
     if gemms or convs:
         # one record per problem: (G, M, N incl. bias column, K, has_bias) drives split and slabs
         dims = [(a[4], a[5], a[6], a[7], a[3] is not None) for a in gemms]
@@ -262,22 +264,25 @@ def _issue() -> None:
         sizes = [query("cmx_gemm_workspace", G, M, N, s) if s > 1 else 0 for (G, M, N, K, hb), s in zip(dims, splits)]
         arena = torch.empty(max(1, sum((z + 255) // 256 * 64 for z in sizes)), dtype=torch.float32, device=device)
         nrec = len(dims)
-        order = list(range(nrec))
-        table = _table(nrec * _GREC)
+        gbytes = (nrec * _GREC + 255) // 256 * 256
+        # the reduce records follow the GEMM records: size the table for both (every split-K
+        # problem adds at most two reduce records)
+        nred_max = len(reds) + 2 * sum(1 for s in splits if s > 1)
+        table = _table(gbytes + nred_max * _RREC)
         base = table.data_ptr()
         blk, off = 0, 0
-        for pos, i in enumerate(order):
+        for i in range(nrec):
             s, sz = splits[i], sizes[i]
             ws = arena.data_ptr() + off if s > 1 else 0
             if i < len(gemms):
                 A, B, Wg, bg, G, M, N, K, lda, ldb, ldc, sA, sB, sC, sdb = gemms[i]
-                nb = LIB.cmx_gemm_group_pack(base + pos * _GREC, ptr(A), ptr(B), ptr(Wg), ptr(bg), ws, G, M, N, K, lda,
+                nb = LIB.cmx_gemm_group_pack(base + i * _GREC, ptr(A), ptr(B), ptr(Wg), ptr(bg), ws, G, M, N, K, lda,
                                              ldb, ldc, sA, sB, sC, sdb, 1, 1, 1, int(bg is not None), s, blk)
                 dst = Wg.data_ptr()
             else:
                 (dy, x, Wg, bg, G, NIg, H, W, C, KH, KW, st, pad, Ho, Wo, Nout, tap, sdy, sx, sC, sdb) = \
                     convs[i - len(gemms)]
-                nb = LIB.cmx_gemm_group_pack_conv_wgrad(base + pos * _GREC, ptr(dy), ptr(x), ptr(Wg), ptr(bg), ws, G, NIg,
+                nb = LIB.cmx_gemm_group_pack_conv_wgrad(base + i * _GREC, ptr(dy), ptr(x), ptr(Wg), ptr(bg), ws, G, NIg,
                                                         H, W, C, KH, KW, st, pad, Ho, Wo, Nout, tap, sdy, sx, sC, sdb, s,
                                                         blk)
                 M, N, ldc = Nout, C + (1 if bg is not None else 0), KH * KW * C
@@ -292,24 +297,32 @@ def _issue() -> None:
                 if bg is not None:
                     reds.append((ws + 4 * G * s * M * Nr, bg.data_ptr(), 0, G, s, s * M, M, 1, M, M, sdb, M, 0, 0, 0))
                 off += (sz + 255) // 256 * 256
-        dev = _upload(table, nrec * _GREC, device)
-        call("cmx_gemm_grouped", dev.data_ptr(), nrec, blk, dcode, stream())
-        keep.append(arena)
-        if observer is not None:
-            # algorithmic work per problem: (G, M, real N, K) and operand / result bytes
-            work = [(G, M, N - (1 if hb else 0), K) for (G, M, N, K, hb) in dims]
-            observer(dev, nrec, blk, work, keep, dcode)
+        gtab = (table, gbytes, nrec, blk, dims, arena)
     if reds:
-        table = _table(len(reds) * _RREC)
-        base = table.data_ptr()
-        blk = 0
+        if gtab is None:
+            table, gbytes = _table(len(reds) * _RREC), 0
+        else:
+            table, gbytes = gtab[0], gtab[1]
+        base = table.data_ptr() + gbytes
+        rblk = 0
         for i, r in enumerate(reds):
-            nb = LIB.cmx_reduce_pack(base + i * _RREC, *r, blk)
+            nb = LIB.cmx_reduce_pack(base + i * _RREC, *r, rblk)
             if nb <= 0:
                 raise _lib.CMXError(f"cmx_reduce_pack failed ({nb}): {_lib.last_error()}")
-            blk += nb
-        dev = _upload(table, len(reds) * _RREC, device)
-        call("cmx_reduce_grouped", dev.data_ptr(), len(reds), blk, stream())
+            rblk += nb
+    if gtab is not None or reds:
+        total = gbytes + len(reds) * _RREC
+        dev = _upload(table, total, device)
+        if gtab is not None:
+            _, _, nrec, blk, dims, arena = gtab
+            call("cmx_gemm_grouped", dev.data_ptr(), nrec, blk, dcode, stream())
+            keep.append(arena)
+            if observer is not None:
+                # algorithmic work per problem: (G, M, real N, K) and operand / result bytes
+                work = [(G, M, N - (1 if hb else 0), K) for (G, M, N, K, hb) in dims]
+                observer(dev, nrec, blk, work, keep, dcode)
+        if reds:
+            call("cmx_reduce_grouped", dev.data_ptr() + gbytes, len(reds), rblk, stream())
     # the caching allocator may hand the queued buffers out again once this stream has
     # passed the launches above (stream-ordered reuse): dropping `keep` here is safe
     del keep
