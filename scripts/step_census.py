@@ -1,5 +1,6 @@
-"""Per-step kernel census from a rocprofv3 kernel trace of bench.py: the launches between the
-last two AdamW launches (one HIP-graph replay = one step), grouped by kernel family.
+"""Per-step kernel census from a rocprofv3 kernel trace of bench.py: the launches between two
+consecutive AdamW launches (one HIP-graph replay = one step; the steady-state step of median wall
+time), grouped by kernel family.
 Usage: python scripts/step_census.py <run_results.db> [top]"""
 import collections
 import re
@@ -10,11 +11,16 @@ c = sqlite3.connect(sys.argv[1])
 top = int(sys.argv[2]) if len(sys.argv) > 2 else 40
 rows = c.execute("select start, end, name from kernels order by start").fetchall()
 idx = [i for i, r in enumerate(rows) if r[2].replace("void ", "").startswith("adamw")]
-seg = rows[idx[-2] + 1:idx[-1] + 1]
-print(f"launches/step {len(seg)}  wall {(seg[-1][1] - seg[0][0]) / 1e3:.0f} us  busy {sum(r[1] - r[0] for r in seg) / 1e3:.0f} us")
+# the step whose wall time is the median over the steady-state steps (the first three replays
+# and the bench's last, host-drained ones aside): one representative replay, not the tail
+walls = [(rows[idx[j + 1]][1] - rows[idx[j] + 1][0], j) for j in range(3, len(idx) - 1)] or [(0, len(idx) - 2)]
+pick = sorted(walls)[len(walls) // 2][1]
+seg = rows[idx[pick] + 1:idx[pick + 1] + 1]
+print(f"launches/step {len(seg)}  wall {(seg[-1][1] - seg[0][0]) / 1e3:.0f} us  busy {sum(r[1] - r[0] for r in seg) / 1e3:.0f} us"
+      f"  (step {pick + 1} of {len(idx) - 1}: median wall of the steady-state steps)")
 # idle time between one step's AdamW and the next step's first kernel (the replay boundary), and
 # the largest idle gaps inside the step
-prev = rows[idx[-2]]
+prev = rows[idx[pick]]
 print(f"boundary gap {(seg[0][0] - prev[1]) / 1e3:.1f} us after {prev[2][:40]}; first kernels: "
       + ", ".join(re.sub(r"\(.*", "", r[2].replace("void ", ""))[:30] for r in seg[:3]))
 gaps, end = [], seg[0][1]
