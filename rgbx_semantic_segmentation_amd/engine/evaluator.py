@@ -24,6 +24,7 @@ launch); ``run`` evaluates a dataset and returns the metric line.
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -77,6 +78,8 @@ class Evaluator(object):
         self.verbose = verbose
         self.save_path = save_path
         self.show_image = show_image
+        # crops per network forward (both mirrors of a crop count as two): batched sliding windows
+        self.eval_batch = int(os.environ.get("CMX_EVAL_BATCH", "8"))
 
     # ------------------------------------------------------------------ per-sample API
     def func_per_iteration(self, data, device):
@@ -99,17 +102,24 @@ class Evaluator(object):
         return t.permute(2, 0, 1).contiguous()
 
     def sliding_scores_rgbX(self, img, modal_x, crop_size, stride_rate, device=None) -> torch.Tensor:
-        """Sum over scales of the per-scale score maps, (K, H, W) fp32 on the device."""
+        """Sum over scales of the per-scale score maps, (K, H, W) fp32 on the device.  The crops
+        of every scale (all of one shape, crop_size) run through the network in batches of
+        ``eval_batch`` (one forward per batch instead of one bs=1 forward per crop); each crop's
+        scores are then added into its scale's accumulator in the reference's window order."""
         dev = self._device(device)
         crop = (int(crop_size[0]), int(crop_size[1])) if not isinstance(crop_size, int) else (crop_size, crop_size)
         img_c, x_c = self._chw(img, dev), self._chw(modal_x, dev)
         u8_img, u8_x = _is_uint8(img), _is_uint8(modal_x)
         _, ori_rows, ori_cols = img_c.shape
-        processed = torch.zeros(self.class_num, ori_rows, ori_cols, device=dev, dtype=torch.float32)
+        plans = []
         for s in self.multi_scales:
             nh, nw = int(round(ori_rows * s)), int(round(ori_cols * s))
-            processed += self.scale_process_rgbX(_resize_chw(img_c, nh, nw, u8_img), _resize_chw(x_c, nh, nw, u8_x),
-                                                 (ori_rows, ori_cols), crop, stride_rate, dev)
+            plans.append(self._scale_plan(_resize_chw(img_c, nh, nw, u8_img), _resize_chw(x_c, nh, nw, u8_x), crop,
+                                            stride_rate))
+        self._run_windows([w for pl in plans for w in pl["windows"]], crop)
+        processed = torch.zeros(self.class_num, ori_rows, ori_cols, device=dev, dtype=torch.float32)
+        for pl in plans:
+            processed += self._scale_result(pl, (ori_rows, ori_cols))
         return processed
 
     def sliding_eval_rgbX(self, img, modal_x, crop_size, stride_rate, device=None):
@@ -123,14 +133,23 @@ class Evaluator(object):
 
     def scale_process_rgbX(self, img, modal_x, ori_shape, crop_size, stride_rate, device=None):
         """evaluator.py:326-372 on (C, h, w) device images; returns (K, H, W) at ori_shape."""
+        crop = (int(crop_size[0]), int(crop_size[1])) if not isinstance(crop_size, int) else (crop_size, crop_size)
+        pl = self._scale_plan(img, modal_x, crop, stride_rate)
+        self._run_windows(pl["windows"], crop)
+        return self._scale_result(pl, ori_shape)
+
+    def _scale_plan(self, img, modal_x, crop_size, stride_rate):
+        """The windows of one scale (evaluator.py:326-368): each one's normalised, padded crop
+        pair and where its scores land in the scale's accumulator."""
         dev = img.device
         _, new_rows, new_cols = img.shape
         K = self.class_num
+        wins = []
         if new_cols <= crop_size[1] or new_rows <= crop_size[0]:
             m = _pad_margin(new_rows, new_cols, crop_size)
-            ph, pw = new_rows + m[0] + m[1], new_cols + m[2] + m[3]
-            score = torch.zeros(K, new_rows, new_cols, device=dev, dtype=torch.float32)
-            self._crop_into(img, modal_x, crop_size, score, 0, 0, m, (ph, pw))
+            acc = torch.zeros(K, new_rows, new_cols, device=dev, dtype=torch.float32)
+            wins.append((img, modal_x, acc, 0, 0, m))
+            view = None
         else:
             stride = (int(math.ceil(crop_size[0] * stride_rate)), int(math.ceil(crop_size[1] * stride_rate)))
             m = _pad_margin(new_rows, new_cols, crop_size)
@@ -139,7 +158,7 @@ class Evaluator(object):
             pad_rows, pad_cols = img_pad.shape[1], img_pad.shape[2]
             r_grid = int(np.ceil((pad_rows - crop_size[0]) / stride[0])) + 1
             c_grid = int(np.ceil((pad_cols - crop_size[1]) / stride[1])) + 1
-            data_scale = torch.zeros(K, pad_rows, pad_cols, device=dev, dtype=torch.float32)
+            acc = torch.zeros(K, pad_rows, pad_cols, device=dev, dtype=torch.float32)
             for gy in range(r_grid):
                 for gx in range(c_grid):
                     s_x = gx * stride[0]                      # (sic) evaluator.py:352-357
@@ -153,21 +172,57 @@ class Evaluator(object):
                     sx0 = s_x if s_x >= 0 else max(pad_cols + s_x, 0)
                     if e_y <= sy0 or e_x <= sx0:
                         continue
-                    sub_i = img_pad[:, sy0:e_y, sx0:e_x]
-                    sub_x = x_pad[:, sy0:e_y, sx0:e_x]
-                    tm = _pad_margin(e_y - sy0, e_x - sx0, crop_size)
-                    self._crop_into(sub_i, sub_x, crop_size, data_scale, sy0, sx0, tm,
-                                    (e_y - sy0 + tm[0] + tm[1], e_x - sx0 + tm[2] + tm[3]))
-            score = data_scale[:, m[0]:pad_rows - m[1], m[2]:pad_cols - m[3]]
+                    wins.append((img_pad[:, sy0:e_y, sx0:e_x], x_pad[:, sy0:e_y, sx0:e_x], acc, sy0, sx0,
+                                 _pad_margin(e_y - sy0, e_x - sx0, crop_size)))
+            view = (m[0], pad_rows - m[1], m[2], pad_cols - m[3])
+        return {"windows": wins, "acc": acc, "view": view}
+
+    def _scale_result(self, plan, ori_shape):
+        acc, v = plan["acc"], plan["view"]
+        score = acc if v is None else acc[:, v[0]:v[1], v[2]:v[3]]
         return _resize_chw(score.contiguous(), ori_shape[0], ori_shape[1])
 
-    def _crop_into(self, img, modal_x, crop_size, acc, sy, sx, margin, padded):
-        """process_image_rgbX + val_func_process_rgbX + margin crop + window add (one kernel)."""
-        d, x = self.process_image_rgbX(img, modal_x, crop_size)
-        s1, s2 = self.val_func_process_rgbX(d, x)
-        K, ch, cw = s1.shape
-        _lib.call("cmx_seg_window_accumulate", _lib.ptr(s1), _lib.ptr(s2), _lib.ptr(acc), K, ch, cw,
-                  margin[0], margin[1], margin[2], margin[3], acc.shape[1], acc.shape[2], sy, sx, _lib.stream())
+    def _run_windows(self, wins, crop_size):
+        """process_image_rgbX + a batched val_func_process_rgbX + margin crop + window add (one
+        kernel per window, in list order)."""
+        nb = max(1, int(self.eval_batch) // (2 if self.is_flip else 1))
+        pairs = [self.process_image_rgbX(w[0], w[1], crop_size) for w in wins]
+        c0 = 0
+        while c0 < len(wins):
+            # runs of consecutive crops of one shape (a scale smaller than the crop on one side
+            # only keeps its other side: that whole-image crop is not crop-sized)
+            c1 = c0 + 1
+            while c1 < len(wins) and c1 - c0 < nb and pairs[c1][0].shape == pairs[c0][0].shape \
+                    and pairs[c1][1].shape == pairs[c0][1].shape:
+                c1 += 1
+            chunk = wins[c0:c1]
+            d = torch.stack([p[0] for p in pairs[c0:c1]])
+            x = torch.stack([p[1] for p in pairs[c0:c1]])
+            c0 = c1
+            s1, s2 = self._val_batch(d, x)
+            for i, (_, _, acc, sy, sx, tm) in enumerate(chunk):
+                a, b = s1[i], (s2[i] if s2 is not None else None)
+                K, ch, cw = a.shape
+                _lib.call("cmx_seg_window_accumulate", _lib.ptr(a), _lib.ptr(b), _lib.ptr(acc), K, ch, cw,
+                          tm[0], tm[1], tm[2], tm[3], acc.shape[1], acc.shape[2], sy, sx, _lib.stream())
+
+    def _val_batch(self, d, x):
+        """(n, 3, h, w) crops -> their logits (n, K, h, w) fp32 and (is_flip) those of the mirrored
+        crops, from one forward over the n (or 2n) images."""
+        net = self.val_func
+        was_training = net.training
+        net.eval()
+        n = d.shape[0]
+        with torch.no_grad():
+            if self.is_flip:
+                out = net(torch.cat([d, d.flip(-1)]).contiguous(), torch.cat([x, x.flip(-1)]).contiguous())
+                out = out.float()
+                s1, s2 = out[:n].contiguous(), out[n:].contiguous()
+            else:
+                s1, s2 = net(d.contiguous(), x.contiguous()).float().contiguous(), None
+        if was_training:
+            net.train()
+        return s1, s2
 
     def val_func_process_rgbX(self, input_data, input_modal_x, device=None):
         """evaluator.py:374-396 up to the exp: the logits of the crop and (is_flip) of its mirror,

@@ -184,3 +184,29 @@ def test_evaluator_runs_hip_model(dev):
     ev = Evaluator(None, K, [0.485, 0.456, 0.406], [0.229, 0.224, 0.225], model, [1.0, 0.5], True, [0])
     pred = ev.sliding_eval_rgbX(img, img, (64, 64), 2 / 3, dev)
     assert pred.shape == (64, 96) and pred.min() >= 0 and pred.max() < K
+    # batched crops (one forward over every crop and mirror) against one bs=1 forward per crop:
+    # the same scores up to the bf16 network's batch-shape-dependent GEMM splits
+    sb = ev.sliding_scores_rgbX(img, img, (64, 64), 2 / 3, dev)
+    ev.eval_batch = 1
+    s1 = ev.sliding_scores_rgbX(img, img, (64, 64), 2 / 3, dev)
+    torch.testing.assert_close(sb, s1, rtol=2e-2, atol=2e-2 * float(s1.abs().max()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flip", [False, True])
+def test_evaluator_batched_windows_match_single(dev, flip):
+    """Crops of every scale batched into shared forwards give the per-crop result (a network
+    whose per-image output does not depend on the batch: exact up to fp32 einsum order)."""
+    from rgbx_semantic_segmentation_amd.engine.evaluator import Evaluator
+    K, H, W = 5, 50, 70
+    net = TorchLinearNet(LinearNet(K, seed=3), dev)
+    rng = np.random.default_rng(1)
+    img = rng.uniform(0, 255, (H, W, 3))
+    x = rng.uniform(0, 255, (H, W, 3))
+    ev = Evaluator(None, K, [0.485, 0.456, 0.406], [0.229, 0.224, 0.225], net, [0.75, 1.0, 1.5], flip, [0])
+    outs = []
+    for nb in (1, 3, 64):
+        ev.eval_batch = nb
+        outs.append(ev.sliding_scores_rgbX(img, x, (32, 32), 2 / 3, dev))
+    for o in outs[1:]:
+        torch.testing.assert_close(o, outs[0], rtol=1e-6, atol=1e-6 * float(outs[0].abs().max()))
