@@ -80,6 +80,9 @@ class Evaluator(object):
         self.show_image = show_image
         # crops per network forward (both mirrors of a crop count as two): batched sliding windows
         self.eval_batch = int(os.environ.get("CMX_EVAL_BATCH", "8"))
+        # one HIP graph per crop-batch shape for capturable networks (CMX_EVAL_GRAPH=0: eager)
+        self.eval_graph = os.environ.get("CMX_EVAL_GRAPH", "1") != "0"
+        self._graphs = {}
 
     # ------------------------------------------------------------------ per-sample API
     def func_per_iteration(self, data, device):
@@ -215,14 +218,39 @@ class Evaluator(object):
         n = d.shape[0]
         with torch.no_grad():
             if self.is_flip:
-                out = net(torch.cat([d, d.flip(-1)]).contiguous(), torch.cat([x, x.flip(-1)]).contiguous())
-                out = out.float()
+                out = self._forward(net, torch.cat([d, d.flip(-1)]), torch.cat([x, x.flip(-1)])).float()
                 s1, s2 = out[:n].contiguous(), out[n:].contiguous()
             else:
-                s1, s2 = net(d.contiguous(), x.contiguous()).float().contiguous(), None
+                s1, s2 = self._forward(net, d, x).float().contiguous(), None
         if was_training:
             net.train()
         return s1, s2
+
+    def _forward(self, net, d, x):
+        """net(d, x); for a network that declares itself graph-capturable (EncoderDecoder), one
+        HIP graph per input shape, replayed from static input buffers (the eager forward of a
+        crop batch is bound by the host's ~600 launches).  The returned logits live in the
+        graph's output buffer: the caller consumes them on this stream before the next replay."""
+        if not (self.eval_graph and getattr(net, "cmx_capturable", False)):
+            return net(d.contiguous(), x.contiguous())
+        key = (tuple(d.shape), tuple(x.shape), str(d.device), id(net))
+        g = self._graphs.get(key)
+        if g is None:
+            sd, sx = d.contiguous().clone(), x.contiguous().clone()
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                net(sd, sx)                          # warm-up: workspaces and allocator pools
+            torch.cuda.current_stream().wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+                out = net(sd, sx)
+            g = self._graphs[key] = (graph, sd, sx, out)
+        graph, sd, sx, out = g
+        sd.copy_(d)
+        sx.copy_(x)
+        graph.replay()
+        return out
 
     def val_func_process_rgbX(self, input_data, input_modal_x, device=None):
         """evaluator.py:374-396 up to the exp: the logits of the crop and (is_flip) of its mirror,

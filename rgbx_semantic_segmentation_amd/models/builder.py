@@ -67,6 +67,10 @@ def backward_segment(name: str) -> int:
 
 
 class EncoderDecoder(nn.Module):
+    # the forward is one stream-ordered sequence of library launches with no host sync: callers
+    # may capture it in a HIP graph (the evaluator does, per crop-batch shape)
+    cmx_capturable = True
+
     def __init__(self, cfg=None, criterion=None, norm_layer=nn.BatchNorm2d):
         super().__init__()
         backbone = _get(cfg, "backbone", "mit_b2")

@@ -187,6 +187,12 @@ def test_evaluator_runs_hip_model(dev):
     # batched crops (one forward over every crop and mirror) against one bs=1 forward per crop:
     # the same scores up to the bf16 network's batch-shape-dependent GEMM splits
     sb = ev.sliding_scores_rgbX(img, img, (64, 64), 2 / 3, dev)
+    assert len(ev._graphs) > 0                       # the crop batches replayed HIP graphs
+    sb2 = ev.sliding_scores_rgbX(img, img, (64, 64), 2 / 3, dev)
+    assert torch.equal(sb, sb2)                      # replays of the cached graphs: identical
+    ev.eval_graph = False
+    se = ev.sliding_scores_rgbX(img, img, (64, 64), 2 / 3, dev)
+    assert torch.equal(sb, se)                       # graph replay = the eager launches
     ev.eval_batch = 1
     s1 = ev.sliding_scores_rgbX(img, img, (64, 64), 2 / 3, dev)
     torch.testing.assert_close(sb, s1, rtol=2e-2, atol=2e-2 * float(s1.abs().max()))
