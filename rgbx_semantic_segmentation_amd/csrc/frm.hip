@@ -212,7 +212,18 @@ __global__ __launch_bounds__(256) void linear_bwd_kernel(const float* __restrict
     int m = 0, n = n0;
     if (e < nval) {
       m = e / rows; n = n0 + e % rows;
-      for (int q = sub; q < nsl; q += T) d += dyp[q * ss + m * sm + n];
+      const float* pp = dyp + m * sm + n;
+      int q = sub;
+      // eight slabs' loads in flight before the adds (same summation order): with T = 1 a lane
+      // walked its 16 slabs one dependent round trip at a time (8 launches: 83 -> 69 us per step)
+      for (; q + 7 * T < nsl; q += 8 * T) {
+        float t8[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t8[u] = pp[(long)(q + u * T) * ss];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) d += t8[u];
+      }
+      for (; q < nsl; q += T) d += pp[(long)q * ss];
     }
     d = group_sum(d, T);
     if (e < nval && sub == 0) dzs[m][n - n0] = d * act_grad_from_out(y[(long)m * Nout + n], act);
