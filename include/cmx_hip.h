@@ -30,6 +30,11 @@ typedef struct ihipStream_t* hipStream_t;
 #endif
 
 /* ---- housekeeping ------------------------------------------------------------------ */
+/* ABI revision of this header; cmx_abi_version() returns the revision the library was built
+ * from, and the Python binding refuses a library whose revision differs (an older .so with the
+ * same symbol names but shifted arguments would otherwise corrupt memory silently).  Bump it
+ * on every change of an entry point's argument list. */
+#define CMX_ABI_VERSION 2
 int cmx_abi_version(void);
 const char* cmx_last_error(void);
 /* pinned host -> device copy of a packed record table on `stream` (see grouped launches) */
@@ -218,7 +223,20 @@ size_t cmx_gemm_group_record_size(void);
 int cmx_gemm_grouped_splitk(int G, int M, int N, int K, int ones_col);
 int cmx_gemm_group_pack(void* rec, const void* A, const void* B, void* C, float* dbias, float* workspace, int G, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t sA, int64_t sB, int64_t sC, int64_t sdb, int transA, int transB, int out_mode, int ones_col, int splitk, int blk0);
 /* cmx_gemm_grouped: dtype = the operands' storage type of every record (1 bf16, 2 fp16) */
+/* cmx_gemm_ln: cmx_gemm's forward (A (G,M,K1) [| A2], B (G,N,K), both k-contiguous; bias, residual
+ *      R with DropPath scale rscale, activation; 16-bit, no split-K) plus the LayerNorm of its output
+ *      rows in the same launch -- the consumer norm of a residual Linear (Block: x + drop_path(proj(.))
+ *      -> norm2, x + drop_path(fc2(.)) -> next norm1 / stage norm; dual_segformer.py:168-169,382):
+ *      ln_y = LN(C) * ln_gamma[g] + ln_beta[g] (C's dtype and strides), ln_mean / ln_rstd (fp32, g*M + i).
+ *      N a multiple of 64, <= 512.  tickets: cmx_gemm_ln_tickets(G, M) uint32 arrival counters, zero
+ *      before the first launch; each launch leaves them zero (stream-ordered launches may share them). */
+int cmx_gemm_ln(const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R, const float* rscale, int G, int M, int N, int K, int K1, int64_t lda, int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias, int rows_per_sample, int act, const float* ln_gamma, const float* ln_beta, int64_t ln_sg, float ln_eps, void* ln_y, float* ln_mean, float* ln_rstd, unsigned* tickets, int dtype, hipStream_t stream);
+size_t cmx_gemm_ln_tickets(int G, int M);
 int cmx_gemm_grouped(const void* recs, int nrec, int total_blocks, int dtype, hipStream_t stream);
+/* cmx_gemm_grouped_capped: the same launch on a grid of at most max_blocks workgroups (a multiple
+ * of 8; <= 0: uncapped), each walking blocks b, b + grid, ...: a grouped weight-gradient launch
+ * beside the backward on a side stream keeps to that share of the chip */
+int cmx_gemm_grouped_capped(const void* recs, int nrec, int total_blocks, int max_blocks, int dtype, hipStream_t stream);
 /* ---- im2col-free convolution on the same GEMM (bf16, NHWC, C % 64 == 0 for the forward): OverlapPatchEmbed.proj
  *      (k3 s2 p1, dual_segformer.py:196-197) and Attention.sr (kR sR, :95-96).  The forward's A operand is DMA'd
  *      tap by tap straight from x (padding = zeros from the buffer range check); the weight gradient is one
@@ -249,6 +267,12 @@ int cmx_adamw_step(float* p, const float* g, float* m, float* v, void* shadow, i
  *      skips the whole update (and the step count) when found_inf[0] != 0; loss_scale_update applies backoff /
  *      growth (after growth_interval clean steps) and clears found_inf. */
 int cmx_adamw_step_scaled(float* p, const float* g, float* m, float* v, void* shadow, int shadow_dtype, const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1, double beta2, float eps, double weight_decay, float grad_scale, const float* loss_scale, const float* found_inf, hipStream_t stream);
+/* adamw_step_segment: the same update on one contiguous range of the flat buffers (p, g, m, v,
+ *      shadow and decay64 offset by the caller; n a multiple of 64), e.g. one backward-completion
+ *      segment updated on a side stream while the backward of the earlier stages runs.  Every launch
+ *      reads the step count; only the one with store_step = 1 (the step's last) stores t + 1.
+ *      max_blocks > 0 caps the grid (the launch then keeps to that share of the chip). */
+int cmx_adamw_step_segment(float* p, const float* g, float* m, float* v, void* shadow, int shadow_dtype, const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1, double beta2, float eps, double weight_decay, float grad_scale, int store_step, int max_blocks, hipStream_t stream);
 /* grad_nonfinite: flags64 (nullable) = the per-64-element decay flags of adamw_step; blocks flagged 2
  *      (frozen slots, in no optimizer group) are not scanned, as GradScaler.unscale_ checks only the
  *      optimizer's parameters. */

@@ -28,6 +28,10 @@ class CMXError(RuntimeError):
     pass
 
 
+# cmx_status codes (csrc/cmx_common.h)
+CMX_OK, CMX_ERR_SHAPE, CMX_ERR_DTYPE, CMX_ERR_LAUNCH, CMX_ERR_ARG = 0, -1, -2, -3, -4
+
+
 def _ctype(decl: str):
     decl = decl.strip()
     if "*" in decl:
@@ -57,11 +61,27 @@ def parse_header(path: str | None = None):
     return out
 
 
+def header_abi_version(path: str | None = None) -> int:
+    """The CMX_ABI_VERSION the header defines (the revision the bindings below are parsed from)."""
+    if path is None:
+        path = next(p for p in HEADER_PATHS if os.path.exists(p))
+    m = re.search(r"^#define\s+CMX_ABI_VERSION\s+(\d+)", open(path).read(), re.M)
+    if m is None:
+        raise CMXError(f"{path} defines no CMX_ABI_VERSION")
+    return int(m.group(1))
+
+
 def _load():
     if not os.path.exists(LIB_PATH):
         raise CMXError(f"libcmx_hip.so not found at {LIB_PATH}; run __graft_entry__.build() "
                        "(or `make -C rgbx_semantic_segmentation_amd/csrc`).  There is no CPU fallback.")
     lib = ctypes.CDLL(LIB_PATH)
+    lib.cmx_abi_version.restype = ctypes.c_int32
+    lib.cmx_abi_version.argtypes = []
+    want, have = header_abi_version(), int(lib.cmx_abi_version())
+    if have != want:
+        raise CMXError(f"{LIB_PATH} was built for C-ABI revision {have}, the header declares {want}: "
+                       "rebuild it (`make -C rgbx_semantic_segmentation_amd/csrc`)")
     sigs = parse_header()
     for name, (rt, argt) in sigs.items():
         fn = getattr(lib, name)
@@ -77,11 +97,19 @@ def last_error() -> str:
     return LIB.cmx_last_error().decode()
 
 
+# measurement hook (roofline.measure_gemm_family): observer(name, fn, args) runs right after a
+# successful call, while the caller still holds every buffer the arguments point to
+observer = None
+
+
 def call(name: str, *args) -> None:
     """Invoke an int-returning entry point; raise CMXError on a negative status."""
-    st = getattr(LIB, name)(*args)
+    fn = getattr(LIB, name)
+    st = fn(*args)
     if st != 0:
         raise CMXError(f"{name} failed ({st}): {last_error()}")
+    if observer is not None:
+        observer(name, fn, args)
 
 
 def query(name: str, *args) -> int:

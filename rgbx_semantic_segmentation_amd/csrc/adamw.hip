@@ -53,7 +53,7 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                              float* __restrict__ v, S* __restrict__ shadow, const uint8_t* __restrict__ decay64,
                              long n, const float* __restrict__ lr_ptr, float* __restrict__ step_ptr, double b1d,
                              double b2d, float eps, double wd, float gscale, const float* __restrict__ loss_scale,
-                             const float* __restrict__ found_inf) {
+                             const float* __restrict__ found_inf, int store_step) {
   // GradScaler semantics (train.py:185-198): a step whose gradients held inf / nan is skipped
   if (found_inf && *found_inf != 0.f) return;
   if (loss_scale) gscale /= *loss_scale;                       // unscale
@@ -100,7 +100,9 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
     const long e = i * 4;
     update(e, ld4<NT>(p + e), ld4<NT>(g + e), ld4<NT>(m + e), ld4<NT>(v + e), decay64[e >> 6]);
   }
-  // the step count: the last block to arrive stores t (every block read t_prev at its start)
+  // the step count: the last block to arrive stores t (every block read t_prev at its start);
+  // a segment launch that is not the step's last (store_step = 0) leaves it to that one
+  if (!store_step) return;
   __syncthreads();
   if (threadIdx.x == 0) {
     // relaxed: every thread of this block consumed t_prev before the barrier above (an
@@ -147,6 +149,11 @@ __global__ void loss_scale_update_kernel(float* scale, int* tracker, float* foun
   *found = 0.f;
 }
 
+static int adamw_launch(float* p, const float* g, float* m, float* v, void* shadow, int shadow_dtype,
+                        const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1,
+                        double beta2, float eps, double weight_decay, float grad_scale, const float* loss_scale,
+                        const float* found_inf, int store_step, int max_blocks, hipStream_t s);
+
 extern "C" {
 
 // n must be a multiple of 64; the step count at step_ptr is incremented by this call and the
@@ -162,20 +169,40 @@ int cmx_adamw_step_scaled(float* p, const float* g, float* m, float* v, void* sh
                           const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1,
                           double beta2, float eps, double weight_decay, float grad_scale, const float* loss_scale,
                           const float* found_inf, hipStream_t s) {
+  return adamw_launch(p, g, m, v, shadow, shadow_dtype, decay64, n, lr_ptr, step_ptr, beta1, beta2, eps, weight_decay,
+                      grad_scale, loss_scale, found_inf, 1, 0, s);
+}
+
+int cmx_adamw_step_segment(float* p, const float* g, float* m, float* v, void* shadow, int shadow_dtype,
+                           const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1,
+                           double beta2, float eps, double weight_decay, float grad_scale, int store_step,
+                           int max_blocks, hipStream_t s) {
+  return adamw_launch(p, g, m, v, shadow, shadow_dtype, decay64, n, lr_ptr, step_ptr, beta1, beta2, eps, weight_decay,
+                      grad_scale, nullptr, nullptr, store_step, max_blocks, s);
+}
+
+}  // extern "C"
+
+static int adamw_launch(float* p, const float* g, float* m, float* v, void* shadow, int shadow_dtype,
+                        const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1,
+                        double beta2, float eps, double weight_decay, float grad_scale, const float* loss_scale,
+                        const float* found_inf, int store_step, int max_blocks, hipStream_t s) {
   CMX_REQUIRE(n % 64 == 0, CMX_ERR_SHAPE, "adamw: n must be a multiple of 64");
   CMX_REQUIRE(!shadow || shadow_dtype == 1 || shadow_dtype == 2, CMX_ERR_DTYPE, "adamw: shadow dtype %d", shadow_dtype);
   // CMX_ADAMW_BLOCKS caps the grid (A/B knob; each block takes one relaxed ticket, so the
-  // cap is a scheduling choice, not a correctness one)
+  // cap is a scheduling choice, not a correctness one); max_blocks > 0 caps one launch (a
+  // segment update beside the backward on a side stream keeps to a share of the chip)
   static int& cap = cmx_knob("ADAMW_BLOCKS", 0);
   long blocks = (n / 4 + 255) / 256;
   if (cap > 0 && blocks > cap) blocks = cap;
+  if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
   CMX_REQUIRE(blocks <= (long)ADAMW_GRP * ADAMW_NGRP, CMX_ERR_SHAPE, "adamw: %ld blocks exceed the ticket groups", blocks);
   // nontemporal p / g / m / v traffic (CMX_ADAMW_NT=0: cached): 375 -> 348 us standalone
   static int& nt = cmx_knob("ADAMW_NT", 1);
 #define CMX_ADAMW(S_, NT_)                                                                                         \
   hipLaunchKernelGGL((adamw_kernel<S_, NT_>), dim3((unsigned)blocks), dim3(256), 0, s, p, g, m, v, (S_*)shadow, \
                      decay64, (long)n, lr_ptr, step_ptr, beta1, beta2, eps, weight_decay, grad_scale, loss_scale,    \
-                     found_inf)
+                     found_inf, store_step)
   if (shadow_dtype == 2) {
     if (nt) CMX_ADAMW(f16, true);
     else CMX_ADAMW(f16, false);
@@ -186,6 +213,8 @@ int cmx_adamw_step_scaled(float* p, const float* g, float* m, float* v, void* sh
 #undef CMX_ADAMW
   return cmx_check_launch("adamw_step");
 }
+
+extern "C" {
 
 int cmx_grad_nonfinite(const float* g, int64_t n, const uint8_t* flags64, float* found_inf, hipStream_t s) {
   CMX_REQUIRE(n % 4 == 0 && found_inf && (!flags64 || n % 64 == 0), CMX_ERR_SHAPE,

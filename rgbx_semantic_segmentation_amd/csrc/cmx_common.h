@@ -9,8 +9,7 @@
 #include <math.h>
 #include <type_traits>
 #include "../../include/cmx_hip.h"  // compiler-checks every definition against the ABI header
-
-#define CMX_ABI_VERSION 1
+                                     // (and defines CMX_ABI_VERSION)
 
 enum cmx_status {
   CMX_OK = 0,

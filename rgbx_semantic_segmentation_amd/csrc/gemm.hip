@@ -135,6 +135,11 @@ struct GemmPlan {
   int tA, tB, dtype, nblk, nk64, pad;
 };
 
+// row-block LayerNorm tail of the epilogue (cmx_gemm_ln)
+struct LnTail {
+  const float* gamma; const float* beta; long sg; void* y; float* mean; float* rstd; unsigned* tickets; float eps;
+};
+
 // upsample-add sources of the epilogue (nup = 0: none)
 struct UpSpec {
   const void* src[3];
@@ -147,7 +152,7 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
               int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode, int ones_col, int splitk,
               int dtype, hipStream_t s, const UpSpec* up, int scR = 0, int scH = 0, int scW = 0, int scC = 0,
               int scHo = 0, int scWo = 0, int gh = 1, int64_t sAh = 0, int64_t sBh = 0, int64_t sCh = 0,
-              GemmPlan* plan = nullptr, const void* mask = nullptr) {
+              GemmPlan* plan = nullptr, const void* mask = nullptr, const LnTail* tail = nullptr) {
   CMX_REQUIRE(G > 0 && M > 0 && N > 0 && K > 0, CMX_ERR_SHAPE, "gemm: empty problem G=%d M=%d N=%d K=%d", G, M, N, K);
   CMX_REQUIRE(dtype >= 0 && dtype <= 2, CMX_ERR_DTYPE, "gemm: unsupported dtype %d", dtype);
   CMX_REQUIRE(out_mode >= 0 && out_mode <= 2 && act >= 0 && act <= 3, CMX_ERR_ARG, "gemm: out_mode/act");
@@ -208,6 +213,18 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
   a.kt_per_split = (nk + splitk - 1) / splitk;
   splitk = (nk + a.kt_per_split - 1) / a.kt_per_split;      // no empty splits
   a.nsplit = splitk;
+  if (tail) {
+    int bm = 0, bn = 0;
+    if (fast) plan_tiles(G, M, nb, K, &bm, &bn);
+    CMX_REQUIRE(fast && bm == 64 && bn == 64 && splitk == 1 && !transA && !transB && out_mode == 0 && !ones_col &&
+                    !a.nup && !a.scatter && gh == 1 && !mask && a.cvec && N % 64 == 0 && N <= 512 && dtype != 0,
+                CMX_ERR_ARG, "gemm_ln: the LayerNorm tail needs the 16-bit 64 x 64 path without split-K, forward "
+                "layouts, a plain aligned store and N a multiple of 64 <= 512 (G=%d M=%d N=%d K=%d)", G, M, N, K);
+    CMX_REQUIRE(tail->gamma && tail->beta && tail->y && tail->mean && tail->rstd && tail->tickets &&
+                    ((uintptr_t)tail->y & 15) == 0 && tail->y != C, CMX_ERR_ARG, "gemm_ln: tail buffers");
+    a.tail = 1; a.ln_gamma = tail->gamma; a.ln_beta = tail->beta; a.ln_sg = tail->sg; a.ln_y = tail->y;
+    a.ln_mean = tail->mean; a.ln_rstd = tail->rstd; a.tickets = tail->tickets; a.ln_eps = tail->eps;
+  }
   if (plan) {
     // planning only (cmx_gemm_plan): eligible for a multi launch = the 16-bit path on 64 x 64
     // tiles, no split-K, no bias-gradient column / upsample / scatter / two-level batch
@@ -269,6 +286,19 @@ int cmx_gemm(const void* A, const void* A2, const void* B, void* C, const float*
                    sC, sbias, sdb, rows_per_sample, transA, transB, act, out_mode, ones_col, splitk, dtype, s, nullptr,
                    0, 0, 0, 0, 0, 0, 1, 0, 0, 0, nullptr, mask);
 }
+
+int cmx_gemm_ln(const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R,
+                const float* rscale, int G, int M, int N, int K, int K1, int64_t lda, int64_t lda2, int64_t ldb,
+                int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias, int rows_per_sample,
+                int act, const float* ln_gamma, const float* ln_beta, int64_t ln_sg, float ln_eps, void* ln_y,
+                float* ln_mean, float* ln_rstd, unsigned* tickets, int dtype, hipStream_t s) {
+  const LnTail t{ln_gamma, ln_beta, (long)ln_sg, ln_y, ln_mean, ln_rstd, tickets, ln_eps};
+  return gemm_impl(A, A2, B, C, bias, R, rscale, nullptr, nullptr, G, M, N, K, K1, lda, lda2, ldb, ldc, sA, sA2, sB,
+                   sC, sbias, 0, rows_per_sample, 0, 0, act, 0, 0, 1, dtype, s, nullptr, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0,
+                   nullptr, nullptr, &t);
+}
+
+size_t cmx_gemm_ln_tickets(int G, int M) { return (size_t)G * ((M + 63) / 64); }
 
 size_t cmx_gemm_plan_size(void) { return sizeof(GemmPlan); }
 
@@ -507,10 +537,21 @@ int cmx_gemm_grouped(const void* recs, int nrec, int total_blocks, int dtype, hi
   // launch: 695-702 us contiguous, 624-633 us for runs of 4..128 tiles
   // (scripts/grouped_chunk_sweep.sh); PMC HBM bytes per launch 3.13 GB at 16-tile runs,
   // 2.48 GB at 64 (contiguous: 2.43 GB), so 64 keeps the L2 reuse of neighbouring tiles
+  return cmx_gemm_grouped_capped(recs, nrec, total_blocks, 0, dtype, s);
+}
+
+int cmx_gemm_grouped_capped(const void* recs, int nrec, int total_blocks, int max_blocks, int dtype, hipStream_t s) {
+  CMX_REQUIRE(dtype == 1 || dtype == 2, CMX_ERR_DTYPE, "gemm_grouped: operands bf16 (1) or fp16 (2), got %d", dtype);
+  CMX_REQUIRE(recs && nrec > 0 && total_blocks > 0, CMX_ERR_ARG, "gemm_grouped: empty launch");
+  CMX_REQUIRE(max_blocks <= 0 || max_blocks % 8 == 0, CMX_ERR_ARG, "gemm_grouped: max_blocks %d not a multiple of 8",
+              max_blocks);
   static int& chunk = cmx_knob("GROUPED_CHUNK", 64);
   const GroupRec* rr = (const GroupRec*)recs;
-  if (dtype == 2) hipLaunchKernelGGL((gemm_grouped_kernel<f16>), dim3(total_blocks), dim3(256), 0, s, rr, nrec, chunk);
-  else hipLaunchKernelGGL((gemm_grouped_kernel<bf16>), dim3(total_blocks), dim3(256), 0, s, rr, nrec, chunk);
+  const int grid = max_blocks > 0 && max_blocks < total_blocks ? max_blocks : total_blocks;
+  if (dtype == 2)
+    hipLaunchKernelGGL((gemm_grouped_kernel<f16>), dim3(grid), dim3(256), 0, s, rr, nrec, chunk, total_blocks);
+  else
+    hipLaunchKernelGGL((gemm_grouped_kernel<bf16>), dim3(grid), dim3(256), 0, s, rr, nrec, chunk, total_blocks);
   return cmx_check_launch("gemm_grouped");
 }
 

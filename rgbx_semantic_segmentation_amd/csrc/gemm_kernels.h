@@ -37,6 +37,22 @@ struct GemmArgs {
   // ReLU-backward mask (NULL: none): after the residual, C(i, j) = 0 where mask(i, j) <= 0; the
   // mask has C's layout and dtype (the saved ReLU output of the layer whose gradient this is)
   const void* mask;
+  // row-block LayerNorm tail (tail = 1; 64 x 64 tiles, forward layouts, no split, plain store,
+  // N <= 512): the consumer norm of a residual Linear's output (Block.norm2 after proj, the next
+  // norm1 / stage norm after fc2, dual_segformer.py:168-169,382) runs inside the producing launch.
+  // Every tile stores its outputs write-through (sc1) and takes an arrival ticket of its 64-row
+  // block (tickets[g * tiles_m + tm], caller-owned, zero at first use, reset by the last
+  // arriver); the last of the row block's tiles_n workgroups to arrive normalises those rows:
+  // ln_y = LN(C rows) * gamma + beta (C's dtype and layout), ln_mean / ln_rstd (fp32, g * M + i)
+  int tail;
+  float ln_eps;
+  const float* ln_gamma;
+  const float* ln_beta;
+  long ln_sg;                                  // gamma / beta group stride
+  void* ln_y;
+  float* ln_mean;
+  float* ln_rstd;
+  unsigned* tickets;
 };
 
 // block id -> tile id, giving each of the 8 XCDs (hardware deals block b to XCD b % 8) a
@@ -155,9 +171,24 @@ __device__ __forceinline__ void dbias_store(const GemmArgs& p, int g, int i, flo
   *d = p.out_mode == 2 ? *d + v : v;
 }
 
+// 16-B write-through store (sc1: through to the device-coherent level, so a workgroup on another
+// XCD reads it back with sc1 loads in the same launch; MI355X_MICROARCH.md "visibility")
+// (base: wave-uniform, e.g. a group's first element -- the resource lives in SGPRs; off: the
+// lane's byte offset, < 2^31)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7ffffff0, 0x00020000);
+}
+__device__ __forceinline__ void st16_sc1(const void* base, int off, uint4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rsrc_of(base), off, 0, 16);
+}
+__device__ __forceinline__ uint4 ld16_sc1(const void* base, int off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsrc_of(base), off, 0, 16));
+}
+
 // 8 consecutive columns j..j+nv-1 of row i (nv <= 8).  p.vec8: C / R rows are 16-B aligned
-// chunks, so a full group moves with one 16-B (bf16) or two 16-B (fp32) accesses.
-template <typename T>
+// chunks, so a full group moves with one 16-B (bf16) or two 16-B (fp32) accesses.  SC1: the
+// plain 16-bit store goes write-through (row-block tail launches)
+template <typename T, bool SC1 = false>
 __device__ __forceinline__ void epi_store8(const GemmArgs& p, int g, int i, int j, int nv, float* v) {
   if (nv < 8 || !p.cvec) {
     for (int e = 0; e < nv; ++e) epi_store<T, true>(p, g, i, j + e, v[e]);
@@ -190,8 +221,15 @@ __device__ __forceinline__ void epi_store8(const GemmArgs& p, int g, int i, int 
     for (int e = 0; e < 8; ++e) v[e] = mv[e] > 0.f ? v[e] : 0.f;
   }
   if (p.out_mode == 0) {
-    store_vec<T>(reinterpret_cast<T*>(p.C) + off, v);
-    if constexpr (sizeof(T) == 4) store_vec<T>(reinterpret_cast<T*>(p.C) + off + 4, v + 4);
+    if constexpr (SC1 && sizeof(T) == 2) {
+      // (tail launches: plain row-major C, so the group's base is uniform and the offset in it < 2^31 B)
+      const long gb = goff(p, g, p.sC, p.sCh);
+      st16_sc1(reinterpret_cast<T*>(p.C) + gb, (int)((off - gb) * 2),
+               make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])));
+    } else {
+      store_vec<T>(reinterpret_cast<T*>(p.C) + off, v);
+      if constexpr (sizeof(T) == 4) store_vec<T>(reinterpret_cast<T*>(p.C) + off + 4, v + 4);
+    }
   } else {
     float4* d = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + off);
     if (p.out_mode == 2) {
@@ -303,7 +341,7 @@ constexpr int gemm_smem_bytes() {
 // One output tile (of one split / group) of problem p.  `lin` = the block's linear index
 // within the problem, in (split, group, tile) order; smem = gemm_smem_bytes<BM, BN, NS>().
 // E = the 16-bit storage type (bf16 or f16: v_mfma_f32_32x32x16_bf16 / _f16, same tiles and rate)
-template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1, typename E = bf16>
+template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1, typename E = bf16, bool SC1 = false>
 __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin, char* smem) {
   constexpr int A_BYTES = BM * FBK * 2, STAGE = (BM + BN) * FBK * 2, SLOT = KW * STAGE;
   constexpr int TM = BM / 64, TN = BN / 64;
@@ -529,7 +567,83 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
         for (int e = 0; e < nv; ++e) d[e] = v[e];
       }
     } else {
-      epi_store8<E>(p, g, i, j, nv, v);
+      epi_store8<E, SC1>(p, g, i, j, nv, v);
+    }
+  }
+}
+
+// Row-block LayerNorm tail (GemmArgs::tail): called by every workgroup after its tile's stores;
+// the last of the row block's tiles_n to arrive normalises the block's <= 64 rows of C.  Its
+// loads of C are sc1 (the other tiles' stores were sc1 and drained before their ticket), every
+// channel chunk of every row it owns is in flight before the first reduction.  A row is
+// TPR = N / 8 lanes x one 16-B chunk (N <= 512: TPR <= 64), RPW = 64 / TPR rows per wave
+// instruction; the block's waves take rows round-robin.  Numerics as ln_fwd_kernel
+// (layernorm.hip): two-pass mean / variance of the stored 16-bit values in fp32.
+template <typename E>
+__device__ __noinline__ void gemm_ln_tail(const GemmArgs& p, const int lin) {
+  const int ntile = p.tiles_m * p.tiles_n;
+  const int t = lin % ntile, g = (lin / ntile) % p.G;
+  const int tm = t / p.tiles_n;
+  if (!last_arrival(p.tickets + g * p.tiles_m + tm, p.tiles_n)) return;
+  // a row: nch = N / 8 chunks on TPR lanes (the power of two >= nch: lanes past nch hold zeros
+  // and stay out of the variance), RPW = 64 / TPR rows per wave instruction
+  const int C = p.N, nch = C / 8;
+  const int TPR = nch <= 8 ? 8 : nch <= 16 ? 16 : nch <= 32 ? 32 : 64, RPW = 64 / TPR;
+  const int nw = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int sub = lane / TPR, ch = lane % TPR;          // row within the wave instruction, chunk
+  const bool live = ch < nch;
+  const int i0 = tm * 64;
+  const int rows = min(64, p.M - i0);
+  const E* Cg = reinterpret_cast<const E*>(p.C) + (long)g * p.sC;
+  E* Yg = reinterpret_cast<E*>(p.ln_y) + (long)g * p.sC;
+  float ga[8], be[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    ga[e] = live ? p.ln_gamma[(long)g * p.ln_sg + ch * 8 + e] : 0.f;
+    be[e] = live ? p.ln_beta[(long)g * p.ln_sg + ch * 8 + e] : 0.f;
+  }
+  constexpr int MAXIT = 16;                              // 64 rows / (4 waves x 1 row) at N = 512
+  uint4 raw[MAXIT];
+  const int step = nw * RPW;                             // rows per pass of the whole block
+#pragma unroll
+  for (int it = 0; it < MAXIT; ++it) {
+    const int r = it * step + wave * RPW + sub;
+    if (it * step < rows && r < rows && live) raw[it] = ld16_sc1(Cg, (int)(((long)(i0 + r) * p.ldc + ch * 8) * 2));
+    else raw[it] = make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int it = 0; it < MAXIT; ++it) {
+    if (it * step >= rows) break;
+    const int r = it * step + wave * RPW + sub;
+    float v[8];
+    const uint32_t w4[4] = {raw[it].x, raw[it].y, raw[it].z, raw[it].w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const cmx_f2 f = unpack2<E>(w4[q]);
+      v[2 * q] = f.x;
+      v[2 * q + 1] = f.y;
+    }
+    float sm = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sm += v[e];
+    sm = group_sum(sm, TPR);
+    const float mu = sm / C;
+    float q2 = 0.f;
+    if (live) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { const float d = v[e] - mu; q2 += d * d; }
+    }
+    q2 = group_sum(q2, TPR);
+    const float rs = rsqrtf(q2 / C + p.ln_eps);
+    if (r < rows && live) {
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (v[e] - mu) * rs * ga[e] + be[e];
+      store_vec<E>(Yg + (long)(i0 + r) * p.ldc + ch * 8, o);
+      if (ch == 0) {
+        p.ln_mean[(long)g * p.M + i0 + r] = mu;
+        p.ln_rstd[(long)g * p.M + i0 + r] = rs;
+      }
     }
   }
 }
@@ -538,11 +652,13 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
 // neighbouring tiles of one (split, group): they share A row panels and the B k-slice in L2
 // (64 x 64 two-stage blocks take 32 KB of LDS: five fit a CU when the kernel stays within 96
 // VGPRs, which the launch bound asks of the register allocator -- at 97 only four are resident)
-template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1, typename E = bf16>
+template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1, typename E = bf16, bool TAIL = false>
 __global__ __launch_bounds__(256 * KW, (BM == 64 && BN == 64 && NS == 2 && KW == 1) ? 5 : (KW == 4 ? 1 : 2))
 void gemm_bf16_kernel(const GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[gemm_smem_bytes<BM, BN, NS, KW>()];
-  gemm_bf16_body<BM, BN, TA, TB, NS, KW, E>(p, xcd_tile(blockIdx.x, p.tiles_m * p.tiles_n * p.G * p.nsplit), smem);
+  const int lin = xcd_tile(blockIdx.x, p.tiles_m * p.tiles_n * p.G * p.nsplit);
+  gemm_bf16_body<BM, BN, TA, TB, NS, KW, E, TAIL>(p, lin, smem);
+  if constexpr (TAIL) gemm_ln_tail<E>(p, lin);
 }
 
 // ============================================================================ multi launch
@@ -594,23 +710,28 @@ __device__ __forceinline__ int xcd_chunk_tile(int b, int nt, int ch) {
 
 // (two-stage DMA ring, two blocks per CU: deeper rings at one block per CU measured 2-17 %
 // slower on the B2 step, round 3)
+// A grid smaller than `total` (a multiple of 8 workgroups: block b + k * gridDim.x stays on block
+// b's XCD) walks the blocks b, b + gridDim.x, ... in turn (cmx_gemm_grouped_capped).
 template <typename E, int NS = 2>
 __global__ __launch_bounds__(256, 2) void gemm_grouped_kernel(const GroupRec* __restrict__ recs, int nrec,
-                                                                             int chunk) {
+                                                                             int chunk, int total) {
   __shared__ __attribute__((aligned(1024))) char smem[gemm_smem_bytes<128, 128, NS>()];
-  const int lin = chunk > 0 ? xcd_chunk_tile(blockIdx.x, gridDim.x, chunk) : xcd_tile(blockIdx.x, gridDim.x);
-  int lo = 0, hi = nrec - 1;                    // last record with blk0 <= lin
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (recs[mid].blk0 <= lin) lo = mid; else hi = mid - 1;
+  for (int b = blockIdx.x; b < total; b += gridDim.x) {
+    if (b != (int)blockIdx.x) __syncthreads();   // every wave is done with the previous tile's LDS
+    const int lin = chunk > 0 ? xcd_chunk_tile(b, total, chunk) : xcd_tile(b, total);
+    int lo = 0, hi = nrec - 1;                    // last record with blk0 <= lin
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (recs[mid].blk0 <= lin) lo = mid; else hi = mid - 1;
+    }
+    const GroupRec& r = recs[lo];
+    const GemmArgs p = r.a;
+    const int local = lin - r.blk0;
+    if (r.bm == 128 && r.bn == 128) gemm_bf16_body<128, 128, true, true, NS, 1, E>(p, local, smem);
+    else if (r.bm == 128) gemm_bf16_body<128, 64, true, true, NS, 1, E>(p, local, smem);
+    else if (r.bn == 128) gemm_bf16_body<64, 128, true, true, NS, 1, E>(p, local, smem);
+    else gemm_bf16_body<64, 64, true, true, NS, 1, E>(p, local, smem);
   }
-  const GroupRec& r = recs[lo];
-  const GemmArgs p = r.a;
-  const int local = lin - r.blk0;
-  if (r.bm == 128 && r.bn == 128) gemm_bf16_body<128, 128, true, true, NS, 1, E>(p, local, smem);
-  else if (r.bm == 128) gemm_bf16_body<128, 64, true, true, NS, 1, E>(p, local, smem);
-  else if (r.bn == 128) gemm_bf16_body<64, 128, true, true, NS, 1, E>(p, local, smem);
-  else gemm_bf16_body<64, 64, true, true, NS, 1, E>(p, local, smem);
 }
 
 // ============================================================================ generic path
@@ -864,6 +985,12 @@ void launch_reduce(const GemmArgs& a, int G, long groups, hipStream_t s) {
 template <int BM, int BN, int NS, int KW = 1, typename E = bf16>
 void launch_bf16(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream_t s) {
   dim3 grid(a.tiles_m * a.tiles_n * G * nsplit);
+  if constexpr (BM == 64 && BN == 64) {
+    if (a.tail) {                     // row-block LayerNorm tail: forward layouts only (checked at launch)
+      hipLaunchKernelGGL((gemm_bf16_kernel<64, 64, false, false, NS, KW, E, true>), grid, dim3(256 * KW), 0, s, a);
+      return;
+    }
+  }
 #define CMX_GEMM_LAUNCH(TA, TB) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, TA, TB, NS, KW, E>), grid, dim3(256 * KW), 0, s, a)
   if (!tA && !tB) CMX_GEMM_LAUNCH(false, false);
   else if (!tA && tB) CMX_GEMM_LAUNCH(false, true);

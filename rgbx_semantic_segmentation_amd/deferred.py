@@ -232,15 +232,16 @@ def _upload(table: torch.Tensor, nbytes: int, device) -> torch.Tensor:
     return dev
 
 
-def flush() -> None:
+def flush(max_blocks: int = 0) -> None:
     """Issue the queued weight-gradient GEMMs (one launch) and reductions (one launch) on the
-    current stream."""
+    current stream.  max_blocks > 0 caps the GEMM launch's grid (a multiple of 8: each
+    workgroup walks several tiles), for a flush issued beside the backward on a side stream."""
     _q.armed = False
     if _q.gemms or _q.convs or _q.reds:
-        _issue()
+        _issue(max_blocks)
 
 
-def _issue() -> None:
+def _issue(max_blocks: int = 0) -> None:
     q = _q
     gemms, convs, reds, keep, dcode = q.gemms, q.convs, list(q.reds), q.keep, q.dtype
     producers = q.streams
@@ -315,7 +316,7 @@ def _issue() -> None:
         dev = _upload(table, total, device)
         if gtab is not None:
             _, _, nrec, blk, dims, arena = gtab
-            call("cmx_gemm_grouped", dev.data_ptr(), nrec, blk, dcode, stream())
+            call("cmx_gemm_grouped_capped", dev.data_ptr(), nrec, blk, int(max_blocks) // 8 * 8, dcode, stream())
             keep.append(arena)
             if observer is not None:
                 # algorithmic work per problem: (G, M, real N, K) and operand / result bytes

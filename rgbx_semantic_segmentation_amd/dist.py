@@ -192,15 +192,24 @@ def broadcast_buffers(flat, group=None, src: int = 0):
     flat buffer (flatten_bn_buffers).  num_batches_tracked is not sent: every rank increments
     it in lockstep, so it is equal already."""
     if flat is not None:
-        dist.broadcast(flat, src=src, group=group)
+        dist.broadcast(flat, src=group_src_rank(group, src), group=group)
+
+
+def group_src_rank(group, src: int = 0) -> int:
+    """Global rank of group rank ``src`` (torch.distributed.broadcast takes a GLOBAL src even with
+    a subgroup; DDP broadcasts from the group's first member, which need not be global rank 0)."""
+    if group is None or group is dist.group.WORLD:
+        return src
+    return dist.get_global_rank(group, src)
 
 
 @torch.no_grad()
 def broadcast_parameters(model, group=None, src: int = 0):
     """DDP's construction-time broadcast of parameters and buffers from rank 0."""
-    dist.broadcast(model.store.flat, src=src, group=group)
+    gsrc = group_src_rank(group, src)
+    dist.broadcast(model.store.flat, src=gsrc, group=group)
     for b in model.buffers():
-        dist.broadcast(b, src=src, group=group)
+        dist.broadcast(b, src=gsrc, group=group)
     model.store.refresh_shadow()
 
 

@@ -148,7 +148,15 @@ class Engine:
 
     def __exit__(self, exc_type, value, tb):
         if torch.cuda.is_available():
+            torch.cuda.synchronize()
             torch.cuda.empty_cache()
+        # the communicator goes last, after the device has drained (a process
+        # group torn down under live RCCL work was the one recorded hang); on an exception the
+        # peers may never reach a barrier, so only the clean path waits for them
+        if self.distributed and torch.distributed.is_available() and torch.distributed.is_initialized():
+            if exc_type is None:
+                torch.distributed.barrier()
+            torch.distributed.destroy_process_group()
         if exc_type is not None:
             logger.warning("A exception occurred during Engine initialization, give up running process")
             return False

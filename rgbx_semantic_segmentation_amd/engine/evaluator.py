@@ -24,6 +24,7 @@ launch); ``run`` evaluates a dataset and returns the metric line.
 from __future__ import annotations
 
 import math
+import collections
 import os
 
 import numpy as np
@@ -82,7 +83,11 @@ class Evaluator(object):
         self.eval_batch = int(os.environ.get("CMX_EVAL_BATCH", "8"))
         # one HIP graph per crop-batch shape for capturable networks (CMX_EVAL_GRAPH=0: eager)
         self.eval_graph = os.environ.get("CMX_EVAL_GRAPH", "1") != "0"
-        self._graphs = {}
+        # at most CMX_EVAL_GRAPHS cached shapes (least recently used evicted); every graph after
+        # the first allocates from the first one's private memory pool
+        self.eval_graph_cap = max(1, int(os.environ.get("CMX_EVAL_GRAPHS", "4")))
+        self._graphs = collections.OrderedDict()
+        self._graph_pool = None
 
     # ------------------------------------------------------------------ per-sample API
     def func_per_iteration(self, data, device):
@@ -236,6 +241,12 @@ class Evaluator(object):
         key = (tuple(d.shape), tuple(x.shape), str(d.device), id(net))
         g = self._graphs.get(key)
         if g is None:
+            # Bounded cache: images of many sizes give many whole-image crop shapes,
+            # and each graph would otherwise keep its own pool holding a full set of forward
+            # activations.  Sharing one pool is safe: replays run in order on this stream and
+            # each output is consumed (window-accumulated) before the next replay.
+            while len(self._graphs) >= self.eval_graph_cap:
+                self._graphs.popitem(last=False)
             sd, sx = d.contiguous().clone(), x.contiguous().clone()
             side = torch.cuda.Stream()
             side.wait_stream(torch.cuda.current_stream())
@@ -243,9 +254,12 @@ class Evaluator(object):
                 net(sd, sx)                          # warm-up: workspaces and allocator pools
             torch.cuda.current_stream().wait_stream(side)
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+            with torch.cuda.graph(graph, pool=self._graph_pool, capture_error_mode="thread_local"):
                 out = net(sd, sx)
+            if self._graph_pool is None:
+                self._graph_pool = graph.pool()
             g = self._graphs[key] = (graph, sd, sx, out)
+        self._graphs.move_to_end(key)
         graph, sd, sx, out = g
         sd.copy_(d)
         sx.copy_(x)

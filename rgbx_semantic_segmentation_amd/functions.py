@@ -54,12 +54,21 @@ class GLinear(Function):
     x + drop_path(proj/fc2(...)), dual_segformer.py:168-169)."""
 
     @staticmethod
-    def forward(ctx, W, Wg, b, bg, anchor, act, res, rscale, rps, x1, x2, tap=None):
+    def forward(ctx, W, Wg, b, bg, anchor, act, res, rscale, rps, x1, x2, tap=None, ln=None):
         G, N, Ktot = W.shape
         M = x1.shape[1]
         assert x1.shape[-1] + (x2.shape[-1] if x2 is not None else 0) == Ktot, (x1.shape, W.shape)
         y = torch.empty(G, M, N, dtype=x1.dtype, device=x1.device)
-        _fwd_gemm(x1, W, b, y, act=act, res=res, rscale=rscale, rps=rps, x2=x2)
+        pre = None
+        if ln is not None:
+            # the consumer LayerNorm of this output in the same launch (cmx_gemm_ln): its result
+            # goes to the LNTail, which that norm's LayerNormResF takes instead of launching
+            gamma, beta, eps, sink = ln
+            pre = K.gemm_ln(x1, W, y, gamma, beta, eps, bias=b, residual=res, rscale=rscale, rows_per_sample=rps,
+                            act=act, A2=x2)
+            sink.pre = pre
+        if pre is None:
+            _fwd_gemm(x1, W, b, y, act=act, res=res, rscale=rscale, rps=rps, x2=x2)
         ctx.save_for_backward(W, x1, x2, y if act == "relu" else None)
         ctx.meta = (Wg, bg, act, res is not None, rscale, rps, tap)
         return y
@@ -89,12 +98,23 @@ class GLinear(Function):
         _wgrad_into(dz, x1, Wg[:, :, :k1], bg)
         if x2 is not None:
             _wgrad_into(dz, x2, Wg[:, :, k1:])
-        return (None, None, None, None, None, None, dres, None, None, dx1, dx2, None)
+        return (None, None, None, None, None, None, dres, None, None, dx1, dx2, None, None)
 
 
-def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1, tap=None):
+class LNTail:
+    """A LayerNorm computed inside the launch that produced its input (cmx_gemm_ln): the
+    producing GLinear fills ``pre`` = (y, mean, rstd), and the norm's layernorm_res consumes it
+    instead of launching ln_fwd (None: not eligible, the norm launches as usual)."""
+    __slots__ = ("mod", "pre")
+
+    def __init__(self, mod):
+        self.mod, self.pre = mod, None
+
+
+def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1, tap=None, ln_tail=None):
     """Grouped linear using parameter ``wp`` (and bias ``bp``) of the store; x2 = second
-    input segment (cat-free), res/rscale/rps = fused DropPath residual (rps = rows per sample)."""
+    input segment (cat-free), res/rscale/rps = fused DropPath residual (rps = rows per sample).
+    ln_tail (LNTail of the norm that consumes the output): that LayerNorm runs in this launch."""
     W = store.w(wp)
     Wg = store.g(wp)
     G = W.shape[0]
@@ -104,8 +124,15 @@ def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1
     if bp is not None:
         b = store.w(bp, compute=False).view(G, -1)
         bg = store.g(bp).view(G, -1)
-    return GLinear.apply(W, Wg, b, bg, wp, act, res, rscale, rps, x1, x2, tap)
+    ln = None
+    if ln_tail is not None and LN_TAIL:
+        m = ln_tail.mod
+        ln = (store.w(m.weight, compute=False).view(G, -1), store.w(m.bias, compute=False).view(G, -1), m.eps, ln_tail)
+    return GLinear.apply(W, Wg, b, bg, wp, act, res, rscale, rps, x1, x2, tap, ln)
 
+
+# CMX_LN_TAIL=0: every LayerNorm forward as its own launch (A/B switch)
+LN_TAIL = os.environ.get("CMX_LN_TAIL", "1") != "0"
 
 # CMX_MULTI_GEMM=0 launches the grouped Linears of GLinearMulti one by one (A/B switch)
 MULTI_GEMM = os.environ.get("CMX_MULTI_GEMM", "1") != "0"
@@ -212,8 +239,11 @@ class LayerNormResF(Function):
     scale[sample] * dx for the producer of x (GradTap)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, gg, bg, eps, G, scale, rps, tap, anchor):
-        y, mean, rstd = K.layernorm_fwd(x, gamma, beta, eps, G=G)
+    def forward(ctx, x, gamma, beta, gg, bg, eps, G, scale, rps, tap, anchor, pre=None):
+        if pre is not None:                  # computed by the producing launch (LNTail)
+            y, mean, rstd = pre
+        else:
+            y, mean, rstd = K.layernorm_fwd(x, gamma, beta, eps, G=G)
         ctx.save_for_backward(x, gamma, mean, rstd)
         ctx.meta = (gg, bg, G, scale, rps, tap)
         ctx.set_materialize_grads(False)     # unused outputs arrive as None, not zero-filled tensors
@@ -244,16 +274,21 @@ class LayerNormResF(Function):
             deferred.reduce(ws, gg, bg, G, nb, nb * 2 * C, 2 * C, 1, 2 * C, C, gg.stride(0), 0, bg.stride(0), 0)
         if dxs is not None:
             tap.put(dxs)
-        return dx, None, None, None, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None, None, None, None
 
 
-def layernorm_res(store, mod, x, G, scale=None, rps=1, tap=None):
-    """(LN(x), LN(x) for a second consumer, x) with the fused backward (LayerNormResF)."""
+def layernorm_res(store, mod, x, G, scale=None, rps=1, tap=None, tail=None):
+    """(LN(x), LN(x) for a second consumer, x) with the fused backward (LayerNormResF).
+    tail: the LNTail whose producing launch already normalised x (its pre is used if set)."""
     gamma = store.w(mod.weight, compute=False).view(G, -1)
     beta = store.w(mod.bias, compute=False).view(G, -1)
     gg = store.g(mod.weight).view(G, -1)
     bg = store.g(mod.bias).view(G, -1)
-    return LayerNormResF.apply(x, gamma, beta, gg, bg, mod.eps, G, scale, rps, tap, mod.weight)
+    pre = None
+    if tail is not None:
+        assert tail.mod is mod
+        pre, tail.pre = tail.pre, None
+    return LayerNormResF.apply(x, gamma, beta, gg, bg, mod.eps, G, scale, rps, tap, mod.weight, pre)
 
 
 class LayerNormF(Function):

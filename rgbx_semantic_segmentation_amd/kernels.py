@@ -177,6 +177,54 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, bias: torch.Tensor |
     return C
 
 
+_TICKETS: dict = {}
+
+
+def _tickets(n: int, device) -> torch.Tensor:
+    """Zeroed uint32 arrival counters for row-block tails (cmx_gemm_ln), one pool per (device,
+    stream): launches on one stream are ordered and each leaves its counters zero, so they share
+    the pool; a concurrent stream gets its own.  Sized once (B4 / B5 stage-1 row blocks fit)
+    so no allocation happens inside a HIP-graph capture."""
+    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
+    t = _TICKETS.get(key)
+    if t is None or t.numel() < n:
+        if torch.cuda.is_current_stream_capturing():
+            raise _lib.CMXError(f"gemm_ln: ticket pool of {0 if t is None else t.numel()} < {n} inside a capture")
+        t = _TICKETS[key] = torch.zeros(max(n, 8192), dtype=torch.int32, device=device)
+    return t
+
+
+def gemm_ln(A, B, C, ln_gamma, ln_beta, ln_eps, bias=None, residual=None, rscale=None, rows_per_sample=1,
+            act="none", A2=None):
+    """K.gemm's forward form (C = epi(A @ B^T)) plus the LayerNorm of C's rows in the same
+    launch (cmx_gemm_ln): returns (y, mean, rstd), y = LN(C) in C's layout, mean / rstd (G, M)
+    fp32; None when the problem is not eligible (the caller runs gemm + the LN kernel)."""
+    G, M, K1 = A.shape
+    Kd = K1 + (A2.shape[2] if A2 is not None else 0)
+    N = B.shape[1]
+    if A.dtype not in (torch.bfloat16, torch.float16) or N % 64 or N > 512 or not C.is_contiguous():
+        return None
+    tA, lda, sA = _operand(A, "A")
+    tB, ldb, sB = _operand(B, "B")
+    _, lda2, sA2 = _operand(A2, "A2") if A2 is not None else (0, 0, 0)
+    if tA or tB:
+        return None
+    sbias = (bias.stride(0) if bias.dim() == 2 else 0) if bias is not None else 0
+    y = torch.empty_like(C)
+    mean = torch.empty(G, M, dtype=torch.float32, device=C.device)
+    rstd = torch.empty_like(mean)
+    tk = _tickets(query("cmx_gemm_ln_tickets", G, M), C.device)
+    st = _lib.LIB.cmx_gemm_ln(ptr(A), ptr(A2), ptr(B), ptr(C), ptr(bias), ptr(residual), ptr(rscale), G, M, N, Kd, K1,
+                         lda, lda2, ldb, C.stride(1), sA, sA2, sB, C.stride(0), sbias, int(rows_per_sample), ACT[act],
+                         ptr(ln_gamma), ptr(ln_beta), ln_gamma.stride(0) if ln_gamma.dim() == 2 else 0,
+                         float(ln_eps), ptr(y), ptr(mean), ptr(rstd), ptr(tk), dtype_code(A), stream())
+    if st == _lib.CMX_ERR_ARG:
+        return None
+    if st != 0:
+        raise _lib.CMXError(f"cmx_gemm_ln failed ({st}): {_lib.last_error()}")
+    return y, mean, rstd
+
+
 _PLAN_BYTES = query("cmx_gemm_plan_size")
 
 

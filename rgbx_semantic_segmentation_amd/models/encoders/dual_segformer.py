@@ -127,18 +127,21 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
                 rows.append((1.0 - self.dp[s][0][i], 1.0 - self.dp[s][1][i]))
         return rows
 
-    def run_block(self, store, blk: Block, x, B, H, W, s_attn, s_mlp, prev=(None, None)):
+    def run_block(self, store, blk: Block, x, B, H, W, s_attn, s_mlp, prev=(None, None), tail=None,
+                  next_norm=None):
         """One Block (dual_segformer.py:166-180) for both streams.  ``prev`` = (DropPath scale,
         GradTap) of the residual branch that produced ``x`` (the previous block's fc2): norm1's
-        backward writes that branch's scaled gradient.  Returns (x_out, (s_mlp, tap)) for the
-        next consumer of x_out."""
+        backward writes that branch's scaled gradient.  ``tail``: the LNTail of norm1 when the
+        producer of x normalised it in its launch; ``next_norm``: the norm that consumes this
+        block's output (the next block's norm1 or the stage norm), computed in fc2's launch.
+        Returns (x_out, (s_mlp, tap), LNTail of next_norm or None) for the next consumer of x_out."""
         G, M, C = x.shape
         N = H * W
         a = blk.attn
         # norm1 also passes x through for the attention residual: its backward sums both gradients
         # (q and the SR path read norm1's output through separate handles: the norm's backward
         # sums their gradients on load)
-        h, h2, xr = F.layernorm_res(store, blk.norm1, x, G, scale=prev[0], rps=N, tap=prev[1])
+        h, h2, xr = F.layernorm_res(store, blk.norm1, x, G, scale=prev[0], rps=N, tap=prev[1], tail=tail)
 
         if a.sr_ratio > 1:
             xs, Hk, Wk = F.conv(store, a.sr, h2, G, G * B, H, W, C, a.sr_ratio, 0)
@@ -150,13 +153,16 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
         o = F.SRAttentionF.apply(q, kv, G * B, N, Nk, a.num_heads, C // a.num_heads)
         # x + drop_path(proj(o)): residual and DropPath scale fused into the proj GEMM epilogue
         tap_a = F.GradTap() if s_attn is not None else None
-        x = F.glinear(store, a.proj.weight, a.proj.bias, o, res=xr, rscale=s_attn, rps=N, tap=tap_a)
-        h, _, xr = F.layernorm_res(store, blk.norm2, x, G, scale=s_attn, rps=N, tap=tap_a)
+        t2 = F.LNTail(blk.norm2)
+        x = F.glinear(store, a.proj.weight, a.proj.bias, o, res=xr, rscale=s_attn, rps=N, tap=tap_a, ln_tail=t2)
+        h, _, xr = F.layernorm_res(store, blk.norm2, x, G, scale=s_attn, rps=N, tap=tap_a, tail=t2)
         f = F.glinear(store, blk.mlp.fc1.weight, blk.mlp.fc1.bias, h)
         f = F.dwconv(store, blk.mlp.dwconv.dwconv, f, G * B, B, H, W, "gelu")
         tap_m = F.GradTap() if s_mlp is not None else None
-        x = F.glinear(store, blk.mlp.fc2.weight, blk.mlp.fc2.bias, f, res=xr, rscale=s_mlp, rps=N, tap=tap_m)
-        return x, (s_mlp, tap_m)
+        tn = F.LNTail(next_norm) if next_norm is not None else None
+        x = F.glinear(store, blk.mlp.fc2.weight, blk.mlp.fc2.bias, f, res=xr, rscale=s_mlp, rps=N, tap=tap_m,
+                      ln_tail=tn)
+        return x, (s_mlp, tap_m), tn
 
     def run(self, store, images, B, H, W, training, dp_scales: Optional[torch.Tensor], bn_group=None):
         """images: (2*B, 3, H, W) fp32 NCHW (RGB batch then X batch), or the pair of (B, 3, H, W)
@@ -173,6 +179,8 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
         bi = 0
         Hc, Wc, Cin = H, W, 3
         sync = getattr(self, "grad_sync", None)     # dist.BucketedGradSync (data parallel) or None
+        if sync is None:                            # optim.SegmentUpdate (update overlap) or None
+            sync = getattr(self, "seg_update", None)
         main = torch.cuda.current_stream() if x.is_cuda else None
         side = streams.ffm_stream(main.device) if (main is not None and streams.FFM_SIDE) else None
         for s in range(4):
@@ -190,14 +198,16 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
             prev = (None, None)
             blocks = getattr(self, f"block{s + 1}")
             snorm = getattr(self, f"norm{s + 1}")
+            tail = None
             for i, blk in enumerate(blocks):
                 sa = sm = None
                 if dp_scales is not None:
                     sa, sm = dp_scales[bi, 0], dp_scales[bi, 1]
-                x, prev = self.run_block(store, blk, x, B, Hc, Wc, sa, sm, prev)
+                nxt = blocks[i + 1].norm1 if i + 1 < len(blocks) else snorm
+                x, prev, tail = self.run_block(store, blk, x, B, Hc, Wc, sa, sm, prev, tail=tail, next_norm=nxt)
                 bi += 1
             # stage norm: its backward also writes the last block's DropPath-scaled gradient
-            x, _, _ = F.layernorm_res(store, snorm, x, G, scale=prev[0], rps=Hc * Wc, tap=prev[1])
+            x, _, _ = F.layernorm_res(store, snorm, x, G, scale=prev[0], rps=Hc * Wc, tap=prev[1], tail=tail)
             C = self.embed_dims[s]
             fr = self.FRMs[s]
             if isinstance(fr, ImprovedFeatureRectifyModule):

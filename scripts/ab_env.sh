@@ -9,6 +9,6 @@ for r in $(seq ${REPS:-2}); do
   for arm in "$@"; do
     envs=""; [ "$arm" != "base" ] && envs="$arm"
     out=$(env $envs timeout -k 10 100 python -u bench.py --steps ${STEPS:-20} --warmup 5 --no-cpu-baseline 2>/dev/null) || { echo "arm '$arm' failed"; exit 1; }
-    echo "$out" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('rep $r', '[$arm]', d['value'], d['ms_per_step'], 'grouped_us', (d.get('roofline') or {}).get('avg_launch_us'))"
+    echo "$out" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d.get('roofline') or {}; print('rep $r', '[$arm]', d['value'], d['ms_per_step'], 'gemm_family_us', r.get('total_us'), 'grouped_us', (r.get('second') or {}).get('avg_launch_us'))"
   done
 done

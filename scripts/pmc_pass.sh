@@ -11,7 +11,7 @@ RE=${3:-gemm_grouped}
 shift 3
 mkdir -p gpurun_out
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 240 rocprofv3 --pmc $C --kernel-include-regex "$RE" -d gpurun_out/pmc_${TAG}_$C -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline "$@" > gpurun_out/pmc_${TAG}_$C.log 2>&1
+  CMX_BENCH_NO_ROOFLINE=1 timeout -k 10 240 rocprofv3 --pmc $C --kernel-include-regex "$RE" -d gpurun_out/pmc_${TAG}_$C -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline "$@" > gpurun_out/pmc_${TAG}_$C.log 2>&1
   rc=$?; echo "pmc $C rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
 python3 scripts/pmc_summary.py gpurun_out/pmc_${TAG}.json $(ls gpurun_out/pmc_${TAG}_FETCH_SIZE/*/*.db gpurun_out/pmc_${TAG}_FETCH_SIZE/*.db 2>/dev/null | head -1) $(ls gpurun_out/pmc_${TAG}_WRITE_SIZE/*/*.db gpurun_out/pmc_${TAG}_WRITE_SIZE/*.db 2>/dev/null | head -1) "$WORKLOAD"

@@ -2,7 +2,13 @@
 a crash ends only that case).  Usage: python scripts/rccl_capture_probe.py CASE
 CASE in {a2a, ag, rs, rs32, ar, bc}_{eager, graph}: all_to_all_single / all_gather (bf16) /
 reduce_scatter (bf16, fp32) / all_reduce (fp32, the default gradient payload and SyncBN) /
-broadcast (fp32, the per-forward BatchNorm buffer sync)."""
+broadcast (fp32, the per-forward BatchNorm buffer sync).
+
+Teardown: each phase prints a marker and a faulthandler watchdog dumps every
+thread's Python stack if a phase blocks for CMX_PROBE_WATCHDOG_S (default 20 s), so a hang names
+its frame.  CMX_PROBE_DEL_GRAPH=1 deletes the captured graph (and synchronises) before
+destroy_process_group -- the order bench.py / train.py use."""
+import faulthandler
 import os
 import sys
 
@@ -54,7 +60,15 @@ def main(case):
         torch.cuda.synchronize()
     ok = torch.equal(out, src)
     print(f"{case}: {'ok' if ok else 'WRONG'}", flush=True)
+    wd = float(os.environ.get("CMX_PROBE_WATCHDOG_S", "20"))
+    faulthandler.dump_traceback_later(wd, repeat=True, exit=False)
+    if case.endswith("graph") and os.environ.get("CMX_PROBE_DEL_GRAPH") == "1":
+        print("teardown: del graph", flush=True)
+        del g
+        torch.cuda.synchronize()
+    print("teardown: destroy_process_group", flush=True)
     dist.destroy_process_group()
+    print("teardown: destroyed; exiting", flush=True)
     sys.exit(0 if ok else 1)
 
 

@@ -7,6 +7,15 @@ import re
 import sqlite3
 import sys
 
+
+def kname(n):
+    """Kernel name without its argument list: 'void ' and '(anonymous namespace)::' dropped, then
+    everything from the first '(' that opens the PARAMETER list (the anonymous-namespace prefix
+    used to be cut at its own '(' and left a blank name)."""
+    n = n.replace("void ", "").replace("(anonymous namespace)::", "")
+    return re.sub(r"\(.*", "", n)
+
+
 c = sqlite3.connect(sys.argv[1])
 top = int(sys.argv[2]) if len(sys.argv) > 2 else 40
 rows = c.execute("select start, end, name from kernels order by start").fetchall()
@@ -22,17 +31,17 @@ print(f"launches/step {len(seg)}  wall {(seg[-1][1] - seg[0][0]) / 1e3:.0f} us  
 # the largest idle gaps inside the step
 prev = rows[idx[pick]]
 print(f"boundary gap {(seg[0][0] - prev[1]) / 1e3:.1f} us after {prev[2][:40]}; first kernels: "
-      + ", ".join(re.sub(r"\(.*", "", r[2].replace("void ", ""))[:30] for r in seg[:3]))
+      + ", ".join(kname(r[2])[:30] for r in seg[:3]))
 gaps, end = [], seg[0][1]
 for s_, e_, n_ in seg[1:]:
     if s_ > end:
-        gaps.append(((s_ - end) / 1e3, re.sub(r"\(.*", "", n_.replace("void ", ""))[:50]))
+        gaps.append(((s_ - end) / 1e3, kname(n_)[:60]))
     end = max(end, e_)
 print(f"idle inside the step {sum(g for g, _ in gaps):.0f} us over {len(gaps)} gaps; largest: "
       + "; ".join(f"{g:.1f} us before {n}" for g, n in sorted(gaps, reverse=True)[:6]))
 cat = collections.defaultdict(lambda: [0, 0.0])
 for s, e, n in seg:
-    k = re.sub(r"\(.*", "", n.replace("void ", "").replace("(anonymous namespace)::", ""))
+    k = kname(n)
     cat[k][0] += 1
     cat[k][1] += (e - s) / 1e3
 for k, (n, t) in sorted(cat.items(), key=lambda x: -x[1][1])[:top]:
@@ -40,8 +49,8 @@ for k, (n, t) in sorted(cat.items(), key=lambda x: -x[1][1])[:top]:
 
 # kernel families of the step (DESIGN.md per-family table)
 FAMILIES = [
-    ("GEMM (MFMA: linear / conv / decoder / attention projections)", r"^gemm_|^splitk_reduce"),
-    ("grouped wgrad + reduce (deferred weight gradients)", r"^gemm_grouped|^reduce_grouped"),
+    ("grouped wgrad + reduce (deferred weight gradients)", r"^(gemmk::)?gemm_grouped|^reduce_grouped"),
+    ("GEMM (MFMA: linear / conv / decoder / attention projections)", r"^(gemmk::)?(gemm_|splitk_reduce)"),
     ("SRA attention (MFMA)", r"^sra_"),
     ("depthwise 3x3 conv + GELU (MixFFN)", r"^dw2_|^dw_"),
     ("LayerNorm", r"^ln_"),
@@ -57,8 +66,6 @@ FAMILIES = [
 fam = collections.defaultdict(lambda: [0, 0.0])
 for k, (n, t) in cat.items():
     name = next((f for f, rx in FAMILIES if re.search(rx, k)), "other")
-    if name == "GEMM (MFMA: linear / conv / decoder / attention projections)" and re.search(r"^gemm_grouped", k):
-        name = "grouped wgrad + reduce (deferred weight gradients)"
     fam[name][0] += n
     fam[name][1] += t
 busy = sum(t for _, t in fam.values())

@@ -34,26 +34,29 @@ pytestmark = pytest.mark.gpu
 
 RATIO = 4.0
 OUTLIER_RATIO = 12.0
-# CM-FRM / FFM tensors of the bf16 cases: at most 2x the emulated error,
-# outliers up to 4x for at most 4 % of them (6 of 148 at B2), with two documented adjustments:
+# CM-FRM / FFM tensors of the bf16 cases: at most 2x the
+# emulated error, outliers up to 4x for at most 4 % of them (6 of 148 at B2), and every
+# yardstick (the error the comparison allows) below YARD_MAX of the tensor's largest gradient, so
+# that no check is vacuous.  Two documented adjustments:
 #  * ChannelWeights' first Linear (FRMs.s.channel_weights.mlp.0): hidden units whose fp64
 #    pre-activation lies within 2^-7 of the layer's typical magnitude, or within RATIO x the
 #    largest error bf16 storage puts on the layer's pre-activations (emulation, per sample), in
-#    some sample are excluded from the row
-#    comparison -- their ReLU decision is decided by rounding, and a flip moves the whole
-#    gradient row (round 4: every FRM outlier row was such a unit, e.g. stage 2 unit 81 with
-#    z = -0.00038, whose fp64 row is exactly zero);
+#    some sample are excluded from the row comparison -- their ReLU decision is decided by
+#    rounding, and a flip moves the whole gradient row (round 4: every FRM outlier row was such a
+#    unit, e.g. stage 2 unit 81 with z = -0.00038, whose fp64 row is exactly zero).  At most
+#    ZBAND_MAX_SHARE of the rows are excluded (the ones nearest zero); the share is recorded;
 #  * SpatialWeights' biases (a sum over all B*H*W pixels with heavy cancellation, e.g. 600 terms
 #    at stage 4 whose sum is ~1/9 of the sum of their magnitudes): the yardstick is at least the
-#    L1 norm of the per-pixel term errors of the bf16-storage emulation, sum|dz_emu - dz_64| /
-#    max|gradient| -- the most any summation order can make of per-term errors of that size --
-#    and at least 2^-8 x sum|per-pixel terms| / max|gradient|, the error bf16 inputs alone allow.
-#    (The emulation's own sum error is one signed realization of those per-term errors; measured
-#    against it, this 2-value tensor moved between 2x and 9.4x with fp32 summation order alone.)
+#    random-walk size of the bf16-storage emulation's per-pixel term errors,
+#    sqrt(sum (dz_emu - dz_64)^2) / max|gradient| (rounding noise adds up like sqrt(N), not like
+#    the L1 worst case N), and at least 2^-8 x sqrt(sum dz_64^2) / max|gradient|, the random-walk
+#    error of bf16 inputs alone.
 RATIO_FUSION = 2.0
 OUTLIER_FUSION = 4.0
 FUSION_OUTLIER_SHARE = 0.04
 ZBAND = 2.0 ** -7
+ZBAND_MAX_SHARE = 0.05
+YARD_MAX = 0.25
 BF16_EPS = 2.0 ** -8
 
 CONFIGS = {
@@ -123,6 +126,7 @@ def _record(case, loss, loss64, rows, bad, grad_bad, notes=None):
     with open(os.path.join(out, f"{case}.json"), "w") as f:
         json.dump({"case": case, "ratio_bound": RATIO, "outlier_ratio_bound": OUTLIER_RATIO,
                    "fusion_ratio_bound": RATIO_FUSION, "fusion_outlier_ratio_bound": OUTLIER_FUSION,
+                   "fusion_yardstick_max": YARD_MAX, "zband_max_share": ZBAND_MAX_SHARE,
                    "loss_gpu": loss, "loss_fp64": loss64, "n_tensors": len(tab),
                    "ratio_median": rs[len(rs) // 2], "ratio_max": rs[-1],
                    "n_over_bound": len(bad) + len(grad_bad), "tensors": tab}, f, indent=1)
@@ -159,22 +163,31 @@ def _fusion_adjust(n, gpu_g, emu_g, g64, den, probes, probes_emu=None):
         if probes_emu and key in probes_emu:         # the pre-activation error bf16 storage allows
             ez = (probes_emu[key].double() - z).abs().amax(1, keepdim=True)    # per sample, over units
             band = torch.maximum(band, RATIO * ez)
-        keep = (z.abs() > band).all(0)
+        # closeness of each unit to its ReLU decision: min over samples of |z| / band; units
+        # inside the band are candidates, at most ZBAND_MAX_SHARE of the rows (nearest zero first)
+        close = (z.abs() / band).amin(0)
+        cap = int(ZBAND_MAX_SHARE * close.numel())
+        order = torch.argsort(close)
+        cand = order[close[order] <= 1.0][:cap]
+        keep = torch.ones_like(close, dtype=torch.bool)
+        keep[cand] = False
         if bool(keep.any()):
             eg = (gpu_g - g64)[keep].abs().max().item() / den
             ee = (emu_g - g64)[keep].abs().max().item() / den
-            return eg, ee, f"{int((~keep).sum())} ReLU-band units excluded"
+            nin = int((close <= 1.0).sum())
+            return eg, ee, (f"{int((~keep).sum())} of {close.numel()} ReLU-band units excluded "
+                            f"({100.0 * (~keep).sum().item() / close.numel():.1f} %; {nin} inside the band)")
     m = re.match(r"backbone\.FRMs\.(\d+)\.spatial_weights\.mlp\.(0|2)\.bias$", n)
     if m and (f"dsw{m.group(2)}", int(m.group(1))) in probes:
         key = (f"dsw{m.group(2)}", int(m.group(1)))
         t = probes[key]
         gmax = max(g64.abs().max().item(), 1e-300)
-        allow = BF16_EPS * t.abs().sum((0, 2, 3)).max().item() / gmax
+        allow = BF16_EPS * t.pow(2).sum((0, 2, 3)).sqrt().max().item() / gmax
         if probes_emu and key in probes_emu:
-            allow = max(allow, (probes_emu[key].double() - t).abs().sum((0, 2, 3)).max().item() / gmax)
+            allow = max(allow, (probes_emu[key].double() - t).pow(2).sum((0, 2, 3)).sqrt().max().item() / gmax)
         eg = (gpu_g - g64).abs().max().item() / den
         ee = (emu_g - g64).abs().max().item() / den
-        return eg, max(ee, allow), f"cancellation allowance {allow:.3g}"
+        return eg, max(ee, allow), f"random-walk allowance {allow:.3g} (emulated sum error {ee:.3g})"
     return None
 
 
@@ -255,7 +268,7 @@ def test_bf16_train_step_vs_fp64_oracle(dev, case):
     p64 = dict(ref64.named_parameters())
     pem = dict(emu.named_parameters())
     gmax = max(p.grad.abs().max().item() for p in ref64.parameters())
-    grad_bad, fusion_bad, notes = [], [], {}
+    grad_bad, fusion_bad, yard_bad, notes = [], [], [], {}
     n_fusion = 0
     for n, p in model.named_parameters():
         g64 = p64[n].grad
@@ -271,6 +284,19 @@ def test_bf16_train_step_vs_fp64_oracle(dev, case):
                 eg, ee, notes[n] = adj
             n_fusion += 1
             _check(n, eg, ee, fusion_bad, ratio=RATIO_FUSION)
+            if g64.abs().max().item() < 1e-6 * gmax:
+                # structurally zero (a bias whose output a BatchNorm re-centres: ChannelEmbed's
+                # channel_embed.3 / .4 biases and norm bias through the decoder's linear_fuse BN):
+                # relative error is meaningless; held to RATIO_FUSION x the emulation's absolute error
+                notes.setdefault(n, "structurally zero gradient (BatchNorm follows)")
+            elif ee > YARD_MAX:
+                # bf16 storage upstream of the block moves this gradient by more than YARD_MAX in
+                # the emulation itself: the end-to-end check cannot bite, so the block's kernels
+                # are held to a yardstick < YARD_MAX on identical inputs at this config's stage
+                # shapes by tests/test_gpu_fusion_local.py
+                yard_bad.append((round(ee, 3), n))
+                notes[n] = (notes.get(n, "") + "; " if n in notes else "") + \
+                    f"yardstick {ee:.3g} > {YARD_MAX}: bounded locally (tests/test_gpu_fusion_local.py)"
         else:
             _check(n, eg, ee, grad_bad)
         rows.append((n, eg, ee))
@@ -301,3 +327,5 @@ def test_bf16_train_step_vs_fp64_oracle(dev, case):
     assert len(grad_bad) <= n_allowed and all(b[0] <= OUTLIER_RATIO for b in grad_bad), grad_bad[:10]
     n_fusion_allowed = max(2, int(FUSION_OUTLIER_SHARE * n_fusion))
     assert len(fusion_bad) <= n_fusion_allowed and all(b[0] <= OUTLIER_FUSION for b in fusion_bad), fusion_bad
+    # the delegated tensors (yard_bad) are few and all in the fusion blocks' spatial / channel heads
+    assert len(yard_bad) <= max(2, int(0.1 * n_fusion)), f"CM-FRM / FFM yardsticks above {YARD_MAX}: {yard_bad}"

@@ -179,6 +179,15 @@ def _worker_buffers(rank, world, port, q):
         allv = [torch.empty_like(flat) for _ in range(world)]
         dist.all_gather(allv, mine)
         ok = ok and not torch.equal(allv[0], allv[1])
+        # a subgroup without global rank 0 (world 3, group {1, 2}): the source is the group's
+        # first member, global rank 1 (every rank creates the group; only members broadcast)
+        sub = dist.new_group([1, 2]) if world >= 3 else None
+        if sub is not None and rank in (1, 2):
+            mine_sub = flat.clone()
+            broadcast_buffers(flat, sub)
+            ok = ok and torch.equal(flat, allv[1]) and (rank == 1 or not torch.equal(mine_sub, flat))
+            flat.copy_(mine_sub)
+        dist.barrier()
         broadcast_buffers(flat)
         ok = ok and torch.equal(flat, allv[0]) and torch.equal(m[3].running_var, allv[0][12:16])
         q.put((rank, bool(ok)))
@@ -186,11 +195,11 @@ def _worker_buffers(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_bn_buffer_broadcast_gloo_world2():
+def test_bn_buffer_broadcast_gloo_world3_subgroup():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 31500 + (os.getpid() % 1000)
-    procs = [ctx.Process(target=_worker_buffers, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker_buffers, args=(r, 3, port, q)) for r in range(3)]
     for p in procs:
         p.start()
     res = [q.get(timeout=180) for _ in procs]

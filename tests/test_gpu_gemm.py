@@ -348,3 +348,40 @@ def test_gemm_h2_per_head(dev, dtype, GB, heads, N, D):
     ref = kh.float() @ ctxT.float().transpose(2, 3)
     assert rel(out, ref) < (1e-5 if dtype == torch.float32 else 1e-2), rel(out, ref)
     assert not wide[..., :C].abs().any()                                     # the other half untouched
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("G,M,N,K,res", [(2, 38400, 64, 256, True), (2, 9600, 128, 512, True), (2, 2400, 320, 1280, True),
+                                         (2, 600, 512, 2048, True), (2, 2400, 320, 320, False), (1, 130, 128, 64, True),
+                                         (2, 600, 512, 512, True)])
+def test_gemm_ln_tail(dev, dtype, G, M, N, K, res):
+    """cmx_gemm_ln: the GEMM output is the plain launch's, bit for bit (the tail only changes the
+    store's cache policy), and the row-block LayerNorm tail equals cmx_layernorm_fwd on that
+    output (same two-pass fp32 statistics; y within one 16-bit rounding).  Several launches in a
+    row on the shared ticket pool: every launch must leave the counters zero."""
+    from rgbx_semantic_segmentation_amd import kernels as Kk
+    torch.manual_seed(1)
+    A = torch.randn(G, M, K, device="cuda").to(dtype)
+    W = (torch.randn(G, N, K, device="cuda") / math.sqrt(K)).to(dtype)
+    bias = torch.randn(G, N, device="cuda")
+    R = torch.randn(G, M, N, device="cuda").to(dtype) if res else None
+    rps = max(1, M // 2)
+    rscale = (torch.rand(G * M // rps, device="cuda") + 0.5) if res else None
+    gamma = torch.rand(G, N, device="cuda") + 0.5
+    beta = torch.randn(G, N, device="cuda")
+    for rep in range(3):
+        C = torch.empty(G, M, N, device="cuda", dtype=dtype)
+        out = Kk.gemm_ln(A, W, C, gamma, beta, 1e-6, bias=bias, residual=R, rscale=rscale, rows_per_sample=rps)
+        assert out is not None, "gemm_ln refused an eligible problem"
+        y, mean, rstd = out
+        C0 = torch.empty_like(C)
+        Kk.gemm(A, W, C0, bias=bias, residual=R, rscale=rscale, rows_per_sample=rps)
+        torch.cuda.synchronize()
+        assert torch.equal(C, C0), rep
+        y0, m0, r0 = Kk.layernorm_fwd(C0, gamma, beta, 1e-6, G=G)
+        torch.cuda.synchronize()
+        assert (mean.flatten() - m0).abs().max().item() < 1e-5 * max(1.0, m0.abs().max().item())
+        assert ((rstd.flatten() - r0).abs() / r0).max().item() < 1e-5
+        ulp = 2.0 ** (-7 if dtype == torch.bfloat16 else -10)
+        assert ((y.float() - y0.float()).abs() / y0.float().abs().clamp_min(1.0)).max().item() <= ulp, rep
+    assert int(Kk._tickets(1, torch.device("cuda")).abs().sum().item()) == 0
