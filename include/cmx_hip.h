@@ -233,6 +233,19 @@ int cmx_gemm_group_pack(void* rec, const void* A, const void* B, void* C, float*
 int cmx_gemm_ln(const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R, const float* rscale, int G, int M, int N, int K, int K1, int64_t lda, int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias, int rows_per_sample, int act, const float* ln_gamma, const float* ln_beta, int64_t ln_sg, float ln_eps, void* ln_y, float* ln_mean, float* ln_rstd, unsigned* tickets, int dtype, hipStream_t stream);
 size_t cmx_gemm_ln_tickets(int G, int M);
 int cmx_gemm_grouped(const void* recs, int nrec, int total_blocks, int dtype, hipStream_t stream);
+/* ---- Mix-FFN bands (Mlp.forward fc1 -> DWConv 3x3 -> GELU, dual_segformer.py:67-71) --------------
+ * x (G, ipg*H*W, C) contiguous 16-bit; W1 (G, Ch, C) (group stride sW), b1 (G, Ch) (stride sb = Ch),
+ * wdw (G, Ch, 9) (stride sdw = 9 Ch) and bdw (G, Ch) fp32.  One launch: h = x W1^T + b1, z = DW(h) + bdw,
+ * a = GELU(z), act'(z) -- bit-identical to cmx_gemm + cmx_dwconv3x3_fwd_save.  A workgroup owns a band of
+ * cmx_mixffn_band_rows(W) image rows (+1 halo row each side, fc1 recomputed there) x 64 hidden channels;
+ * 0 = the band kernels do not apply (W > 85).
+ * bwd: dz2 (G, ipg*H*W, C) = fc2's output gradient, W2 (G, C, Ch): da = dz2 W2 (as fc2's dgrad would),
+ * dz = da * act'(z), dh = DW^T(dz), and the DW dW / db partials (G, P, Ch * 10) in the workspace
+ * (cmx_mixffn_bwd_workspace bytes, P = workspace / (40 G Ch)) for cmx_reduce_grouped. */
+int cmx_mixffn_band_rows(int W);
+size_t cmx_mixffn_bwd_workspace(int G, int ipg, int H, int W, int Ch);
+int cmx_mixffn_fwd(const void* x, const void* W1, const float* b1, const float* wdw, const float* bdw, void* h, void* gprime, void* a, int G, int ipg, int H, int W, int C, int Ch, int64_t sW, int64_t sb, int64_t sdw, int dtype, hipStream_t stream);
+int cmx_mixffn_bwd(const void* dz2, const void* W2, const float* wdw, const void* h, const void* gprime, void* dh, float* workspace, int G, int ipg, int H, int W, int C, int Ch, int64_t sW, int64_t sdw, int dtype, hipStream_t stream);
 /* cmx_gemm_grouped_capped: the same launch on a grid of at most max_blocks workgroups (a multiple
  * of 8; <= 0: uncapped), each walking blocks b, b + grid, ...: a grouped weight-gradient launch
  * beside the backward on a side stream keeps to that share of the chip */

@@ -580,7 +580,7 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
 // instruction; the block's waves take rows round-robin.  Numerics as ln_fwd_kernel
 // (layernorm.hip): two-pass mean / variance of the stored 16-bit values in fp32.
 template <typename E>
-__device__ __noinline__ void gemm_ln_tail(const GemmArgs& p, const int lin) {
+__device__ __forceinline__ void gemm_ln_tail(const GemmArgs& p, const int lin) {
   const int ntile = p.tiles_m * p.tiles_n;
   const int t = lin % ntile, g = (lin / ntile) % p.G;
   const int tm = t / p.tiles_n;
@@ -602,47 +602,53 @@ __device__ __noinline__ void gemm_ln_tail(const GemmArgs& p, const int lin) {
     ga[e] = live ? p.ln_gamma[(long)g * p.ln_sg + ch * 8 + e] : 0.f;
     be[e] = live ? p.ln_beta[(long)g * p.ln_sg + ch * 8 + e] : 0.f;
   }
-  constexpr int MAXIT = 16;                              // 64 rows / (4 waves x 1 row) at N = 512
-  uint4 raw[MAXIT];
+  // rows in two halves of up to 8 per lane (all of a half's loads in flight before its first
+  // reduction; fully unrolled with guards, so the staging stays in registers)
+  constexpr int HALF = 8;
   const int step = nw * RPW;                             // rows per pass of the whole block
+  const int npass = (rows + step - 1) / step;            // <= 16 (64 rows, 4 waves, 1 row per wave)
 #pragma unroll
-  for (int it = 0; it < MAXIT; ++it) {
-    const int r = it * step + wave * RPW + sub;
-    if (it * step < rows && r < rows && live) raw[it] = ld16_sc1(Cg, (int)(((long)(i0 + r) * p.ldc + ch * 8) * 2));
-    else raw[it] = make_uint4(0, 0, 0, 0);
-  }
+  for (int h0 = 0; h0 < 16; h0 += HALF) {
+    if (h0 >= npass) break;
+    uint4 raw[HALF];
 #pragma unroll
-  for (int it = 0; it < MAXIT; ++it) {
-    if (it * step >= rows) break;
-    const int r = it * step + wave * RPW + sub;
-    float v[8];
-    const uint32_t w4[4] = {raw[it].x, raw[it].y, raw[it].z, raw[it].w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const cmx_f2 f = unpack2<E>(w4[q]);
-      v[2 * q] = f.x;
-      v[2 * q + 1] = f.y;
+    for (int u = 0; u < HALF; ++u) {
+      const int r = (h0 + u) * step + wave * RPW + sub;
+      raw[u] = make_uint4(0, 0, 0, 0);
+      if (h0 + u < npass && r < rows && live) raw[u] = ld16_sc1(Cg, (int)(((long)(i0 + r) * p.ldc + ch * 8) * 2));
     }
-    float sm = 0.f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) sm += v[e];
-    sm = group_sum(sm, TPR);
-    const float mu = sm / C;
-    float q2 = 0.f;
-    if (live) {
+    for (int u = 0; u < HALF; ++u) {
+      const int r = (h0 + u) * step + wave * RPW + sub;
+      float v[8];
+      const uint32_t w4[4] = {raw[u].x, raw[u].y, raw[u].z, raw[u].w};
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { const float d = v[e] - mu; q2 += d * d; }
-    }
-    q2 = group_sum(q2, TPR);
-    const float rs = rsqrtf(q2 / C + p.ln_eps);
-    if (r < rows && live) {
-      float o[8];
+      for (int q = 0; q < 4; ++q) {
+        const cmx_f2 f = unpack2<E>(w4[q]);
+        v[2 * q] = f.x;
+        v[2 * q + 1] = f.y;
+      }
+      float sm = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = (v[e] - mu) * rs * ga[e] + be[e];
-      store_vec<E>(Yg + (long)(i0 + r) * p.ldc + ch * 8, o);
-      if (ch == 0) {
-        p.ln_mean[(long)g * p.M + i0 + r] = mu;
-        p.ln_rstd[(long)g * p.M + i0 + r] = rs;
+      for (int e = 0; e < 8; ++e) sm += v[e];
+      sm = group_sum(sm, TPR);
+      const float mu = sm / C;
+      float q2 = 0.f;
+      if (live) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { const float d = v[e] - mu; q2 += d * d; }
+      }
+      q2 = group_sum(q2, TPR);
+      const float rs = rsqrtf(q2 / C + p.ln_eps);
+      if (h0 + u < npass && r < rows && live) {
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (v[e] - mu) * rs * ga[e] + be[e];
+        store_vec<E>(Yg + (long)(i0 + r) * p.ldc + ch * 8, o);
+        if (ch == 0) {
+          p.ln_mean[(long)g * p.M + i0 + r] = mu;
+          p.ln_rstd[(long)g * p.M + i0 + r] = rs;
+        }
       }
     }
   }

@@ -54,7 +54,7 @@ class GLinear(Function):
     x + drop_path(proj/fc2(...)), dual_segformer.py:168-169)."""
 
     @staticmethod
-    def forward(ctx, W, Wg, b, bg, anchor, act, res, rscale, rps, x1, x2, tap=None, ln=None):
+    def forward(ctx, W, Wg, b, bg, anchor, act, res, rscale, rps, x1, x2, tap=None, ln=None, dgrad_tap=None):
         G, N, Ktot = W.shape
         M = x1.shape[1]
         assert x1.shape[-1] + (x2.shape[-1] if x2 is not None else 0) == Ktot, (x1.shape, W.shape)
@@ -70,13 +70,13 @@ class GLinear(Function):
         if pre is None:
             _fwd_gemm(x1, W, b, y, act=act, res=res, rscale=rscale, rps=rps, x2=x2)
         ctx.save_for_backward(W, x1, x2, y if act == "relu" else None)
-        ctx.meta = (Wg, bg, act, res is not None, rscale, rps, tap)
+        ctx.meta = (Wg, bg, act, res is not None, rscale, rps, tap, dgrad_tap)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         W, x1, x2, y = ctx.saved_tensors
-        Wg, bg, act, has_res, rscale, rps, tap = ctx.meta
+        Wg, bg, act, has_res, rscale, rps, tap, dgrad_tap = ctx.meta
         dy = _c(dy)
         G, M, N = dy.shape
         dres = dy if has_res else None
@@ -91,14 +91,18 @@ class GLinear(Function):
             dz = K.act_bwd(dz, y, "relu")
         k1 = x1.shape[-1]
         dx1 = dx2 = None
-        if ctx.needs_input_grad[9]:
+        if dgrad_tap is not None and ctx.needs_input_grad[9] and dz.is_contiguous():
+            # the producer of x1 computes this input gradient inside its own backward launch
+            # (MixFFNF: fc2's dgrad fused with the DWConv / GELU backward)
+            dgrad_tap.put((dz, W[:, :, :k1]))
+        elif ctx.needs_input_grad[9]:
             dx1 = _dgrad(dz, W[:, :, :k1], torch.empty_like(x1))
         if x2 is not None and ctx.needs_input_grad[10]:
             dx2 = _dgrad(dz, W[:, :, k1:], torch.empty_like(x2))
         _wgrad_into(dz, x1, Wg[:, :, :k1], bg)
         if x2 is not None:
             _wgrad_into(dz, x2, Wg[:, :, k1:])
-        return (None, None, None, None, None, None, dres, None, None, dx1, dx2, None, None)
+        return (None, None, None, None, None, None, dres, None, None, dx1, dx2, None, None, None)
 
 
 class LNTail:
@@ -111,7 +115,8 @@ class LNTail:
         self.mod, self.pre = mod, None
 
 
-def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1, tap=None, ln_tail=None):
+def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1, tap=None, ln_tail=None,
+            dgrad_tap=None):
     """Grouped linear using parameter ``wp`` (and bias ``bp``) of the store; x2 = second
     input segment (cat-free), res/rscale/rps = fused DropPath residual (rps = rows per sample).
     ln_tail (LNTail of the norm that consumes the output): that LayerNorm runs in this launch."""
@@ -125,14 +130,17 @@ def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1
         b = store.w(bp, compute=False).view(G, -1)
         bg = store.g(bp).view(G, -1)
     ln = None
-    if ln_tail is not None and LN_TAIL:
+    if ln_tail is not None and LN_TAIL and x1.shape[1] <= LN_TAIL_MAXM:
         m = ln_tail.mod
         ln = (store.w(m.weight, compute=False).view(G, -1), store.w(m.bias, compute=False).view(G, -1), m.eps, ln_tail)
-    return GLinear.apply(W, Wg, b, bg, wp, act, res, rscale, rps, x1, x2, tap, ln)
+    return GLinear.apply(W, Wg, b, bg, wp, act, res, rscale, rps, x1, x2, tap, ln, dgrad_tap)
 
 
-# CMX_LN_TAIL=0: every LayerNorm forward as its own launch (A/B switch)
+# CMX_LN_TAIL=0: every LayerNorm forward as its own launch (A/B switch); CMX_LN_TAIL_MAXM: only
+# GEMMs of at most that many rows per group take the tail (the stage-3/4 Linears: their tail
+# variants keep the occupancy of the k-group blocks they run as)
 LN_TAIL = os.environ.get("CMX_LN_TAIL", "1") != "0"
+LN_TAIL_MAXM = int(os.environ.get("CMX_LN_TAIL_MAXM", "1000000000"))
 
 # CMX_MULTI_GEMM=0 launches the grouped Linears of GLinearMulti one by one (A/B switch)
 MULTI_GEMM = os.environ.get("CMX_MULTI_GEMM", "1") != "0"
@@ -631,6 +639,103 @@ def dwconv(store, conv, h, NI, ipg, H, W, act):
     wg = store.g(conv.weight).view(G, -1, 9)
     bg = store.g(conv.bias).view(G, -1)
     return DWConvF.apply(h, w, b, wg, bg, NI, ipg, H, W, act, conv.weight)
+
+
+# ---------------------------------------------------------------------------- Mix-FFN bands
+# CMX_MIXFFN=0: fc1, DWConv+GELU and fc2's input gradient as separate launches (A/B switch)
+MIXFFN_BAND = os.environ.get("CMX_MIXFFN", "1") != "0"
+# bands of fewer rows recompute too much of fc1 on their halo rows ((R + 2) / R): stage 3 / 4 of
+# B2 / B4 at 480 x 640 get R = 4 / 10, stage 2 (W = 80) would get R = 1
+MIXFFN_MIN_ROWS = int(os.environ.get("CMX_MIXFFN_MIN_ROWS", "4"))
+
+
+class MixFFNF(Function):
+    """fc1 + DWConv3x3 + GELU of Mix-FFN (dual_segformer.py:67-71) as ONE launch per direction
+    (csrc/mixffn.hip): forward cmx_mixffn_fwd (h = fc1(x), a = GELU(DW(h)), act'(z) saved);
+    backward cmx_mixffn_bwd computes fc2's input gradient da = dz2 W2 itself (fc2's GLinear
+    hands over dz2 and W2 through ``tap`` instead of launching its dgrad), the DWConv / GELU
+    backward and the DW weight-gradient partials; then fc1's input gradient and its queued
+    weight gradient, as GLinear's backward would."""
+
+    @staticmethod
+    def forward(ctx, W1, Wg1, b1, bg1, wdw, bdw, wgdw, bgdw, anchor, x, B, H, W, tap):
+        G, M, C = x.shape
+        Ch = W1.shape[1]
+        h = torch.empty(G, M, Ch, dtype=x.dtype, device=x.device)
+        gp = torch.empty_like(h)
+        a = torch.empty_like(h)
+        K.call("cmx_mixffn_fwd", K.ptr(x), K.ptr(W1), K.ptr(b1), K.ptr(wdw), K.ptr(bdw), K.ptr(h), K.ptr(gp), K.ptr(a),
+               G, B, H, W, C, Ch, W1.stride(0), b1.stride(0), wdw.stride(0), K.dtype_code(x), K.stream())
+        ctx.save_for_backward(W1, x, h, gp, wdw)
+        ctx.meta = (Wg1, bg1, wgdw, bgdw, B, H, W, tap)
+        ctx.set_materialize_grads(False)
+        return a
+
+    @staticmethod
+    def backward(ctx, da):
+        W1, x, h, gp, wdw = ctx.saved_tensors
+        Wg1, bg1, wgdw, bgdw, B, H, W, tap = ctx.meta
+        G, M, Ch = h.shape
+        C = x.shape[-1]
+        handed = tap.take() if tap is not None else None
+        nbytes = K.query("cmx_mixffn_bwd_workspace", G, B, H, W, Ch)
+        ws = K._ws(nbytes, h.device)
+        dh = torch.empty_like(h)
+        if handed is not None:
+            dz2, W2 = handed
+            K.call("cmx_mixffn_bwd", K.ptr(dz2), K.ptr(W2), K.ptr(wdw), K.ptr(h), K.ptr(gp), K.ptr(dh), K.ptr(ws), G, B,
+                   H, W, C, Ch, W2.stride(0), wdw.stride(0), K.dtype_code(h), K.stream())
+            P = nbytes // (40 * G * Ch)
+        else:            # fc2 ran its own input gradient: the separate DWConv / GELU backward
+            assert da is not None
+            nbytes = K.query("cmx_dwconv3x3_bwd_workspace", G * B, B, H, W, Ch)
+            ws = K._ws(nbytes, h.device)
+            K.call("cmx_dwconv3x3_bwd_saved", K.ptr(_c(da)), K.ptr(h), K.ptr(gp), K.ptr(wdw), K.ptr(dh), 0, 0,
+                   K.ptr(ws), G * B, B, H, W, Ch, 0, K.dtype_code(h), K.stream())
+            P = K.query("cmx_dwconv3x3_bwd_saved_tiles", B, H, W)
+        deferred.reduce(ws, wgdw, bgdw, G, P, P * Ch * 10, Ch * 10, Ch, 10, 9, wgdw.stride(0), 9, bgdw.stride(0), 1)
+        dx = _dgrad(dh, W1, torch.empty_like(x)) if ctx.needs_input_grad[9] else None
+        _wgrad_into(dh, x, Wg1, bg1)
+        return (None,) * 9 + (dx, None, None, None, None)
+
+
+class DgradTap:
+    """Side channel from a GLinear's backward to the producer of its input: (dz, W) handed over
+    instead of the GLinear launching dx = dz W itself (MixFFNF fuses it into its backward)."""
+    __slots__ = ("t",)
+
+    def __init__(self):
+        self.t = None
+
+    def put(self, t):
+        self.t = t
+
+    def take(self):
+        t, self.t = self.t, None
+        return t
+
+
+def mixffn_ok(x, Ch, B, H, W) -> bool:
+    """The band kernels apply: 16-bit, a band of >= 1 row + halo within 256 tokens, hidden % 64,
+    every operand in the ParamStore layout (deferred weight gradients)."""
+    return (MIXFFN_BAND and deferred.ENABLED and x.dtype in (torch.bfloat16, torch.float16) and x.is_contiguous()
+            and Ch % 64 == 0 and x.shape[-1] % 8 == 0 and K.query("cmx_mixffn_band_rows", W) >= MIXFFN_MIN_ROWS)
+
+
+def mixffn(store, mlp, x, B, H, W, tap):
+    """a = GELU(DWConv(fc1(x))) (MixFFNF); ``tap`` is the DgradTap fc2's glinear hands dz2 to."""
+    G = x.shape[0]
+    W1 = store.w(mlp.fc1.weight)
+    W1 = W1.view(G, W1.shape[1], -1)
+    Wg1 = store.g(mlp.fc1.weight).view(G, W1.shape[1], -1)
+    b1 = store.w(mlp.fc1.bias, compute=False).view(G, -1)
+    bg1 = store.g(mlp.fc1.bias).view(G, -1)
+    conv = mlp.dwconv.dwconv
+    wdw = store.w(conv.weight, compute=False).view(G, -1, 9)
+    bdw = store.w(conv.bias, compute=False).view(G, -1)
+    wgdw = store.g(conv.weight).view(G, -1, 9)
+    bgdw = store.g(conv.bias).view(G, -1)
+    return MixFFNF.apply(W1, Wg1, b1, bg1, wdw, bdw, wgdw, bgdw, mlp.fc1.weight, x, B, H, W, tap)
 
 
 # ---------------------------------------------------------------------------- conv (implicit GEMM / im2col + GEMM)

@@ -181,11 +181,12 @@ _TICKETS: dict = {}
 
 
 def _tickets(n: int, device) -> torch.Tensor:
-    """Zeroed uint32 arrival counters for row-block tails (cmx_gemm_ln), one pool per (device,
-    stream): launches on one stream are ordered and each leaves its counters zero, so they share
-    the pool; a concurrent stream gets its own.  Sized once (B4 / B5 stage-1 row blocks fit)
-    so no allocation happens inside a HIP-graph capture."""
-    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
+    """Zeroed uint32 arrival counters for row-block tails (cmx_gemm_ln), one pool per device:
+    every tail launch leaves its counters zero and the tails are issued by the encoder's main
+    chain, in stream order (a HIP-graph capture of the step keeps that order), so they share the
+    pool.  Sized once (B4 / B5 stage-1 row blocks fit), before any capture."""
+    device = torch.device(device)
+    key = device.index if device.index is not None else torch.cuda.current_device()
     t = _TICKETS.get(key)
     if t is None or t.numel() < n:
         if torch.cuda.is_current_stream_capturing():

@@ -156,12 +156,18 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
         t2 = F.LNTail(blk.norm2)
         x = F.glinear(store, a.proj.weight, a.proj.bias, o, res=xr, rscale=s_attn, rps=N, tap=tap_a, ln_tail=t2)
         h, _, xr = F.layernorm_res(store, blk.norm2, x, G, scale=s_attn, rps=N, tap=tap_a, tail=t2)
-        f = F.glinear(store, blk.mlp.fc1.weight, blk.mlp.fc1.bias, h)
-        f = F.dwconv(store, blk.mlp.dwconv.dwconv, f, G * B, B, H, W, "gelu")
+        dtap = None
+        if F.mixffn_ok(h, blk.mlp.fc1.weight.shape[0], B, H, W):
+            # fc1 + DWConv + GELU in one launch; fc2's input gradient joins their backward launch
+            dtap = F.DgradTap()
+            f = F.mixffn(store, blk.mlp, h, B, H, W, dtap)
+        else:
+            f = F.glinear(store, blk.mlp.fc1.weight, blk.mlp.fc1.bias, h)
+            f = F.dwconv(store, blk.mlp.dwconv.dwconv, f, G * B, B, H, W, "gelu")
         tap_m = F.GradTap() if s_mlp is not None else None
         tn = F.LNTail(next_norm) if next_norm is not None else None
         x = F.glinear(store, blk.mlp.fc2.weight, blk.mlp.fc2.bias, f, res=xr, rscale=s_mlp, rps=N, tap=tap_m,
-                      ln_tail=tn)
+                      ln_tail=tn, dgrad_tap=dtap)
         return x, (s_mlp, tap_m), tn
 
     def run(self, store, images, B, H, W, training, dp_scales: Optional[torch.Tensor], bn_group=None):

@@ -53,6 +53,9 @@ class SegmentUpdate:
         self.done = []
         self.wgrad_blocks = int(os.environ.get("CMX_SIDE_WGRAD_BLOCKS", "0"))
         self.adamw_blocks = int(os.environ.get("CMX_SIDE_ADAMW_BLOCKS", "0"))
+        # CMX_SIDE_WGRAD=0: a segment's weight-gradient launches stay on the main stream (in
+        # backward order, at the segment boundary); only its AdamW update goes to the side stream
+        self.wgrad_side = os.environ.get("CMX_SIDE_WGRAD", "1") == "1"
 
     def arm(self):
         self.armed, self.done = True, []
@@ -75,6 +78,8 @@ class SegmentUpdate:
         main = torch.cuda.current_stream()
         if self.side is None:
             self.side = torch.cuda.Stream(device=main.device)
+        if not self.wgrad_side:
+            deferred.flush()
         self.side.wait_stream(main)
         with torch.cuda.stream(self.side):
             deferred.flush(max_blocks=0 if last else self.wgrad_blocks)

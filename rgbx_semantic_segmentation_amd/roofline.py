@@ -60,7 +60,8 @@ def _pmc_traffic(kernel: str, workload: str, blocks: int):
 
 # the C-ABI entry points whose launches make up the tile-GEMM family (the FFM per-head context
 # products, cmx_gemm_h2, are floor.py's "ffm" family and stay out of both the time and the work)
-GEMM_FAMILY = ("cmx_gemm", "cmx_gemm_multi", "cmx_conv_implicit_fwd", "cmx_decoder_fuse_fwd", "cmx_conv_patch_dgrad")
+GEMM_FAMILY = ("cmx_gemm", "cmx_gemm_ln", "cmx_gemm_multi", "cmx_conv_implicit_fwd", "cmx_decoder_fuse_fwd",
+               "cmx_conv_patch_dgrad")
 
 
 def _family_traffic(kernels, workload: str):

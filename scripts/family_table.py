@@ -51,6 +51,7 @@ def work():
 
 FAMILIES = [
     ("grouped wgrad GEMM + grouped reduce", r"gemm_grouped_kernel|reduce_grouped_kernel"),
+    ("Mix-FFN bands", r"mixffn_"),
     ("GEMM fwd+dgrad (tile / k-group / multi / split-K)", r"gemm_bf16_kernel|gemm_multi|gemm_generic|splitk_reduce"),
     ("SRA attention (fwd, dQ, dK/dV, reduce)", r"sra_"),
     ("DWConv 3x3 + GELU (fwd_save, bwd_saved)", r"dw2_|dw_"),

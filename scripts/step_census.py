@@ -53,6 +53,7 @@ FAMILIES = [
     ("GEMM (MFMA: linear / conv / decoder / attention projections)", r"^(gemmk::)?(gemm_|splitk_reduce)"),
     ("SRA attention (MFMA)", r"^sra_"),
     ("depthwise 3x3 conv + GELU (MixFFN)", r"^dw2_|^dw_"),
+    ("Mix-FFN bands (fc1+DW+GELU, fc2 dgrad+DW bwd)", r"^mixffn_"),
     ("LayerNorm", r"^ln_"),
     ("BatchNorm", r"^bn_"),
     ("FRM (CM-FRM)", r"^pool_|^linear_|^combine_|^ifrm"),
