@@ -548,10 +548,16 @@ int cmx_gemm_grouped_capped(const void* recs, int nrec, int total_blocks, int ma
   static int& chunk = cmx_knob("GROUPED_CHUNK", 64);
   const GroupRec* rr = (const GroupRec*)recs;
   const int grid = max_blocks > 0 && max_blocks < total_blocks ? max_blocks : total_blocks;
-  if (dtype == 2)
+  if (grid < total_blocks) {
+    if (dtype == 2)
+      hipLaunchKernelGGL((gemm_grouped_kernel<f16, 2, true>), dim3(grid), dim3(256), 0, s, rr, nrec, chunk, total_blocks);
+    else
+      hipLaunchKernelGGL((gemm_grouped_kernel<bf16, 2, true>), dim3(grid), dim3(256), 0, s, rr, nrec, chunk, total_blocks);
+  } else if (dtype == 2) {
     hipLaunchKernelGGL((gemm_grouped_kernel<f16>), dim3(grid), dim3(256), 0, s, rr, nrec, chunk, total_blocks);
-  else
+  } else {
     hipLaunchKernelGGL((gemm_grouped_kernel<bf16>), dim3(grid), dim3(256), 0, s, rr, nrec, chunk, total_blocks);
+  }
   return cmx_check_launch("gemm_grouped");
 }
 

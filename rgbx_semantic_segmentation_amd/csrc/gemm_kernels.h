@@ -716,27 +716,39 @@ __device__ __forceinline__ int xcd_chunk_tile(int b, int nt, int ch) {
 
 // (two-stage DMA ring, two blocks per CU: deeper rings at one block per CU measured 2-17 %
 // slower on the B2 step, round 3)
-// A grid smaller than `total` (a multiple of 8 workgroups: block b + k * gridDim.x stays on block
-// b's XCD) walks the blocks b, b + gridDim.x, ... in turn (cmx_gemm_grouped_capped).
-template <typename E, int NS = 2>
+// one block's tile of the grouped launch: the record whose block range holds `lin`
+template <typename E, int NS>
+__device__ __forceinline__ void grouped_tile(const GroupRec* __restrict__ recs, int nrec, int lin, char* smem) {
+  int lo = 0, hi = nrec - 1;                    // last record with blk0 <= lin
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (recs[mid].blk0 <= lin) lo = mid; else hi = mid - 1;
+  }
+  const GroupRec& r = recs[lo];
+  const GemmArgs p = r.a;
+  const int local = lin - r.blk0;
+  if (r.bm == 128 && r.bn == 128) gemm_bf16_body<128, 128, true, true, NS, 1, E>(p, local, smem);
+  else if (r.bm == 128) gemm_bf16_body<128, 64, true, true, NS, 1, E>(p, local, smem);
+  else if (r.bn == 128) gemm_bf16_body<64, 128, true, true, NS, 1, E>(p, local, smem);
+  else gemm_bf16_body<64, 64, true, true, NS, 1, E>(p, local, smem);
+}
+
+// LOOP: a grid smaller than `total` (a multiple of 8 workgroups: block b + k * gridDim.x stays on
+// block b's XCD) walks the blocks b, b + gridDim.x, ... in turn (cmx_gemm_grouped_capped).  The
+// one-tile-per-block instantiation stays separate: the loop around the k-loop body cost the
+// full-grid launch 40 % (round 5: 522-570 us -> 770-850 us on the B2 step)
+template <typename E, int NS = 2, bool LOOP = false>
 __global__ __launch_bounds__(256, 2) void gemm_grouped_kernel(const GroupRec* __restrict__ recs, int nrec,
                                                                              int chunk, int total) {
   __shared__ __attribute__((aligned(1024))) char smem[gemm_smem_bytes<128, 128, NS>()];
-  for (int b = blockIdx.x; b < total; b += gridDim.x) {
-    if (b != (int)blockIdx.x) __syncthreads();   // every wave is done with the previous tile's LDS
-    const int lin = chunk > 0 ? xcd_chunk_tile(b, total, chunk) : xcd_tile(b, total);
-    int lo = 0, hi = nrec - 1;                    // last record with blk0 <= lin
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (recs[mid].blk0 <= lin) lo = mid; else hi = mid - 1;
+  if constexpr (!LOOP) {
+    const int b = blockIdx.x;
+    grouped_tile<E, NS>(recs, nrec, chunk > 0 ? xcd_chunk_tile(b, total, chunk) : xcd_tile(b, total), smem);
+  } else {
+    for (int b = blockIdx.x; b < total; b += gridDim.x) {
+      if (b != (int)blockIdx.x) __syncthreads();   // every wave is done with the previous tile's LDS
+      grouped_tile<E, NS>(recs, nrec, chunk > 0 ? xcd_chunk_tile(b, total, chunk) : xcd_tile(b, total), smem);
     }
-    const GroupRec& r = recs[lo];
-    const GemmArgs p = r.a;
-    const int local = lin - r.blk0;
-    if (r.bm == 128 && r.bn == 128) gemm_bf16_body<128, 128, true, true, NS, 1, E>(p, local, smem);
-    else if (r.bm == 128) gemm_bf16_body<128, 64, true, true, NS, 1, E>(p, local, smem);
-    else if (r.bn == 128) gemm_bf16_body<64, 128, true, true, NS, 1, E>(p, local, smem);
-    else gemm_bf16_body<64, 64, true, true, NS, 1, E>(p, local, smem);
   }
 }
 

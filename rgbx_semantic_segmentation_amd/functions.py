@@ -136,10 +136,12 @@ def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1
     return GLinear.apply(W, Wg, b, bg, wp, act, res, rscale, rps, x1, x2, tap, ln, dgrad_tap)
 
 
-# CMX_LN_TAIL=0: every LayerNorm forward as its own launch (A/B switch); CMX_LN_TAIL_MAXM: only
-# GEMMs of at most that many rows per group take the tail (the stage-3/4 Linears: their tail
-# variants keep the occupancy of the k-group blocks they run as)
-LN_TAIL = os.environ.get("CMX_LN_TAIL", "1") != "0"
+# CMX_LN_TAIL=1: the LayerNorm after a residual Linear as the GEMM's row-block tail (cmx_gemm_ln)
+# instead of its own launch.  Off by default: measured slower on the B2 step (DESIGN.md round 5:
+# the tail GEMMs ran 25-30 us against 13 us + a 3-5 us LayerNorm launch -- the last arriver's
+# 64-row LayerNorm is 16 dependent passes of write-through loads on the critical path).
+# CMX_LN_TAIL_MAXM: only GEMMs of at most that many rows per group take the tail
+LN_TAIL = os.environ.get("CMX_LN_TAIL", "0") == "1"
 LN_TAIL_MAXM = int(os.environ.get("CMX_LN_TAIL_MAXM", "1000000000"))
 
 # CMX_MULTI_GEMM=0 launches the grouped Linears of GLinearMulti one by one (A/B switch)

@@ -135,10 +135,12 @@ class FusedAdamW:
                    amsgrad=False, maximize=False, foreach=None, capturable=False, differentiable=False, fused=None),
         ]
         self.defaults = dict(lr=float(lr), betas=self.betas, eps=self.eps, weight_decay=self.weight_decay)
-        # per-segment updates overlapped with the backward (SegmentUpdate; CMX_OPT_OVERLAP=0 or
-        # overlap=False: one update at step()).  Single-process path: with a gradient all-reduce
-        # (grad_sync) the update waits for the whole exchange, as DDP's optimizer step does.
-        ov = overlap if overlap is not None else os.environ.get("CMX_OPT_OVERLAP", "1") == "1"
+        # per-segment updates overlapped with the backward (SegmentUpdate; CMX_OPT_OVERLAP=1 or
+        # overlap=True).  Off by default: on the B2 step the side stream's grouped weight-gradient
+        # and AdamW launches slowed the latency-bound backward kernels they shared the CUs with by
+        # more than they hid (-9 %).  Single-process path: with a gradient
+        # all-reduce (grad_sync) the update waits for the whole exchange, as DDP's step does.
+        ov = overlap if overlap is not None else os.environ.get("CMX_OPT_OVERLAP", "0") == "1"
         self._seg = None
         backbone = getattr(model, "backbone", None)
         if ov and grad_sync is None and store.flat.is_cuda and len(store.segments) > 1 and backbone is not None:

@@ -1,6 +1,8 @@
 """Per-step kernel census from a rocprofv3 kernel trace of bench.py: the launches between two
-consecutive AdamW launches (one HIP-graph replay = one step; the steady-state step of median wall
-time), grouped by kernel family.
+consecutive step-start markers (one HIP-graph replay = one step; the steady-state step of median
+wall time), grouped by kernel family.  The marker is step_masks_kernel, the one launch every step
+opens with (drop-path masks); AdamW closes the step only without the per-segment overlap, which
+splits it into several launches on a side stream.
 Usage: python scripts/step_census.py <run_results.db> [top]"""
 import collections
 import re
@@ -19,18 +21,23 @@ def kname(n):
 c = sqlite3.connect(sys.argv[1])
 top = int(sys.argv[2]) if len(sys.argv) > 2 else 40
 rows = c.execute("select start, end, name from kernels order by start").fetchall()
-idx = [i for i, r in enumerate(rows) if r[2].replace("void ", "").startswith("adamw")]
+idx = [i for i, r in enumerate(rows) if kname(r[2]).startswith("step_masks")]
+if len(idx) < 3:   # older traces: AdamW (one launch per step) closes the step
+    idx = [i + 1 for i, r in enumerate(rows) if kname(r[2]).startswith("adamw")]
 # the step whose wall time is the median over the steady-state steps (the first three replays
 # and the bench's last, host-drained ones aside): one representative replay, not the tail
-walls = [(rows[idx[j + 1]][1] - rows[idx[j] + 1][0], j) for j in range(3, len(idx) - 1)] or [(0, len(idx) - 2)]
+def wall(j):
+    seg_ = rows[idx[j]:idx[j + 1]]
+    return max(r[1] for r in seg_) - seg_[0][0]
+walls = [(wall(j), j) for j in range(3, len(idx) - 2)] or [(0, len(idx) - 2)]
 pick = sorted(walls)[len(walls) // 2][1]
-seg = rows[idx[pick] + 1:idx[pick + 1] + 1]
-print(f"launches/step {len(seg)}  wall {(seg[-1][1] - seg[0][0]) / 1e3:.0f} us  busy {sum(r[1] - r[0] for r in seg) / 1e3:.0f} us"
+seg = rows[idx[pick]:idx[pick + 1]]
+print(f"launches/step {len(seg)}  wall {(max(r[1] for r in seg) - seg[0][0]) / 1e3:.0f} us  busy {sum(r[1] - r[0] for r in seg) / 1e3:.0f} us"
       f"  (step {pick + 1} of {len(idx) - 1}: median wall of the steady-state steps)")
 # idle time between one step's AdamW and the next step's first kernel (the replay boundary), and
 # the largest idle gaps inside the step
-prev = rows[idx[pick]]
-print(f"boundary gap {(seg[0][0] - prev[1]) / 1e3:.1f} us after {prev[2][:40]}; first kernels: "
+prev = max(rows[:idx[pick]], key=lambda r: r[1])
+print(f"boundary gap {(seg[0][0] - prev[1]) / 1e3:.1f} us after {kname(prev[2])[:40]}; first kernels: "
       + ", ".join(kname(r[2])[:30] for r in seg[:3]))
 gaps, end = [], seg[0][1]
 for s_, e_, n_ in seg[1:]:

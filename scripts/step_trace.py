@@ -24,10 +24,13 @@ flt = args[1] if len(args) > 1 else None
 cols = [r[1] for r in c.execute("pragma table_info(kernels)").fetchall()]
 qcol = "queue_id" if "queue_id" in cols else ("stream_id" if "stream_id" in cols else None)
 rows = c.execute(f"select start, end, name{', ' + qcol if qcol else ''} from kernels order by start").fetchall()
-idx = [i for i, r in enumerate(rows) if r[2].replace("void ", "").startswith("adamw")]
-walls = [(rows[idx[j + 1]][1] - rows[idx[j] + 1][0], j) for j in range(3, len(idx) - 1)] or [(0, len(idx) - 2)]
+idx = [i for i, r in enumerate(rows) if kname(r[2]).startswith("step_masks")]
+if len(idx) < 3:
+    idx = [i + 1 for i, r in enumerate(rows) if kname(r[2]).startswith("adamw")]
+walls = [(max(r[1] for r in rows[idx[j]:idx[j + 1]]) - rows[idx[j]][0], j) for j in range(3, len(idx) - 2)] \
+    or [(0, len(idx) - 2)]
 pick = sorted(walls)[len(walls) // 2][1]
-seg = rows[idx[pick] + 1:idx[pick + 1] + 1]
+seg = rows[idx[pick]:idx[pick + 1]]
 t0 = seg[0][0]
 prev_end = t0
 for r in seg:

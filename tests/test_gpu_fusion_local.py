@@ -7,8 +7,9 @@ cancellation) bf16 storage upstream of the block already moves the gradient by 2
 emulation itself, so that yardstick says little about the kernels.  Here the block is checked
 in isolation: the kernels (bf16) and the fp64 oracle module see the SAME bf16-rounded inputs
 and upstream gradient, the emulated oracle (oracle/bf16_emul.py: bf16 storage at the kernels'
-rounding points) gives the yardstick, and every tensor's yardstick must stay below YARD_MAX --
-the check bites on every tensor.  Records: $CMX_PARITY_OUT/local_<module>_<case>.json.
+rounding points) gives the yardstick, and every tensor's error must stay below both RATIO x its
+yardstick and YARD_MAX -- the check bites on every tensor, also where the emulation itself is
+loose (the SpatialWeights output bias: emulated 0.36 at B0 stage 3, the kernels 0.056).  Records: $CMX_PARITY_OUT/local_<module>_<case>.json.
 
 Reference: models/net_utils.py:124-152 (FeatureRectifyModule), :354-384 (FeatureFusionModule)."""
 import copy
@@ -66,8 +67,11 @@ def _judge(module, case, got, gmax):
     _record(module, case, rows)
     over = [(round(eg / y, 2), n) for n, eg, ee, y in rows if eg > RATIO * y]
     assert len(over) <= max(1, int(OUTLIER_SHARE * len(rows))) and all(r <= OUTLIER for r, _ in over), over
-    yard = [(round(y, 3), n) for n, eg, ee, y in rows if y > YARD_MAX]
-    assert not yard, f"{module} {case}: yardsticks above {YARD_MAX}: {yard}"
+    # the absolute cap bites where the emulation itself is loose (a yardstick above YARD_MAX: the
+    # SpatialWeights output bias, a sum over every pixel with heavy cancellation): the kernels'
+    # own error must still stay below YARD_MAX there
+    loose = [(round(eg, 3), round(y, 3), n) for n, eg, ee, y in rows if eg > YARD_MAX]
+    assert not loose, f"{module} {case}: errors above {YARD_MAX}: {loose}"
 
 
 def _inputs(B, C, H, W, cdt, n=3):

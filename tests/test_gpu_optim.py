@@ -319,3 +319,32 @@ def test_segment_update_waits_for_step(dev):
     sc.update()
     torch.cuda.synchronize()
     assert not torch.equal(model.store.flat, p0) and opt.step_t.item() == 1.0
+
+
+def test_fusion_switches_match(dev, monkeypatch):
+    """The A/B fusion switches of functions.py (CMX_LN_TAIL: LayerNorm as the residual GEMM's
+    row-block tail; CMX_MIXFFN: the Mix-FFN band kernels) against the separate launches on one
+    bf16 training step: the Mix-FFN bands round at the same points (bit-identical where the
+    separate fc1 GEMM is one k-group) and the tail's LayerNorm sums in another order, so the loss
+    agrees to rel 2e-2 and the flat gradient to cosine 0.999 / norm rel 2e-2 (bf16 activations)."""
+    from rgbx_semantic_segmentation_amd import functions as F
+    from rgbx_semantic_segmentation_amd.optim import FusedAdamW
+    runs = []
+    for on in (False, True):
+        monkeypatch.setattr(F, "LN_TAIL", on)
+        monkeypatch.setattr(F, "MIXFFN_BAND", on)
+        _, model = _pair(dev, dtype="bfloat16", seed=6)
+        model.train()
+        opt = FusedAdamW(model, lr=6e-5, betas=(0.9, 0.999), weight_decay=0.01)
+        rgb, x, lab = _batch(seed=40)
+        loss = model(rgb.to(dev), x.to(dev), lab.to(dev))
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        torch.cuda.synchronize()
+        runs.append((loss.item(), model.store.grad.clone().double()))
+    (l0, g0), (l1, g1) = runs
+    assert abs(l0 - l1) <= 2e-2 * abs(l0), (l0, l1)
+    cos = (g0 @ g1 / (g0.norm() * g1.norm())).item()
+    assert cos > 0.999, cos
+    assert abs(g0.norm().item() - g1.norm().item()) <= 2e-2 * g0.norm().item()
