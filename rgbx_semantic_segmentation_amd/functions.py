@@ -644,8 +644,11 @@ def dwconv(store, conv, h, NI, ipg, H, W, act):
 
 
 # ---------------------------------------------------------------------------- Mix-FFN bands
-# CMX_MIXFFN=0: fc1, DWConv+GELU and fc2's input gradient as separate launches (A/B switch)
-MIXFFN_BAND = os.environ.get("CMX_MIXFFN", "1") != "0"
+# CMX_MIXFFN=1: the band kernels below instead of fc1, DWConv+GELU and fc2's input gradient as
+# separate launches.  Off by default: measured slower on the B2 step (41 / 27 us
+# per stage-3 / stage-4 band launch against ~22 / ~15 us for the GEMM + DWConv pair it replaces;
+# 3 interleaved A/B pairs 264.8 vs 268.9 img/s, profiles/r05_b_ab_mixffn.txt)
+MIXFFN_BAND = os.environ.get("CMX_MIXFFN", "0") == "1"
 # bands of fewer rows recompute too much of fc1 on their halo rows ((R + 2) / R): stage 3 / 4 of
 # B2 / B4 at 480 x 640 get R = 4 / 10, stage 2 (W = 80) would get R = 1
 MIXFFN_MIN_ROWS = int(os.environ.get("CMX_MIXFFN_MIN_ROWS", "4"))
