@@ -213,16 +213,22 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
   a.kt_per_split = (nk + splitk - 1) / splitk;
   splitk = (nk + a.kt_per_split - 1) / a.kt_per_split;      // no empty splits
   a.nsplit = splitk;
+  // LayerNorm of C's rows in the same launch: N <= 128 -> in the epilogue (tail = 2: one 64 x 64 /
+  // 64 x 128 tile spans the row), else the row-block tail with arrival tickets (tail = 1)
+  const bool row_ln = tail && N <= 128 && N % 8 == 0;
   if (tail) {
     int bm = 0, bn = 0;
     if (fast) plan_tiles(G, M, nb, K, &bm, &bn);
-    CMX_REQUIRE(fast && bm == 64 && bn == 64 && splitk == 1 && !transA && !transB && out_mode == 0 && !ones_col &&
-                    !a.nup && !a.scatter && gh == 1 && !mask && a.cvec && N % 64 == 0 && N <= 512 && dtype != 0,
-                CMX_ERR_ARG, "gemm_ln: the LayerNorm tail needs the 16-bit 64 x 64 path without split-K, forward "
-                "layouts, a plain aligned store and N a multiple of 64 <= 512 (G=%d M=%d N=%d K=%d)", G, M, N, K);
-    CMX_REQUIRE(tail->gamma && tail->beta && tail->y && tail->mean && tail->rstd && tail->tickets &&
+    if (row_ln) bm = 64, bn = N <= 64 ? 64 : 128;
+    CMX_REQUIRE(fast && bm == 64 && (bn == 64 || row_ln) && splitk == 1 && !transA && !transB && out_mode == 0 &&
+                    !ones_col && !a.nup && !a.scatter && gh == 1 && !mask && a.cvec &&
+                    (row_ln || (N % 64 == 0 && N <= 512)) && dtype != 0,
+                CMX_ERR_ARG, "gemm_ln: the LayerNorm tail needs the 16-bit path without split-K, forward layouts, a "
+                "plain aligned store and N <= 128 (N %% 8 == 0) or N a multiple of 64 <= 512 (G=%d M=%d N=%d K=%d)",
+                G, M, N, K);
+    CMX_REQUIRE(tail->gamma && tail->beta && tail->y && tail->mean && tail->rstd && (row_ln || tail->tickets) &&
                     ((uintptr_t)tail->y & 15) == 0 && tail->y != C, CMX_ERR_ARG, "gemm_ln: tail buffers");
-    a.tail = 1; a.ln_gamma = tail->gamma; a.ln_beta = tail->beta; a.ln_sg = tail->sg; a.ln_y = tail->y;
+    a.tail = row_ln ? 2 : 1; a.ln_gamma = tail->gamma; a.ln_beta = tail->beta; a.ln_sg = tail->sg; a.ln_y = tail->y;
     a.ln_mean = tail->mean; a.ln_rstd = tail->rstd; a.tickets = tail->tickets; a.ln_eps = tail->eps;
   }
   if (plan) {
@@ -242,6 +248,7 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
   if (fast) {
     int bm, bn;
     plan_tiles(G, M, nb, K, &bm, &bn);
+    if (row_ln) bm = 64, bn = N <= 64 ? 64 : 128;
     a.tiles_m = cdiv(M, bm); a.tiles_n = cdiv(nb, bn);
     launch_fast(a, bm, bn, G, splitk, transA, transB, dtype, s);
   } else {

@@ -44,6 +44,8 @@ struct GemmArgs {
   // block (tickets[g * tiles_m + tm], caller-owned, zero at first use, reset by the last
   // arriver); the last of the row block's tiles_n workgroups to arrive normalises those rows:
   // ln_y = LN(C rows) * gamma + beta (C's dtype and layout), ln_mean / ln_rstd (fp32, g * M + i)
+  // tail = 2 (N <= 128, N % 8 == 0: 64 x 64 / 64 x 128 tiles span the row): the same LayerNorm
+  // in the epilogue by the lanes that store the row (row_layernorm), no tickets, no re-read
   int tail;
   float ln_eps;
   const float* ln_gamma;
@@ -338,10 +340,55 @@ constexpr int gemm_smem_bytes() {
                                                                  : KW * BM * (BN + 4) * 4;
 }
 
+// Row LayerNorm in the epilogue (GemmArgs::tail = 2): the tile spans the whole output row
+// (tiles_n = 1, N <= BN), so the TPR lanes that store a row's 8-column chunks also normalise it:
+// ln_y = LN(C row) * gamma + beta in C's dtype and layout, ln_mean / ln_rstd (fp32, g * M + i).
+// The statistics are those of the stored (rounded) values, summed exactly as ln_fwd_kernel
+// (layernorm.hip) sums a row of TPR 16-B chunks: 8 values per lane, then the xor tree over the
+// TPR lanes -- so mean, rstd and the normalised row are bit-identical to the separate launch.
+// Consumer norms of the residual Linears (Block.norm2 after proj, the next norm1 / stage norm
+// after fc2, dual_segformer.py:168-169,382) at C <= 128 (stages 1-2) run here.
+template <typename E, int TPR>
+__device__ __forceinline__ void row_layernorm(const GemmArgs& p, int g, int i, int j, int jl, bool live,
+                                              const float* v) {
+  float x[8];
+#pragma unroll
+  for (int e = 0; e < 8; e += 2) {
+    const cmx_f2 r = unpack2<E>(pack2<E>(v[e], v[e + 1]));
+    x[e] = live ? r.x : 0.f;
+    x[e + 1] = live ? r.y : 0.f;
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s += x[e];
+  s = group_sum(s, TPR);
+  const int C = p.N;
+  const float mu = s / C;
+  float q = 0.f;
+  if (live) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { const float d = x[e] - mu; q += d * d; }
+  }
+  q = group_sum(q, TPR);
+  const float rs = rsqrtf(q / C + p.ln_eps);
+  if (live) {
+    const float* ga = p.ln_gamma + (long)g * p.ln_sg + j;
+    const float* be = p.ln_beta + (long)g * p.ln_sg + j;
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (x[e] - mu) * rs * ga[e] + be[e];
+    store_vec<E>(reinterpret_cast<E*>(p.ln_y) + (long)g * p.sC + (long)i * p.ldc + j, o);
+  }
+  if (jl == 0) {
+    p.ln_mean[(long)g * p.M + i] = mu;
+    p.ln_rstd[(long)g * p.M + i] = rs;
+  }
+}
+
 // One output tile (of one split / group) of problem p.  `lin` = the block's linear index
 // within the problem, in (split, group, tile) order; smem = gemm_smem_bytes<BM, BN, NS>().
 // E = the 16-bit storage type (bf16 or f16: v_mfma_f32_32x32x16_bf16 / _f16, same tiles and rate)
-template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1, typename E = bf16, bool SC1 = false>
+template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1, typename E = bf16, int EPI = 0>
 __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin, char* smem) {
   constexpr int A_BYTES = BM * FBK * 2, STAGE = (BM + BN) * FBK * 2, SLOT = KW * STAGE;
   constexpr int TM = BM / 64, TN = BN / 64;
@@ -540,7 +587,8 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
   constexpr int TPR = BN / 8, RPP = 256 * KW / TPR, NPASS = (BM + RPP - 1) / RPP;
   const int jl = (threadIdx.x % TPR) * 8;
   const int j = j0 + jl;
-  if (j >= nreal) return;
+  const bool live = j < nreal;
+  if (EPI != 2 && !live) return;            // (row LayerNorm: every lane of a row takes part)
   const int nv = min(8, nreal - j);
   float* wsz = p.nsplit > 1 ? slab(p, g, z) : nullptr;
 #pragma unroll 2
@@ -558,7 +606,10 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
       const float4 w1 = *reinterpret_cast<const float4*>(cs + q * BM * CP + il * CP + jl + 4);
       v[0] += w0.x; v[1] += w0.y; v[2] += w0.z; v[3] += w0.w; v[4] += w1.x; v[5] += w1.y; v[6] += w1.z; v[7] += w1.w;
     }
-    if (wsz) {
+    if constexpr (EPI == 2) {
+      if (live) epi_store8<E>(p, g, i, j, 8, v);   // v: the stored row values before rounding
+      row_layernorm<E, TPR>(p, g, i, j, jl, live, v);
+    } else if (wsz) {
       float* d = wsz + (long)i * nreal + j;
       if (nv == 8 && (nreal & 3) == 0) {
         reinterpret_cast<float4*>(d)[0] = make_float4(v[0], v[1], v[2], v[3]);
@@ -567,7 +618,7 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
         for (int e = 0; e < nv; ++e) d[e] = v[e];
       }
     } else {
-      epi_store8<E, SC1>(p, g, i, j, nv, v);
+      epi_store8<E, EPI == 1>(p, g, i, j, nv, v);
     }
   }
 }
@@ -658,13 +709,13 @@ __device__ __forceinline__ void gemm_ln_tail(const GemmArgs& p, const int lin) {
 // neighbouring tiles of one (split, group): they share A row panels and the B k-slice in L2
 // (64 x 64 two-stage blocks take 32 KB of LDS: five fit a CU when the kernel stays within 96
 // VGPRs, which the launch bound asks of the register allocator -- at 97 only four are resident)
-template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1, typename E = bf16, bool TAIL = false>
+template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1, typename E = bf16, int TAIL = 0>
 __global__ __launch_bounds__(256 * KW, (BM == 64 && BN == 64 && NS == 2 && KW == 1) ? 5 : (KW == 4 ? 1 : 2))
 void gemm_bf16_kernel(const GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[gemm_smem_bytes<BM, BN, NS, KW>()];
   const int lin = xcd_tile(blockIdx.x, p.tiles_m * p.tiles_n * p.G * p.nsplit);
   gemm_bf16_body<BM, BN, TA, TB, NS, KW, E, TAIL>(p, lin, smem);
-  if constexpr (TAIL) gemm_ln_tail<E>(p, lin);
+  if constexpr (TAIL == 1) gemm_ln_tail<E>(p, lin);
 }
 
 // ============================================================================ multi launch
@@ -1004,8 +1055,14 @@ template <int BM, int BN, int NS, int KW = 1, typename E = bf16>
 void launch_bf16(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream_t s) {
   dim3 grid(a.tiles_m * a.tiles_n * G * nsplit);
   if constexpr (BM == 64 && BN == 64) {
-    if (a.tail) {                     // row-block LayerNorm tail: forward layouts only (checked at launch)
-      hipLaunchKernelGGL((gemm_bf16_kernel<64, 64, false, false, NS, KW, E, true>), grid, dim3(256 * KW), 0, s, a);
+    if (a.tail == 1) {                // row-block LayerNorm tail: forward layouts only (checked at launch)
+      hipLaunchKernelGGL((gemm_bf16_kernel<64, 64, false, false, NS, KW, E, 1>), grid, dim3(256 * KW), 0, s, a);
+      return;
+    }
+  }
+  if constexpr (BM == 64 && (BN == 64 || (BN == 128 && KW == 1))) {
+    if (a.tail == 2) {                // whole-row LayerNorm in the epilogue (forward layouts, tiles_n = 1)
+      hipLaunchKernelGGL((gemm_bf16_kernel<64, BN, false, false, NS, KW, E, 2>), grid, dim3(256 * KW), 0, s, a);
       return;
     }
   }

@@ -130,7 +130,8 @@ def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1
         b = store.w(bp, compute=False).view(G, -1)
         bg = store.g(bp).view(G, -1)
     ln = None
-    if ln_tail is not None and LN_TAIL and x1.shape[1] <= LN_TAIL_MAXM:
+    N = W.shape[1]
+    if ln_tail is not None and ((LN_ROW and N <= 128 and N % 8 == 0) or (LN_TAIL and x1.shape[1] <= LN_TAIL_MAXM)):
         m = ln_tail.mod
         ln = (store.w(m.weight, compute=False).view(G, -1), store.w(m.bias, compute=False).view(G, -1), m.eps, ln_tail)
     return GLinear.apply(W, Wg, b, bg, wp, act, res, rscale, rps, x1, x2, tap, ln, dgrad_tap)
@@ -143,6 +144,10 @@ def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1
 # CMX_LN_TAIL_MAXM: only GEMMs of at most that many rows per group take the tail
 LN_TAIL = os.environ.get("CMX_LN_TAIL", "0") == "1"
 LN_TAIL_MAXM = int(os.environ.get("CMX_LN_TAIL_MAXM", "1000000000"))
+# CMX_LN_ROW=0: every LayerNorm forward as its own launch (A/B switch).  Default: a residual
+# Linear whose output row fits one GEMM tile (C <= 128: stages 1-2) normalises it in its epilogue
+# (cmx_gemm_ln, tail = 2): bit-identical statistics, no tickets, no second pass over the rows
+LN_ROW = os.environ.get("CMX_LN_ROW", "1") != "0"
 
 # CMX_MULTI_GEMM=0 launches the grouped Linears of GLinearMulti one by one (A/B switch)
 MULTI_GEMM = os.environ.get("CMX_MULTI_GEMM", "1") != "0"

@@ -199,11 +199,15 @@ def gemm_ln(A, B, C, ln_gamma, ln_beta, ln_eps, bias=None, residual=None, rscale
             act="none", A2=None):
     """K.gemm's forward form (C = epi(A @ B^T)) plus the LayerNorm of C's rows in the same
     launch (cmx_gemm_ln): returns (y, mean, rstd), y = LN(C) in C's layout, mean / rstd (G, M)
-    fp32; None when the problem is not eligible (the caller runs gemm + the LN kernel)."""
+    fp32; None when the problem is not eligible (the caller runs gemm + the LN kernel).
+    N <= 128 (N % 8 == 0): the LayerNorm runs in the GEMM's epilogue (one tile spans a row);
+    N % 64 == 0 up to 512: the row-block tail with arrival tickets."""
     G, M, K1 = A.shape
     Kd = K1 + (A2.shape[2] if A2 is not None else 0)
     N = B.shape[1]
-    if A.dtype not in (torch.bfloat16, torch.float16) or N % 64 or N > 512 or not C.is_contiguous():
+    row = N <= 128 and N % 8 == 0
+    if A.dtype not in (torch.bfloat16, torch.float16) or not (row or (N % 64 == 0 and N <= 512)) \
+            or not C.is_contiguous():
         return None
     tA, lda, sA = _operand(A, "A")
     tB, ldb, sB = _operand(B, "B")
@@ -214,7 +218,7 @@ def gemm_ln(A, B, C, ln_gamma, ln_beta, ln_eps, bias=None, residual=None, rscale
     y = torch.empty_like(C)
     mean = torch.empty(G, M, dtype=torch.float32, device=C.device)
     rstd = torch.empty_like(mean)
-    tk = _tickets(query("cmx_gemm_ln_tickets", G, M), C.device)
+    tk = None if row else _tickets(query("cmx_gemm_ln_tickets", G, M), C.device)
     st = _lib.LIB.cmx_gemm_ln(ptr(A), ptr(A2), ptr(B), ptr(C), ptr(bias), ptr(residual), ptr(rscale), G, M, N, Kd, K1,
                          lda, lda2, ldb, C.stride(1), sA, sA2, sB, C.stride(0), sbias, int(rows_per_sample), ACT[act],
                          ptr(ln_gamma), ptr(ln_beta), ln_gamma.stride(0) if ln_gamma.dim() == 2 else 0,
