@@ -34,7 +34,7 @@ typedef struct ihipStream_t* hipStream_t;
  * from, and the Python binding refuses a library whose revision differs (an older .so with the
  * same symbol names but shifted arguments would otherwise corrupt memory silently).  Bump it
  * on every change of an entry point's argument list. */
-#define CMX_ABI_VERSION 2
+#define CMX_ABI_VERSION 3
 int cmx_abi_version(void);
 const char* cmx_last_error(void);
 /* pinned host -> device copy of a packed record table on `stream` (see grouped launches) */
@@ -232,6 +232,16 @@ int cmx_gemm_group_pack(void* rec, const void* A, const void* B, void* C, float*
  *      before the first launch; each launch leaves them zero (stream-ordered launches may share them). */
 int cmx_gemm_ln(const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R, const float* rscale, int G, int M, int N, int K, int K1, int64_t lda, int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias, int rows_per_sample, int act, const float* ln_gamma, const float* ln_beta, int64_t ln_sg, float ln_eps, void* ln_y, float* ln_mean, float* ln_rstd, unsigned* tickets, int dtype, hipStream_t stream);
 size_t cmx_gemm_ln_tickets(int G, int M);
+/* cmx_gemm_ln_bwd: a Linear's input gradient dy = A (G,M,K) B^T (B (G,N,K) logical, row-contiguous: the
+ *      weight W (G,K,N) read transposed, as cmx_gemm's transB = 1 dgrad) fed straight into the backward
+ *      of the LayerNorm that produced that Linear's input (Block.norm2 -> fc1, dual_segformer.py:169;
+ *      nn.LayerNorm backward): dx = rstd (g - mean(g) - xhat mean(g xhat)) + dres, g = (dy [+ dy2]) * gamma,
+ *      xhat = (x - mean) rstd; dxs = sscale[(g*M + i) / rows_per_sample] * dx (may be NULL); partials =
+ *      (G, ceil(M/64), 2N) fp32 dgamma | dbeta column sums per 64-row tile (cmx_gemm_ln_bwd_partials
+ *      bytes) for cmx_reduce_grouped.  dx, x, dres, dy2, dxs share C's layout (ldc, sC); mean / rstd
+ *      (G*M) fp32 as cmx_layernorm_fwd saves them; N <= 128, N % 8 == 0, 16-bit.  dy never reaches HBM. */
+int cmx_gemm_ln_bwd(const void* A, const void* B, void* dx, int G, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t sA, int64_t sB, int64_t sC, const void* x, const float* gamma, int64_t sg, const float* mean, const float* rstd, const void* dres, const void* dy2, const float* sscale, int rows_per_sample, void* dxs, float* partials, int dtype, hipStream_t stream);
+size_t cmx_gemm_ln_bwd_partials(int G, int M, int N);
 int cmx_gemm_grouped(const void* recs, int nrec, int total_blocks, int dtype, hipStream_t stream);
 /* ---- Mix-FFN bands (Mlp.forward fc1 -> DWConv 3x3 -> GELU, dual_segformer.py:67-71) --------------
  * x (G, ipg*H*W, C) contiguous 16-bit; W1 (G, Ch, C) (group stride sW), b1 (G, Ch) (stride sb = Ch),

@@ -140,6 +140,12 @@ struct LnTail {
   const float* gamma; const float* beta; long sg; void* y; float* mean; float* rstd; unsigned* tickets; float eps;
 };
 
+// LayerNorm backward of the epilogue (cmx_gemm_ln_bwd)
+struct LnBwd {
+  const void* x; const float* gamma; long sg; const float* mean; const float* rstd; const void* dy2; void* dxs;
+  float* part;
+};
+
 // upsample-add sources of the epilogue (nup = 0: none)
 struct UpSpec {
   const void* src[3];
@@ -152,7 +158,8 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
               int64_t sdb, int rows_per_sample, int transA, int transB, int act, int out_mode, int ones_col, int splitk,
               int dtype, hipStream_t s, const UpSpec* up, int scR = 0, int scH = 0, int scW = 0, int scC = 0,
               int scHo = 0, int scWo = 0, int gh = 1, int64_t sAh = 0, int64_t sBh = 0, int64_t sCh = 0,
-              GemmPlan* plan = nullptr, const void* mask = nullptr, const LnTail* tail = nullptr) {
+              GemmPlan* plan = nullptr, const void* mask = nullptr, const LnTail* tail = nullptr,
+              const LnBwd* lnb = nullptr) {
   CMX_REQUIRE(G > 0 && M > 0 && N > 0 && K > 0, CMX_ERR_SHAPE, "gemm: empty problem G=%d M=%d N=%d K=%d", G, M, N, K);
   CMX_REQUIRE(dtype >= 0 && dtype <= 2, CMX_ERR_DTYPE, "gemm: unsupported dtype %d", dtype);
   CMX_REQUIRE(out_mode >= 0 && out_mode <= 2 && act >= 0 && act <= 3, CMX_ERR_ARG, "gemm: out_mode/act");
@@ -231,6 +238,17 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
     a.tail = row_ln ? 2 : 1; a.ln_gamma = tail->gamma; a.ln_beta = tail->beta; a.ln_sg = tail->sg; a.ln_y = tail->y;
     a.ln_mean = tail->mean; a.ln_rstd = tail->rstd; a.tickets = tail->tickets; a.ln_eps = tail->eps;
   }
+  if (lnb) {
+    const bool al = ((uintptr_t)C & 15) == 0 && ((uintptr_t)lnb->x & 15) == 0 && ((uintptr_t)R & 15) == 0 &&
+                    ((uintptr_t)lnb->dy2 & 15) == 0 && ((uintptr_t)lnb->dxs & 15) == 0;
+    CMX_REQUIRE(fast && splitk == 1 && !transA && transB && out_mode == 0 && !ones_col && !bias && act == 0 && !mask &&
+                    !a.nup && !a.scatter && gh == 1 && !A2 && a.cvec && al && N <= 128 && N % 8 == 0 && dtype != 0 &&
+                    !tail && lnb->x && lnb->gamma && lnb->mean && lnb->rstd && lnb->part && (!lnb->dxs || rscale),
+                CMX_ERR_ARG, "gemm_ln_bwd: needs the 16-bit dgrad path (transB) without split-K, 16-B aligned rows, "
+                "N <= 128 (N %% 8 == 0), no bias / activation (G=%d M=%d N=%d K=%d)", G, M, N, K);
+    a.tail = 3; a.ln_gamma = lnb->gamma; a.ln_sg = lnb->sg; a.ln_mean = const_cast<float*>(lnb->mean); a.ln_rstd = const_cast<float*>(lnb->rstd);
+    a.lnb_x = lnb->x; a.lnb_dy2 = lnb->dy2; a.lnb_dxs = lnb->dxs; a.lnb_part = lnb->part;
+  }
   if (plan) {
     // planning only (cmx_gemm_plan): eligible for a multi launch = the 16-bit path on 64 x 64
     // tiles, no split-K, no bias-gradient column / upsample / scatter / two-level batch
@@ -248,7 +266,7 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
   if (fast) {
     int bm, bn;
     plan_tiles(G, M, nb, K, &bm, &bn);
-    if (row_ln) bm = 64, bn = N <= 64 ? 64 : 128;
+    if (row_ln || lnb) bm = 64, bn = N <= 64 ? 64 : 128;   // one tile spans the row
     a.tiles_m = cdiv(M, bm); a.tiles_n = cdiv(nb, bn);
     launch_fast(a, bm, bn, G, splitk, transA, transB, dtype, s);
   } else {
@@ -306,6 +324,18 @@ int cmx_gemm_ln(const void* A, const void* A2, const void* B, void* C, const flo
 }
 
 size_t cmx_gemm_ln_tickets(int G, int M) { return (size_t)G * ((M + 63) / 64); }
+
+int cmx_gemm_ln_bwd(const void* A, const void* B, void* dx, int G, int M, int N, int K, int64_t lda, int64_t ldb,
+                    int64_t ldc, int64_t sA, int64_t sB, int64_t sC, const void* x, const float* gamma, int64_t sg,
+                    const float* mean, const float* rstd, const void* dres, const void* dy2, const float* sscale,
+                    int rows_per_sample, void* dxs, float* partials, int dtype, hipStream_t s) {
+  const LnBwd l{x, gamma, (long)sg, mean, rstd, dy2, dxs, partials};
+  return gemm_impl(A, nullptr, B, dx, nullptr, dres, sscale, nullptr, nullptr, G, M, N, K, K, lda, 0, ldb, ldc, sA, 0,
+                   sB, sC, 0, 0, rows_per_sample, 0, 1, 0, 0, 0, 1, dtype, s, nullptr, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0,
+                   nullptr, nullptr, nullptr, &l);
+}
+
+size_t cmx_gemm_ln_bwd_partials(int G, int M, int N) { return (size_t)G * ((M + 63) / 64) * 2 * N * sizeof(float); }
 
 size_t cmx_gemm_plan_size(void) { return sizeof(GemmPlan); }
 

@@ -46,6 +46,11 @@ struct GemmArgs {
   // ln_y = LN(C rows) * gamma + beta (C's dtype and layout), ln_mean / ln_rstd (fp32, g * M + i)
   // tail = 2 (N <= 128, N % 8 == 0: 64 x 64 / 64 x 128 tiles span the row): the same LayerNorm
   // in the epilogue by the lanes that store the row (row_layernorm), no tickets, no re-read
+  // tail = 3: the LayerNorm BACKWARD in a dgrad's epilogue (row_layernorm_bwd): the GEMM result is
+  // dy of a norm (rounded as it would be stored), C receives that norm's dx = LN'(dy [+ lnb_dy2])
+  // + R (the residual branch's gradient), lnb_dxs = rscale[row / rows_per_sample] * dx, and
+  // lnb_part[(g * tiles_m + tm) * 2N + (0 | N) + j] the tile's dgamma | dbeta column partials;
+  // lnb_x = the norm's input, ln_gamma / ln_mean / ln_rstd its weight and saved statistics
   int tail;
   float ln_eps;
   const float* ln_gamma;
@@ -55,6 +60,10 @@ struct GemmArgs {
   float* ln_mean;
   float* ln_rstd;
   unsigned* tickets;
+  const void* lnb_x;
+  const void* lnb_dy2;
+  void* lnb_dxs;
+  float* lnb_part;
 };
 
 // block id -> tile id, giving each of the 8 XCDs (hardware deals block b to XCD b % 8) a
@@ -385,6 +394,76 @@ __device__ __forceinline__ void row_layernorm(const GemmArgs& p, int g, int i, i
   }
 }
 
+// LayerNorm backward in the epilogue (GemmArgs::tail = 3) of the dgrad that produces the norm's
+// output gradient dy (Block.norm2's consumer fc1, dual_segformer.py:169): the TPR lanes of a row
+// hold dy's 8-column chunks and finish the norm's backward without dy ever reaching HBM:
+//   dx = rstd * (g - mean(g) - xhat * mean(g * xhat)) + dres,  g = dy * gamma,  xhat = (x - mu) rstd
+// exactly as ln_bwd_kernel (layernorm.hip) computes a row of TPR 16-B chunks (dy rounded to the
+// storage type first, as that kernel reads it), so dx and dxs are bit-identical to the separate
+// launches; the lane's dgamma / dbeta terms accumulate in dga / dba for the tile's partials.
+template <typename E, int TPR>
+__device__ __forceinline__ void row_layernorm_bwd(const GemmArgs& p, int g, int i, int j, bool live, const float* v,
+                                                  float* dga, float* dba) {
+  const long off = (long)g * p.sC + (long)i * p.ldc + j;
+  const long grow = (long)g * p.M + i;
+  const float mu = p.ln_mean[grow], rs = p.ln_rstd[grow];
+  float dv[8], xh[8], gv[8];
+  if (live) {
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      const cmx_f2 r = unpack2<E>(pack2<E>(v[e], v[e + 1]));
+      dv[e] = r.x;
+      dv[e + 1] = r.y;
+    }
+    if (p.lnb_dy2) {
+      float d2[8];
+      load_vec<E>(reinterpret_cast<const E*>(p.lnb_dy2) + off, d2);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dv[e] += d2[e];
+    }
+    float xv[8];
+    load_vec<E>(reinterpret_cast<const E*>(p.lnb_x) + off, xv);
+    const float* ga = p.ln_gamma + (long)g * p.ln_sg + j;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      xh[e] = (xv[e] - mu) * rs;
+      gv[e] = dv[e] * ga[e];
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dv[e] = xh[e] = gv[e] = 0.f;
+  }
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    s1 += gv[e];
+    s2 += gv[e] * xh[e];
+  }
+  s1 = group_sum(s1, TPR) / p.N;
+  s2 = group_sum(s2, TPR) / p.N;
+  if (!live) return;
+  float o[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    dga[e] += dv[e] * xh[e];
+    dba[e] += dv[e];
+    o[e] = rs * (gv[e] - s1 - xh[e] * s2);
+  }
+  if (p.R) {
+    float rv[8];
+    load_vec<E>(reinterpret_cast<const E*>(p.R) + off, rv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] += rv[e];
+  }
+  store_vec<E>(reinterpret_cast<E*>(p.C) + off, o);
+  if (p.lnb_dxs) {
+    const float sc = p.rscale[grow / p.rows_per_sample];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] *= sc;
+    store_vec<E>(reinterpret_cast<E*>(p.lnb_dxs) + off, o);
+  }
+}
+
 // One output tile (of one split / group) of problem p.  `lin` = the block's linear index
 // within the problem, in (split, group, tile) order; smem = gemm_smem_bytes<BM, BN, NS>().
 // E = the 16-bit storage type (bf16 or f16: v_mfma_f32_32x32x16_bf16 / _f16, same tiles and rate)
@@ -588,9 +667,12 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
   const int jl = (threadIdx.x % TPR) * 8;
   const int j = j0 + jl;
   const bool live = j < nreal;
-  if (EPI != 2 && !live) return;            // (row LayerNorm: every lane of a row takes part)
+  if (EPI < 2 && !live) return;             // (row LayerNorm: every lane of a row takes part)
   const int nv = min(8, nreal - j);
   float* wsz = p.nsplit > 1 ? slab(p, g, z) : nullptr;
+  float dga[8], dba[8];                      // (tail = 3: this lane's dgamma / dbeta column terms)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) dga[e] = dba[e] = 0.f;
 #pragma unroll 2
   for (int pass = 0; pass < NPASS; ++pass) {
     const int il = pass * RPP + threadIdx.x / TPR;
@@ -609,6 +691,8 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
     if constexpr (EPI == 2) {
       if (live) epi_store8<E>(p, g, i, j, 8, v);   // v: the stored row values before rounding
       row_layernorm<E, TPR>(p, g, i, j, jl, live, v);
+    } else if constexpr (EPI == 3) {
+      row_layernorm_bwd<E, TPR>(p, g, i, j, live, v, dga, dba);
     } else if (wsz) {
       float* d = wsz + (long)i * nreal + j;
       if (nv == 8 && (nreal & 3) == 0) {
@@ -619,6 +703,25 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
       }
     } else {
       epi_store8<E, EPI == 1>(p, g, i, j, nv, v);
+    }
+  }
+  if constexpr (EPI == 3) {
+    // the tile's dgamma | dbeta column partials: the RPP row slots' lane sums meet in LDS
+    __syncthreads();                                  // every lane is done with the fp32 C image
+    float* red = reinterpret_cast<float*>(smem);      // [RPP][2][BN]
+    const int rsl = threadIdx.x / TPR;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(rsl * 2) * BN + jl + e] = dga[e];
+      red[(rsl * 2 + 1) * BN + jl + e] = dba[e];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < 2 * BN; c += 256 * KW) {
+      const int which = c / BN, col = c - which * BN;
+      if (col >= nreal) continue;
+      float a = 0.f;
+      for (int q = 0; q < RPP; ++q) a += red[(q * 2 + which) * BN + col];
+      p.lnb_part[((long)g * p.tiles_m + tm) * 2 * p.N + which * p.N + col] = a;
     }
   }
 }
@@ -1063,6 +1166,10 @@ void launch_bf16(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream
   if constexpr (BM == 64 && (BN == 64 || (BN == 128 && KW == 1))) {
     if (a.tail == 2) {                // whole-row LayerNorm in the epilogue (forward layouts, tiles_n = 1)
       hipLaunchKernelGGL((gemm_bf16_kernel<64, BN, false, false, NS, KW, E, 2>), grid, dim3(256 * KW), 0, s, a);
+      return;
+    }
+    if (a.tail == 3) {                // LayerNorm backward in a dgrad's epilogue (transB = 1, tiles_n = 1)
+      hipLaunchKernelGGL((gemm_bf16_kernel<64, BN, false, true, NS, KW, E, 3>), grid, dim3(256 * KW), 0, s, a);
       return;
     }
   }

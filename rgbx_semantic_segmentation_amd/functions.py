@@ -254,13 +254,13 @@ class LayerNormResF(Function):
     scale[sample] * dx for the producer of x (GradTap)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, gg, bg, eps, G, scale, rps, tap, anchor, pre=None):
+    def forward(ctx, x, gamma, beta, gg, bg, eps, G, scale, rps, tap, anchor, pre=None, dtap=None):
         if pre is not None:                  # computed by the producing launch (LNTail)
             y, mean, rstd = pre
         else:
             y, mean, rstd = K.layernorm_fwd(x, gamma, beta, eps, G=G)
         ctx.save_for_backward(x, gamma, mean, rstd)
-        ctx.meta = (gg, bg, G, scale, rps, tap)
+        ctx.meta = (gg, bg, G, scale, rps, tap, dtap)
         ctx.set_materialize_grads(False)     # unused outputs arrive as None, not zero-filled tensors
         # y twice (a view for the second consumer, so its gradient arrives separately) and x
         return y, y.view_as(y), x
@@ -268,10 +268,31 @@ class LayerNormResF(Function):
     @staticmethod
     def backward(ctx, dy, dy2, dres):
         x, gamma, mean, rstd = ctx.saved_tensors
-        gg, bg, G, scale, rps, tap = ctx.meta
+        gg, bg, G, scale, rps, tap, dtap = ctx.meta
         C = x.shape[-1]
         R = x.numel() // C // G
-        if dy is None:
+        handed = dtap.take() if dtap is not None else None
+        if handed is not None:
+            # the consumer Linear handed over (dz, W) instead of launching its dgrad: dy = dz W and
+            # this norm's backward run as ONE launch (cmx_gemm_ln_bwd, dy never stored)
+            dz, Wd = handed
+            other = dy if dy is not None else dy2
+            other = _c(other) if other is not None else None
+            dres_c = _c(dres) if dres is not None else None
+            dxs = torch.empty_like(x) if (tap is not None and scale is not None) else None
+            out = K.gemm_ln_bwd(dz, Wd, x, gamma, mean, rstd, dres=dres_c, dy2=other,
+                                sscale=scale if dxs is not None else None, rows_per_sample=rps, dxs=dxs)
+            if out is None:                  # not eligible after all: the separate dgrad
+                dy = _dgrad(dz, Wd, torch.empty_like(x))
+                dy2 = other
+            else:
+                dx, part = out
+                nb = part.shape[1]
+                deferred.reduce(part, gg, bg, G, nb, nb * 2 * C, 2 * C, 1, 2 * C, C, gg.stride(0), 0, bg.stride(0), 0)
+                if dxs is not None:
+                    tap.put(dxs)
+                return dx, None, None, None, None, None, None, None, None, None, None, None, None
+        elif dy is None:
             dy, dy2 = dy2, None
         dy = _c(dy) if dy is not None else torch.zeros_like(x)
         dy2 = _c(dy2) if dy2 is not None else None
@@ -289,12 +310,25 @@ class LayerNormResF(Function):
             deferred.reduce(ws, gg, bg, G, nb, nb * 2 * C, 2 * C, 1, 2 * C, C, gg.stride(0), 0, bg.stride(0), 0)
         if dxs is not None:
             tap.put(dxs)
-        return dx, None, None, None, None, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None, None, None, None, None
 
 
-def layernorm_res(store, mod, x, G, scale=None, rps=1, tap=None, tail=None):
+# CMX_LN_BWD_FUSE=0: the LayerNorm backward as its own launch after the consumer's dgrad (A/B switch)
+LN_BWD_FUSE = os.environ.get("CMX_LN_BWD_FUSE", "1") != "0"
+
+
+def ln_bwd_fusable(x) -> bool:
+    """The consumer Linear's dgrad can carry this norm's backward (cmx_gemm_ln_bwd): 16-bit,
+    C <= 128 (a dgrad tile spans the row), partials into the deferred reduce."""
+    C = x.shape[-1]
+    return (LN_BWD_FUSE and deferred.ENABLED and x.dtype in (torch.bfloat16, torch.float16) and C <= 128
+            and C % 8 == 0 and x.is_contiguous())
+
+
+def layernorm_res(store, mod, x, G, scale=None, rps=1, tap=None, tail=None, dtap=None):
     """(LN(x), LN(x) for a second consumer, x) with the fused backward (LayerNormResF).
-    tail: the LNTail whose producing launch already normalised x (its pre is used if set)."""
+    tail: the LNTail whose producing launch already normalised x (its pre is used if set).
+    dtap: the DgradTap the consumer Linear hands its (dz, W) to (backward as one launch)."""
     gamma = store.w(mod.weight, compute=False).view(G, -1)
     beta = store.w(mod.bias, compute=False).view(G, -1)
     gg = store.g(mod.weight).view(G, -1)
@@ -303,7 +337,7 @@ def layernorm_res(store, mod, x, G, scale=None, rps=1, tap=None, tail=None):
     if tail is not None:
         assert tail.mod is mod
         pre, tail.pre = tail.pre, None
-    return LayerNormResF.apply(x, gamma, beta, gg, bg, mod.eps, G, scale, rps, tap, mod.weight, pre)
+    return LayerNormResF.apply(x, gamma, beta, gg, bg, mod.eps, G, scale, rps, tap, mod.weight, pre, dtap)
 
 
 class LayerNormF(Function):

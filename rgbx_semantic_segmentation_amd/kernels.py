@@ -230,6 +230,33 @@ def gemm_ln(A, B, C, ln_gamma, ln_beta, ln_eps, bias=None, residual=None, rscale
     return y, mean, rstd
 
 
+def gemm_ln_bwd(dz, W, x, gamma, mean, rstd, dres=None, dy2=None, sscale=None, rows_per_sample=1, dxs=None):
+    """dx of the LayerNorm that produced a Linear's input, with the Linear's input gradient
+    dy = dz @ W (dz (G, M, K), W (G, K, N) = the weight's (out, in) view) computed in the same launch
+    (cmx_gemm_ln_bwd): dx = LN'(dy [+ dy2]) + dres; dxs (when given) = sscale[row // rps] * dx.
+    Returns (dx, partials (G, ceil(M / 64), 2N) fp32: dgamma | dbeta per 64-row tile), or None when
+    not eligible (the caller runs the dgrad GEMM and the LayerNorm backward kernel)."""
+    G, M, Kd = dz.shape
+    N = W.shape[2]
+    if dz.dtype not in (torch.bfloat16, torch.float16) or N > 128 or N % 8 or not dz.is_contiguous() \
+            or not x.is_contiguous() or W.shape[:2] != (G, Kd):
+        return None
+    tB, ldb, sB = _operand(W.transpose(1, 2), "B")
+    if not tB:
+        return None
+    dx = torch.empty_like(x)
+    part = torch.empty(G, (M + 63) // 64, 2 * N, dtype=torch.float32, device=x.device)
+    st = _lib.LIB.cmx_gemm_ln_bwd(ptr(dz), ptr(W), ptr(dx), G, M, N, Kd, dz.stride(1), ldb, x.stride(1), dz.stride(0),
+                                  sB, x.stride(0), ptr(x), ptr(gamma), gamma.stride(0) if gamma.dim() == 2 else 0,
+                                  ptr(mean), ptr(rstd), ptr(dres), ptr(dy2), ptr(sscale), int(rows_per_sample), ptr(dxs),
+                                  ptr(part), dtype_code(dz), stream())
+    if st == _lib.CMX_ERR_ARG:
+        return None
+    if st != 0:
+        raise _lib.CMXError(f"cmx_gemm_ln_bwd failed ({st}): {_lib.last_error()}")
+    return dx, part
+
+
 _PLAN_BYTES = query("cmx_gemm_plan_size")
 
 

@@ -390,3 +390,54 @@ def test_gemm_ln_tail(dev, dtype, G, M, N, K, res):
         if N <= 128:
             assert torch.equal(mean.flatten(), m0) and torch.equal(rstd.flatten(), r0) and torch.equal(y, y0), rep
     assert int(Kk._tickets(1, torch.device("cuda")).abs().sum().item()) == 0
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("G,M,N,K,res,dy2", [(2, 38400, 64, 256, True, False), (2, 9600, 128, 512, True, True),
+                                             (2, 4800, 32, 128, True, False), (1, 77, 128, 512, False, True),
+                                             (2, 1200, 64, 256, True, True), (2, 300, 128, 512, False, False)])
+def test_gemm_ln_bwd(dev, dtype, G, M, N, K, res, dy2):
+    """cmx_gemm_ln_bwd: the LayerNorm backward in the epilogue of the dgrad that produces its input
+    (Block.norm2 -> fc1).  dx and the DropPath-scaled dxs are bit-identical to the separate path
+    (cmx_gemm dgrad stored in the 16-bit type, then cmx_layernorm_bwd_res), and the per-tile
+    dgamma / dbeta partials sum to that kernel's column sums (fp32, another grouping)."""
+    from rgbx_semantic_segmentation_amd import kernels as Kk
+    torch.manual_seed(2)
+    dz = torch.randn(G, M, K, device="cuda").to(dtype)
+    W = (torch.randn(G, K, N, device="cuda") / math.sqrt(K)).to(dtype)        # (out = K, in = N)
+    x = (torch.randn(G, M, N, device="cuda") * 2 + 0.5).to(dtype)
+    gamma = torch.rand(G, N, device="cuda") + 0.5
+    beta = torch.randn(G, N, device="cuda")
+    _, mean, rstd = Kk.layernorm_fwd(x, gamma, beta, 1e-6, G=G)
+    dres = torch.randn(G, M, N, device="cuda").to(dtype) if res else None
+    d2 = torch.randn(G, M, N, device="cuda").to(dtype) if dy2 else None
+    rps = max(1, M // 2)
+    sc = torch.rand(G * M // rps, device="cuda") + 0.5
+    dxs = torch.empty_like(x)
+    out = Kk.gemm_ln_bwd(dz, W, x, gamma, mean, rstd, dres=dres, dy2=d2, sscale=sc, rows_per_sample=rps, dxs=dxs)
+    assert out is not None, "gemm_ln_bwd refused an eligible problem"
+    dx, part = out
+    # the separate path
+    dy = torch.empty_like(x)
+    Kk.gemm(dz, W.transpose(1, 2), dy)
+    dx0, dxs0 = torch.empty_like(x), torch.empty_like(x)
+    nbytes = Kk.query("cmx_layernorm_bwd_workspace", M, G, N, Kk.dtype_code(x))
+    ws = Kk._ws(nbytes, x.device)
+    gg = torch.zeros(G, N, device="cuda")
+    bg = torch.zeros(G, N, device="cuda")
+    Kk.call("cmx_layernorm_bwd_res", Kk.ptr(dy), Kk.ptr(d2), Kk.ptr(x), Kk.ptr(gamma), Kk.ptr(mean), Kk.ptr(rstd),
+            Kk.ptr(dres), Kk.ptr(sc), Kk.ptr(dxs0), Kk.ptr(dx0), Kk.ptr(gg), Kk.ptr(bg), Kk.ptr(ws), M, G, N, rps, 0,
+            Kk.dtype_code(x), Kk.stream())
+    torch.cuda.synchronize()
+    if N <= 64 or G * ((M + 63) // 64) * 2 > 512:
+        assert torch.equal(dx, dx0) and torch.equal(dxs, dxs0)
+    else:
+        # a small N = 128 grid: the separate dgrad runs 64 x 64 k-group blocks (two k-groups summed
+        # at the end) where the fused launch runs one 64 x 128 tile over k in order, so dy -- and dx
+        # -- may differ by a rounding
+        ulp = 2.0 ** (-7 if dtype == torch.bfloat16 else -10)
+        for a, b in ((dx, dx0), (dxs, dxs0)):
+            assert (a.float() - b.float()).abs().max().item() <= 4 * ulp * b.float().abs().max().item()
+    ps = part.double().sum(1)
+    assert torch.allclose(ps[:, :N], gg.double(), rtol=1e-4, atol=1e-3 * gg.abs().max().item())
+    assert torch.allclose(ps[:, N:], bg.double(), rtol=1e-4, atol=1e-3 * bg.abs().max().item())
