@@ -147,10 +147,12 @@ int cmx_small_linear_bwd(const float* dy_part, int dy_nslice, int64_t dy_slice_s
  * grid was co-resident; synchronous, for tests). */
 int cmx_frm_combine_fwd(const void* x, const float* cw, const void* h, const float* w2, const float* b2, float* sw, void* out, int B, int N, int C, int dtype, hipStream_t stream);
 /* backward: dx direct path (2,B,N,C), dh (B*N, C); workspace = dcw partials (B, nblk, 2C) followed by the
- * [dw2 (2C) | db2 (2)] partials (B*nblk, 2C+2); nblk = cmx_frm_combine_bwd_nblk(N, C, dtype) */
+ * [dw2 (2C) | db2 (2)] partials (B*nblk, 2C+2); nblk = cmx_frm_combine_bwd_nblk(N, C, dtype).
+ * dout2 (may be NULL): the gradient of the output's second consumer (the next stage beside the FFM),
+ * summed on load and rounded to the storage type, as autograd's add of the two would */
 int cmx_frm_combine_bwd_nblk(int N, int C, int dtype);
 size_t cmx_frm_combine_bwd_workspace(int B, int N, int C, int dtype);
-int cmx_frm_combine_bwd(const void* dout, const void* x, const float* cw, const float* sw, const void* h, const float* w2, void* dx, void* dh, float* workspace, int B, int N, int C, int dtype, hipStream_t stream);
+int cmx_frm_combine_bwd(const void* dout, const void* dout2, const void* x, const float* cw, const float* sw, const void* h, const float* w2, void* dx, void* dh, float* workspace, int B, int N, int C, int dtype, hipStream_t stream);
 
 /* ---- BatchNorm (ChannelEmbed BNs net_utils.py:319-329, decoder SyncBN MLPDecoder.py:51-55):
  *      fp64 channel sums -> (all-reduce for SyncBN) -> finalize; fused residual / act / Dropout2d. */
@@ -242,6 +244,14 @@ size_t cmx_gemm_ln_tickets(int G, int M);
  *      (G*M) fp32 as cmx_layernorm_fwd saves them; N <= 128, N % 8 == 0, 16-bit.  dy never reaches HBM. */
 int cmx_gemm_ln_bwd(const void* A, const void* B, void* dx, int G, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t sA, int64_t sB, int64_t sC, const void* x, const float* gamma, int64_t sg, const float* mean, const float* rstd, const void* dres, const void* dy2, const float* sscale, int rows_per_sample, void* dxs, float* partials, int dtype, hipStream_t stream);
 size_t cmx_gemm_ln_bwd_partials(int G, int M, int N);
+/* cmx_conv_patch_dgrad_ln_bwd: cmx_conv_patch_dgrad (Attention.sr's input gradient, col2im in the epilogue)
+ *      fed straight into the backward of the LayerNorm that produced the conv's input (Block.norm1 ->
+ *      Attention.sr, dual_segformer.py:95-96,167): dx = LN'(col2im(dy W) [+ dy2]) + dres as cmx_gemm_ln_bwd,
+ *      x / dres / dy2 / dxs / dx NHWC (G*NIg, H, W, C), mean / rstd per pixel (G*NIg*H*W) fp32; exact
+ *      patches (H = Ho R, W = Wo R), C 64 or 128, 16-bit.  partials: (G, ceil(NIg Ho Wo / 64) R^2, 2C)
+ *      dgamma | dbeta per (64-patch, tap) tile (cmx_conv_patch_dgrad_ln_bwd_partials bytes). */
+int cmx_conv_patch_dgrad_ln_bwd(const void* dy, const void* Wt, void* dx, int G, int NIg, int H, int Wd, int C, int R, int Ho, int Wo, int N, int64_t sdy, int64_t sW, int64_t sdx, const void* x, const float* gamma, int64_t sg, const float* mean, const float* rstd, const void* dres, const void* dy2, const float* sscale, int rows_per_sample, void* dxs, float* partials, int dtype, hipStream_t stream);
+size_t cmx_conv_patch_dgrad_ln_bwd_partials(int G, int NIg, int Ho, int Wo, int C, int R);
 int cmx_gemm_grouped(const void* recs, int nrec, int total_blocks, int dtype, hipStream_t stream);
 /* ---- Mix-FFN bands (Mlp.forward fc1 -> DWConv 3x3 -> GELU, dual_segformer.py:67-71) --------------
  * x (G, ipg*H*W, C) contiguous 16-bit; W1 (G, Ch, C) (group stride sW), b1 (G, Ch) (stride sb = Ch),

@@ -354,7 +354,8 @@ __global__ __launch_bounds__(256) void combine_fwd_kernel(const T* __restrict__ 
 // dcw (B, nblk, 2C) = [dcw0 | dcw1] and [dw2 (2C) | db2 (2)] (B * nblk, 2C + 2), combined over
 // the block's row slots in LDS (no atomics: deterministic).
 template <typename T, int TPR, int MCH>
-__global__ __launch_bounds__(256) void combine_bwd_kernel(const T* __restrict__ dout, const T* __restrict__ x,
+__global__ __launch_bounds__(256) void combine_bwd_kernel(const T* __restrict__ dout, const T* __restrict__ dout2,
+                                                          const T* __restrict__ x,
                                                           const float* __restrict__ cw, const float* __restrict__ sw,
                                                           const T* __restrict__ h, const float* __restrict__ w2,
                                                           T* __restrict__ dx, T* __restrict__ dh,
@@ -399,6 +400,16 @@ __global__ __launch_bounds__(256) void combine_bwd_kernel(const T* __restrict__ 
       float d1[V], d2[V], x1[V], x2[V], o1[V], o2[V];
       load_vec<T>(dout + e, d1);
       load_vec<T>(dout + per + e, d2);
+      if (dout2) {    // the output's second consumer: summed (and rounded) as autograd's add would
+        float e1[V], e2[V];
+        load_vec<T>(dout2 + e, e1);
+        load_vec<T>(dout2 + per + e, e2);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          d1[j] = to_f32(from_f32<T>(d1[j] + e1[j]));
+          d2[j] = to_f32(from_f32<T>(d2[j] + e2[j]));
+        }
+      }
       load_vec<T>(x + e, x1);
       load_vec<T>(x + per + e, x2);
 #pragma unroll
@@ -642,8 +653,8 @@ size_t cmx_frm_combine_bwd_workspace(int B, int N, int C, int dtype) {
 }
 
 // dx (2,B,N,C) direct path, dh (B*N, C); workspace: dcw partials (B, nblk, 2C) then the
-// [dw2 | db2] partials (B * nblk, 2C + 2)
-int cmx_frm_combine_bwd(const void* dout, const void* x, const float* cw, const float* sw, const void* h,
+// [dw2 | db2] partials (B * nblk, 2C + 2); dout2 (may be NULL): a second gradient of the output
+int cmx_frm_combine_bwd(const void* dout, const void* dout2, const void* x, const float* cw, const float* sw, const void* h,
                         const float* w2, void* dx, void* dh, float* workspace, int B, int N, int C, int dtype,
                         hipStream_t s) {
   const int V = dtype == 0 ? 4 : 8;
@@ -655,7 +666,7 @@ int cmx_frm_combine_bwd(const void* dout, const void* x, const float* cw, const 
   // chunks per lane: 1 unless the row has more than 64 chunks (fp32 with C > 256); the
   // one-chunk instantiation keeps the per-channel accumulators at half the registers
 #define CMX_CB(MCH_) FRM_TPR_DISPATCH(tpr, TPR, hipLaunchKernelGGL((combine_bwd_kernel<T, TPR, MCH_>), dim3(nb, B), \
-                                                  dim3(256), 0, s, (const T*)dout, (const T*)x, cw, sw, (const T*)h, \
+                                                  dim3(256), 0, s, (const T*)dout, (const T*)dout2, (const T*)x, cw, sw, (const T*)h, \
                                                   w2, (T*)dx, (T*)dh, pcw, psp, B, N, C))
   CMX_DISPATCH(dtype, T, {
     if (C / V <= tpr) CMX_CB(1);

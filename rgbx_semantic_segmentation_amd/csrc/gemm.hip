@@ -211,8 +211,8 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
   }
   if (scR > 0) {
     CMX_REQUIRE(G == 1 || sC > 0, CMX_ERR_ARG, "gemm: scatter");
-    CMX_REQUIRE(!R && out_mode == 0 && !ones_col && N == scR * scR * scC && M % (scHo * scWo) == 0, CMX_ERR_ARG,
-                "gemm: patch scatter needs a plain store of N = R*R*C columns");
+    CMX_REQUIRE((!R || lnb) && out_mode == 0 && !ones_col && N == scR * scR * scC && M % (scHo * scWo) == 0,
+                CMX_ERR_ARG, "gemm: patch scatter needs a plain store of N = R*R*C columns");
     a.scatter = 1; a.scH = scH; a.scW = scW; a.scC = scC; a.scR = scR; a.scHo = scHo; a.scWo = scWo;
   }
   const int kstep = fast ? FBK : BK;
@@ -241,8 +241,11 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
   if (lnb) {
     const bool al = ((uintptr_t)C & 15) == 0 && ((uintptr_t)lnb->x & 15) == 0 && ((uintptr_t)R & 15) == 0 &&
                     ((uintptr_t)lnb->dy2 & 15) == 0 && ((uintptr_t)lnb->dxs & 15) == 0;
+    // (under the patch scatter a 64 x C tile is one tap of 64 patches: C must be a tile width)
+    const bool rows_ok = a.scatter ? (scC == 64 || scC == 128) && scH == scHo * scR && scW == scWo * scR
+                                   : N <= 128 && N % 8 == 0;
     CMX_REQUIRE(fast && splitk == 1 && !transA && transB && out_mode == 0 && !ones_col && !bias && act == 0 && !mask &&
-                    !a.nup && !a.scatter && gh == 1 && !A2 && a.cvec && al && N <= 128 && N % 8 == 0 && dtype != 0 &&
+                    !a.nup && gh == 1 && !A2 && a.cvec && al && rows_ok && dtype != 0 &&
                     !tail && lnb->x && lnb->gamma && lnb->mean && lnb->rstd && lnb->part && (!lnb->dxs || rscale),
                 CMX_ERR_ARG, "gemm_ln_bwd: needs the 16-bit dgrad path (transB) without split-K, 16-B aligned rows, "
                 "N <= 128 (N %% 8 == 0), no bias / activation (G=%d M=%d N=%d K=%d)", G, M, N, K);
@@ -267,6 +270,7 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
     int bm, bn;
     plan_tiles(G, M, nb, K, &bm, &bn);
     if (row_ln || lnb) bm = 64, bn = N <= 64 ? 64 : 128;   // one tile spans the row
+    if (lnb && a.scatter) bn = scC;                         // (one tap's C channels)
     a.tiles_m = cdiv(M, bm); a.tiles_n = cdiv(nb, bn);
     launch_fast(a, bm, bn, G, splitk, transA, transB, dtype, s);
   } else {
@@ -336,6 +340,27 @@ int cmx_gemm_ln_bwd(const void* A, const void* B, void* dx, int G, int M, int N,
 }
 
 size_t cmx_gemm_ln_bwd_partials(int G, int M, int N) { return (size_t)G * ((M + 63) / 64) * 2 * N * sizeof(float); }
+
+// cmx_conv_patch_dgrad with the backward of the LayerNorm that produced the conv's input in the
+// epilogue: dx = LN'(col2im(dy W) [+ dy2]) + dres (the norm's input gradient), never storing the conv's
+int cmx_conv_patch_dgrad_ln_bwd(const void* dy, const void* Wt, void* dx, int G, int NIg, int H, int Wd, int C, int R,
+                                int Ho, int Wo, int N, int64_t sdy, int64_t sW, int64_t sdx, const void* x,
+                                const float* gamma, int64_t sg, const float* mean, const float* rstd, const void* dres,
+                                const void* dy2, const float* sscale, int rows_per_sample, void* dxs, float* partials,
+                                int dtype, hipStream_t s) {
+  CMX_REQUIRE(G > 0 && NIg > 0 && (C == 64 || C == 128) && R > 0 && Ho * R == H && Wo * R == Wd, CMX_ERR_SHAPE,
+              "conv_patch_dgrad_ln_bwd: H=%d W=%d R=%d Ho=%d Wo=%d C=%d (exact patches, C 64 / 128)", H, Wd, R, Ho, Wo,
+              C);
+  const int M = NIg * Ho * Wo, Kc = R * R * C;
+  const LnBwd l{x, gamma, (long)sg, mean, rstd, dy2, dxs, partials};
+  return gemm_impl(dy, nullptr, Wt, dx, nullptr, dres, sscale, nullptr, nullptr, G, M, Kc, N, N, N, 0, Kc, Kc, sdy, 0,
+                   sW, sdx, 0, 0, rows_per_sample, 0, 1, 0, 0, 0, 1, dtype, s, nullptr, R, H, Wd, C, Ho, Wo, 1, 0, 0, 0,
+                   nullptr, nullptr, nullptr, &l);
+}
+
+size_t cmx_conv_patch_dgrad_ln_bwd_partials(int G, int NIg, int Ho, int Wo, int C, int R) {
+  return (size_t)G * ((NIg * Ho * Wo + 63) / 64) * R * R * 2 * C * sizeof(float);
+}
 
 size_t cmx_gemm_plan_size(void) { return sizeof(GemmPlan); }
 

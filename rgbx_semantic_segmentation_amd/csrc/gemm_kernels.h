@@ -401,11 +401,15 @@ __device__ __forceinline__ void row_layernorm(const GemmArgs& p, int g, int i, i
 // exactly as ln_bwd_kernel (layernorm.hip) computes a row of TPR 16-B chunks (dy rounded to the
 // storage type first, as that kernel reads it), so dx and dxs are bit-identical to the separate
 // launches; the lane's dgamma / dbeta terms accumulate in dga / dba for the tile's partials.
+// Under the patch scatter (cmx_conv_patch_dgrad_ln_bwd: the SR conv's input gradient, Attention.sr
+// dual_segformer.py:95-96) a tile is one tap of 64 patches, i.e. 64 whole input-pixel rows of C =
+// BN channels: the norm row is the scattered pixel, its statistics index the pixel.
 template <typename E, int TPR>
-__device__ __forceinline__ void row_layernorm_bwd(const GemmArgs& p, int g, int i, int j, bool live, const float* v,
-                                                  float* dga, float* dba) {
-  const long off = (long)g * p.sC + (long)i * p.ldc + j;
-  const long grow = (long)g * p.M + i;
+__device__ __forceinline__ void row_layernorm_bwd(const GemmArgs& p, int g, int i, int j, int jl, bool live,
+                                                  const float* v, float* dga, float* dba) {
+  const int C = p.scatter ? p.scC : p.N;          // the norm's width
+  const long off = c_offset(p, g, i, j);
+  const long grow = p.scatter ? off / C : (long)g * p.M + i;
   const float mu = p.ln_mean[grow], rs = p.ln_rstd[grow];
   float dv[8], xh[8], gv[8];
   if (live) {
@@ -423,7 +427,7 @@ __device__ __forceinline__ void row_layernorm_bwd(const GemmArgs& p, int g, int 
     }
     float xv[8];
     load_vec<E>(reinterpret_cast<const E*>(p.lnb_x) + off, xv);
-    const float* ga = p.ln_gamma + (long)g * p.ln_sg + j;
+    const float* ga = p.ln_gamma + (long)g * p.ln_sg + jl;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       xh[e] = (xv[e] - mu) * rs;
@@ -439,8 +443,8 @@ __device__ __forceinline__ void row_layernorm_bwd(const GemmArgs& p, int g, int 
     s1 += gv[e];
     s2 += gv[e] * xh[e];
   }
-  s1 = group_sum(s1, TPR) / p.N;
-  s2 = group_sum(s2, TPR) / p.N;
+  s1 = group_sum(s1, TPR) / C;
+  s2 = group_sum(s2, TPR) / C;
   if (!live) return;
   float o[8];
 #pragma unroll
@@ -692,7 +696,7 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
       if (live) epi_store8<E>(p, g, i, j, 8, v);   // v: the stored row values before rounding
       row_layernorm<E, TPR>(p, g, i, j, jl, live, v);
     } else if constexpr (EPI == 3) {
-      row_layernorm_bwd<E, TPR>(p, g, i, j, live, v, dga, dba);
+      row_layernorm_bwd<E, TPR>(p, g, i, j, jl, live, v, dga, dba);
     } else if (wsz) {
       float* d = wsz + (long)i * nreal + j;
       if (nv == 8 && (nreal & 3) == 0) {
@@ -716,12 +720,13 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
       red[(rsl * 2 + 1) * BN + jl + e] = dba[e];
     }
     __syncthreads();
+    const int C = p.scatter ? p.scC : p.N;         // the norm's width (= BN under the scatter)
     for (int c = threadIdx.x; c < 2 * BN; c += 256 * KW) {
       const int which = c / BN, col = c - which * BN;
-      if (col >= nreal) continue;
+      if (col >= C || j0 + col >= nreal) continue;
       float a = 0.f;
       for (int q = 0; q < RPP; ++q) a += red[(q * 2 + which) * BN + col];
-      p.lnb_part[((long)g * p.tiles_m + tm) * 2 * p.N + which * p.N + col] = a;
+      p.lnb_part[(((long)g * p.tiles_m + tm) * p.tiles_n + tn) * 2 * C + which * C + col] = a;
     }
   }
 }

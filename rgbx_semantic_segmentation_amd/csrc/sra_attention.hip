@@ -451,6 +451,8 @@ void sra_dkv_fast_launch(const void* q, const void* k, const void* v, const void
                          long kvs, long dos, int nchunk, float sl2, float scale, int dtype, hipStream_t s);
 
 bool sra_small_ok(int D, int N, int Nk, int dtype, const void* const* ptrs, int nptr, const long* strides, int nstr);
+bool sra_small_fwd_ok(int D, int N, int Nk, int dtype, const void* const* ptrs, int nptr, const long* strides,
+                      int nstr);
 void sra_fwd_small_launch(const void* q, const void* k, const void* v, void* o, float* lse, int Bt, int N, int Nk,
                           int heads, long qs, long kvs, long os, float sl2, int dtype, hipStream_t s);
 void sra_dq_small_launch(const void* q, const void* k, const void* v, const void* o, const void* dout,
@@ -479,7 +481,7 @@ int cmx_sra_attn_fwd(const void* q, const void* k, const void* v, void* o, float
   {
     const void* ptrs[] = {q, k, v, o};
     const long strides[] = {qs, kvs, os};
-    if (sra_small_ok(D, N, Nk, dtype, ptrs, 4, strides, 3)) {
+    if (sra_small_fwd_ok(D, N, Nk, dtype, ptrs, 4, strides, 3)) {
       sra_fwd_small_launch(q, k, v, o, lse, Bt, N, Nk, heads, qs, kvs, os, sl2, dtype, s);
       return cmx_check_launch("sra_fwd");
     }

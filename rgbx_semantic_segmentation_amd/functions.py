@@ -275,17 +275,34 @@ class LayerNormResF(Function):
         if handed is not None:
             # the consumer Linear handed over (dz, W) instead of launching its dgrad: dy = dz W and
             # this norm's backward run as ONE launch (cmx_gemm_ln_bwd, dy never stored)
-            dz, Wd = handed
             other = dy if dy is not None else dy2
             other = _c(other) if other is not None else None
             dres_c = _c(dres) if dres is not None else None
             dxs = torch.empty_like(x) if (tap is not None and scale is not None) else None
-            out = K.gemm_ln_bwd(dz, Wd, x, gamma, mean, rstd, dres=dres_c, dy2=other,
-                                sscale=scale if dxs is not None else None, rows_per_sample=rps, dxs=dxs)
-            if out is None:                  # not eligible after all: the separate dgrad
-                dy = _dgrad(dz, Wd, torch.empty_like(x))
-                dy2 = other
+            sc = scale if dxs is not None else None
+            if len(handed) == 3:             # a patchify conv's (dy, W, geometry): Attention.sr
+                dyc, Wc, pg = handed
+                Gc, NIg, H, Wd_, Cc, Rp, Ho, Wo = pg
+                xv = x.view(Gc * NIg, H, Wd_, Cc)
+                out = K.conv_patch_dgrad_ln_bwd(dyc, Wc, pg, xv, gamma, mean, rstd,
+                                                dres=dres_c.view_as(xv) if dres_c is not None else None,
+                                                dy2=other.view_as(xv) if other is not None else None, sscale=sc,
+                                                rows_per_sample=rps, dxs=dxs.view_as(xv) if dxs is not None else None)
+                if out is not None:
+                    out = (out[0].view_as(x), out[1])
+                else:                        # not eligible after all: the separate patch dgrad
+                    dy = torch.empty(Gc * NIg, H, Wd_, Cc, dtype=dyc.dtype, device=dyc.device)
+                    K.call("cmx_conv_patch_dgrad", K.ptr(dyc), K.ptr(Wc), K.ptr(dy), Gc, NIg, H, Wd_, Cc, Rp, Ho, Wo,
+                           Wc.shape[1], dyc.stride(0), Wc.stride(0), NIg * H * Wd_ * Cc, K.dtype_code(dyc), K.stream())
+                    dy, dy2 = dy.view_as(x), other
             else:
+                dz, Wd = handed
+                out = K.gemm_ln_bwd(dz, Wd, x, gamma, mean, rstd, dres=dres_c, dy2=other, sscale=sc,
+                                    rows_per_sample=rps, dxs=dxs)
+                if out is None:              # not eligible after all: the separate dgrad
+                    dy = _dgrad(dz, Wd, torch.empty_like(x))
+                    dy2 = other
+            if out is not None:
                 dx, part = out
                 nb = part.shape[1]
                 deferred.reduce(part, gg, bg, G, nb, nb * 2 * C, 2 * C, 1, 2 * C, C, gg.stride(0), 0, bg.stride(0), 0)
@@ -317,12 +334,18 @@ class LayerNormResF(Function):
 LN_BWD_FUSE = os.environ.get("CMX_LN_BWD_FUSE", "1") != "0"
 
 
-def ln_bwd_fusable(x) -> bool:
+def ln_bwd_fusable(x, patch=None) -> bool:
     """The consumer Linear's dgrad can carry this norm's backward (cmx_gemm_ln_bwd): 16-bit,
-    C <= 128 (a dgrad tile spans the row), partials into the deferred reduce."""
+    C <= 128 (a dgrad tile spans the row), partials into the deferred reduce.  patch = (H, W, R):
+    the consumer is a non-overlapping R x R patchify conv (Attention.sr) on an H x W grid
+    (cmx_conv_patch_dgrad_ln_bwd: C 64 / 128, exact patches)."""
     C = x.shape[-1]
-    return (LN_BWD_FUSE and deferred.ENABLED and x.dtype in (torch.bfloat16, torch.float16) and C <= 128
-            and C % 8 == 0 and x.is_contiguous())
+    ok = (LN_BWD_FUSE and deferred.ENABLED and x.dtype in (torch.bfloat16, torch.float16) and C <= 128
+          and C % 8 == 0 and x.is_contiguous())
+    if ok and patch is not None:
+        H, W, R = patch
+        ok = C in (64, 128) and H % R == 0 and W % R == 0
+    return ok
 
 
 def layernorm_res(store, mod, x, G, scale=None, rps=1, tap=None, tail=None, dtap=None):
@@ -795,11 +818,13 @@ class ConvF(Function):
     (patch_embed1.hip), else im2col + grouped GEMM."""
 
     @staticmethod
-    def forward(ctx, x, W, Wg, b, bg, geom, anchor, x2=None):
+    def forward(ctx, x, W, Wg, b, bg, geom, anchor, x2=None, dtap=None):
         # geom: (G, NI, H, Wd, C, KH, KW, stride, pad, Ho, Wo, nchw); x2: the second image batch
-        # of an NCHW input given as two tensors (x holds the first NI - len(x2) images)
+        # of an NCHW input given as two tensors (x holds the first NI - len(x2) images).  dtap: the
+        # DgradTap of the LayerNorm that produced x (its backward takes over the input gradient)
         G, NI, H, Wd, C, KH, KW, st, pad, Ho, Wo, nchw = geom
         ctx.x2 = x2
+        ctx.dtap = dtap
         ctx.pe1 = None
         Kp = W.shape[-1]
         if IMPLICIT_CONV and not nchw and x.dtype in (torch.bfloat16, torch.float16) and C % 64 == 0 \
@@ -870,7 +895,7 @@ class ConvF(Function):
                    pad, Ho, Wo, N, Kp, dy.stride(0), K.dtype_code(dy), K.stream())
             deferred.reduce(ws, Wg, bg, G, nblk, nblk * N * (Kp + 1), N * (Kp + 1), N, Kp + 1, Kp, Wg.stride(0),
                             Wg.stride(1), bg.stride(0), 1)
-            return None, None, None, None, None, None, None, None
+            return None, None, None, None, None, None, None, None, None
         if ctx.implicit:
             x = cols                 # the conv input (no cols were materialised)
             if not deferred.conv_wgrad(dy, x, Wg, bg, (G, NI // G, H, Wd, C, KH, KW, st, pad, Ho, Wo)):
@@ -881,7 +906,12 @@ class ConvF(Function):
         else:
             _wgrad_into(dy, cols, Wg, bg)
         dx = None
-        if ctx.needs_input_grad[0] and not nchw and KH == KW == st and pad == 0 and H // st == Ho and Wd // st == Wo:
+        if ctx.needs_input_grad[0] and ctx.dtap is not None and KH == KW == st and pad == 0 and H == Ho * st \
+                and Wd == Wo * st:
+            # the producing LayerNorm runs this input gradient inside its own backward launch
+            # (cmx_conv_patch_dgrad_ln_bwd): hand (dy, W, patch geometry) over, return no dx
+            ctx.dtap.put((dy, W, (G, NI // G, H, Wd, C, st, Ho, Wo)))
+        elif ctx.needs_input_grad[0] and not nchw and KH == KW == st and pad == 0 and H // st == Ho and Wd // st == Wo:
             # non-overlapping patches (Attention.sr): col2im folded into the dgrad GEMM's epilogue
             exact = H % st == 0 and Wd % st == 0
             dx = (torch.empty if exact else torch.zeros)(NI, H, Wd, C, dtype=dy.dtype, device=dy.device)
@@ -894,7 +924,7 @@ class ConvF(Function):
             K.call("cmx_col2im_nhwc", K.ptr(dcols), K.ptr(dx), NI, H, Wd, C, KH, KW, st, pad, Ho, Wo, W.shape[-1],
                    K.dtype_code(dx), K.stream())
             dx = dx.view(ctx.xshape)
-        return dx, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None
 
 
 class PatchEmbed1F(Function):
@@ -969,7 +999,7 @@ def patch_embed1(store, pe, x, G, NI, H, W, x2=None):
     return layernorm(store, pe.norm, y, G), Ho, Wo
 
 
-def conv(store, mod, x, G, NI, H, W, C, stride, pad, nchw=False, x2=None):
+def conv(store, mod, x, G, NI, H, W, C, stride, pad, nchw=False, x2=None, dtap=None):
     KH, KW = mod.kernel_size
     Ho = (H + 2 * pad - KH) // stride + 1
     Wo = (W + 2 * pad - KW) // stride + 1
@@ -980,7 +1010,7 @@ def conv(store, mod, x, G, NI, H, W, C, stride, pad, nchw=False, x2=None):
     b = store.w(mod.bias, compute=False).view(G, -1) if mod.bias is not None else None
     bg = store.g(mod.bias).view(G, -1) if mod.bias is not None else None
     geom = (G, NI, H, W, C, KH, KW, stride, pad, Ho, Wo, nchw)
-    return ConvF.apply(x, Wt, Wgt, b, bg, geom, mod.weight, x2), Ho, Wo
+    return ConvF.apply(x, Wt, Wgt, b, bg, geom, mod.weight, x2, dtap), Ho, Wo
 
 
 # ---------------------------------------------------------------------------- FFM cross attention
@@ -1219,21 +1249,29 @@ class FRMF(Function):
                N, C, dt, K.stream())
         ctx.save_for_backward(x, pooled, argmax, y1, cw, h, sw)
         ctx.prm = prm
-        return out
+        ctx.set_materialize_grads(False)
+        # the output twice (a view for the second consumer: the FFM beside the next stage), so the
+        # two gradients arrive separately and the combine backward sums them on load (no add launch)
+        return out, out.view_as(out)
 
     @staticmethod
-    def backward(ctx, dout):
+    def backward(ctx, dout, dout2):
         x, pooled, argmax, y1, cw, h, sw = ctx.saved_tensors
         (W1, b1, W2, b2, W0, b0, w2s, b2s) = ctx.prm["w"]
         (gW1, gb1, gW2, gb2, gW0, gb0, gw2s, gb2s) = ctx.prm["g"]
         G, B, N, C = x.shape
         dt = K.dtype_code(x)
+        if dout is None:
+            dout, dout2 = dout2, None
+        if dout is None:
+            return None, None, None
         dout = _c(dout)
+        dout2 = _c(dout2) if dout2 is not None else None
         dx = torch.empty_like(x)
         dh = torch.empty_like(h)
         nb = K.query("cmx_frm_combine_bwd_nblk", N, C, dt)
         ws = K._ws(K.query("cmx_frm_combine_bwd_workspace", B, N, C, dt), x.device)
-        K.call("cmx_frm_combine_bwd", K.ptr(dout), K.ptr(x), K.ptr(cw), K.ptr(sw), K.ptr(h), K.ptr(w2s), K.ptr(dx),
+        K.call("cmx_frm_combine_bwd", K.ptr(dout), K.ptr(dout2), K.ptr(x), K.ptr(cw), K.ptr(sw), K.ptr(h), K.ptr(w2s), K.ptr(dx),
                K.ptr(dh), K.ptr(ws), B, N, C, dt, K.stream())
         psp = ws[B * nb * 2 * C:B * nb * 2 * C + B * nb * (2 * C + 2)]
         if deferred.ENABLED:          # [dw2 | db2] partials: weight gradients, summed by the grouped reduce
@@ -1270,6 +1308,7 @@ class FRMF(Function):
 
 
 def frm(store, mod, x):
+    """FRMF on x (2, B, N, C): (rectified pair for the FFM, the same for the next stage)."""
     cwm, swm = mod.channel_weights.mlp, mod.spatial_weights.mlp
     C = x.shape[-1]
     f32 = lambda p: store.w(p, stacked=False, compute=False)

@@ -257,6 +257,31 @@ def gemm_ln_bwd(dz, W, x, gamma, mean, rstd, dres=None, dy2=None, sscale=None, r
     return dx, part
 
 
+def conv_patch_dgrad_ln_bwd(dy, W, geom, x, gamma, mean, rstd, dres=None, dy2=None, sscale=None, rows_per_sample=1,
+                            dxs=None):
+    """dx of the LayerNorm that produced a non-overlapping patchify conv's input, with the conv's
+    input gradient col2im(dy @ W) computed in the same launch (cmx_conv_patch_dgrad_ln_bwd).
+    dy (G, NIg*Ho*Wo, N), W (G, N, R*R*C) tap-major, x / dres / dy2 / dxs NHWC (G*NIg, H, W, C).
+    Returns (dx, partials (G, nb, 2C)) or None when not eligible."""
+    G, NIg, H, Wd, C, R, Ho, Wo = geom
+    if dy.dtype not in (torch.bfloat16, torch.float16) or C not in (64, 128) or Ho * R != H or Wo * R != Wd \
+            or not (dy.is_contiguous() and x.is_contiguous()):
+        return None
+    dx = torch.empty_like(x)
+    nb = (NIg * Ho * Wo + 63) // 64 * R * R
+    part = torch.empty(G, nb, 2 * C, dtype=torch.float32, device=x.device)
+    st = _lib.LIB.cmx_conv_patch_dgrad_ln_bwd(ptr(dy), ptr(W), ptr(dx), G, NIg, H, Wd, C, R, Ho, Wo, W.shape[1],
+                                              dy.stride(0), W.stride(0), NIg * H * Wd * C, ptr(x), ptr(gamma),
+                                              gamma.stride(0) if gamma.dim() == 2 else 0, ptr(mean), ptr(rstd),
+                                              ptr(dres), ptr(dy2), ptr(sscale), int(rows_per_sample), ptr(dxs),
+                                              ptr(part), dtype_code(dy), stream())
+    if st == _lib.CMX_ERR_ARG or st == _lib.CMX_ERR_SHAPE:
+        return None
+    if st != 0:
+        raise _lib.CMXError(f"cmx_conv_patch_dgrad_ln_bwd failed ({st}): {_lib.last_error()}")
+    return dx, part
+
+
 _PLAN_BYTES = query("cmx_gemm_plan_size")
 
 

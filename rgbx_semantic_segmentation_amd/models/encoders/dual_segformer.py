@@ -141,10 +141,12 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
         # norm1 also passes x through for the attention residual: its backward sums both gradients
         # (q and the SR path read norm1's output through separate handles: the norm's backward
         # sums their gradients on load)
-        h, h2, xr = F.layernorm_res(store, blk.norm1, x, G, scale=prev[0], rps=N, tap=prev[1], tail=tail)
+        # norm1's backward rides on the SR conv's input-gradient launch (C 64 / 128, exact patches)
+        stap = F.DgradTap() if (a.sr_ratio > 1 and F.ln_bwd_fusable(x, (H, W, a.sr_ratio))) else None
+        h, h2, xr = F.layernorm_res(store, blk.norm1, x, G, scale=prev[0], rps=N, tap=prev[1], tail=tail, dtap=stap)
 
         if a.sr_ratio > 1:
-            xs, Hk, Wk = F.conv(store, a.sr, h2, G, G * B, H, W, C, a.sr_ratio, 0)
+            xs, Hk, Wk = F.conv(store, a.sr, h2, G, G * B, H, W, C, a.sr_ratio, 0, dtap=stap)
             xs, Nk = F.layernorm(store, a.norm, xs, G), Hk * Wk
         else:
             xs, Nk = h2, N
@@ -220,9 +222,9 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
             C = self.embed_dims[s]
             fr = self.FRMs[s]
             if isinstance(fr, ImprovedFeatureRectifyModule):
-                r = fr.rectify(store, x.view(G, B, Hc * Wc, C), training)
+                r = rn = fr.rectify(store, x.view(G, B, Hc * Wc, C), training)
             else:
-                r = F.frm(store, fr, x.view(G, B, Hc * Wc, C))
+                r, rn = F.frm(store, fr, x.view(G, B, Hc * Wc, C))     # rn: the next stage's handle
             if side is not None:
                 # FFM_s only feeds the decoder: run it beside stage s + 1 on the side stream
                 # (its backward then runs there too, beside the encoder's backward)
@@ -233,7 +235,7 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
             else:
                 outs.append(self.FFMs[s].run(store, r, B, Hc, Wc, training))
             grids.append((Hc, Wc))
-            x = r.view(G, B * Hc * Wc, C)
+            x = rn.view(G, B * Hc * Wc, C)
         if side is not None:
             main.wait_stream(side)
             for o in outs:

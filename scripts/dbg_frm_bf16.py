@@ -42,7 +42,7 @@ for cdt in (torch.float32, torch.bfloat16):
     dx = torch.empty_like(r); dh = torch.empty_like(h)
     nb = K.query("cmx_frm_combine_bwd_nblk", N, C, dt)
     ws = K._ws(K.query("cmx_frm_combine_bwd_workspace", B, N, C, dt), "cuda")
-    K.call("cmx_frm_combine_bwd", K.ptr(dout), K.ptr(r), K.ptr(cw), K.ptr(sw), K.ptr(h), K.ptr(w2s), K.ptr(dx), K.ptr(dh), K.ptr(ws), B, N, C, dt, K.stream())
+    K.call("cmx_frm_combine_bwd", K.ptr(dout), 0, K.ptr(r), K.ptr(cw), K.ptr(sw), K.ptr(h), K.ptr(w2s), K.ptr(dx), K.ptr(dh), K.ptr(ws), B, N, C, dt, K.stream())
     torch.cuda.synchronize(); st.update(dx_direct=dx.clone(), dh=dh.clone(), pcw=ws[:B * nb * 2 * C].clone())
     Wd = W0.view(C, 2, C).permute(1, 0, 2); dx2 = dx.view(2, B * N, C)
     K.gemm(dh[None].expand(2, B * N, C), Wd.transpose(1, 2), dx2, residual=dx2)

@@ -101,7 +101,7 @@ def test_frm_local(dev, case, C, heads, B, H, W):
     ((o1 * w).sum() + (o2 * w2).sum()).backward()
     tok = lambda t: t.detach().flatten(2).transpose(1, 2)
     r = torch.stack([tok(a1), tok(a2)]).contiguous().to(cdt).cuda().requires_grad_(True)
-    out = F.frm(store, prod, r)
+    out, _ = F.frm(store, prod, r)
     (out * torch.stack([tok(w), tok(w2)]).to(cdt).cuda()).sum().backward()
     deferred.flush()
     torch.cuda.synchronize()

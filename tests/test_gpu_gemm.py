@@ -441,3 +441,48 @@ def test_gemm_ln_bwd(dev, dtype, G, M, N, K, res, dy2):
     ps = part.double().sum(1)
     assert torch.allclose(ps[:, :N], gg.double(), rtol=1e-4, atol=1e-3 * gg.abs().max().item())
     assert torch.allclose(ps[:, N:], bg.double(), rtol=1e-4, atol=1e-3 * bg.abs().max().item())
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("G,NIg,H,W,C,R,N,dy2", [(2, 2, 120, 160, 64, 8, 64, True), (2, 2, 60, 80, 128, 4, 128, True),
+                                                 (1, 3, 16, 24, 64, 8, 64, False), (2, 1, 20, 12, 128, 4, 128, True)])
+def test_conv_patch_dgrad_ln_bwd(dev, dtype, G, NIg, H, W, C, R, N, dy2):
+    """cmx_conv_patch_dgrad_ln_bwd: Attention.sr's input gradient (col2im of dy W in the epilogue)
+    carried straight into norm1's backward (dy2 = the q projection's gradient of the same norm
+    output).  dx / dxs bit-identical to cmx_conv_patch_dgrad + cmx_layernorm_bwd_res; the per-tile
+    dgamma / dbeta partials sum to that kernel's column sums."""
+    from rgbx_semantic_segmentation_amd import kernels as Kk
+    torch.manual_seed(3)
+    Ho, Wo = H // R, W // R
+    M = NIg * Ho * Wo
+    dy = torch.randn(G, M, N, device="cuda").to(dtype)
+    Wt = (torch.randn(G, N, R * R * C, device="cuda") / math.sqrt(N)).to(dtype)
+    x = (torch.randn(G * NIg, H, W, C, device="cuda") * 2 + 0.5).to(dtype)
+    gamma = torch.rand(G, C, device="cuda") + 0.5
+    beta = torch.randn(G, C, device="cuda")
+    _, mean, rstd = Kk.layernorm_fwd(x, gamma, beta, 1e-6, G=G)
+    dres = torch.randn_like(x, dtype=torch.float32).to(dtype)
+    d2 = torch.randn_like(x, dtype=torch.float32).to(dtype) if dy2 else None
+    rps = H * W
+    sc = torch.rand(G * NIg, device="cuda") + 0.5
+    dxs = torch.empty_like(x)
+    out = Kk.conv_patch_dgrad_ln_bwd(dy, Wt, (G, NIg, H, W, C, R, Ho, Wo), x, gamma, mean, rstd, dres=dres, dy2=d2,
+                                     sscale=sc, rows_per_sample=rps, dxs=dxs)
+    assert out is not None, "conv_patch_dgrad_ln_bwd refused an eligible problem"
+    dx, part = out
+    dyc = torch.empty_like(x)
+    Kk.call("cmx_conv_patch_dgrad", Kk.ptr(dy), Kk.ptr(Wt), Kk.ptr(dyc), G, NIg, H, W, C, R, Ho, Wo, N, dy.stride(0),
+            Wt.stride(0), NIg * H * W * C, Kk.dtype_code(dy), Kk.stream())
+    Rr = NIg * H * W
+    dx0, dxs0 = torch.empty_like(x), torch.empty_like(x)
+    ws = Kk._ws(Kk.query("cmx_layernorm_bwd_workspace", Rr, G, C, Kk.dtype_code(x)), x.device)
+    gg = torch.zeros(G, C, device="cuda")
+    bg = torch.zeros(G, C, device="cuda")
+    Kk.call("cmx_layernorm_bwd_res", Kk.ptr(dyc), Kk.ptr(d2), Kk.ptr(x), Kk.ptr(gamma), Kk.ptr(mean), Kk.ptr(rstd),
+            Kk.ptr(dres), Kk.ptr(sc), Kk.ptr(dxs0), Kk.ptr(dx0), Kk.ptr(gg), Kk.ptr(bg), Kk.ptr(ws), Rr, G, C, rps, 0,
+            Kk.dtype_code(x), Kk.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dx, dx0) and torch.equal(dxs, dxs0)
+    ps = part.double().sum(1)
+    assert torch.allclose(ps[:, :C], gg.double(), rtol=1e-4, atol=1e-3 * gg.abs().max().item())
+    assert torch.allclose(ps[:, C:], bg.double(), rtol=1e-4, atol=1e-3 * bg.abs().max().item())

@@ -131,9 +131,11 @@ def test_frm(dev, C, B, H, W, dtype):
     ((o1 * w1).sum() + (o2 * w2).sum()).backward()
     tok = lambda t: t.detach().flatten(2).transpose(1, 2)
     r = torch.stack([tok(x1), tok(x2)]).contiguous().to(cdt).cuda().requires_grad_(True)
-    out = F.frm(store, prod, r)
+    out, out2 = F.frm(store, prod, r)
     wt = torch.stack([tok(w1), tok(w2)]).to(cdt).cuda()
-    (out * wt).sum().backward()
+    # both output handles carry half the weight (exact halves): the combine backward sums the two
+    # gradients on load (FRMF's second consumer, the next stage beside the FFM)
+    ((out * (wt / 2)).sum() + (out2 * (wt / 2)).sum()).backward()
     deferred.flush()
     torch.cuda.synchronize()
     refp = dict(ref.named_parameters())
