@@ -257,12 +257,14 @@ int cmx_gemm_grouped(const void* recs, int nrec, int total_blocks, int dtype, hi
  * x (G, ipg*H*W, C) contiguous 16-bit; W1 (G, Ch, C) (group stride sW), b1 (G, Ch) (stride sb = Ch),
  * wdw (G, Ch, 9) (stride sdw = 9 Ch) and bdw (G, Ch) fp32.  One launch: h = x W1^T + b1, z = DW(h) + bdw,
  * a = GELU(z), act'(z) -- bit-identical to cmx_gemm + cmx_dwconv3x3_fwd_save.  A workgroup owns a band of
- * cmx_mixffn_band_rows(W) image rows (+1 halo row each side, fc1 recomputed there) x 64 hidden channels;
- * 0 = the band kernels do not apply (W > 85).
+ * cmx_mixffn_band_rows(W) image rows (+1 halo row each side, fc1 recomputed there) x 64 hidden channels,
+ * or (cmx_mixffn_mode(W) = 2: W > 42) a 12 x 16-pixel tile (+1 halo pixel each side) x 64 hidden channels.
  * bwd: dz2 (G, ipg*H*W, C) = fc2's output gradient, W2 (G, C, Ch): da = dz2 W2 (as fc2's dgrad would),
  * dz = da * act'(z), dh = DW^T(dz), and the DW dW / db partials (G, P, Ch * 10) in the workspace
  * (cmx_mixffn_bwd_workspace bytes, P = workspace / (40 G Ch)) for cmx_reduce_grouped. */
 int cmx_mixffn_band_rows(int W);
+/* cmx_mixffn_mode: 1 = bands of cmx_mixffn_band_rows(W) full rows (>= 4), 2 = 12 x 16-pixel tiles (wide images) */
+int cmx_mixffn_mode(int W);
 size_t cmx_mixffn_bwd_workspace(int G, int ipg, int H, int W, int Ch);
 int cmx_mixffn_fwd(const void* x, const void* W1, const float* b1, const float* wdw, const float* bdw, void* h, void* gprime, void* a, int G, int ipg, int H, int W, int C, int Ch, int64_t sW, int64_t sb, int64_t sdw, int dtype, hipStream_t stream);
 int cmx_mixffn_bwd(const void* dz2, const void* W2, const float* wdw, const void* h, const void* gprime, void* dh, float* workspace, int G, int ipg, int H, int W, int C, int Ch, int64_t sW, int64_t sdw, int dtype, hipStream_t stream);

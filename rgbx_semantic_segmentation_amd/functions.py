@@ -711,6 +711,12 @@ def dwconv(store, conv, h, NI, ipg, H, W, act):
 # per stage-3 / stage-4 band launch against ~22 / ~15 us for the GEMM + DWConv pair it replaces;
 # 3 interleaved A/B pairs 264.8 vs 268.9 img/s, profiles/r05_b_ab_mixffn.txt)
 MIXFFN_BAND = os.environ.get("CMX_MIXFFN", "0") == "1"
+# CMX_MIXFFN_TILE=1: the wide stages (W > 42: 1-2 of B2 / B4 480 x 640) run fc1 + DWConv + GELU (and
+# fc2's dgrad + the DW backward) as one launch over 12 x 16-pixel tiles (csrc/mixffn.hip 2-D tiles,
+# K = C = 64 / 128: one or two k-tiles).  Off by default: measured slower (69 us
+# per fused launch against 54 / 38 us for the stage-1 / stage-2 GEMM + DWConv pair; 260.7 vs 270.3
+# img/s, profiles/r05_l_ab_mixffn_tile.txt)
+MIXFFN_TILE = os.environ.get("CMX_MIXFFN_TILE", "0") == "1"
 # bands of fewer rows recompute too much of fc1 on their halo rows ((R + 2) / R): stage 3 / 4 of
 # B2 / B4 at 480 x 640 get R = 4 / 10, stage 2 (W = 80) would get R = 1
 MIXFFN_MIN_ROWS = int(os.environ.get("CMX_MIXFFN_MIN_ROWS", "4"))
@@ -725,7 +731,7 @@ class MixFFNF(Function):
     weight gradient, as GLinear's backward would."""
 
     @staticmethod
-    def forward(ctx, W1, Wg1, b1, bg1, wdw, bdw, wgdw, bgdw, anchor, x, B, H, W, tap):
+    def forward(ctx, W1, Wg1, b1, bg1, wdw, bdw, wgdw, bgdw, anchor, x, B, H, W, tap, ltap=None):
         G, M, C = x.shape
         Ch = W1.shape[1]
         h = torch.empty(G, M, Ch, dtype=x.dtype, device=x.device)
@@ -734,14 +740,14 @@ class MixFFNF(Function):
         K.call("cmx_mixffn_fwd", K.ptr(x), K.ptr(W1), K.ptr(b1), K.ptr(wdw), K.ptr(bdw), K.ptr(h), K.ptr(gp), K.ptr(a),
                G, B, H, W, C, Ch, W1.stride(0), b1.stride(0), wdw.stride(0), K.dtype_code(x), K.stream())
         ctx.save_for_backward(W1, x, h, gp, wdw)
-        ctx.meta = (Wg1, bg1, wgdw, bgdw, B, H, W, tap)
+        ctx.meta = (Wg1, bg1, wgdw, bgdw, B, H, W, tap, ltap)
         ctx.set_materialize_grads(False)
         return a
 
     @staticmethod
     def backward(ctx, da):
         W1, x, h, gp, wdw = ctx.saved_tensors
-        Wg1, bg1, wgdw, bgdw, B, H, W, tap = ctx.meta
+        Wg1, bg1, wgdw, bgdw, B, H, W, tap, ltap = ctx.meta
         G, M, Ch = h.shape
         C = x.shape[-1]
         handed = tap.take() if tap is not None else None
@@ -761,9 +767,15 @@ class MixFFNF(Function):
                    K.ptr(ws), G * B, B, H, W, Ch, 0, K.dtype_code(h), K.stream())
             P = K.query("cmx_dwconv3x3_bwd_saved_tiles", B, H, W)
         deferred.reduce(ws, wgdw, bgdw, G, P, P * Ch * 10, Ch * 10, Ch, 10, 9, wgdw.stride(0), 9, bgdw.stride(0), 1)
-        dx = _dgrad(dh, W1, torch.empty_like(x)) if ctx.needs_input_grad[9] else None
+        dx = None
+        if ctx.needs_input_grad[9]:
+            if ltap is not None:
+                # norm2's backward computes fc1's input gradient in its own launch (cmx_gemm_ln_bwd)
+                ltap.put((dh, W1))
+            else:
+                dx = _dgrad(dh, W1, torch.empty_like(x))
         _wgrad_into(dh, x, Wg1, bg1)
-        return (None,) * 9 + (dx, None, None, None, None)
+        return (None,) * 9 + (dx, None, None, None, None, None)
 
 
 class DgradTap:
@@ -783,14 +795,20 @@ class DgradTap:
 
 
 def mixffn_ok(x, Ch, B, H, W) -> bool:
-    """The band kernels apply: 16-bit, a band of >= 1 row + halo within 256 tokens, hidden % 64,
-    every operand in the ParamStore layout (deferred weight gradients)."""
-    return (MIXFFN_BAND and deferred.ENABLED and x.dtype in (torch.bfloat16, torch.float16) and x.is_contiguous()
-            and Ch % 64 == 0 and x.shape[-1] % 8 == 0 and K.query("cmx_mixffn_band_rows", W) >= MIXFFN_MIN_ROWS)
+    """The fused Mix-FFN kernels apply: 16-bit, hidden % 64, every operand in the ParamStore layout
+    (deferred weight gradients); 2-D tiles for wide images with C <= 128 (CMX_MIXFFN_TILE), bands
+    of >= CMX_MIXFFN_MIN_ROWS rows otherwise (CMX_MIXFFN=1)."""
+    if not (deferred.ENABLED and x.dtype in (torch.bfloat16, torch.float16) and x.is_contiguous() and Ch % 64 == 0
+            and x.shape[-1] % 8 == 0):
+        return False
+    if K.query("cmx_mixffn_mode", W) == 2:          # 2-D tiles (wide images, short K)
+        return MIXFFN_TILE and x.shape[-1] <= 128
+    return MIXFFN_BAND and K.query("cmx_mixffn_band_rows", W) >= MIXFFN_MIN_ROWS
 
 
-def mixffn(store, mlp, x, B, H, W, tap):
-    """a = GELU(DWConv(fc1(x))) (MixFFNF); ``tap`` is the DgradTap fc2's glinear hands dz2 to."""
+def mixffn(store, mlp, x, B, H, W, tap, ltap=None):
+    """a = GELU(DWConv(fc1(x))) (MixFFNF); ``tap`` is the DgradTap fc2's glinear hands dz2 to,
+    ``ltap`` the one this node hands fc1's (dh, W1) to (the producing norm's fused backward)."""
     G = x.shape[0]
     W1 = store.w(mlp.fc1.weight)
     W1 = W1.view(G, W1.shape[1], -1)
@@ -802,7 +820,7 @@ def mixffn(store, mlp, x, B, H, W, tap):
     bdw = store.w(conv.bias, compute=False).view(G, -1)
     wgdw = store.g(conv.weight).view(G, -1, 9)
     bgdw = store.g(conv.bias).view(G, -1)
-    return MixFFNF.apply(W1, Wg1, b1, bg1, wdw, bdw, wgdw, bgdw, mlp.fc1.weight, x, B, H, W, tap)
+    return MixFFNF.apply(W1, Wg1, b1, bg1, wdw, bdw, wgdw, bgdw, mlp.fc1.weight, x, B, H, W, tap, ltap)
 
 
 # ---------------------------------------------------------------------------- conv (implicit GEMM / im2col + GEMM)

@@ -159,13 +159,13 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
         x = F.glinear(store, a.proj.weight, a.proj.bias, o, res=xr, rscale=s_attn, rps=N, tap=tap_a, ln_tail=t2)
         mix = F.mixffn_ok(x, blk.mlp.fc1.weight.shape[0], B, H, W)
         # norm2's backward rides on fc1's dgrad launch (C <= 128): fc1 hands (dz, W1) over
-        ltap = F.DgradTap() if (not mix and F.ln_bwd_fusable(x)) else None
+        ltap = F.DgradTap() if F.ln_bwd_fusable(x) else None
         h, _, xr = F.layernorm_res(store, blk.norm2, x, G, scale=s_attn, rps=N, tap=tap_a, tail=t2, dtap=ltap)
         dtap = None
         if mix:
             # fc1 + DWConv + GELU in one launch; fc2's input gradient joins their backward launch
             dtap = F.DgradTap()
-            f = F.mixffn(store, blk.mlp, h, B, H, W, dtap)
+            f = F.mixffn(store, blk.mlp, h, B, H, W, dtap, ltap)
         else:
             f = F.glinear(store, blk.mlp.fc1.weight, blk.mlp.fc1.bias, h, dgrad_tap=ltap)
             f = F.dwconv(store, blk.mlp.dwconv.dwconv, f, G * B, B, H, W, "gelu")
