@@ -24,8 +24,31 @@ import os
 import sys
 import time
 
-import torch
-import torch.distributed as dist
+
+def _graph_streams_env(argv, env):
+    """The HIP graph executor's stream count for a single-GPU run: 2 (CMX_GRAPH_STREAMS, 0 = the
+    runtime default of 4).  The replayed step has two concurrent chains (the encoder / decoder
+    and the FFM branch on its side stream); with the default four executor streams the main
+    chain's nodes are dealt round-robin over several hardware queues and every hand-over is a
+    cross-queue wait (~9 us each in the kernel traces).  Measured (DESIGN.md round 5, 3
+    interleaved pairs): 272.5 vs 269.5 img/s.  Set before torch loads the HIP runtime (the
+    runtime reads its flags at load); multi-rank runs keep the runtime default."""
+    gpus = 1
+    for i, a in enumerate(argv):
+        if a == "--gpus" and i + 1 < len(argv):
+            gpus = int(argv[i + 1])
+        elif a.startswith("--gpus="):
+            gpus = int(a.split("=", 1)[1])
+    n = env.get("CMX_GRAPH_STREAMS", "2")
+    if n != "0" and "DEBUG_HIP_FORCE_GRAPH_QUEUES" not in env and gpus == 1 and int(env.get("WORLD_SIZE", "1")) == 1:
+        env["DEBUG_HIP_FORCE_GRAPH_QUEUES"] = n
+
+
+if __name__ == "__main__":
+    _graph_streams_env(sys.argv[1:], os.environ)
+
+import torch  # noqa: E402  (after the HIP runtime flags above)
+import torch.distributed as dist  # noqa: E402
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
@@ -466,6 +489,7 @@ def main():
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "image": [args.height, args.width], "classes": args.classes,
                        "parallelism": f"dp{world}", "hip_graph": graph is not None,
+                       "hip_graph_streams": os.environ.get("DEBUG_HIP_FORCE_GRAPH_QUEUES", "runtime default"),
                        "loss_scaling": bool(args.loss_scaling)},
             "step_mfma_roofline": {"train_gflop_per_image": round(fl_img / 1e9, 3),
                                    "achieved_tflops": round((ips / world) * fl_img / 1e12, 2),

@@ -54,3 +54,21 @@ def test_gpus_2_launches_two_ranks_end_to_end():
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [json.loads(s) for s in r.stdout.splitlines() if s.startswith("{")]
     assert lines == [{"dry_run": True, "n_gpus": 2, "ranks_seen": 2}]
+
+
+def test_graph_streams_env_single_gpu_only():
+    """bench.py sets the HIP graph executor's stream count (2) only for a one-GPU run, before
+    torch loads the runtime; an explicit setting, CMX_GRAPH_STREAMS=0 or any multi-rank run keeps
+    the runtime's own choice."""
+    import bench
+    env = {}
+    bench._graph_streams_env(["--steps", "5"], env)
+    assert env["DEBUG_HIP_FORCE_GRAPH_QUEUES"] == "2"
+    for argv, e in ((["--gpus", "2"], {}), (["--gpus=8"], {}), ([], {"WORLD_SIZE": "4"}),
+                    ([], {"CMX_GRAPH_STREAMS": "0"}), ([], {"DEBUG_HIP_FORCE_GRAPH_QUEUES": "3"})):
+        before = dict(e)
+        bench._graph_streams_env(argv, e)
+        assert e.get("DEBUG_HIP_FORCE_GRAPH_QUEUES") == before.get("DEBUG_HIP_FORCE_GRAPH_QUEUES"), (argv, e)
+    e = {"CMX_GRAPH_STREAMS": "3"}
+    bench._graph_streams_env([], e)
+    assert e["DEBUG_HIP_FORCE_GRAPH_QUEUES"] == "3"
