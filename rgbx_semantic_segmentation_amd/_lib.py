@@ -112,6 +112,16 @@ def call(name: str, *args) -> None:
         observer(name, fn, args)
 
 
+def try_call(name: str, *args) -> int:
+    """Invoke an int-returning entry point and return its status (the caller decides what a
+    refusal means); the measurement observer sees it only when it succeeded."""
+    fn = getattr(LIB, name)
+    st = int(fn(*args))
+    if st == 0 and observer is not None:
+        observer(name, fn, args)
+    return st
+
+
 def query(name: str, *args) -> int:
     return int(getattr(LIB, name)(*args))
 

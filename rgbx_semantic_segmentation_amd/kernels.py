@@ -219,7 +219,7 @@ def gemm_ln(A, B, C, ln_gamma, ln_beta, ln_eps, bias=None, residual=None, rscale
     mean = torch.empty(G, M, dtype=torch.float32, device=C.device)
     rstd = torch.empty_like(mean)
     tk = None if row else _tickets(query("cmx_gemm_ln_tickets", G, M), C.device)
-    st = _lib.LIB.cmx_gemm_ln(ptr(A), ptr(A2), ptr(B), ptr(C), ptr(bias), ptr(residual), ptr(rscale), G, M, N, Kd, K1,
+    st = _lib.try_call("cmx_gemm_ln", ptr(A), ptr(A2), ptr(B), ptr(C), ptr(bias), ptr(residual), ptr(rscale), G, M, N, Kd, K1,
                          lda, lda2, ldb, C.stride(1), sA, sA2, sB, C.stride(0), sbias, int(rows_per_sample), ACT[act],
                          ptr(ln_gamma), ptr(ln_beta), ln_gamma.stride(0) if ln_gamma.dim() == 2 else 0,
                          float(ln_eps), ptr(y), ptr(mean), ptr(rstd), ptr(tk), dtype_code(A), stream())
@@ -246,7 +246,7 @@ def gemm_ln_bwd(dz, W, x, gamma, mean, rstd, dres=None, dy2=None, sscale=None, r
         return None
     dx = torch.empty_like(x)
     part = torch.empty(G, (M + 63) // 64, 2 * N, dtype=torch.float32, device=x.device)
-    st = _lib.LIB.cmx_gemm_ln_bwd(ptr(dz), ptr(W), ptr(dx), G, M, N, Kd, dz.stride(1), ldb, x.stride(1), dz.stride(0),
+    st = _lib.try_call("cmx_gemm_ln_bwd", ptr(dz), ptr(W), ptr(dx), G, M, N, Kd, dz.stride(1), ldb, x.stride(1), dz.stride(0),
                                   sB, x.stride(0), ptr(x), ptr(gamma), gamma.stride(0) if gamma.dim() == 2 else 0,
                                   ptr(mean), ptr(rstd), ptr(dres), ptr(dy2), ptr(sscale), int(rows_per_sample), ptr(dxs),
                                   ptr(part), dtype_code(dz), stream())
@@ -270,7 +270,7 @@ def conv_patch_dgrad_ln_bwd(dy, W, geom, x, gamma, mean, rstd, dres=None, dy2=No
     dx = torch.empty_like(x)
     nb = (NIg * Ho * Wo + 63) // 64 * R * R
     part = torch.empty(G, nb, 2 * C, dtype=torch.float32, device=x.device)
-    st = _lib.LIB.cmx_conv_patch_dgrad_ln_bwd(ptr(dy), ptr(W), ptr(dx), G, NIg, H, Wd, C, R, Ho, Wo, W.shape[1],
+    st = _lib.try_call("cmx_conv_patch_dgrad_ln_bwd", ptr(dy), ptr(W), ptr(dx), G, NIg, H, Wd, C, R, Ho, Wo, W.shape[1],
                                               dy.stride(0), W.stride(0), NIg * H * Wd * C, ptr(x), ptr(gamma),
                                               gamma.stride(0) if gamma.dim() == 2 else 0, ptr(mean), ptr(rstd),
                                               ptr(dres), ptr(dy2), ptr(sscale), int(rows_per_sample), ptr(dxs),

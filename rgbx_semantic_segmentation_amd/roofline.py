@@ -61,7 +61,9 @@ def _pmc_traffic(kernel: str, workload: str, blocks: int):
 # the C-ABI entry points whose launches make up the tile-GEMM family (the FFM per-head context
 # products, cmx_gemm_h2, are floor.py's "ffm" family and stay out of both the time and the work)
 GEMM_FAMILY = ("cmx_gemm", "cmx_gemm_ln", "cmx_gemm_multi", "cmx_conv_implicit_fwd", "cmx_decoder_fuse_fwd",
-               "cmx_conv_patch_dgrad")
+               "cmx_conv_patch_dgrad", "cmx_gemm_ln_bwd", "cmx_conv_patch_dgrad_ln_bwd")
+# (the LayerNorm-epilogue launches -- cmx_gemm_ln and the two *_ln_bwd -- are timed whole: their time
+# includes the norm's work, their algorithmic bytes only the GEMM's, so the family's fraction errs low)
 
 
 def _family_traffic(kernels, workload: str):
