@@ -34,7 +34,7 @@ typedef struct ihipStream_t* hipStream_t;
  * from, and the Python binding refuses a library whose revision differs (an older .so with the
  * same symbol names but shifted arguments would otherwise corrupt memory silently).  Bump it
  * on every change of an entry point's argument list. */
-#define CMX_ABI_VERSION 3
+#define CMX_ABI_VERSION 4
 int cmx_abi_version(void);
 const char* cmx_last_error(void);
 /* pinned host -> device copy of a packed record table on `stream` (see grouped launches) */
@@ -125,7 +125,10 @@ int cmx_ffm_ctx_bwd(const float* ctx, const float* dctx, void* da, int G, int B,
 /* ---- CM-FRM (FeatureRectifyModule, net_utils.py:124-152): ChannelWeights pooling (:22-27)
  *      + tiny-M MLP (:16-20), SpatialWeights 1x1 C->2 + sigmoid (:74-83), rectification. */
 size_t cmx_frm_pool_workspace(int B, int N, int C);
-int cmx_frm_pool_fwd(const void* x, float* pooled, int* argmax, float* workspace, int B, int N, int C, int dtype, hipStream_t stream);
+/* tickets: cmx_frm_pool_tickets(B, C) zeroed uint32 arrival counters owned by the caller (each launch leaves
+ * them zero; launches that may overlap need their own); NULL = the library's device-global set */
+size_t cmx_frm_pool_tickets(int B, int C);
+int cmx_frm_pool_fwd(const void* x, float* pooled, int* argmax, float* workspace, unsigned* tickets, int B, int N, int C, int dtype, hipStream_t stream);
 /* dx += pooling backward; dpooled (B, 4C) given as partial slices dp[b][k] = sum_s part[s*slice_stride + b*4C + k] */
 int cmx_frm_pool_bwd(const float* dpooled_part, int nslice, int64_t slice_stride, const int* argmax, void* dx, int B, int N, int C, int dtype, hipStream_t stream);
 /* tiny-M linear y = act(x w^T + b) (x (M, K) fp32, M <= 8); backward in one pass over w: dy given as partial slabs
@@ -295,19 +298,22 @@ int cmx_reduce_pack(void* rec, const float* src, float* dst, float* dst2, int G,
 int cmx_reduce_grouped(const void* recs, int nrec, int total_blocks, hipStream_t stream);
 
 /* ---- fused AdamW over the flat parameter buffer (train.py:128-129, init_func.py:33-57). */
-int cmx_adamw_step(float* p, const float* g, float* m, float* v, void* shadow, int shadow_dtype, const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1, double beta2, float eps, double weight_decay, float grad_scale, hipStream_t stream);
+/* tickets (all three steps): cmx_adamw_tickets() zeroed uint32s owned by the optimizer (the step count's
+ * arrival counters; each launch leaves them zero); NULL = the library's device-global set */
+size_t cmx_adamw_tickets(void);
+int cmx_adamw_step(float* p, const float* g, float* m, float* v, void* shadow, int shadow_dtype, const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1, double beta2, float eps, double weight_decay, float grad_scale, unsigned* tickets, hipStream_t stream);
 /* ---- dynamic loss scaling: torch.cuda.amp.GradScaler of the reference's AMP path (train.py:13,56,185-198, config 5).
  *      The scale, growth tracker and found-inf flag live on the device, so a scaled step replays from a HIP graph:
  *      grad_nonfinite sets found_inf if any gradient is inf/nan; adamw_step_scaled unscales by 1/loss_scale[0] and
  *      skips the whole update (and the step count) when found_inf[0] != 0; loss_scale_update applies backoff /
  *      growth (after growth_interval clean steps) and clears found_inf. */
-int cmx_adamw_step_scaled(float* p, const float* g, float* m, float* v, void* shadow, int shadow_dtype, const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1, double beta2, float eps, double weight_decay, float grad_scale, const float* loss_scale, const float* found_inf, hipStream_t stream);
+int cmx_adamw_step_scaled(float* p, const float* g, float* m, float* v, void* shadow, int shadow_dtype, const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1, double beta2, float eps, double weight_decay, float grad_scale, const float* loss_scale, const float* found_inf, unsigned* tickets, hipStream_t stream);
 /* adamw_step_segment: the same update on one contiguous range of the flat buffers (p, g, m, v,
  *      shadow and decay64 offset by the caller; n a multiple of 64), e.g. one backward-completion
  *      segment updated on a side stream while the backward of the earlier stages runs.  Every launch
  *      reads the step count; only the one with store_step = 1 (the step's last) stores t + 1.
  *      max_blocks > 0 caps the grid (the launch then keeps to that share of the chip). */
-int cmx_adamw_step_segment(float* p, const float* g, float* m, float* v, void* shadow, int shadow_dtype, const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1, double beta2, float eps, double weight_decay, float grad_scale, int store_step, int max_blocks, hipStream_t stream);
+int cmx_adamw_step_segment(float* p, const float* g, float* m, float* v, void* shadow, int shadow_dtype, const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1, double beta2, float eps, double weight_decay, float grad_scale, int store_step, int max_blocks, unsigned* tickets, hipStream_t stream);
 /* grad_nonfinite: flags64 (nullable) = the per-64-element decay flags of adamw_step; blocks flagged 2
  *      (frozen slots, in no optimizer group) are not scanned, as GradScaler.unscale_ checks only the
  *      optimizer's parameters. */

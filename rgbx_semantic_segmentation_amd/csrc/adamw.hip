@@ -17,8 +17,9 @@
 // HBM-bound: 16 B read (p,g,m,v) + 12 B written (p,m,v) [+2 B shadow] per parameter.
 // The step count is read at every block's start as t_prev and used as t = t_prev + 1; the LAST
 // block to finish (arrival ticket) stores t, after every block has read t_prev -- the increment
-// needs no launch of its own.  One AdamW launch in flight per device at a time (the ticket is
-// a device global that the last block resets).
+// needs no launch of its own.  The tickets live in caller-owned memory (cmx_adamw_tickets()
+// zeroed uint32s per optimizer; the last block resets them), so launches of different optimizers may
+// overlap; NULL takes the library's device-global set (one such launch in flight per device).
 #include "cmx_common.h"
 
 // step-count tickets: a block takes a ticket of its group of ADAMW_GRP consecutive blocks; the
@@ -53,7 +54,7 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                              float* __restrict__ v, S* __restrict__ shadow, const uint8_t* __restrict__ decay64,
                              long n, const float* __restrict__ lr_ptr, float* __restrict__ step_ptr, double b1d,
                              double b2d, float eps, double wd, float gscale, const float* __restrict__ loss_scale,
-                             const float* __restrict__ found_inf, int store_step) {
+                             const float* __restrict__ found_inf, int store_step, unsigned* __restrict__ tickets) {
   // GradScaler semantics (train.py:185-198): a step whose gradients held inf / nan is skipped
   if (found_inf && *found_inf != 0.f) return;
   if (loss_scale) gscale /= *loss_scale;                       // unscale
@@ -109,12 +110,14 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
     // acquire / release here would write back and invalidate the L2 once per block)
     const unsigned grp = blockIdx.x / ADAMW_GRP, ngrp = (gridDim.x + ADAMW_GRP - 1) / ADAMW_GRP;
     const unsigned gsize = min((unsigned)ADAMW_GRP, gridDim.x - grp * ADAMW_GRP);
-    const unsigned pg = __hip_atomic_fetch_add(&g_adamw_grp_ticket[grp], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned* top = tickets ? tickets : &g_adamw_ticket;
+    unsigned* gt = (tickets ? tickets + 1 : g_adamw_grp_ticket) + grp;
+    const unsigned pg = __hip_atomic_fetch_add(gt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (pg == gsize - 1) {
-      __hip_atomic_store(&g_adamw_grp_ticket[grp], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned prev = __hip_atomic_fetch_add(&g_adamw_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(gt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned prev = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (prev == ngrp - 1) {
-        __hip_atomic_store(&g_adamw_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *step_ptr = (float)t;
       }
     }
@@ -152,33 +155,35 @@ __global__ void loss_scale_update_kernel(float* scale, int* tracker, float* foun
 static int adamw_launch(float* p, const float* g, float* m, float* v, void* shadow, int shadow_dtype,
                         const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1,
                         double beta2, float eps, double weight_decay, float grad_scale, const float* loss_scale,
-                        const float* found_inf, int store_step, int max_blocks, hipStream_t s);
+                        const float* found_inf, int store_step, int max_blocks, unsigned* tickets, hipStream_t s);
 
 extern "C" {
 
 // n must be a multiple of 64; the step count at step_ptr is incremented by this call and the
 // incremented value used (torch order); a step skipped for found_inf leaves it unchanged
+size_t cmx_adamw_tickets(void) { return 1 + ADAMW_NGRP; }
+
 int cmx_adamw_step(float* p, const float* g, float* m, float* v, void* shadow, int shadow_dtype, const uint8_t* decay64,
                    int64_t n, const float* lr_ptr, float* step_ptr, double beta1, double beta2, float eps,
-                   double weight_decay, float grad_scale, hipStream_t s) {
+                   double weight_decay, float grad_scale, unsigned* tickets, hipStream_t s) {
   return cmx_adamw_step_scaled(p, g, m, v, shadow, shadow_dtype, decay64, n, lr_ptr, step_ptr, beta1, beta2, eps,
-                               weight_decay, grad_scale, nullptr, nullptr, s);
+                               weight_decay, grad_scale, nullptr, nullptr, tickets, s);
 }
 
 int cmx_adamw_step_scaled(float* p, const float* g, float* m, float* v, void* shadow, int shadow_dtype,
                           const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1,
                           double beta2, float eps, double weight_decay, float grad_scale, const float* loss_scale,
-                          const float* found_inf, hipStream_t s) {
+                          const float* found_inf, unsigned* tickets, hipStream_t s) {
   return adamw_launch(p, g, m, v, shadow, shadow_dtype, decay64, n, lr_ptr, step_ptr, beta1, beta2, eps, weight_decay,
-                      grad_scale, loss_scale, found_inf, 1, 0, s);
+                      grad_scale, loss_scale, found_inf, 1, 0, tickets, s);
 }
 
 int cmx_adamw_step_segment(float* p, const float* g, float* m, float* v, void* shadow, int shadow_dtype,
                            const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1,
                            double beta2, float eps, double weight_decay, float grad_scale, int store_step,
-                           int max_blocks, hipStream_t s) {
+                           int max_blocks, unsigned* tickets, hipStream_t s) {
   return adamw_launch(p, g, m, v, shadow, shadow_dtype, decay64, n, lr_ptr, step_ptr, beta1, beta2, eps, weight_decay,
-                      grad_scale, nullptr, nullptr, store_step, max_blocks, s);
+                      grad_scale, nullptr, nullptr, store_step, max_blocks, tickets, s);
 }
 
 }  // extern "C"
@@ -186,7 +191,7 @@ int cmx_adamw_step_segment(float* p, const float* g, float* m, float* v, void* s
 static int adamw_launch(float* p, const float* g, float* m, float* v, void* shadow, int shadow_dtype,
                         const uint8_t* decay64, int64_t n, const float* lr_ptr, float* step_ptr, double beta1,
                         double beta2, float eps, double weight_decay, float grad_scale, const float* loss_scale,
-                        const float* found_inf, int store_step, int max_blocks, hipStream_t s) {
+                        const float* found_inf, int store_step, int max_blocks, unsigned* tickets, hipStream_t s) {
   CMX_REQUIRE(n % 64 == 0, CMX_ERR_SHAPE, "adamw: n must be a multiple of 64");
   CMX_REQUIRE(!shadow || shadow_dtype == 1 || shadow_dtype == 2, CMX_ERR_DTYPE, "adamw: shadow dtype %d", shadow_dtype);
   // CMX_ADAMW_BLOCKS caps the grid (A/B knob; each block takes one relaxed ticket, so the
@@ -202,7 +207,7 @@ static int adamw_launch(float* p, const float* g, float* m, float* v, void* shad
 #define CMX_ADAMW(S_, NT_)                                                                                         \
   hipLaunchKernelGGL((adamw_kernel<S_, NT_>), dim3((unsigned)blocks), dim3(256), 0, s, p, g, m, v, (S_*)shadow, \
                      decay64, (long)n, lr_ptr, step_ptr, beta1, beta2, eps, weight_decay, grad_scale, loss_scale,    \
-                     found_inf, store_step)
+                     found_inf, store_step, tickets)
   if (shadow_dtype == 2) {
     if (nt) CMX_ADAMW(f16, true);
     else CMX_ADAMW(f16, false);

@@ -59,7 +59,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void pool_kernel(const T* __restrict__ x, float* __restrict__ psum,
                                                    float* __restrict__ pmax, int* __restrict__ pidx,
                                                    float* __restrict__ pooled, int* __restrict__ argmax, int B,
-                                                   int N, int C, int chunk) {
+                                                   int N, int C, int chunk, unsigned* __restrict__ tickets) {
   constexpr int V = VecT<T>::N, LPR = PG / V, RPB = 256 / LPR;
   __shared__ float rs[RPB][PG + 1], rm[RPB][PG + 1];
   __shared__ int ri[RPB][PG + 1];
@@ -95,7 +95,7 @@ __global__ __launch_bounds__(256) void pool_kernel(const T* __restrict__ x, floa
   group8_merge(s, m, mi);
   const long po = ((long)(gb * ng + cg) * nz + z) * PG + c;
   if (k == 0) { st_agent(psum + po, s); st_agent(pmax + po, m); st_agent(pidx + po, mi); }
-  if (!last_arrival(&g_pool_ticket[gb * ng + cg], nz)) return;
+  if (!last_arrival((tickets ? tickets : g_pool_ticket) + gb * ng + cg, nz)) return;
   // fold: channel c, chunks z = k, k + 8, k + 16, k + 24 (all loads issued before the merge)
   const long pb = (long)(gb * ng + cg) * nz * PG + c;
   float ls[PZ_MAX / 8], lm[PZ_MAX / 8];
@@ -573,8 +573,10 @@ size_t cmx_frm_pool_workspace(int B, int N, int C) {
   return (size_t)2 * B * nz * (C > 0 ? C : 0) * 3 * sizeof(float);
 }
 
-int cmx_frm_pool_fwd(const void* x, float* pooled, int* argmax, float* workspace, int B, int N, int C, int dtype,
-                     hipStream_t s) {
+size_t cmx_frm_pool_tickets(int B, int C) { return (size_t)2 * B * (C / PG); }
+
+int cmx_frm_pool_fwd(const void* x, float* pooled, int* argmax, float* workspace, unsigned* tickets, int B, int N, int C,
+                     int dtype, hipStream_t s) {
   CMX_REQUIRE(B > 0 && N > 0 && C > 0 && C % PG == 0 && 2L * B * (C / PG) <= POOL_TICKETS, CMX_ERR_SHAPE,
               "frm_pool: B=%d N=%d C=%d (C %% %d == 0)", B, N, C, PG);
   const int nz = pool_nchunk(N, 2 * B, C);
@@ -584,7 +586,7 @@ int cmx_frm_pool_fwd(const void* x, float* pooled, int* argmax, float* workspace
   int* pidx = (int*)(pmax + (size_t)2 * B * nz * C);
   CMX_DISPATCH(dtype, T, {
     hipLaunchKernelGGL(pool_kernel<T>, dim3(nz, C / PG, 2 * B), dim3(256), 0, s, (const T*)x, psum, pmax, pidx,
-                       pooled, argmax, B, N, C, chunk);
+                       pooled, argmax, B, N, C, chunk, tickets);
   });
   return cmx_check_launch("frm_pool_fwd");
 }

@@ -581,7 +581,8 @@ class IFRMF(Function):
         pooled = torch.empty(B, 4 * C, **f32)
         argmax = torch.empty(B, 2 * C, dtype=torch.int32, device=x.device)
         ws = K._ws(K.query("cmx_frm_pool_workspace", B, N, C), x.device)
-        K.call("cmx_frm_pool_fwd", K.ptr(x), K.ptr(pooled), K.ptr(argmax), K.ptr(ws), B, N, C, dt, K.stream())
+        K.call("cmx_frm_pool_fwd", K.ptr(x), K.ptr(pooled), K.ptr(argmax), K.ptr(ws), K.ptr(pool_tickets(anchor, x, B, C)), B, N, C, dt,
+               K.stream())
         h1 = torch.empty(B, 4 * C, **f32)
         K.call("cmx_small_linear_fwd", K.ptr(pooled), K.ptr(W1), K.ptr(b1), K.ptr(h1), B, 4 * C, 4 * C, 0, K.stream())
         n1, m1, r1 = _rowln(h1, g1, e1, eps1)
@@ -1228,6 +1229,22 @@ def pair_embed(store, ce, o):
 
 
 # ---------------------------------------------------------------------------- FRM
+_POOL_TK: dict = {}
+
+
+def pool_tickets(owner, x, B, C):
+    """Zeroed arrival counters of one ChannelWeights pooling call site (cmx_frm_pool_tickets; each
+    launch leaves them zero): one set per (module -- ``owner`` is its anchor Parameter -- device,
+    size), so poolings that may run
+    concurrently (two models, two streams) never share counters.  Allocated at the first, eager
+    call (the step runs eagerly before its HIP-graph capture)."""
+    key = (id(owner), x.device, B, C)
+    t = _POOL_TK.get(key)
+    if t is None:
+        t = _POOL_TK[key] = torch.zeros(K.query("cmx_frm_pool_tickets", B, C), dtype=torch.int32, device=x.device)
+    return t
+
+
 class FRMF(Function):
     """FeatureRectifyModule (net_utils.py:124-152) on x (2, B, N, C).
 
@@ -1254,7 +1271,8 @@ class FRMF(Function):
         cw = torch.empty(B, 2 * C, dtype=torch.float32, device=x.device)
         # ChannelWeights (net_utils.py:11-30): avg || max pool + both MLP GEMVs
         ws = K._ws(K.query("cmx_frm_pool_workspace", B, N, C), x.device)
-        K.call("cmx_frm_pool_fwd", K.ptr(x), K.ptr(pooled), K.ptr(argmax), K.ptr(ws), B, N, C, dt, K.stream())
+        K.call("cmx_frm_pool_fwd", K.ptr(x), K.ptr(pooled), K.ptr(argmax), K.ptr(ws), K.ptr(pool_tickets(anchor, x, B, C)), B, N, C, dt,
+               K.stream())
         K.call("cmx_small_linear_fwd", K.ptr(pooled), K.ptr(W1), K.ptr(b1), K.ptr(y1), B, 4 * C, 4 * C, 2, K.stream())
         K.call("cmx_small_linear_fwd", K.ptr(y1), K.ptr(W2), K.ptr(b2), K.ptr(cw), B, 4 * C, 2 * C, 3, K.stream())
         # h = cat(x1, x2) W0^T + b0 (SpatialWeights' first 1x1 conv, net_utils.py:72-73), cat-free

@@ -22,7 +22,7 @@ from typing import Optional
 import torch
 
 from . import _lib
-from ._lib import call, ptr, stream
+from ._lib import call, ptr, query, stream
 
 # set by GradScaler.scale() while a loss-scaled backward is pending: its updates must wait for
 # the whole-gradient inf / nan check, so the per-segment overlap stands aside
@@ -123,6 +123,8 @@ class FusedAdamW:
         self.exp_avg_sq = torch.zeros_like(store.flat)
         self.lr_t = torch.full((1,), float(lr), dtype=torch.float32, device=dev)
         self.step_t = torch.zeros(1, dtype=torch.float32, device=dev)
+        # this optimizer's own step-count arrival counters (zero; every launch leaves them zero)
+        self.tickets = torch.zeros(query("cmx_adamw_tickets"), dtype=torch.int32, device=dev)
         self.grad_sync = grad_sync          # callable(flat_grad) -> grad scale, or None
         names = list(store.params.keys())
         decay = [store.params[n] for n in names if store.slots[n].decay]
@@ -168,7 +170,7 @@ class FusedAdamW:
         call("cmx_adamw_step_segment", ptr(s.flat) + f4 * a, ptr(s.grad) + f4 * a, ptr(self.exp_avg) + f4 * a,
              ptr(self.exp_avg_sq) + f4 * a, sh, s.shadow_code, ptr(s.decay64) + a // 64, b - a, ptr(self.lr_t),
              ptr(self.step_t), self.betas[0], self.betas[1], self.eps, self.weight_decay, float(gscale),
-             int(store_step), int(max_blocks), stream())
+             int(store_step), int(max_blocks), ptr(self.tickets), stream())
 
     @torch.no_grad()
     def step(self, closure=None, scaler: "GradScaler | None" = None):
@@ -190,11 +192,11 @@ class FusedAdamW:
             call("cmx_adamw_step_scaled", ptr(s.flat), ptr(s.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq),
                  ptr(s.shadow), s.shadow_code, ptr(s.decay64), s.numel, ptr(self.lr_t), ptr(self.step_t), self.betas[0],
                  self.betas[1], self.eps, self.weight_decay, gscale, ptr(scaler.scale_t), ptr(scaler.found_inf),
-                 stream())
+                 ptr(self.tickets), stream())
             return None
         call("cmx_adamw_step", ptr(s.flat), ptr(s.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq), ptr(s.shadow),
              s.shadow_code, ptr(s.decay64), s.numel, ptr(self.lr_t), ptr(self.step_t), self.betas[0], self.betas[1], self.eps,
-             self.weight_decay, gscale, stream())
+             self.weight_decay, gscale, ptr(self.tickets), stream())
         return None
 
     # ------------------------------------------------------------------ checkpoint format

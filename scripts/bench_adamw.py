@@ -24,7 +24,7 @@ step = torch.zeros(1, device="cuda")
 
 def run():
     call("cmx_adamw_step", ptr(p), ptr(g), ptr(m), ptr(v), ptr(sh), 1, ptr(dec), n, ptr(lr), ptr(step), 0.9, 0.999,
-         1e-8, 0.01, 1.0, stream())
+         1e-8, 0.01, 1.0, 0, stream())
 
 
 for rep in range(2):

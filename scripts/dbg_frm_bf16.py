@@ -27,7 +27,7 @@ for cdt in (torch.float32, torch.bfloat16):
     st = {}
     pooled = torch.empty(B, 4 * C, device="cuda"); argmax = torch.empty(B, 2 * C, dtype=torch.int32, device="cuda")
     ws = K._ws(K.query("cmx_frm_pool_workspace", B, N, C), "cuda")
-    K.call("cmx_frm_pool_fwd", K.ptr(r), K.ptr(pooled), K.ptr(argmax), K.ptr(ws), B, N, C, dt, K.stream())
+    K.call("cmx_frm_pool_fwd", K.ptr(r), K.ptr(pooled), K.ptr(argmax), K.ptr(ws), 0, B, N, C, dt, K.stream())
     y1 = torch.empty(B, 4 * C, device="cuda")
     K.call("cmx_small_linear_fwd", K.ptr(pooled), K.ptr(W1), K.ptr(b1), K.ptr(y1), B, 4 * C, 4 * C, 2, K.stream())
     cw = torch.empty(B, 2 * C, device="cuda")

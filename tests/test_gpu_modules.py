@@ -178,10 +178,13 @@ def test_frm_pool_one_launch(dev, C, B, N, dtype):
     pooled = torch.empty(B, 4 * C, **f32)
     argmax = torch.empty(B, 2 * C, dtype=torch.int32, device=dev)
     ws = K._ws(K.query("cmx_frm_pool_workspace", B, N, C), dev)
+    tk = torch.zeros(K.query("cmx_frm_pool_tickets", B, C), dtype=torch.int32, device=dev)
 
     def run():
-        K.call("cmx_frm_pool_fwd", K.ptr(x), K.ptr(pooled), K.ptr(argmax), K.ptr(ws), B, N, C, K.dtype_code(x),
-               K.stream())
+        # caller-owned arrival counters (odd runs) and the library's device-global set (even runs)
+        run.n = getattr(run, "n", 0) + 1
+        K.call("cmx_frm_pool_fwd", K.ptr(x), K.ptr(pooled), K.ptr(argmax), K.ptr(ws), K.ptr(tk) if run.n % 2 else 0,
+               B, N, C, K.dtype_code(x), K.stream())
 
     run()
     torch.cuda.synchronize()
@@ -191,6 +194,7 @@ def test_frm_pool_one_launch(dev, C, B, N, dtype):
     assert rel(pooled[:, :2 * C], avg, 1e-8) < 1e-6
     assert torch.equal(pooled[:, 2 * C:], mx)
     assert torch.equal(argmax, first)
+    assert int(tk.abs().sum().item()) == 0                                # the last arriver reset them
     eager = (pooled.clone(), argmax.clone())
     st = torch.cuda.Stream()
     st.wait_stream(torch.cuda.current_stream())
