@@ -269,6 +269,10 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
   if (fast) {
     int bm, bn;
     plan_tiles(G, M, nb, K, &bm, &bn);
+    // the upsample-add epilogue (decoder fuse): CMX_GEMM_UP_TILE = 64 takes 64 x 64 tiles (more
+    // resident workgroups to overlap the epilogue's gathered bilinear loads), 0 = the usual policy
+    static int& up_tile = cmx_knob("GEMM_UP_TILE", 0);
+    if (a.nup && up_tile == 64) bm = bn = 64;
     if (row_ln || lnb) bm = 64, bn = N <= 64 ? 64 : 128;   // one tile spans the row
     if (lnb && a.scatter) bn = scC;                         // (one tap's C channels)
     a.tiles_m = cdiv(M, bm); a.tiles_n = cdiv(nb, bn);
