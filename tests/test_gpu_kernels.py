@@ -88,7 +88,10 @@ def sra_ref(q, kv, heads, D):
                                               # ragged query / key tiles, one-wave and five-wave key
                                               # splits, the N threshold; N = 4800 stays on the fast path
                                               (3, 333, 70, 2, 64), (2, 129, 257, 3, 64), (1, 2048, 320, 1, 64),
-                                              (2, 4800, 300, 2, 64), (1, 37, 33, 1, 64)])
+                                              (2, 4800, 300, 2, 64), (1, 37, 33, 1, 64),
+                                              # stage 1 (one 320-key tile, 64 query chunks) and a
+                                              # ragged query / key count past the short-sequence N
+                                              (1, 19200, 300, 1, 64), (2, 2101, 289, 3, 64)])
 def test_sra_attention(dev, dtype, Bt, N, Nk, heads, D, qmul=1.0):
     from rgbx_semantic_segmentation_amd import kernels as K
     torch.manual_seed(1)
