@@ -39,13 +39,20 @@ print(f"launches/step {len(seg)}  wall {(max(r[1] for r in seg) - seg[0][0]) / 1
 prev = max(rows[:idx[pick]], key=lambda r: r[1])
 print(f"boundary gap {(seg[0][0] - prev[1]) / 1e3:.1f} us after {kname(prev[2])[:40]}; first kernels: "
       + ", ".join(kname(r[2])[:30] for r in seg[:3]))
-gaps, end = [], seg[0][1]
-for s_, e_, n_ in seg[1:]:
+gaps, end, last = [], seg[0][1], seg[0]
+for r in seg[1:]:
+    s_, e_, n_ = r
     if s_ > end:
-        gaps.append(((s_ - end) / 1e3, kname(n_)[:60]))
-    end = max(end, e_)
-print(f"idle inside the step {sum(g for g, _ in gaps):.0f} us over {len(gaps)} gaps; largest: "
-      + "; ".join(f"{g:.1f} us before {n}" for g, n in sorted(gaps, reverse=True)[:6]))
+        gaps.append(((s_ - end) / 1e3, kname(n_)[:60], (end - seg[0][0]) / 1e3, kname(last[2])[:60]))
+    if e_ > end:
+        end, last = e_, r
+print(f"idle inside the step {sum(g[0] for g in gaps):.0f} us over {len(gaps)} gaps; largest: "
+      + "; ".join(f"{g:.1f} us before {n}" for g, n, _, _ in sorted(gaps, reverse=True)[:6]))
+# every gap over 20 us with the kernel that ended last before it and where it sits in the step
+for g, n, at, prev_ in sorted(gaps, reverse=True):
+    if g <= 20:
+        break
+    print(f"  gap {g:.1f} us at {at:.0f} us into the step: after {prev_} -> before {n}")
 cat = collections.defaultdict(lambda: [0, 0.0])
 for s, e, n in seg:
     k = kname(n)
