@@ -48,11 +48,16 @@ for r in seg[1:]:
         end, last = e_, r
 print(f"idle inside the step {sum(g[0] for g in gaps):.0f} us over {len(gaps)} gaps; largest: "
       + "; ".join(f"{g:.1f} us before {n}" for g, n, _, _ in sorted(gaps, reverse=True)[:6]))
-# every gap over 20 us with the kernel that ended last before it and where it sits in the step
+# every gap over 20 us with the kernel that ended last before it, where it sits in the step, and
+# the launches around it in start order (which stream feeds which is not in the trace)
 for g, n, at, prev_ in sorted(gaps, reverse=True):
     if g <= 20:
         break
     print(f"  gap {g:.1f} us at {at:.0f} us into the step: after {prev_} -> before {n}")
+    t0 = seg[0][0] + at * 1e3
+    near = [r for r in seg if t0 - 60e3 <= r[1] <= t0 + g * 1e3 + 30e3 or t0 - 60e3 <= r[0] <= t0 + g * 1e3 + 30e3]
+    for r in near[:14]:
+        print(f"      {(r[0] - seg[0][0]) / 1e3:8.1f} .. {(r[1] - seg[0][0]) / 1e3:8.1f}  {kname(r[2])[:70]}")
 cat = collections.defaultdict(lambda: [0, 0.0])
 for s, e, n in seg:
     k = kname(n)
