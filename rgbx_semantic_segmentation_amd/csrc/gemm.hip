@@ -276,7 +276,18 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
     if (row_ln || lnb) bm = 64, bn = N <= 64 ? 64 : 128;   // one tile spans the row
     if (lnb && a.scatter) bn = scC;                         // (one tap's C channels)
     a.tiles_m = cdiv(M, bm); a.tiles_n = cdiv(nb, bn);
-    launch_fast(a, bm, bn, G, splitk, transA, transB, dtype, s);
+    // tall 64 x 64 problems of at least CMX_GEMM_STREAM tiles (0 = off) and K <= CMX_GEMM_STREAM_K:
+    // the resident streaming grid (gemm_stream_kernel) instead of one block per tile
+    static int& stream_min = cmx_knob("GEMM_STREAM", 1024);
+    static int& stream_k = cmx_knob("GEMM_STREAM_K", 128);
+    const long tiles = (long)a.tiles_m * a.tiles_n * G;
+    if (stream_min > 0 && tiles >= stream_min && K <= stream_k && bm == 64 && bn == 64 && splitk == 1 && !transA && !A2 &&
+        !ones_col && !a.nup && !a.scatter && gh == 1 && !lnb && (!tail || (row_ln && N <= 64))) {
+      if (dtype == 2) launch_stream<f16>(a, G, transB, s);
+      else launch_stream<bf16>(a, G, transB, s);
+    } else {
+      launch_fast(a, bm, bn, G, splitk, transA, transB, dtype, s);
+    }
   } else {
     // tile shape: the output's narrow side gets 64 (stage-1 C = 64 outputs, 64-row wgrads)
     const bool m64 = M <= 64, n64 = N <= 64;

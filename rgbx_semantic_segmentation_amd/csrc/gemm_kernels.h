@@ -826,6 +826,117 @@ void gemm_bf16_kernel(const GemmArgs p) {
   if constexpr (TAIL == 1) gemm_ln_tail<E>(p, lin);
 }
 
+// ============================================================================ streaming launch
+// Tall products on 64 x 64 tiles (tens of thousands of rows, a few k-steps: the stage-1/2
+// Linears and their input gradients, G = 2 modalities).  The one-tile block above is a latency
+// chain -- DMA, MFMA, epilogue store, retire -- and the chip runs ~2-4 rounds of them.  Here a
+// resident grid (5 blocks per CU) walks the tiles, and each block's 2-slot LDS ring runs ACROSS
+// tile boundaries: the next tile's first k-step is in flight while this tile's epilogue stores.
+// Tiles are dealt to XCDs in contiguous ranges (block b sits on XCD b % 8), so the column tiles
+// of one row panel share that XCD's L2.  The epilogue's fp32 image takes the slot just consumed
+// (64 x 64 floats, 16-B chunks XOR-swizzled by row instead of padded: it fits one 16 KB stage).
+// Epilogues: the plain one (bias / act / residual / mask / fp32 out) and the row LayerNorm
+// (EPI = 2, N <= 64).  No split-K, transA, A2, implicit conv, bias column, upsample or scatter.
+constexpr int STREAM_SLOT = 64 * FBK * 2 * 2;   // one stage: A + B images, 64 x 64 each (16 KB)
+template <bool TB, typename E, int EPI>
+__global__ __launch_bounds__(256, 4) void gemm_stream_kernel(const GemmArgs p) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STREAM_SLOT];
+  constexpr int A_BYTES = 64 * FBK * 2;
+  const int ntile = p.tiles_m * p.tiles_n, total = ntile * p.G;
+  const int nk = (p.K + FBK - 1) / FBK;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
+  const int nreal = p.N;
+  // XCD x = blockIdx.x % 8 takes tiles [lo, hi) round-robin over its nbx blocks
+  const int nbx = gridDim.x >> 3, xb = blockIdx.x & 7, bi = blockIdx.x >> 3;
+  const int per = (total + 7) >> 3, lo = xb * per, hi = min(total, lo + per);
+  const int first = lo + bi;
+  const int nq = first < hi ? (hi - first + nbx - 1) / nbx : 0;
+  const int S = nq * nk;
+  if (S == 0) return;
+  auto tile_of = [&](int q, int& g, int& tm, int& tn) {
+    const int lin = first + q * nbx;
+    const int t = lin % ntile;
+    g = lin / ntile;
+    tm = t / p.tiles_n;
+    tn = t - tm * p.tiles_n;
+  };
+  auto stage = [&](int st, char* buf) {
+    const int q = st / nk, kt = st - q * nk;
+    int g, tm, tn;
+    tile_of(q, g, tm, tn);
+    const i32x4 rA = make_rsrc(reinterpret_cast<const E*>(p.A) + goff(p, g, p.sA, p.sAh));
+    const i32x4 rB = make_rsrc(reinterpret_cast<const E*>(p.B) + goff(p, g, p.sB, p.sBh));
+    const int k0 = kt * FBK;
+    stage_k<64>(rA, buf, p.lda, tm * 64, p.M, k0, p.K, w, lane);
+    if constexpr (TB) stage_r<64>(rB, buf + A_BYTES, p.ldb, tn * 64, nreal, k0, p.K, w, lane);
+    else stage_k<64>(rB, buf + A_BYTES, p.ldb, tn * 64, nreal, k0, p.K, w, lane);
+  };
+  f32x16 acc = zero16();
+  auto compute = [&](const char* buf) {
+    const char* ai = buf;
+    const char* bi_ = buf + A_BYTES;
+#pragma unroll
+    for (int s = 0; s < FBK / 16; ++s) {
+      const frag8<E> fa = frag_k<E>(ai, wm * 32, s, lane);
+      frag8<E> fb;
+      if constexpr (TB) fb = frag_r<E, 64>(bi_, wn * 32, s, lane);
+      else fb = frag_k<E>(bi_, wn * 32, s, lane);
+      acc = MF<E>::mma(fb, fa, acc);
+    }
+  };
+  // image element (row il, column jl): 16-B chunk jl / 4 of the row at position chunk ^ (il & 15)
+  auto img = [](float* cs, int il, int c4) { return cs + il * 64 + ((c4 ^ (il & 15)) << 2); };
+  auto epilogue = [&](int q, float* cs) {
+    int g, tm, tn;
+    tile_of(q, g, tm, tn);
+    const int i0 = tm * 64, j0 = tn * 64;
+    const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int il = wm * 32 + r, c4 = wn * 8 + 2 * g4 + h;
+      *reinterpret_cast<float4*>(img(cs, il, c4)) =
+          make_float4(acc[4 * g4], acc[4 * g4 + 1], acc[4 * g4 + 2], acc[4 * g4 + 3]);
+    }
+    __syncthreads();
+    constexpr int TPR = 8, RPP = 256 / TPR;
+    const int jl = (threadIdx.x % TPR) * 8, j = j0 + jl;
+    const bool live = j < nreal;
+    const int nv = min(8, nreal - j);
+#pragma unroll
+    for (int pass = 0; pass < 64 / RPP; ++pass) {
+      const int il = pass * RPP + threadIdx.x / TPR;
+      const int i = i0 + il;
+      if (i >= p.M) break;
+      const float4 u0 = *reinterpret_cast<const float4*>(img(cs, il, jl / 4));
+      const float4 u1 = *reinterpret_cast<const float4*>(img(cs, il, jl / 4 + 1));
+      float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+      if constexpr (EPI == 2) {
+        if (live) epi_store8<E>(p, g, i, j, 8, v);
+        row_layernorm<E, TPR>(p, g, i, j, jl, live, v);
+      } else {
+        if (live) epi_store8<E>(p, g, i, j, nv, v);
+      }
+    }
+  };
+  stage(0, smem);
+  vm_wait<0>();
+  __syncthreads();
+  int cur = 0;
+  for (int st = 0; st < S; ++st) {
+    if (st + 1 < S) stage(st + 1, smem + (cur ^ 1) * STREAM_SLOT);
+    compute(smem + cur * STREAM_SLOT);
+    const int q = st / nk;
+    if (st - q * nk == nk - 1) {
+      __syncthreads();                          // every wave has read its last fragments of slot cur
+      epilogue(q, reinterpret_cast<float*>(smem + cur * STREAM_SLOT));
+      acc = zero16();
+    }
+    vm_wait<0>();                               // the next stage has landed (and this tile's stores)
+    __syncthreads();                            // ... and slot cur is free for the stage after it
+    cur ^= 1;
+  }
+}
+
 // ============================================================================ multi launch
 // Up to four independent forward / dgrad problems (64 x 64 tiles, no split-K, same B layout) in
 // ONE grid, records passed by value: e.g. Attention.q beside Attention.kv (dual_segformer.py:
@@ -1236,6 +1347,22 @@ inline int cu_count() {
     return c > 0 ? c : 256;
   }();
   return n;
+}
+
+template <typename E>
+void launch_stream(const GemmArgs& a, int G, int tB, hipStream_t s) {
+  const long total = (long)a.tiles_m * a.tiles_n * G;
+  static int& bpc = cmx_knob("GEMM_STREAM_BPC", 4);      // resident blocks per CU (<= 4: VGPR-bound)
+  long grid = (long)(bpc > 0 && bpc <= 4 ? bpc : 4) * cu_count();
+  if (grid > total) grid = total;
+  grid = (grid + 7) / 8 * 8;
+  if (a.tail == 2) {
+    hipLaunchKernelGGL((gemm_stream_kernel<false, E, 2>), dim3((unsigned)grid), dim3(256), 0, s, a);
+  } else if (tB) {
+    hipLaunchKernelGGL((gemm_stream_kernel<true, E, 0>), dim3((unsigned)grid), dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((gemm_stream_kernel<false, E, 0>), dim3((unsigned)grid), dim3(256), 0, s, a);
+  }
 }
 
 template <typename T, int BM, int BN, bool EXT>

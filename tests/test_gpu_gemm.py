@@ -354,7 +354,9 @@ def test_gemm_h2_per_head(dev, dtype, GB, heads, N, D):
 @pytest.mark.parametrize("G,M,N,K,res", [(2, 38400, 64, 256, True), (2, 9600, 128, 512, True), (2, 2400, 320, 1280, True),
                                          (2, 600, 512, 2048, True), (2, 2400, 320, 320, False), (1, 130, 128, 64, True),
                                          (2, 600, 512, 512, True), (2, 4800, 32, 128, True), (2, 1000, 64, 64, True),
-                                         (1, 77, 128, 128, False), (2, 2400, 128, 128, True)])
+                                         (1, 77, 128, 128, False), (2, 2400, 128, 128, True),
+                                         # stage-1 proj -> norm2 (1200 tiles, K = 64): the streaming grid
+                                         (2, 38400, 64, 64, True)])
 def test_gemm_ln_tail(dev, dtype, G, M, N, K, res):
     """cmx_gemm_ln: the GEMM output is the plain launch's, bit for bit (the tail only changes the
     store's cache policy), and the row-block LayerNorm tail equals cmx_layernorm_fwd on that
@@ -486,3 +488,48 @@ def test_conv_patch_dgrad_ln_bwd(dev, dtype, G, NIg, H, W, C, R, N, dy2):
     ps = part.double().sum(1)
     assert torch.allclose(ps[:, :C], gg.double(), rtol=1e-4, atol=1e-3 * gg.abs().max().item())
     assert torch.allclose(ps[:, C:], bg.double(), rtol=1e-4, atol=1e-3 * bg.abs().max().item())
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("G,M,N,K,tB,epi", [(2, 38400, 64, 64, 0, "plain"), (2, 38400, 256, 64, 1, "plain"),
+                                            (2, 38400, 64, 256, 0, "res"), (2, 9600, 512, 128, 0, "gelu"),
+                                            (1, 99999, 72, 200, 1, "res"), (2, 38400, 64, 64, 0, "fp32"),
+                                            (2, 38400, 256, 64, 0, "mask")])
+def test_gemm_stream(dev, dt, G, M, N, K, tB, epi):
+    """Tall 64 x 64 problems of >= CMX_GEMM_STREAM tiles run on the resident streaming grid
+    (gemm_stream_kernel: the LDS ring crosses tile boundaries).  Each tile's k-loop and epilogue
+    are the one-tile kernel's, so the result is bit-identical to the one-tile launch of the same
+    problem (the knob switched off for one call); ragged M / N / K, every epilogue kind."""
+    from rgbx_semantic_segmentation_amd import kernels as Kn
+    torch.manual_seed(9)
+    A = torch.randn(G, M, K, device="cuda").to(dt)
+    B = (torch.randn(G, N, K, device="cuda") / math.sqrt(K)).to(dt)
+    Bv = B.transpose(1, 2).contiguous().transpose(1, 2) if tB else B
+    kw = {}
+    if epi == "gelu":
+        kw = dict(bias=torch.randn(G, N, device="cuda"), act="gelu")
+    if epi in ("res", "mask"):
+        kw = dict(bias=torch.randn(G, N, device="cuda"), residual=torch.randn(G, M, N, device="cuda").to(dt),
+                  rscale=torch.rand(G * M, device="cuda") + 0.5, rows_per_sample=1)   # one scale per row
+    if epi == "mask":
+        kw["mask"] = (torch.randn(G, M, N, device="cuda") > 0).to(dt)
+    out_dt = torch.float32 if epi == "fp32" else dt
+    om = 1 if epi == "fp32" else 0
+    C = torch.empty(G, M, N, device="cuda", dtype=out_dt)
+    C0 = torch.empty_like(C)
+    Kn.gemm(A[:, :64], Bv, C[:, :64], out_mode=om)          # (registers the knob)
+    base, base_k = Kn.tune_get("GEMM_STREAM"), Kn.tune_get("GEMM_STREAM_K")
+    try:
+        Kn.tune("GEMM_STREAM", 256)                          # every shape here on the streaming grid
+        Kn.tune("GEMM_STREAM_K", 4096)
+        Kn.gemm(A, Bv, C, out_mode=om, **kw)
+        Kn.tune("GEMM_STREAM", 0)                            # ... and on one block per tile
+        Kn.gemm(A, Bv, C0, out_mode=om, **kw)
+    finally:
+        Kn.tune("GEMM_STREAM", base)
+        Kn.tune("GEMM_STREAM_K", base_k)
+    torch.cuda.synchronize()
+    assert torch.equal(C, C0)
+    ref = torch.bmm(A.float(), B.float().transpose(1, 2))
+    if epi == "plain" or epi == "fp32":
+        assert rel(C, ref) < (1e-5 if epi == "fp32" else 1e-2)
