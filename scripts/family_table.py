@@ -40,7 +40,7 @@ def work():
     sys.path.insert(0, __file__.rsplit("/scripts/", 1)[0])
     from rgbx_semantic_segmentation_amd.floor import step_work
     w = step_work(backbone="mit_b2", H=H, W=W, B=B, K=K, E=E, n_params=66.58e6)
-    names = {"gemm": "GEMM fwd+dgrad (tile / k-group / multi / split-K)", "wgrad": "grouped wgrad GEMM + grouped reduce",
+    names = {"gemm": "GEMM fwd+dgrad (tile / streaming / k-group / multi / split-K)", "wgrad": "grouped wgrad GEMM + grouped reduce",
              "sra": "SRA attention (fwd, dQ, dK/dV, reduce)", "dwconv": "DWConv 3x3 + GELU (fwd_save, bwd_saved)",
              "layernorm": "LayerNorm (fwd, bwd)", "adamw": "AdamW", "batchnorm": "BatchNorm (stats, fold, apply, bwd)",
              "frm": "FRM (pool, channel MLP, combine)", "ffm": "FFM context / cross attention",
@@ -52,7 +52,7 @@ def work():
 FAMILIES = [
     ("grouped wgrad GEMM + grouped reduce", r"gemm_grouped_kernel|reduce_grouped_kernel"),
     ("Mix-FFN bands", r"mixffn_"),
-    ("GEMM fwd+dgrad (tile / k-group / multi / split-K)", r"gemm_bf16_kernel|gemm_multi|gemm_generic|splitk_reduce"),
+    ("GEMM fwd+dgrad (tile / streaming / k-group / multi / split-K)", r"gemm_bf16_kernel|gemm_stream|gemm_multi|gemm_generic|splitk_reduce"),
     ("SRA attention (fwd, dQ, dK/dV, reduce)", r"sra_"),
     ("DWConv 3x3 + GELU (fwd_save, bwd_saved)", r"dw2_|dw_"),
     ("LayerNorm (fwd, bwd)", r"ln_fwd|ln_bwd|rowln"),
