@@ -116,7 +116,8 @@ def measure_gemm_family(model, batch, workload: str, shape: dict, warm: int = 4,
     t = sum(per)
     flops, nbytes = step_work(**shape)["gemm"]
     n = len(per)
-    traffic, src = _family_traffic(("gemm_bf16_kernel", "gemm_multi_kernel", "splitk_reduce_kernel"), workload)
+    traffic, src = _family_traffic(("gemm_bf16_kernel", "gemm_stream_kernel", "gemm_multi_kernel", "splitk_reduce_kernel"),
+                                  workload)
     gbs, tflops = nbytes / t / 1e9, flops / t / 1e12
     hbm = flops / nbytes < RIDGE_FLOP_PER_BYTE
     out = {"kernel": f"tile-GEMM family: gemm_bf16_kernel / gemm_multi_kernel / splitk_reduce_kernel ({n} forward and "

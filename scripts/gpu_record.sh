@@ -27,7 +27,7 @@ bash scripts/pmc_pass.sh $TAG "CMX-B2 train step 480x640 bs=2 K=40" gemm_grouped
 cp gpurun_out/pmc_$TAG.json gpurun_out/profiles/${TAG}_pmc_gemm_grouped.json
 rm -rf gpurun_out/pmc_${TAG}_FETCH_SIZE gpurun_out/pmc_${TAG}_WRITE_SIZE
 # the tile-GEMM family (the bench line's roofline kernel): PMC bytes per launch
-bash scripts/pmc_pass.sh ${TAG}f "CMX-B2 train step 480x640 bs=2 K=40" "gemm_bf16_kernel|gemm_multi_kernel|splitk_reduce_kernel" > gpurun_out/pmc_${TAG}f.out 2>&1 || exit $?
+bash scripts/pmc_pass.sh ${TAG}f "CMX-B2 train step 480x640 bs=2 K=40" "gemm_bf16_kernel|gemm_stream_kernel|gemm_multi_kernel|splitk_reduce_kernel" > gpurun_out/pmc_${TAG}f.out 2>&1 || exit $?
 cp gpurun_out/pmc_${TAG}f.json gpurun_out/profiles/${TAG}_pmc_gemm_family.json
 rm -rf gpurun_out/pmc_${TAG}f_FETCH_SIZE gpurun_out/pmc_${TAG}f_WRITE_SIZE
 if [ -z "$SKIP_SUITE" ]; then
