@@ -838,8 +838,11 @@ void gemm_bf16_kernel(const GemmArgs p) {
 // Epilogues: the plain one (bias / act / residual / mask / fp32 out) and the row LayerNorm
 // (EPI = 2, N <= 64).  No split-K, transA, A2, implicit conv, bias column, upsample or scatter.
 constexpr int STREAM_SLOT = 64 * FBK * 2 * 2;   // one stage: A + B images, 64 x 64 each (16 KB)
+#ifndef CMX_STREAM_LB
+#define CMX_STREAM_LB 4                          // resident blocks per CU the registers are sized for
+#endif
 template <bool TB, typename E, int EPI>
-__global__ __launch_bounds__(256, 4) void gemm_stream_kernel(const GemmArgs p) {
+__global__ __launch_bounds__(256, CMX_STREAM_LB) void gemm_stream_kernel(const GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * STREAM_SLOT];
   constexpr int A_BYTES = 64 * FBK * 2;
   const int ntile = p.tiles_m * p.tiles_n, total = ntile * p.G;
@@ -1352,8 +1355,8 @@ inline int cu_count() {
 template <typename E>
 void launch_stream(const GemmArgs& a, int G, int tB, hipStream_t s) {
   const long total = (long)a.tiles_m * a.tiles_n * G;
-  static int& bpc = cmx_knob("GEMM_STREAM_BPC", 4);      // resident blocks per CU (<= 4: VGPR-bound)
-  long grid = (long)(bpc > 0 && bpc <= 4 ? bpc : 4) * cu_count();
+  static int& bpc = cmx_knob("GEMM_STREAM_BPC", CMX_STREAM_LB);   // resident blocks per CU (VGPR-bound)
+  long grid = (long)(bpc > 0 && bpc <= CMX_STREAM_LB ? bpc : CMX_STREAM_LB) * cu_count();
   if (grid > total) grid = total;
   grid = (grid + 7) / 8 * 8;
   if (a.tail == 2) {
