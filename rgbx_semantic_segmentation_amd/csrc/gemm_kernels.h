@@ -830,7 +830,7 @@ void gemm_bf16_kernel(const GemmArgs p) {
 // Tall products on 64 x 64 tiles (tens of thousands of rows, a few k-steps: the stage-1/2
 // Linears and their input gradients, G = 2 modalities).  The one-tile block above is a latency
 // chain -- DMA, MFMA, epilogue store, retire -- and the chip runs ~2-4 rounds of them.  Here a
-// resident grid (5 blocks per CU) walks the tiles, and each block's 2-slot LDS ring runs ACROSS
+// resident grid (CMX_STREAM_LB = 4 blocks per CU) walks the tiles, and each block's 2-slot LDS ring runs ACROSS
 // tile boundaries: the next tile's first k-step is in flight while this tile's epilogue stores.
 // Tiles are dealt to XCDs in contiguous ranges (block b sits on XCD b % 8), so the column tiles
 // of one row panel share that XCD's L2.  The epilogue's fp32 image takes the slot just consumed
