@@ -839,6 +839,103 @@ __global__ __launch_bounds__(64 * SKT) void sra_dq_small(const E* __restrict__ q
   }
 }
 
+// The same dQ with the two 32-query halves of a wave taken one after the other (their Q / dO
+// fragments loaded per half) and the K and V fragments of a sub-tile live one at a time: under
+// 168 VGPRs, so two 5-wave workgroups share a CU (sra_dq_small holds both halves: 223 VGPRs,
+// one workgroup per CU -- stage 3 of B2 480 x 640 runs its 380 workgroups in 1.5 rounds).
+// Same MFMA order per output element as sra_dq_small (bit-identical).  Default; CMX_SRA_DQ_SEQ=0
+// restores sra_dq_small.  Standalone (scripts/bench_sra.py, Bt = 4): stage-3 backward 36.8 -> 34.5 us,
+// stage 4 26.2 -> 25.0 us; the bench pairs are within noise (profiles/r05_dqseq_ab.txt).
+template <typename E>
+__global__ __launch_bounds__(64 * SKT, 2) void sra_dq_small_seq(const E* __restrict__ q, const E* __restrict__ k,
+                                                               const E* __restrict__ v, const E* __restrict__ o,
+                                                               const E* __restrict__ dout,
+                                                               const float* __restrict__ lse, float* __restrict__ Dws,
+                                                               E* __restrict__ dq, int N, int Nk, int heads, long qs,
+                                                               long kvs, long os, long dos, long dqs, float sl2,
+                                                               float scale) {
+  __shared__ __attribute__((aligned(1024))) char smem[SKT * SREG];
+  const int nw = blockDim.x >> 6;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int b = blockIdx.z, head = blockIdx.y, q0 = blockIdx.x * 64;
+  char* Ki = smem + wave * SREG;
+  char* Vi = Ki + KTILE * ROWB;
+  const int t0 = wave * KTILE, nkw = min(KTILE, Nk - t0);
+  stage_rows<E>(k + ((long)b * Nk + t0) * kvs + head * HD, kvs, nkw, KTILE, Ki, 0, lane, 1);
+  stage_rows<E>(v + ((long)b * Nk + t0) * kvs + head * HD, kvs, nkw, KTILE, Vi, 0, lane, 1);
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) acc[u][0] = acc[u][1] = zero16();
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int qi = q0 + 32 * u + r;
+    const bool live = qi < N;
+    const E* qrow = q + ((long)b * N + qi) * qs + head * HD;
+    const E* orow = o + ((long)b * N + qi) * os + head * HD;
+    const E* drow = dout + ((long)b * N + qi) * dos + head * HD;
+    frag8<E> qf[4], df[4];
+    float dot = 0.f;
+#pragma unroll
+    for (int s_ = 0; s_ < 4; ++s_) {
+      if (live) {
+        qf[s_] = frag_bits<E>(*reinterpret_cast<const uint4*>(qrow + 16 * s_ + 8 * h));
+        df[s_] = frag_bits<E>(*reinterpret_cast<const uint4*>(drow + 16 * s_ + 8 * h));
+        float x[8], y[8];
+        load_vec<E>(drow + 16 * s_ + 8 * h, x);
+        load_vec<E>(orow + 16 * s_ + 8 * h, y);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dot += x[j] * y[j];
+      } else {
+        qf[s_] = df[s_] = zfrag<E>();
+      }
+    }
+    dot += __shfl_xor(dot, 32, 64);
+    const float Dq = dot;
+    const long sidx = ((long)b * heads + head) * N + qi;
+    const float lse2 = live ? lse[sidx] * 1.4426950408889634f : 0.f;
+    if (live && h == 0 && wave == 0) Dws[sidx] = dot;
+    if (u == 0) vm_wait<0>();                  // (the K / V images of this wave have landed)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      f32x16 sa = zero16(), dp = zero16();
+#pragma unroll
+      for (int s_ = 0; s_ < 4; ++s_) sa = MF<E>::mma(frag_k<E>(Ki, 32 * ks, s_, lane), qf[s_], sa);
+#pragma unroll
+      for (int s_ = 0; s_ < 4; ++s_) dp = MF<E>::mma(frag_k<E>(Vi, 32 * ks, s_, lane), df[s_], dp);
+      const f2 sl2v = {sl2, sl2}, nl = {-lse2, -lse2}, nD = {-Dq, -Dq};
+#pragma unroll
+      for (int i = 0; i < 16; i += 2) {
+        const f2 a = f2{sa[i], sa[i + 1]} * sl2v + nl;
+        f2 p = {fexp2(a.x), fexp2(a.y)};
+        if (nkw < KTILE) {                       // the last wave's ragged tile (uniform branch)
+          if (32 * ks + accrow(i, h) >= nkw) p.x = 0.f;
+          if (32 * ks + accrow(i + 1, h) >= nkw) p.y = 0.f;
+        }
+        const f2 d = p * (f2{dp[i], dp[i + 1]} + nD);
+        sa[i] = d.x;
+        sa[i + 1] = d.y;
+      }
+#pragma unroll
+      for (int s_ = 0; s_ < 2; ++s_) {
+        const frag8<E> sf = MF<E>::from_acc(sa, s_);
+        acc[u][0] = MF<E>::mma(frag_t<E>(Ki, 32 * ks, 0, s_, lane), sf, acc[u][0]);
+        acc[u][1] = MF<E>::mma(frag_t<E>(Ki, 32 * ks, 32, s_, lane), sf, acc[u][1]);
+      }
+    }
+  }
+  // own region: every read of it fed an MFMA whose result is in acc, so it is free
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    put_tile(Ki, acc[u][0], 32 * u, 0, lane, scale);
+    put_tile(Ki, acc[u][1], 32 * u, 1, lane, scale);
+  }
+  __syncthreads();
+  for (int it = threadIdx.x; it < 64 * 8; it += blockDim.x) {
+    const int row = it >> 3, dg = it & 7, qi = q0 + row;
+    if (qi < N) sum_store8<E>(smem, nw, SREG, row, dg, 1.f, dq + ((long)b * N + qi) * dqs + head * HD + 8 * dg);
+  }
+}
+
 // dK / dV: workgroup = 32 keys of one (b, head) on the lanes; wave w sweeps query tiles
 // w, w + nw, ... (its own Q / dO images), and the waves' sums meet in LDS: every key's dK / dV
 // is complete inside the workgroup (written directly, no slabs)
@@ -1142,9 +1239,14 @@ void sra_dq_small_launch(const void* q, const void* k, const void* v, const void
                          const float* lse, float* Dws, void* dq, int Bt, int N, int Nk, int heads, long qs, long kvs,
                          long os, long dos, long dqs, float sl2, float scale, int dtype, hipStream_t s) {
   const dim3 grid(cdiv(N, 64), heads, Bt), block(64 * cdiv(Nk, KTILE));
+  static int& seq = cmx_knob("SRA_DQ_SEQ", 1);      // sra_dq_small_seq (0: sra_dq_small)
 #define CMX_SRA_DQS(E_)                                                                                            \
-  hipLaunchKernelGGL(sra_dq_small<E_>, grid, block, 0, s, (const E_*)q, (const E_*)k, (const E_*)v, (const E_*)o,   \
-                     (const E_*)dout, lse, Dws, (E_*)dq, N, Nk, heads, qs, kvs, os, dos, dqs, sl2, scale)
+  if (seq) hipLaunchKernelGGL(sra_dq_small_seq<E_>, grid, block, 0, s, (const E_*)q, (const E_*)k, (const E_*)v,   \
+                              (const E_*)o, (const E_*)dout, lse, Dws, (E_*)dq, N, Nk, heads, qs, kvs, os, dos, dqs, \
+                              sl2, scale);                                                                          \
+  else hipLaunchKernelGGL(sra_dq_small<E_>, grid, block, 0, s, (const E_*)q, (const E_*)k, (const E_*)v,           \
+                          (const E_*)o, (const E_*)dout, lse, Dws, (E_*)dq, N, Nk, heads, qs, kvs, os, dos, dqs,     \
+                          sl2, scale)
   if (dtype == 2) CMX_SRA_DQS(f16);
   else CMX_SRA_DQS(bf16);
 #undef CMX_SRA_DQS

@@ -215,6 +215,30 @@ def test_batchnorm(dev, dtype, M, C, rps, act, use_res, use_ds, training):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("Bt,N,Nk,heads", [(4, 1200, 300, 5), (4, 300, 300, 8), (2, 333, 70, 2), (1, 129, 257, 3)])
+def test_sra_dq_small_seq(dev, dtype, Bt, N, Nk, heads):
+    """sra_dq_small_seq (CMX_SRA_DQ_SEQ=1: the two 32-query halves of a wave one after the other,
+    under 168 VGPRs) gives the short-sequence dQ bit for bit, dK / dV untouched."""
+    from rgbx_semantic_segmentation_amd import kernels as K
+    torch.manual_seed(3)
+    D, C = 64, heads * 64
+    q = torch.randn(Bt, N, C, device=dev).to(dtype)
+    kv = torch.randn(Bt, Nk, 2 * C, device=dev).to(dtype)
+    do = torch.randn(Bt, N, C, device=dev).to(dtype)
+    o, lse = K.sra_attn_fwd(q, kv, kv[..., C:], Bt, N, Nk, heads, D, D ** -0.5, C, 2 * C)
+    base = K.tune_get("SRA_DQ_SEQ") if K.tune_get("SRA_DQ_SEQ") >= 0 else 0
+    outs = []
+    try:
+        for seq in (0, 1):
+            K.tune("SRA_DQ_SEQ", seq)
+            outs.append(K.sra_attn_bwd(q, kv, kv[..., C:], o, do, lse, Bt, N, Nk, heads, D, D ** -0.5, C, 2 * C))
+    finally:
+        K.tune("SRA_DQ_SEQ", base)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("Bt,N,Nk,heads", [(2, 300, 300, 4), (1, 1200, 300, 5), (1, 4800, 300, 2)])
 def test_sra_attention_peaked(dev, dtype, Bt, N, Nk, heads):
     """Sharply peaked softmax (q x 6): the per-wave maxima of the short-sequence kernels differ by
