@@ -275,6 +275,14 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
     if (a.nup && up_tile == 64) bm = bn = 64;
     if (row_ln || lnb) bm = 64, bn = N <= 64 ? 64 : 128;   // one tile spans the row
     if (lnb && a.scatter) bn = scC;                         // (one tap's C channels)
+    // 64 x 64 tiles that overflow one round of resident blocks by less than CMX_GEMM_MID percent
+    // (5 per CU) take 64 x 128 tiles instead: one round of blocks twice as long, not a second
+    // partial round (0 = off; default 50: GEMM census 1380 -> 1361 us, stage-3 fc1 14.3 -> 13.0 us)
+    static int& mid = cmx_knob("GEMM_MID", 50);
+    if (mid > 0 && bm == 64 && bn == 64 && !row_ln && !lnb && !a.scatter && !a.nup && splitk == 1 && nb >= 128) {
+      const long t64 = (long)cdiv(M, 64) * cdiv(nb, 64) * G, slots = 5L * cu_count();
+      if (t64 > slots && t64 * 100 <= slots * (100 + mid)) bn = 128;
+    }
     a.tiles_m = cdiv(M, bm); a.tiles_n = cdiv(nb, bn);
     // tall 64 x 64 problems of at least CMX_GEMM_STREAM tiles (0 = off) and K <= CMX_GEMM_STREAM_K:
     // the resident streaming grid (gemm_stream_kernel) instead of one block per tile
