@@ -846,7 +846,7 @@ __global__ __launch_bounds__(64 * SKT) void sra_dq_small(const E* __restrict__ q
 // Same MFMA order per output element as sra_dq_small (bit-identical).  Default; CMX_SRA_DQ_SEQ=0
 // restores sra_dq_small.  Standalone (scripts/bench_sra.py, Bt = 4): stage-3 backward 36.8 -> 34.5 us,
 // stage 4 26.2 -> 25.0 us; the bench pairs are within noise (profiles/r05_dqseq_ab.txt).
-template <typename E>
+template <typename E, int NU>
 __global__ __launch_bounds__(64 * SKT, 2) void sra_dq_small_seq(const E* __restrict__ q, const E* __restrict__ k,
                                                                const E* __restrict__ v, const E* __restrict__ o,
                                                                const E* __restrict__ dout,
@@ -857,17 +857,17 @@ __global__ __launch_bounds__(64 * SKT, 2) void sra_dq_small_seq(const E* __restr
   __shared__ __attribute__((aligned(1024))) char smem[SKT * SREG];
   const int nw = blockDim.x >> 6;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  const int b = blockIdx.z, head = blockIdx.y, q0 = blockIdx.x * 64;
+  const int b = blockIdx.z, head = blockIdx.y, q0 = blockIdx.x * 32 * NU;
   char* Ki = smem + wave * SREG;
   char* Vi = Ki + KTILE * ROWB;
   const int t0 = wave * KTILE, nkw = min(KTILE, Nk - t0);
   stage_rows<E>(k + ((long)b * Nk + t0) * kvs + head * HD, kvs, nkw, KTILE, Ki, 0, lane, 1);
   stage_rows<E>(v + ((long)b * Nk + t0) * kvs + head * HD, kvs, nkw, KTILE, Vi, 0, lane, 1);
-  f32x16 acc[2][2];
+  f32x16 acc[NU][2];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) acc[u][0] = acc[u][1] = zero16();
+  for (int u = 0; u < NU; ++u) acc[u][0] = acc[u][1] = zero16();
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < NU; ++u) {
     const int qi = q0 + 32 * u + r;
     const bool live = qi < N;
     const E* qrow = q + ((long)b * N + qi) * qs + head * HD;
@@ -925,12 +925,12 @@ __global__ __launch_bounds__(64 * SKT, 2) void sra_dq_small_seq(const E* __restr
   }
   // own region: every read of it fed an MFMA whose result is in acc, so it is free
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < NU; ++u) {
     put_tile(Ki, acc[u][0], 32 * u, 0, lane, scale);
     put_tile(Ki, acc[u][1], 32 * u, 1, lane, scale);
   }
   __syncthreads();
-  for (int it = threadIdx.x; it < 64 * 8; it += blockDim.x) {
+  for (int it = threadIdx.x; it < 32 * NU * 8; it += blockDim.x) {
     const int row = it >> 3, dg = it & 7, qi = q0 + row;
     if (qi < N) sum_store8<E>(smem, nw, SREG, row, dg, 1.f, dq + ((long)b * N + qi) * dqs + head * HD + 8 * dg);
   }
@@ -1240,10 +1240,19 @@ void sra_dq_small_launch(const void* q, const void* k, const void* v, const void
                          long os, long dos, long dqs, float sl2, float scale, int dtype, hipStream_t s) {
   const dim3 grid(cdiv(N, 64), heads, Bt), block(64 * cdiv(Nk, KTILE));
   static int& seq = cmx_knob("SRA_DQ_SEQ", 1);      // sra_dq_small_seq (0: sra_dq_small)
+  // CMX_SRA_DQ_HALF=1: 32-query workgroups when the 64-query grid would leave CUs without a
+  // workgroup.  Measured slower (stage 4 of B2: 160 -> 320 workgroups, backward 25.0 -> 28.4 us:
+  // each one stages the (b, head)'s K / V for half the queries), so off by default
+  static int& half = cmx_knob("SRA_DQ_HALF", 0);
+  const bool h32 = seq && half && (long)grid.x * grid.y * grid.z < sra_cus();
+  const dim3 grid32(cdiv(N, 32), heads, Bt);
 #define CMX_SRA_DQS(E_)                                                                                            \
-  if (seq) hipLaunchKernelGGL(sra_dq_small_seq<E_>, grid, block, 0, s, (const E_*)q, (const E_*)k, (const E_*)v,   \
-                              (const E_*)o, (const E_*)dout, lse, Dws, (E_*)dq, N, Nk, heads, qs, kvs, os, dos, dqs, \
-                              sl2, scale);                                                                          \
+  if (h32) hipLaunchKernelGGL((sra_dq_small_seq<E_, 1>), grid32, block, 0, s, (const E_*)q, (const E_*)k,          \
+                              (const E_*)v, (const E_*)o, (const E_*)dout, lse, Dws, (E_*)dq, N, Nk, heads, qs, kvs, \
+                              os, dos, dqs, sl2, scale);                                                            \
+  else if (seq) hipLaunchKernelGGL((sra_dq_small_seq<E_, 2>), grid, block, 0, s, (const E_*)q, (const E_*)k,       \
+                              (const E_*)v, (const E_*)o, (const E_*)dout, lse, Dws, (E_*)dq, N, Nk, heads, qs, kvs, \
+                              os, dos, dqs, sl2, scale);                                                            \
   else hipLaunchKernelGGL(sra_dq_small<E_>, grid, block, 0, s, (const E_*)q, (const E_*)k, (const E_*)v,           \
                           (const E_*)o, (const E_*)dout, lse, Dws, (E_*)dq, N, Nk, heads, qs, kvs, os, dos, dqs,     \
                           sl2, scale)
