@@ -445,22 +445,35 @@ def main():
     step_floor = {"floor_us": round(ftot, 1), "frac": round(ftot / (ms * 1e3), 4),
                   "families_us": {f: round(us, 1) for f, _, _, us, _ in frows}}
 
-    # every rank runs the roofline step (its SyncBN collectives need all ranks); rank 0 reports.
-    # No optimizer step follows it, so the gradient all-reduce hooks are detached first.
-    # The bench line's ``roofline`` is the step's dominant kernel FAMILY by device time (the tile
-    # GEMMs); the largest single launch (grouped weight gradients) rides along
-    # as ``roofline.second``.  Both measurement steps run after the timed window (their in-place
-    # re-launches leave the activations and BN statistics meaningless).
-    from rgbx_semantic_segmentation_amd.roofline import measure_dominant, measure_gemm_family
-    model.backbone.grad_sync = None
+    # The bench line's ``roofline`` is the step's dominant kernel FAMILY by device time INSIDE the
+    # replayed step: a kernel trace of 10 replays after the timed window,
+    # every launch classified by name, the family's summed kernel time per step against its
+    # algorithmic work.  Beside it: ``reissue`` (the same family with each launch re-issued in
+    # place, warm -- the round-5 figure) and ``second`` (the grouped weight-gradient launch
+    # re-launched standalone).  Every rank runs those two eager measurement steps (their SyncBN
+    # collectives need all ranks); no optimizer step follows, so the gradient all-reduce hooks
+    # are detached first.  They run last: their in-place re-launches leave the activations and
+    # BN statistics meaningless.
+    from rgbx_semantic_segmentation_amd.roofline import measure_dominant, measure_gemm_family, measure_in_step
     workload = f"CMX-{args.backbone.replace('mit_', '').upper()} train step {args.height}x{args.width} " \
                f"bs={args.batch} K={args.classes}"
     shape = dict(backbone=args.backbone, H=args.height, W=args.width, B=args.batch, K=args.classes)
-    # (CMX_BENCH_NO_ROOFLINE=1: skipped, for the PMC passes, whose per-launch bytes must be the
-    # graph replays' and not the in-place re-launches')
+    # (CMX_BENCH_NO_ROOFLINE=1: skipped, for the PMC / kernel-trace passes, whose per-launch
+    # records must be the graph replays' only)
     skip = os.environ.get("CMX_BENCH_NO_ROOFLINE") == "1"
-    roof = None if skip else measure_gemm_family(model, (rgb, x, lab), workload, shape)
+    roof = families = None
+    if not skip and graph is not None:
+        try:
+            roof, families = measure_in_step(run_one, workload, shape, float(model.store.flat.numel()))
+        except Exception as e:  # pragma: no cover - tracer availability is the box's
+            print(f"[bench] in-step kernel trace failed: {e!r}", file=sys.stderr)
+    model.backbone.grad_sync = None
+    reissue = None if skip else measure_gemm_family(model, (rgb, x, lab), workload, shape)
     second = None if skip else measure_dominant(model, (rgb, x, lab), workload)
+    if roof is None:
+        roof = reissue
+    else:
+        roof["reissue"] = reissue
     if roof is None:
         roof = second
     elif second is not None:
@@ -496,6 +509,7 @@ def main():
                                    "peak_tflops": PEAK_BF16_TFLOPS, "frac": round(step_frac, 5)},
             "step_floor": step_floor,
             "roofline": roof,
+            "families_in_step": families,
             "cpu_baseline": cpu,
             "replay_ms": {"warmup": replay_stats(warm_ms), "timed": replay_stats(timed_ms),
                           "settle": {"replays": settle_n, "device_s": round(settle_t, 3),

@@ -34,7 +34,7 @@ typedef struct ihipStream_t* hipStream_t;
  * from, and the Python binding refuses a library whose revision differs (an older .so with the
  * same symbol names but shifted arguments would otherwise corrupt memory silently).  Bump it
  * on every change of an entry point's argument list. */
-#define CMX_ABI_VERSION 4
+#define CMX_ABI_VERSION 5
 int cmx_abi_version(void);
 const char* cmx_last_error(void);
 /* pinned host -> device copy of a packed record table on `stream` (see grouped launches) */
@@ -233,10 +233,9 @@ int cmx_gemm_group_pack(void* rec, const void* A, const void* B, void* C, float*
  *      rows in the same launch -- the consumer norm of a residual Linear (Block: x + drop_path(proj(.))
  *      -> norm2, x + drop_path(fc2(.)) -> next norm1 / stage norm; dual_segformer.py:168-169,382):
  *      ln_y = LN(C) * ln_gamma[g] + ln_beta[g] (C's dtype and strides), ln_mean / ln_rstd (fp32, g*M + i).
- *      N a multiple of 64, <= 512.  tickets: cmx_gemm_ln_tickets(G, M) uint32 arrival counters, zero
- *      before the first launch; each launch leaves them zero (stream-ordered launches may share them). */
-int cmx_gemm_ln(const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R, const float* rscale, int G, int M, int N, int K, int K1, int64_t lda, int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias, int rows_per_sample, int act, const float* ln_gamma, const float* ln_beta, int64_t ln_sg, float ln_eps, void* ln_y, float* ln_mean, float* ln_rstd, unsigned* tickets, int dtype, hipStream_t stream);
-size_t cmx_gemm_ln_tickets(int G, int M);
+ *      N <= 128, N % 8 == 0: one output tile spans the row and normalises it in the epilogue
+ *      (statistics bit-identical to cmx_layernorm_fwd).  CMX_ERR_ARG when not eligible. */
+int cmx_gemm_ln(const void* A, const void* A2, const void* B, void* C, const float* bias, const void* R, const float* rscale, int G, int M, int N, int K, int K1, int64_t lda, int64_t lda2, int64_t ldb, int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias, int rows_per_sample, int act, const float* ln_gamma, const float* ln_beta, int64_t ln_sg, float ln_eps, void* ln_y, float* ln_mean, float* ln_rstd, int dtype, hipStream_t stream);
 /* cmx_gemm_ln_bwd: a Linear's input gradient dy = A (G,M,K) B^T (B (G,N,K) logical, row-contiguous: the
  *      weight W (G,K,N) read transposed, as cmx_gemm's transB = 1 dgrad) fed straight into the backward
  *      of the LayerNorm that produced that Linear's input (Block.norm2 -> fc1, dual_segformer.py:169;
@@ -256,21 +255,6 @@ size_t cmx_gemm_ln_bwd_partials(int G, int M, int N);
 int cmx_conv_patch_dgrad_ln_bwd(const void* dy, const void* Wt, void* dx, int G, int NIg, int H, int Wd, int C, int R, int Ho, int Wo, int N, int64_t sdy, int64_t sW, int64_t sdx, const void* x, const float* gamma, int64_t sg, const float* mean, const float* rstd, const void* dres, const void* dy2, const float* sscale, int rows_per_sample, void* dxs, float* partials, int dtype, hipStream_t stream);
 size_t cmx_conv_patch_dgrad_ln_bwd_partials(int G, int NIg, int Ho, int Wo, int C, int R);
 int cmx_gemm_grouped(const void* recs, int nrec, int total_blocks, int dtype, hipStream_t stream);
-/* ---- Mix-FFN bands (Mlp.forward fc1 -> DWConv 3x3 -> GELU, dual_segformer.py:67-71) --------------
- * x (G, ipg*H*W, C) contiguous 16-bit; W1 (G, Ch, C) (group stride sW), b1 (G, Ch) (stride sb = Ch),
- * wdw (G, Ch, 9) (stride sdw = 9 Ch) and bdw (G, Ch) fp32.  One launch: h = x W1^T + b1, z = DW(h) + bdw,
- * a = GELU(z), act'(z) -- bit-identical to cmx_gemm + cmx_dwconv3x3_fwd_save.  A workgroup owns a band of
- * cmx_mixffn_band_rows(W) image rows (+1 halo row each side, fc1 recomputed there) x 64 hidden channels,
- * or (cmx_mixffn_mode(W) = 2: W > 42) a 12 x 16-pixel tile (+1 halo pixel each side) x 64 hidden channels.
- * bwd: dz2 (G, ipg*H*W, C) = fc2's output gradient, W2 (G, C, Ch): da = dz2 W2 (as fc2's dgrad would),
- * dz = da * act'(z), dh = DW^T(dz), and the DW dW / db partials (G, P, Ch * 10) in the workspace
- * (cmx_mixffn_bwd_workspace bytes, P = workspace / (40 G Ch)) for cmx_reduce_grouped. */
-int cmx_mixffn_band_rows(int W);
-/* cmx_mixffn_mode: 1 = bands of cmx_mixffn_band_rows(W) full rows (>= 4), 2 = 12 x 16-pixel tiles (wide images) */
-int cmx_mixffn_mode(int W);
-size_t cmx_mixffn_bwd_workspace(int G, int ipg, int H, int W, int Ch);
-int cmx_mixffn_fwd(const void* x, const void* W1, const float* b1, const float* wdw, const float* bdw, void* h, void* gprime, void* a, int G, int ipg, int H, int W, int C, int Ch, int64_t sW, int64_t sb, int64_t sdw, int dtype, hipStream_t stream);
-int cmx_mixffn_bwd(const void* dz2, const void* W2, const float* wdw, const void* h, const void* gprime, void* dh, float* workspace, int G, int ipg, int H, int W, int C, int Ch, int64_t sW, int64_t sdw, int dtype, hipStream_t stream);
 /* cmx_gemm_grouped_capped: the same launch on a grid of at most max_blocks workgroups (a multiple
  * of 8; <= 0: uncapped), each walking blocks b, b + grid, ...: a grouped weight-gradient launch
  * beside the backward on a side stream keeps to that share of the chip */

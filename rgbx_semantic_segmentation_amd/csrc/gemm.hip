@@ -135,9 +135,9 @@ struct GemmPlan {
   int tA, tB, dtype, nblk, nk64, pad;
 };
 
-// row-block LayerNorm tail of the epilogue (cmx_gemm_ln)
+// LayerNorm of the output rows in the epilogue (cmx_gemm_ln)
 struct LnTail {
-  const float* gamma; const float* beta; long sg; void* y; float* mean; float* rstd; unsigned* tickets; float eps;
+  const float* gamma; const float* beta; long sg; void* y; float* mean; float* rstd; float eps;
 };
 
 // LayerNorm backward of the epilogue (cmx_gemm_ln_bwd)
@@ -220,23 +220,18 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
   a.kt_per_split = (nk + splitk - 1) / splitk;
   splitk = (nk + a.kt_per_split - 1) / a.kt_per_split;      // no empty splits
   a.nsplit = splitk;
-  // LayerNorm of C's rows in the same launch: N <= 128 -> in the epilogue (tail = 2: one 64 x 64 /
-  // 64 x 128 tile spans the row), else the row-block tail with arrival tickets (tail = 1)
-  const bool row_ln = tail && N <= 128 && N % 8 == 0;
+  // LayerNorm of C's rows in the same launch (tail = 2): N <= 128, one 64 x 64 / 64 x 128 tile
+  // spans the row and the lanes that store it normalise it
+  const bool row_ln = tail != nullptr;
   if (tail) {
-    int bm = 0, bn = 0;
-    if (fast) plan_tiles(G, M, nb, K, &bm, &bn);
-    if (row_ln) bm = 64, bn = N <= 64 ? 64 : 128;
-    CMX_REQUIRE(fast && bm == 64 && (bn == 64 || row_ln) && splitk == 1 && !transA && !transB && out_mode == 0 &&
-                    !ones_col && !a.nup && !a.scatter && gh == 1 && !mask && a.cvec &&
-                    (row_ln || (N % 64 == 0 && N <= 512)) && dtype != 0,
-                CMX_ERR_ARG, "gemm_ln: the LayerNorm tail needs the 16-bit path without split-K, forward layouts, a "
-                "plain aligned store and N <= 128 (N %% 8 == 0) or N a multiple of 64 <= 512 (G=%d M=%d N=%d K=%d)",
-                G, M, N, K);
-    CMX_REQUIRE(tail->gamma && tail->beta && tail->y && tail->mean && tail->rstd && (row_ln || tail->tickets) &&
-                    ((uintptr_t)tail->y & 15) == 0 && tail->y != C, CMX_ERR_ARG, "gemm_ln: tail buffers");
-    a.tail = row_ln ? 2 : 1; a.ln_gamma = tail->gamma; a.ln_beta = tail->beta; a.ln_sg = tail->sg; a.ln_y = tail->y;
-    a.ln_mean = tail->mean; a.ln_rstd = tail->rstd; a.tickets = tail->tickets; a.ln_eps = tail->eps;
+    CMX_REQUIRE(fast && N <= 128 && N % 8 == 0 && splitk == 1 && !transA && !transB && out_mode == 0 && !ones_col &&
+                    !a.nup && !a.scatter && gh == 1 && !mask && a.cvec && dtype != 0,
+                CMX_ERR_ARG, "gemm_ln: the LayerNorm epilogue needs the 16-bit path without split-K, forward layouts, a "
+                "plain aligned store and N <= 128, N %% 8 == 0 (G=%d M=%d N=%d K=%d)", G, M, N, K);
+    CMX_REQUIRE(tail->gamma && tail->beta && tail->y && tail->mean && tail->rstd && ((uintptr_t)tail->y & 15) == 0 &&
+                    tail->y != C, CMX_ERR_ARG, "gemm_ln: LayerNorm buffers");
+    a.tail = 2; a.ln_gamma = tail->gamma; a.ln_beta = tail->beta; a.ln_sg = tail->sg; a.ln_y = tail->y;
+    a.ln_mean = tail->mean; a.ln_rstd = tail->rstd; a.ln_eps = tail->eps;
   }
   if (lnb) {
     const bool al = ((uintptr_t)C & 15) == 0 && ((uintptr_t)lnb->x & 15) == 0 && ((uintptr_t)R & 15) == 0 &&
@@ -269,10 +264,6 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
   if (fast) {
     int bm, bn;
     plan_tiles(G, M, nb, K, &bm, &bn);
-    // the upsample-add epilogue (decoder fuse): CMX_GEMM_UP_TILE = 64 takes 64 x 64 tiles (more
-    // resident workgroups to overlap the epilogue's gathered bilinear loads), 0 = the usual policy
-    static int& up_tile = cmx_knob("GEMM_UP_TILE", 0);
-    if (a.nup && up_tile == 64) bm = bn = 64;
     if (row_ln || lnb) bm = 64, bn = N <= 64 ? 64 : 128;   // one tile spans the row
     if (lnb && a.scatter) bn = scC;                         // (one tap's C channels)
     // 64 x 64 tiles that overflow one round of resident blocks by less than CMX_GEMM_MID percent
@@ -343,14 +334,13 @@ int cmx_gemm_ln(const void* A, const void* A2, const void* B, void* C, const flo
                 const float* rscale, int G, int M, int N, int K, int K1, int64_t lda, int64_t lda2, int64_t ldb,
                 int64_t ldc, int64_t sA, int64_t sA2, int64_t sB, int64_t sC, int64_t sbias, int rows_per_sample,
                 int act, const float* ln_gamma, const float* ln_beta, int64_t ln_sg, float ln_eps, void* ln_y,
-                float* ln_mean, float* ln_rstd, unsigned* tickets, int dtype, hipStream_t s) {
-  const LnTail t{ln_gamma, ln_beta, (long)ln_sg, ln_y, ln_mean, ln_rstd, tickets, ln_eps};
+                float* ln_mean, float* ln_rstd, int dtype, hipStream_t s) {
+  const LnTail t{ln_gamma, ln_beta, (long)ln_sg, ln_y, ln_mean, ln_rstd, ln_eps};
   return gemm_impl(A, A2, B, C, bias, R, rscale, nullptr, nullptr, G, M, N, K, K1, lda, lda2, ldb, ldc, sA, sA2, sB,
                    sC, sbias, 0, rows_per_sample, 0, 0, act, 0, 0, 1, dtype, s, nullptr, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0,
                    nullptr, nullptr, &t);
 }
 
-size_t cmx_gemm_ln_tickets(int G, int M) { return (size_t)G * ((M + 63) / 64); }
 
 int cmx_gemm_ln_bwd(const void* A, const void* B, void* dx, int G, int M, int N, int K, int64_t lda, int64_t ldb,
                     int64_t ldc, int64_t sA, int64_t sB, int64_t sC, const void* x, const float* gamma, int64_t sg,

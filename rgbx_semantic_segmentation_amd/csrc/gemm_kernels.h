@@ -37,13 +37,8 @@ struct GemmArgs {
   // ReLU-backward mask (NULL: none): after the residual, C(i, j) = 0 where mask(i, j) <= 0; the
   // mask has C's layout and dtype (the saved ReLU output of the layer whose gradient this is)
   const void* mask;
-  // row-block LayerNorm tail (tail = 1; 64 x 64 tiles, forward layouts, no split, plain store,
-  // N <= 512): the consumer norm of a residual Linear's output (Block.norm2 after proj, the next
-  // norm1 / stage norm after fc2, dual_segformer.py:168-169,382) runs inside the producing launch.
-  // Every tile stores its outputs write-through (sc1) and takes an arrival ticket of its 64-row
-  // block (tickets[g * tiles_m + tm], caller-owned, zero at first use, reset by the last
-  // arriver); the last of the row block's tiles_n workgroups to arrive normalises those rows:
-  // ln_y = LN(C rows) * gamma + beta (C's dtype and layout), ln_mean / ln_rstd (fp32, g * M + i)
+  // LayerNorm in the epilogue (the consumer norm of a residual Linear's output: Block.norm2 after
+  // proj, the next norm1 / stage norm after fc2, dual_segformer.py:168-169,382):
   // tail = 2 (N <= 128, N % 8 == 0: 64 x 64 / 64 x 128 tiles span the row): the same LayerNorm
   // in the epilogue by the lanes that store the row (row_layernorm), no tickets, no re-read
   // tail = 3: the LayerNorm BACKWARD in a dgrad's epilogue (row_layernorm_bwd): the GEMM result is
@@ -59,7 +54,6 @@ struct GemmArgs {
   void* ln_y;
   float* ln_mean;
   float* ln_rstd;
-  unsigned* tickets;
   const void* lnb_x;
   const void* lnb_dy2;
   void* lnb_dxs;
@@ -182,24 +176,9 @@ __device__ __forceinline__ void dbias_store(const GemmArgs& p, int g, int i, flo
   *d = p.out_mode == 2 ? *d + v : v;
 }
 
-// 16-B write-through store (sc1: through to the device-coherent level, so a workgroup on another
-// XCD reads it back with sc1 loads in the same launch; MI355X_MICROARCH.md "visibility")
-// (base: wave-uniform, e.g. a group's first element -- the resource lives in SGPRs; off: the
-// lane's byte offset, < 2^31)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7ffffff0, 0x00020000);
-}
-__device__ __forceinline__ void st16_sc1(const void* base, int off, uint4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rsrc_of(base), off, 0, 16);
-}
-__device__ __forceinline__ uint4 ld16_sc1(const void* base, int off) {
-  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsrc_of(base), off, 0, 16));
-}
-
 // 8 consecutive columns j..j+nv-1 of row i (nv <= 8).  p.vec8: C / R rows are 16-B aligned
-// chunks, so a full group moves with one 16-B (bf16) or two 16-B (fp32) accesses.  SC1: the
-// plain 16-bit store goes write-through (row-block tail launches)
-template <typename T, bool SC1 = false>
+// chunks, so a full group moves with one 16-B (bf16) or two 16-B (fp32) accesses
+template <typename T>
 __device__ __forceinline__ void epi_store8(const GemmArgs& p, int g, int i, int j, int nv, float* v) {
   if (nv < 8 || !p.cvec) {
     for (int e = 0; e < nv; ++e) epi_store<T, true>(p, g, i, j + e, v[e]);
@@ -232,15 +211,8 @@ __device__ __forceinline__ void epi_store8(const GemmArgs& p, int g, int i, int 
     for (int e = 0; e < 8; ++e) v[e] = mv[e] > 0.f ? v[e] : 0.f;
   }
   if (p.out_mode == 0) {
-    if constexpr (SC1 && sizeof(T) == 2) {
-      // (tail launches: plain row-major C, so the group's base is uniform and the offset in it < 2^31 B)
-      const long gb = goff(p, g, p.sC, p.sCh);
-      st16_sc1(reinterpret_cast<T*>(p.C) + gb, (int)((off - gb) * 2),
-               make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])));
-    } else {
-      store_vec<T>(reinterpret_cast<T*>(p.C) + off, v);
-      if constexpr (sizeof(T) == 4) store_vec<T>(reinterpret_cast<T*>(p.C) + off + 4, v + 4);
-    }
+    store_vec<T>(reinterpret_cast<T*>(p.C) + off, v);
+    if constexpr (sizeof(T) == 4) store_vec<T>(reinterpret_cast<T*>(p.C) + off + 4, v + 4);
   } else {
     float4* d = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + off);
     if (p.out_mode == 2) {
@@ -400,7 +372,10 @@ __device__ __forceinline__ void row_layernorm(const GemmArgs& p, int g, int i, i
 //   dx = rstd * (g - mean(g) - xhat * mean(g * xhat)) + dres,  g = dy * gamma,  xhat = (x - mu) rstd
 // exactly as ln_bwd_kernel (layernorm.hip) computes a row of TPR 16-B chunks (dy rounded to the
 // storage type first, as that kernel reads it), so dx and dxs are bit-identical to the separate
-// launches; the lane's dgamma / dbeta terms accumulate in dga / dba for the tile's partials.
+// launches whenever the separate dgrad sums k in the same order -- every shape but N = 128 on
+// grids small enough for its 64 x 64 k-group blocks (two k-halves added at the end), where dy and
+// so dx may differ by one rounding (tests/test_gpu_gemm.py::test_gemm_ln_bwd); the lane's dgamma /
+// dbeta terms accumulate in dga / dba for the tile's partials.
 // Under the patch scatter (cmx_conv_patch_dgrad_ln_bwd: the SR conv's input gradient, Attention.sr
 // dual_segformer.py:95-96) a tile is one tap of 64 patches, i.e. 64 whole input-pixel rows of C =
 // BN channels: the norm row is the scattered pixel, its statistics index the pixel.
@@ -706,7 +681,7 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
         for (int e = 0; e < nv; ++e) d[e] = v[e];
       }
     } else {
-      epi_store8<E, EPI == 1>(p, g, i, j, nv, v);
+      epi_store8<E>(p, g, i, j, nv, v);
     }
   }
   if constexpr (EPI == 3) {
@@ -731,88 +706,6 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
   }
 }
 
-// Row-block LayerNorm tail (GemmArgs::tail): called by every workgroup after its tile's stores;
-// the last of the row block's tiles_n to arrive normalises the block's <= 64 rows of C.  Its
-// loads of C are sc1 (the other tiles' stores were sc1 and drained before their ticket), every
-// channel chunk of every row it owns is in flight before the first reduction.  A row is
-// TPR = N / 8 lanes x one 16-B chunk (N <= 512: TPR <= 64), RPW = 64 / TPR rows per wave
-// instruction; the block's waves take rows round-robin.  Numerics as ln_fwd_kernel
-// (layernorm.hip): two-pass mean / variance of the stored 16-bit values in fp32.
-template <typename E>
-__device__ __forceinline__ void gemm_ln_tail(const GemmArgs& p, const int lin) {
-  const int ntile = p.tiles_m * p.tiles_n;
-  const int t = lin % ntile, g = (lin / ntile) % p.G;
-  const int tm = t / p.tiles_n;
-  if (!last_arrival(p.tickets + g * p.tiles_m + tm, p.tiles_n)) return;
-  // a row: nch = N / 8 chunks on TPR lanes (the power of two >= nch: lanes past nch hold zeros
-  // and stay out of the variance), RPW = 64 / TPR rows per wave instruction
-  const int C = p.N, nch = C / 8;
-  const int TPR = nch <= 8 ? 8 : nch <= 16 ? 16 : nch <= 32 ? 32 : 64, RPW = 64 / TPR;
-  const int nw = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int sub = lane / TPR, ch = lane % TPR;          // row within the wave instruction, chunk
-  const bool live = ch < nch;
-  const int i0 = tm * 64;
-  const int rows = min(64, p.M - i0);
-  const E* Cg = reinterpret_cast<const E*>(p.C) + (long)g * p.sC;
-  E* Yg = reinterpret_cast<E*>(p.ln_y) + (long)g * p.sC;
-  float ga[8], be[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    ga[e] = live ? p.ln_gamma[(long)g * p.ln_sg + ch * 8 + e] : 0.f;
-    be[e] = live ? p.ln_beta[(long)g * p.ln_sg + ch * 8 + e] : 0.f;
-  }
-  // rows in two halves of up to 8 per lane (all of a half's loads in flight before its first
-  // reduction; fully unrolled with guards, so the staging stays in registers)
-  constexpr int HALF = 8;
-  const int step = nw * RPW;                             // rows per pass of the whole block
-  const int npass = (rows + step - 1) / step;            // <= 16 (64 rows, 4 waves, 1 row per wave)
-#pragma unroll
-  for (int h0 = 0; h0 < 16; h0 += HALF) {
-    if (h0 >= npass) break;
-    uint4 raw[HALF];
-#pragma unroll
-    for (int u = 0; u < HALF; ++u) {
-      const int r = (h0 + u) * step + wave * RPW + sub;
-      raw[u] = make_uint4(0, 0, 0, 0);
-      if (h0 + u < npass && r < rows && live) raw[u] = ld16_sc1(Cg, (int)(((long)(i0 + r) * p.ldc + ch * 8) * 2));
-    }
-#pragma unroll
-    for (int u = 0; u < HALF; ++u) {
-      const int r = (h0 + u) * step + wave * RPW + sub;
-      float v[8];
-      const uint32_t w4[4] = {raw[u].x, raw[u].y, raw[u].z, raw[u].w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const cmx_f2 f = unpack2<E>(w4[q]);
-        v[2 * q] = f.x;
-        v[2 * q + 1] = f.y;
-      }
-      float sm = 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) sm += v[e];
-      sm = group_sum(sm, TPR);
-      const float mu = sm / C;
-      float q2 = 0.f;
-      if (live) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { const float d = v[e] - mu; q2 += d * d; }
-      }
-      q2 = group_sum(q2, TPR);
-      const float rs = rsqrtf(q2 / C + p.ln_eps);
-      if (h0 + u < npass && r < rows && live) {
-        float o[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = (v[e] - mu) * rs * ga[e] + be[e];
-        store_vec<E>(Yg + (long)(i0 + r) * p.ldc + ch * 8, o);
-        if (ch == 0) {
-          p.ln_mean[(long)g * p.M + i0 + r] = mu;
-          p.ln_rstd[(long)g * p.M + i0 + r] = rs;
-        }
-      }
-    }
-  }
-}
-
 // 1-D grid over (split, group, tile); each XCD gets a contiguous run of that order, i.e.
 // neighbouring tiles of one (split, group): they share A row panels and the B k-slice in L2
 // (64 x 64 two-stage blocks take 32 KB of LDS: five fit a CU when the kernel stays within 96
@@ -823,7 +716,6 @@ void gemm_bf16_kernel(const GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[gemm_smem_bytes<BM, BN, NS, KW>()];
   const int lin = xcd_tile(blockIdx.x, p.tiles_m * p.tiles_n * p.G * p.nsplit);
   gemm_bf16_body<BM, BN, TA, TB, NS, KW, E, TAIL>(p, lin, smem);
-  if constexpr (TAIL == 1) gemm_ln_tail<E>(p, lin);
 }
 
 // ============================================================================ streaming launch
@@ -1276,12 +1168,6 @@ void launch_reduce(const GemmArgs& a, int G, long groups, hipStream_t s) {
 template <int BM, int BN, int NS, int KW = 1, typename E = bf16>
 void launch_bf16(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream_t s) {
   dim3 grid(a.tiles_m * a.tiles_n * G * nsplit);
-  if constexpr (BM == 64 && BN == 64) {
-    if (a.tail == 1) {                // row-block LayerNorm tail: forward layouts only (checked at launch)
-      hipLaunchKernelGGL((gemm_bf16_kernel<64, 64, false, false, NS, KW, E, 1>), grid, dim3(256 * KW), 0, s, a);
-      return;
-    }
-  }
   if constexpr (BM == 64 && (BN == 64 || (BN == 128 && KW == 1))) {
     if (a.tail == 2) {                // whole-row LayerNorm in the epilogue (forward layouts, tiles_n = 1)
       hipLaunchKernelGGL((gemm_bf16_kernel<64, BN, false, false, NS, KW, E, 2>), grid, dim3(256 * KW), 0, s, a);

@@ -1240,17 +1240,8 @@ void sra_dq_small_launch(const void* q, const void* k, const void* v, const void
                          long os, long dos, long dqs, float sl2, float scale, int dtype, hipStream_t s) {
   const dim3 grid(cdiv(N, 64), heads, Bt), block(64 * cdiv(Nk, KTILE));
   static int& seq = cmx_knob("SRA_DQ_SEQ", 1);      // sra_dq_small_seq (0: sra_dq_small)
-  // CMX_SRA_DQ_HALF=1: 32-query workgroups when the 64-query grid would leave CUs without a
-  // workgroup.  Measured slower (stage 4 of B2: 160 -> 320 workgroups, backward 25.0 -> 28.4 us:
-  // each one stages the (b, head)'s K / V for half the queries), so off by default
-  static int& half = cmx_knob("SRA_DQ_HALF", 0);
-  const bool h32 = seq && half && (long)grid.x * grid.y * grid.z < sra_cus();
-  const dim3 grid32(cdiv(N, 32), heads, Bt);
 #define CMX_SRA_DQS(E_)                                                                                            \
-  if (h32) hipLaunchKernelGGL((sra_dq_small_seq<E_, 1>), grid32, block, 0, s, (const E_*)q, (const E_*)k,          \
-                              (const E_*)v, (const E_*)o, (const E_*)dout, lse, Dws, (E_*)dq, N, Nk, heads, qs, kvs, \
-                              os, dos, dqs, sl2, scale);                                                            \
-  else if (seq) hipLaunchKernelGGL((sra_dq_small_seq<E_, 2>), grid, block, 0, s, (const E_*)q, (const E_*)k,       \
+  if (seq) hipLaunchKernelGGL((sra_dq_small_seq<E_, 2>), grid, block, 0, s, (const E_*)q, (const E_*)k,            \
                               (const E_*)v, (const E_*)o, (const E_*)dout, lse, Dws, (E_*)dq, N, Nk, heads, qs, kvs, \
                               os, dos, dqs, sl2, scale);                                                            \
   else hipLaunchKernelGGL(sra_dq_small<E_>, grid, block, 0, s, (const E_*)q, (const E_*)k, (const E_*)v,           \

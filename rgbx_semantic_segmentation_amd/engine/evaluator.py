@@ -244,9 +244,10 @@ class Evaluator(object):
             # Bounded cache: images of many sizes give many whole-image crop shapes,
             # and each graph would otherwise keep its own pool holding a full set of forward
             # activations.  Sharing one pool is safe: replays run in order on this stream and
-            # each output is consumed (window-accumulated) before the next replay.
-            while len(self._graphs) >= self.eval_graph_cap:
-                self._graphs.popitem(last=False)
+            # each output is consumed (window-accumulated) before the next replay.  The new graph
+            # is captured BEFORE the oldest are evicted: a graph sharing the pool must
+            # stay alive across the capture, or at cap 1 the pool's last user goes and the capture
+            # would draw on a released pool handle.
             sd, sx = d.contiguous().clone(), x.contiguous().clone()
             side = torch.cuda.Stream()
             side.wait_stream(torch.cuda.current_stream())
@@ -259,6 +260,8 @@ class Evaluator(object):
             if self._graph_pool is None:
                 self._graph_pool = graph.pool()
             g = self._graphs[key] = (graph, sd, sx, out)
+            while len(self._graphs) > self.eval_graph_cap:
+                self._graphs.popitem(last=False)
         self._graphs.move_to_end(key)
         graph, sd, sx, out = g
         sd.copy_(d)

@@ -93,7 +93,7 @@ class GLinear(Function):
         dx1 = dx2 = None
         if dgrad_tap is not None and ctx.needs_input_grad[9] and dz.is_contiguous():
             # the producer of x1 computes this input gradient inside its own backward launch
-            # (MixFFNF: fc2's dgrad fused with the DWConv / GELU backward)
+            # (the consumer norm's LayerNorm backward in the dgrad epilogue, cmx_gemm_ln_bwd)
             dgrad_tap.put((dz, W[:, :, :k1]))
         elif ctx.needs_input_grad[9]:
             dx1 = _dgrad(dz, W[:, :, :k1], torch.empty_like(x1))
@@ -131,19 +131,12 @@ def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1
         bg = store.g(bp).view(G, -1)
     ln = None
     N = W.shape[1]
-    if ln_tail is not None and ((LN_ROW and N <= 128 and N % 8 == 0) or (LN_TAIL and x1.shape[1] <= LN_TAIL_MAXM)):
+    if ln_tail is not None and LN_ROW and N <= 128 and N % 8 == 0:
         m = ln_tail.mod
         ln = (store.w(m.weight, compute=False).view(G, -1), store.w(m.bias, compute=False).view(G, -1), m.eps, ln_tail)
     return GLinear.apply(W, Wg, b, bg, wp, act, res, rscale, rps, x1, x2, tap, ln, dgrad_tap)
 
 
-# CMX_LN_TAIL=1: the LayerNorm after a residual Linear as the GEMM's row-block tail (cmx_gemm_ln)
-# instead of its own launch.  Off by default: measured slower on the B2 step (DESIGN.md round 5:
-# the tail GEMMs ran 25-30 us against 13 us + a 3-5 us LayerNorm launch -- the last arriver's
-# 64-row LayerNorm is 16 dependent passes of write-through loads on the critical path).
-# CMX_LN_TAIL_MAXM: only GEMMs of at most that many rows per group take the tail
-LN_TAIL = os.environ.get("CMX_LN_TAIL", "0") == "1"
-LN_TAIL_MAXM = int(os.environ.get("CMX_LN_TAIL_MAXM", "1000000000"))
 # CMX_LN_ROW=0: every LayerNorm forward as its own launch (A/B switch).  Default: a residual
 # Linear whose output row fits one GEMM tile (C <= 128: stages 1-2) normalises it in its epilogue
 # (cmx_gemm_ln, tail = 2): bit-identical statistics, no tickets, no second pass over the rows
@@ -706,82 +699,10 @@ def dwconv(store, conv, h, NI, ipg, H, W, act):
     return DWConvF.apply(h, w, b, wg, bg, NI, ipg, H, W, act, conv.weight)
 
 
-# ---------------------------------------------------------------------------- Mix-FFN bands
-# CMX_MIXFFN=1: the band kernels below instead of fc1, DWConv+GELU and fc2's input gradient as
-# separate launches.  Off by default: measured slower on the B2 step (41 / 27 us
-# per stage-3 / stage-4 band launch against ~22 / ~15 us for the GEMM + DWConv pair it replaces;
-# 3 interleaved A/B pairs 264.8 vs 268.9 img/s, profiles/r05_b_ab_mixffn.txt)
-MIXFFN_BAND = os.environ.get("CMX_MIXFFN", "0") == "1"
-# CMX_MIXFFN_TILE=1: the wide stages (W > 42: 1-2 of B2 / B4 480 x 640) run fc1 + DWConv + GELU (and
-# fc2's dgrad + the DW backward) as one launch over 12 x 16-pixel tiles (csrc/mixffn.hip 2-D tiles,
-# K = C = 64 / 128: one or two k-tiles).  Off by default: measured slower (69 us
-# per fused launch against 54 / 38 us for the stage-1 / stage-2 GEMM + DWConv pair; 260.7 vs 270.3
-# img/s, profiles/r05_l_ab_mixffn_tile.txt)
-MIXFFN_TILE = os.environ.get("CMX_MIXFFN_TILE", "0") == "1"
-# bands of fewer rows recompute too much of fc1 on their halo rows ((R + 2) / R): stage 3 / 4 of
-# B2 / B4 at 480 x 640 get R = 4 / 10, stage 2 (W = 80) would get R = 1
-MIXFFN_MIN_ROWS = int(os.environ.get("CMX_MIXFFN_MIN_ROWS", "4"))
-
-
-class MixFFNF(Function):
-    """fc1 + DWConv3x3 + GELU of Mix-FFN (dual_segformer.py:67-71) as ONE launch per direction
-    (csrc/mixffn.hip): forward cmx_mixffn_fwd (h = fc1(x), a = GELU(DW(h)), act'(z) saved);
-    backward cmx_mixffn_bwd computes fc2's input gradient da = dz2 W2 itself (fc2's GLinear
-    hands over dz2 and W2 through ``tap`` instead of launching its dgrad), the DWConv / GELU
-    backward and the DW weight-gradient partials; then fc1's input gradient and its queued
-    weight gradient, as GLinear's backward would."""
-
-    @staticmethod
-    def forward(ctx, W1, Wg1, b1, bg1, wdw, bdw, wgdw, bgdw, anchor, x, B, H, W, tap, ltap=None):
-        G, M, C = x.shape
-        Ch = W1.shape[1]
-        h = torch.empty(G, M, Ch, dtype=x.dtype, device=x.device)
-        gp = torch.empty_like(h)
-        a = torch.empty_like(h)
-        K.call("cmx_mixffn_fwd", K.ptr(x), K.ptr(W1), K.ptr(b1), K.ptr(wdw), K.ptr(bdw), K.ptr(h), K.ptr(gp), K.ptr(a),
-               G, B, H, W, C, Ch, W1.stride(0), b1.stride(0), wdw.stride(0), K.dtype_code(x), K.stream())
-        ctx.save_for_backward(W1, x, h, gp, wdw)
-        ctx.meta = (Wg1, bg1, wgdw, bgdw, B, H, W, tap, ltap)
-        ctx.set_materialize_grads(False)
-        return a
-
-    @staticmethod
-    def backward(ctx, da):
-        W1, x, h, gp, wdw = ctx.saved_tensors
-        Wg1, bg1, wgdw, bgdw, B, H, W, tap, ltap = ctx.meta
-        G, M, Ch = h.shape
-        C = x.shape[-1]
-        handed = tap.take() if tap is not None else None
-        nbytes = K.query("cmx_mixffn_bwd_workspace", G, B, H, W, Ch)
-        ws = K._ws(nbytes, h.device)
-        dh = torch.empty_like(h)
-        if handed is not None:
-            dz2, W2 = handed
-            K.call("cmx_mixffn_bwd", K.ptr(dz2), K.ptr(W2), K.ptr(wdw), K.ptr(h), K.ptr(gp), K.ptr(dh), K.ptr(ws), G, B,
-                   H, W, C, Ch, W2.stride(0), wdw.stride(0), K.dtype_code(h), K.stream())
-            P = nbytes // (40 * G * Ch)
-        else:            # fc2 ran its own input gradient: the separate DWConv / GELU backward
-            assert da is not None
-            nbytes = K.query("cmx_dwconv3x3_bwd_workspace", G * B, B, H, W, Ch)
-            ws = K._ws(nbytes, h.device)
-            K.call("cmx_dwconv3x3_bwd_saved", K.ptr(_c(da)), K.ptr(h), K.ptr(gp), K.ptr(wdw), K.ptr(dh), 0, 0,
-                   K.ptr(ws), G * B, B, H, W, Ch, 0, K.dtype_code(h), K.stream())
-            P = K.query("cmx_dwconv3x3_bwd_saved_tiles", B, H, W)
-        deferred.reduce(ws, wgdw, bgdw, G, P, P * Ch * 10, Ch * 10, Ch, 10, 9, wgdw.stride(0), 9, bgdw.stride(0), 1)
-        dx = None
-        if ctx.needs_input_grad[9]:
-            if ltap is not None:
-                # norm2's backward computes fc1's input gradient in its own launch (cmx_gemm_ln_bwd)
-                ltap.put((dh, W1))
-            else:
-                dx = _dgrad(dh, W1, torch.empty_like(x))
-        _wgrad_into(dh, x, Wg1, bg1)
-        return (None,) * 9 + (dx, None, None, None, None, None)
-
-
 class DgradTap:
     """Side channel from a GLinear's backward to the producer of its input: (dz, W) handed over
-    instead of the GLinear launching dx = dz W itself (MixFFNF fuses it into its backward)."""
+    instead of the GLinear launching dx = dz W itself (the producing norm's backward runs that
+    dgrad with the LayerNorm backward in its epilogue)."""
     __slots__ = ("t",)
 
     def __init__(self):
@@ -793,35 +714,6 @@ class DgradTap:
     def take(self):
         t, self.t = self.t, None
         return t
-
-
-def mixffn_ok(x, Ch, B, H, W) -> bool:
-    """The fused Mix-FFN kernels apply: 16-bit, hidden % 64, every operand in the ParamStore layout
-    (deferred weight gradients); 2-D tiles for wide images with C <= 128 (CMX_MIXFFN_TILE), bands
-    of >= CMX_MIXFFN_MIN_ROWS rows otherwise (CMX_MIXFFN=1)."""
-    if not (deferred.ENABLED and x.dtype in (torch.bfloat16, torch.float16) and x.is_contiguous() and Ch % 64 == 0
-            and x.shape[-1] % 8 == 0):
-        return False
-    if K.query("cmx_mixffn_mode", W) == 2:          # 2-D tiles (wide images, short K)
-        return MIXFFN_TILE and x.shape[-1] <= 128
-    return MIXFFN_BAND and K.query("cmx_mixffn_band_rows", W) >= MIXFFN_MIN_ROWS
-
-
-def mixffn(store, mlp, x, B, H, W, tap, ltap=None):
-    """a = GELU(DWConv(fc1(x))) (MixFFNF); ``tap`` is the DgradTap fc2's glinear hands dz2 to,
-    ``ltap`` the one this node hands fc1's (dh, W1) to (the producing norm's fused backward)."""
-    G = x.shape[0]
-    W1 = store.w(mlp.fc1.weight)
-    W1 = W1.view(G, W1.shape[1], -1)
-    Wg1 = store.g(mlp.fc1.weight).view(G, W1.shape[1], -1)
-    b1 = store.w(mlp.fc1.bias, compute=False).view(G, -1)
-    bg1 = store.g(mlp.fc1.bias).view(G, -1)
-    conv = mlp.dwconv.dwconv
-    wdw = store.w(conv.weight, compute=False).view(G, -1, 9)
-    bdw = store.w(conv.bias, compute=False).view(G, -1)
-    wgdw = store.g(conv.weight).view(G, -1, 9)
-    bgdw = store.g(conv.bias).view(G, -1)
-    return MixFFNF.apply(W1, Wg1, b1, bg1, wdw, bdw, wgdw, bgdw, mlp.fc1.weight, x, B, H, W, tap, ltap)
 
 
 # ---------------------------------------------------------------------------- conv (implicit GEMM / im2col + GEMM)
@@ -1245,6 +1137,12 @@ def pool_tickets(owner, x, B, C):
     return t
 
 
+# test hook (tests/test_config_parity.py): a dict makes FRMF's forward record each call's
+# post-ReLU channel-MLP hidden activation y1 (B, 4C) under id() of its ChannelWeights mlp.0 weight,
+# so a parity test can see which hidden units' ReLU decisions the GPU step took
+FRM_PROBE = None
+
+
 class FRMF(Function):
     """FeatureRectifyModule (net_utils.py:124-152) on x (2, B, N, C).
 
@@ -1275,6 +1173,8 @@ class FRMF(Function):
                K.stream())
         K.call("cmx_small_linear_fwd", K.ptr(pooled), K.ptr(W1), K.ptr(b1), K.ptr(y1), B, 4 * C, 4 * C, 2, K.stream())
         K.call("cmx_small_linear_fwd", K.ptr(y1), K.ptr(W2), K.ptr(b2), K.ptr(cw), B, 4 * C, 2 * C, 3, K.stream())
+        if FRM_PROBE is not None:
+            FRM_PROBE[id(anchor)] = y1.detach().clone()
         # h = cat(x1, x2) W0^T + b0 (SpatialWeights' first 1x1 conv, net_utils.py:72-73), cat-free
         h = torch.empty(1, B * N, C, dtype=x.dtype, device=x.device)
         K.gemm(x[0].view(1, B * N, C), W0[None], h, bias=b0[None], A2=x[1].view(1, B * N, C))

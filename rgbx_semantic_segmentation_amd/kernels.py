@@ -177,37 +177,16 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, bias: torch.Tensor |
     return C
 
 
-_TICKETS: dict = {}
-
-
-def _tickets(n: int, device) -> torch.Tensor:
-    """Zeroed uint32 arrival counters for row-block tails (cmx_gemm_ln), one pool per device:
-    every tail launch leaves its counters zero and the tails are issued by the encoder's main
-    chain, in stream order (a HIP-graph capture of the step keeps that order), so they share the
-    pool.  Sized once (B4 / B5 stage-1 row blocks fit), before any capture."""
-    device = torch.device(device)
-    key = device.index if device.index is not None else torch.cuda.current_device()
-    t = _TICKETS.get(key)
-    if t is None or t.numel() < n:
-        if torch.cuda.is_current_stream_capturing():
-            raise _lib.CMXError(f"gemm_ln: ticket pool of {0 if t is None else t.numel()} < {n} inside a capture")
-        t = _TICKETS[key] = torch.zeros(max(n, 8192), dtype=torch.int32, device=device)
-    return t
-
-
 def gemm_ln(A, B, C, ln_gamma, ln_beta, ln_eps, bias=None, residual=None, rscale=None, rows_per_sample=1,
             act="none", A2=None):
     """K.gemm's forward form (C = epi(A @ B^T)) plus the LayerNorm of C's rows in the same
     launch (cmx_gemm_ln): returns (y, mean, rstd), y = LN(C) in C's layout, mean / rstd (G, M)
     fp32; None when the problem is not eligible (the caller runs gemm + the LN kernel).
-    N <= 128 (N % 8 == 0): the LayerNorm runs in the GEMM's epilogue (one tile spans a row);
-    N % 64 == 0 up to 512: the row-block tail with arrival tickets."""
+    N <= 128 (N % 8 == 0): the LayerNorm runs in the GEMM's epilogue (one tile spans a row)."""
     G, M, K1 = A.shape
     Kd = K1 + (A2.shape[2] if A2 is not None else 0)
     N = B.shape[1]
-    row = N <= 128 and N % 8 == 0
-    if A.dtype not in (torch.bfloat16, torch.float16) or not (row or (N % 64 == 0 and N <= 512)) \
-            or not C.is_contiguous():
+    if A.dtype not in (torch.bfloat16, torch.float16) or not (N <= 128 and N % 8 == 0) or not C.is_contiguous():
         return None
     tA, lda, sA = _operand(A, "A")
     tB, ldb, sB = _operand(B, "B")
@@ -218,11 +197,10 @@ def gemm_ln(A, B, C, ln_gamma, ln_beta, ln_eps, bias=None, residual=None, rscale
     y = torch.empty_like(C)
     mean = torch.empty(G, M, dtype=torch.float32, device=C.device)
     rstd = torch.empty_like(mean)
-    tk = None if row else _tickets(query("cmx_gemm_ln_tickets", G, M), C.device)
     st = _lib.try_call("cmx_gemm_ln", ptr(A), ptr(A2), ptr(B), ptr(C), ptr(bias), ptr(residual), ptr(rscale), G, M, N, Kd, K1,
                          lda, lda2, ldb, C.stride(1), sA, sA2, sB, C.stride(0), sbias, int(rows_per_sample), ACT[act],
                          ptr(ln_gamma), ptr(ln_beta), ln_gamma.stride(0) if ln_gamma.dim() == 2 else 0,
-                         float(ln_eps), ptr(y), ptr(mean), ptr(rstd), ptr(tk), dtype_code(A), stream())
+                         float(ln_eps), ptr(y), ptr(mean), ptr(rstd), dtype_code(A), stream())
     if st == _lib.CMX_ERR_ARG:
         return None
     if st != 0:

@@ -157,22 +157,15 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
         tap_a = F.GradTap() if s_attn is not None else None
         t2 = F.LNTail(blk.norm2)
         x = F.glinear(store, a.proj.weight, a.proj.bias, o, res=xr, rscale=s_attn, rps=N, tap=tap_a, ln_tail=t2)
-        mix = F.mixffn_ok(x, blk.mlp.fc1.weight.shape[0], B, H, W)
         # norm2's backward rides on fc1's dgrad launch (C <= 128): fc1 hands (dz, W1) over
         ltap = F.DgradTap() if F.ln_bwd_fusable(x) else None
         h, _, xr = F.layernorm_res(store, blk.norm2, x, G, scale=s_attn, rps=N, tap=tap_a, tail=t2, dtap=ltap)
-        dtap = None
-        if mix:
-            # fc1 + DWConv + GELU in one launch; fc2's input gradient joins their backward launch
-            dtap = F.DgradTap()
-            f = F.mixffn(store, blk.mlp, h, B, H, W, dtap, ltap)
-        else:
-            f = F.glinear(store, blk.mlp.fc1.weight, blk.mlp.fc1.bias, h, dgrad_tap=ltap)
-            f = F.dwconv(store, blk.mlp.dwconv.dwconv, f, G * B, B, H, W, "gelu")
+        f = F.glinear(store, blk.mlp.fc1.weight, blk.mlp.fc1.bias, h, dgrad_tap=ltap)
+        f = F.dwconv(store, blk.mlp.dwconv.dwconv, f, G * B, B, H, W, "gelu")
         tap_m = F.GradTap() if s_mlp is not None else None
         tn = F.LNTail(next_norm) if next_norm is not None else None
         x = F.glinear(store, blk.mlp.fc2.weight, blk.mlp.fc2.bias, f, res=xr, rscale=s_mlp, rps=N, tap=tap_m,
-                      ln_tail=tn, dgrad_tap=dtap)
+                      ln_tail=tn)
         return x, (s_mlp, tap_m), tn
 
     def run(self, store, images, B, H, W, training, dp_scales: Optional[torch.Tensor], bn_group=None):
@@ -190,8 +183,6 @@ class RGBXTransformer(nn.Module):                 # dual_segformer.py:228-446
         bi = 0
         Hc, Wc, Cin = H, W, 3
         sync = getattr(self, "grad_sync", None)     # dist.BucketedGradSync (data parallel) or None
-        if sync is None:                            # optim.SegmentUpdate (update overlap) or None
-            sync = getattr(self, "seg_update", None)
         main = torch.cuda.current_stream() if x.is_cuda else None
         side = streams.ffm_stream(main.device) if (main is not None and streams.FFM_SIDE) else None
         for s in range(4):

@@ -1,6 +1,12 @@
-"""Roofline of the step's dominant kernels, measured live with HIP events on their launch stream.
+"""Roofline of the step's dominant kernels, measured live inside bench.py.
 
-1. ``measure_gemm_family`` -- the DOMINANT family of the CMX-B2 step by device time (the census
+0. ``measure_in_step`` -- the bench line's ``roofline`` since round 6: a
+   kernel trace (torch.profiler's roctracer activity records) of 10 replays of the captured
+   step; every launch is classified into its family by kernel name (the census regexes of
+   scripts/family_table.py), the family's device time per step is its summed kernel durations
+   / 10, and ``achieved`` = its algorithmic work per step (floor.step_work) / that time.  This
+   is the figure the committed ``profiles/*_family_table.md`` tables give for the same tree.
+1. ``measure_gemm_family`` -- kept as ``roofline.reissue``: the DOMINANT family of the CMX-B2 step by device time (the census
    of profiles/r05_*_step_census.txt: ~3.2 ms of ~7.3 ms): the MFMA tile GEMMs of the forward and
    input-gradient passes (``gemm_bf16_kernel`` / ``gemm_multi_kernel`` / split-K reduce: every
    Linear, 1x1 / implicit conv, the decoder's fuse products), ~250 launches per step.  During one
@@ -82,6 +88,141 @@ def _family_traffic(kernels, workload: str):
             n = sum(k["launches"] for k in ks)
             return sum(k["hbm_bytes_per_launch"] * k["launches"] for k in ks) / n, os.path.relpath(path, _ROOT)
     return None, None
+
+
+# kernel-name -> family of the step census (the regexes of scripts/family_table.py; first match wins,
+# so the grouped weight-gradient launch is not counted as a tile GEMM)
+FAMILY_RE = (
+    ("wgrad", r"gemm_grouped_kernel|reduce_grouped_kernel"),
+    ("gemm", r"gemm_bf16_kernel|gemm_stream|gemm_multi|gemm_generic|splitk_reduce"),
+    ("sra", r"sra_"),
+    ("dwconv", r"dw2_|dw_"),
+    ("layernorm", r"ln_fwd|ln_bwd|rowln"),
+    ("adamw", r"adamw"),
+    ("batchnorm", r"bn_"),
+    ("frm", r"pool_|linear_fwd|linear_bwd|combine_|frm_|reduce_partials"),
+    ("ffm", r"ffm_"),
+    ("ce", r"ce_|upsample"),
+    ("bilinear", r"bilinear"),
+    ("im2col", r"im2col|col2im"),
+    ("pe1", r"pe1_"),
+)
+
+
+def family_of(kernel: str) -> str:
+    import re
+    for fam, rx in FAMILY_RE:
+        if re.search(rx, kernel):
+            return fam
+    return "other"
+
+
+def trace_kernels(run_step, steps: int):
+    """Kernel records [(name, start_us, duration_us)] of ``steps`` calls of ``run_step`` (graph
+    replays), from the in-process kineto / roctracer activity trace (the same dispatch
+    timestamps a ``rocprofv3 --kernel-trace`` run reports).  [] when the tracer delivers none."""
+    from torch.profiler import profile, ProfilerActivity
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        for _ in range(steps):
+            run_step()
+        torch.cuda.synchronize()
+    out = []
+    for e in prof.profiler.kineto_results.events():
+        if e.device_type() != torch.autograd.DeviceType.CUDA:
+            continue
+        name = e.name()
+        if "Memcpy" in name or "Memset" in name:
+            continue
+        out.append((name, e.start_ns() / 1e3, e.duration_ns() / 1e3))
+    out.sort(key=lambda r: r[1])
+    return out
+
+
+# the first kernel of every training step (the DropPath / Dropout2d mask draw): step boundary
+STEP_FIRST = "step_masks_kernel"
+
+
+def split_steps(recs):
+    """The traced kernels cut into steps at each STEP_FIRST launch; only COMPLETE steps are kept
+    (the activity tracer can drop records: a step is complete when it holds the largest launch
+    count seen, the count of the captured graph).  Returns a list of per-step record lists."""
+    idx = [i for i, r in enumerate(recs) if STEP_FIRST in r[0]]
+    if not idx:
+        return []
+    segs = [recs[a:b] for a, b in zip(idx, idx[1:] + [len(recs)])]
+    full = max(len(sg) for sg in segs)
+    return [sg for sg in segs if len(sg) == full]
+
+
+def measure_in_step(run_step, workload: str, shape: dict, n_params: float, steps: int = 10):
+    """The step's kernel families from a kernel trace of ``steps`` graph replays: device time and
+    launches per step of each family, against its algorithmic work (floor.step_work: FLOPs and
+    bytes, each tensor read once and written once).  ``roofline`` is the dominant family by time:
+    ``achieved`` = its algorithmic bytes (HBM-bound) or FLOPs per step / its summed in-step
+    kernel time -- the time those launches take inside the replayed step, next to their
+    neighbours, not re-issued in isolation."""
+    recs = trace_kernels(run_step, steps)
+    if not recs:
+        return None, None
+    segs = split_steps(recs)
+    if segs:                         # complete steps only
+        recs = [r for sg in segs for r in sg]
+        steps = len(segs)
+    work = step_work(n_params=n_params, **shape)
+    fams = {}
+    for name, _, us in recs:
+        f = fams.setdefault(family_of(name), [0.0, 0])
+        f[0] += us
+        f[1] += 1
+    busy = sum(v[0] for v in fams.values()) / steps
+    table = {}
+    for fam, (us, n) in sorted(fams.items(), key=lambda kv: -kv[1][0]):
+        t = us / steps * 1e-6
+        fl, by = work[fam] if fam in work else (0.0, 0.0)
+        row = {"us_per_step": round(t * 1e6, 1), "launches_per_step": round(n / steps, 1),
+               "share_of_busy": round(t * 1e6 / busy, 4)}
+        if by:
+            row.update({"alg_gb": round(by / 1e9, 4), "tbs": round(by / t / 1e12, 3),
+                        "hbm_frac": round(by / t / (PEAK_HBM_GBS * 1e9), 4)})
+        if fl:
+            row.update({"alg_gflop": round(fl / 1e9, 2), "mfma_frac": round(fl / t / (PEAK_BF16_TFLOPS * 1e12), 4)})
+        table[fam] = row
+    dom = max((f for f in fams if f in work and work[f][1] > 0), key=lambda f: fams[f][0])
+    us, n = fams[dom]
+    t = us / steps * 1e-6
+    nl = n / steps
+    flops, nbytes = work[dom]
+    hbm = flops / nbytes < RIDGE_FLOP_PER_BYTE
+    gbs, tflops = nbytes / t / 1e9, flops / t / 1e12
+    kern = {"gemm": ("gemm_bf16_kernel", "gemm_stream_kernel", "gemm_multi_kernel", "splitk_reduce_kernel"),
+            "wgrad": ("gemm_grouped_kernel",)}.get(dom, ())
+    traffic, src = _family_traffic(kern, workload) if kern else (None, None)
+    roof = {"kernel": f"{dom} family in the replayed step ({nl:.0f} launches per step; kernel trace of {steps} "
+                      f"HIP-graph replays)",
+            "family": dom, "bound": "hbm" if hbm else "mfma",
+            "achieved": round(gbs, 1) if hbm else round(tflops, 2),
+            "peak": PEAK_HBM_GBS if hbm else PEAK_BF16_TFLOPS,
+            "unit": "GB/s" if hbm else "TFLOP/s",
+            "frac": round(gbs / PEAK_HBM_GBS if hbm else tflops / PEAK_BF16_TFLOPS, 4),
+            "traffic": traffic,
+            "arithmetic_intensity_flop_per_byte": round(flops / nbytes, 1),
+            "ridge_flop_per_byte": round(RIDGE_FLOP_PER_BYTE, 1),
+            "achieved_tflops": round(tflops, 2), "mfma_frac": round(tflops / PEAK_BF16_TFLOPS, 4),
+            "achieved_hbm_gbs": round(gbs, 1), "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
+            "launches": round(nl, 1), "avg_launch_us": round(t / nl * 1e6, 2), "total_us": round(t * 1e6, 1),
+            "algorithmic_flop_per_launch": flops / nl, "algorithmic_bytes_per_launch": nbytes / nl,
+            "algorithmic_bytes_per_step": nbytes, "workload": workload,
+            "timing": f"in-step: kernel durations of {steps} complete replayed steps (torch.profiler / roctracer "
+                      f"activity records, steps cut at {STEP_FIRST}), summed per family and divided by {steps}"}
+    if src:
+        roof["traffic_source"] = src
+        roof["traffic_over_algorithmic"] = round(traffic / (nbytes / nl), 3)
+    walls = [sg[-1][1] + sg[-1][2] - sg[0][1] for sg in segs] if segs else []
+    return roof, {"busy_us_per_step": round(busy, 1), "launches_per_step": round(len(recs) / steps, 1),
+                  "complete_steps_traced": steps if segs else None,
+                  "wall_us_per_step_median": round(sorted(walls)[len(walls) // 2], 1) if walls else None,
+                  "families": table}
 
 
 def measure_gemm_family(model, batch, workload: str, shape: dict, warm: int = 4, iters: int = 16):

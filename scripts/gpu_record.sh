@@ -14,7 +14,7 @@ TAG=${1:?tag}
 SKIP_SUITE=${2:-}
 timeout -k 10 400 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
 rc=$?; echo "bench rc=$rc"; cut -c1-400 gpurun_out/bench_$TAG.json; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run -- python3 bench.py --steps 20 --warmup 5 \
+CMX_BENCH_NO_ROOFLINE=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run -- python3 bench.py --steps 20 --warmup 5 \
   --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1 || exit $?
 db=$(ls gpurun_out/prof_$TAG/*.db gpurun_out/prof_$TAG/*/*.db 2>/dev/null | head -1)
 python3 scripts/prof_summary.py $db 10 > gpurun_out/profiles/${TAG}_kernel_stats.txt 2>&1

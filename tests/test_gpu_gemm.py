@@ -351,19 +351,15 @@ def test_gemm_h2_per_head(dev, dtype, GB, heads, N, D):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("G,M,N,K,res", [(2, 38400, 64, 256, True), (2, 9600, 128, 512, True), (2, 2400, 320, 1280, True),
-                                         (2, 600, 512, 2048, True), (2, 2400, 320, 320, False), (1, 130, 128, 64, True),
-                                         (2, 600, 512, 512, True), (2, 4800, 32, 128, True), (2, 1000, 64, 64, True),
+@pytest.mark.parametrize("G,M,N,K,res", [(2, 38400, 64, 256, True), (2, 9600, 128, 512, True), (1, 130, 128, 64, True),
+                                         (2, 4800, 32, 128, True), (2, 1000, 64, 64, True),
                                          (1, 77, 128, 128, False), (2, 2400, 128, 128, True),
                                          # stage-1 proj -> norm2 (1200 tiles, K = 64): the streaming grid
                                          (2, 38400, 64, 64, True)])
 def test_gemm_ln_tail(dev, dtype, G, M, N, K, res):
-    """cmx_gemm_ln: the GEMM output is the plain launch's, bit for bit (the tail only changes the
-    store's cache policy), and the row-block LayerNorm tail equals cmx_layernorm_fwd on that
-    output (same two-pass fp32 statistics; y within one 16-bit rounding).  Several launches in a
-    row on the shared ticket pool: every launch must leave the counters zero.  N <= 128: the
-    LayerNorm runs in the epilogue (tail = 2) and sums exactly as ln_fwd_kernel -- statistics and
-    y bit-identical."""
+    """cmx_gemm_ln: the GEMM output is the plain launch's, bit for bit, and the LayerNorm in its
+    epilogue (N <= 128: one tile spans the row) sums exactly as ln_fwd_kernel -- statistics and y
+    bit-identical to cmx_layernorm_fwd on that output.  Wider rows are refused (None)."""
     from rgbx_semantic_segmentation_amd import kernels as Kk
     torch.manual_seed(1)
     A = torch.randn(G, M, K, device="cuda").to(dtype)
@@ -387,11 +383,10 @@ def test_gemm_ln_tail(dev, dtype, G, M, N, K, res):
         torch.cuda.synchronize()
         assert (mean.flatten() - m0).abs().max().item() < 1e-5 * max(1.0, m0.abs().max().item())
         assert ((rstd.flatten() - r0).abs() / r0).max().item() < 1e-5
-        ulp = 2.0 ** (-7 if dtype == torch.bfloat16 else -10)
-        assert ((y.float() - y0.float()).abs() / y0.float().abs().clamp_min(1.0)).max().item() <= ulp, rep
-        if N <= 128:
-            assert torch.equal(mean.flatten(), m0) and torch.equal(rstd.flatten(), r0) and torch.equal(y, y0), rep
-    assert int(Kk._tickets(1, torch.device("cuda")).abs().sum().item()) == 0
+        assert torch.equal(mean.flatten(), m0) and torch.equal(rstd.flatten(), r0) and torch.equal(y, y0), rep
+    Cw = torch.empty(G, M, 320, device="cuda", dtype=dtype)
+    Ww = (torch.randn(G, 320, K, device="cuda") / math.sqrt(K)).to(dtype)
+    assert Kk.gemm_ln(A, Ww, Cw, torch.ones(G, 320, device="cuda"), torch.zeros(G, 320, device="cuda"), 1e-6) is None
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])

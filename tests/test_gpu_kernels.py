@@ -114,6 +114,39 @@ def test_sra_attention(dev, dtype, Bt, N, Nk, heads, D, qmul=1.0):
     assert relerr(dkv[..., C:], kvr.grad[..., C:]) < TOL[dtype] * 2, relerr(dkv[..., C:], kvr.grad[..., C:])
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("Bt,N,Nk,heads", [(4, 1200, 300, 5), (8, 1200, 300, 5), (4, 300, 300, 8), (8, 300, 300, 8)])
+def test_sra_fwd_kernel_choice(dev, dtype, Bt, N, Nk, heads):
+    """Stage-3 / 4 SRA forward of B2 (Bt = 2 x 2) and B4 (Bt = 2 x 4) at 480 x 640
+    (dual_segformer.py:119-134) on both forward kernels: the short-sequence one (keys split over
+    waves) and the general LDS-resident one (CMX_SRA_SMALL_FWD_N below N).  Both must sit at the
+    bf16 storage error against fp64, and neither more than 2x the other's error (+ one bf16 ulp of
+    the output scale): they differ only in summation order."""
+    from rgbx_semantic_segmentation_amd import kernels as K
+    torch.manual_seed(11)
+    D = 64
+    C = heads * D
+    q = torch.randn(Bt, N, C, dtype=torch.float64)
+    kv = torch.randn(Bt, Nk, 2 * C, dtype=torch.float64)
+    qd = q.to(dev, dtype)
+    kvd = kv.to(dev, dtype).contiguous()
+    o_ref = sra_ref(qd.double().cpu(), kvd.double().cpu(), heads, D)   # exact on the rounded inputs
+    base = K.tune_get("SRA_SMALL_FWD_N")
+    errs = {}
+    try:
+        for name, thr in (("small", 1 << 20), ("general", 0)):
+            K.tune("SRA_SMALL_FWD_N", thr)
+            o, lse = K.sra_attn_fwd(qd, kvd, kvd[..., C:], Bt, N, Nk, heads, D, D ** -0.5, C, 2 * C)
+            torch.cuda.synchronize()
+            errs[name] = relerr(o, o_ref)
+    finally:
+        K.tune("SRA_SMALL_FWD_N", base if base >= 0 else 2048)
+    ulp = 2.0 ** -8 if dtype == torch.bfloat16 else 2.0 ** -11
+    for e in errs.values():
+        assert e < ulp, errs
+    assert errs["general"] <= 2 * errs["small"] + ulp and errs["small"] <= 2 * errs["general"] + ulp, errs
+
+
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("B,h,w,K", [(2, 120, 160, 40), (1, 15, 20, 9), (2, 16, 24, 19)])
 @pytest.mark.parametrize("fused", [True, False])

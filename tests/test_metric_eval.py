@@ -199,6 +199,29 @@ def test_evaluator_runs_hip_model(dev):
 
 
 @pytest.mark.gpu
+def test_evaluator_graph_cache_of_one(dev):
+    """CMX_EVAL_GRAPHS=1: with a one-graph cache, a second crop shape must capture
+    while the first shape's graph -- the shared pool's only user -- is still alive, and then
+    evict it; both shapes replay the eager result."""
+    from rgbx_semantic_segmentation_amd.engine.evaluator import Evaluator
+    from rgbx_semantic_segmentation_amd.models.builder import EncoderDecoder
+    torch.manual_seed(0)
+    K = 9
+    model = EncoderDecoder(dict(backbone="mit_b0", num_classes=K, compute_dtype="bfloat16",
+                                decoder_embed_dim=256)).to(dev)
+    rng = np.random.default_rng(2)
+    img = rng.uniform(0, 255, (64, 96, 3))
+    ev = Evaluator(None, K, [0.485, 0.456, 0.406], [0.229, 0.224, 0.225], model, [1.0], False, [0])
+    ev.eval_graph_cap = 1
+    got = [ev.sliding_scores_rgbX(img, img, c, 2 / 3, dev).clone() for c in ((64, 64), (64, 96), (64, 64))]
+    assert len(ev._graphs) == 1
+    ev.eval_graph = False
+    exp = [ev.sliding_scores_rgbX(img, img, c, 2 / 3, dev) for c in ((64, 64), (64, 96), (64, 64))]
+    for a, b in zip(got, exp):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("flip", [False, True])
 def test_evaluator_batched_windows_match_single(dev, flip):
     """Crops of every scale batched into shared forwards give the per-crop result (a network
