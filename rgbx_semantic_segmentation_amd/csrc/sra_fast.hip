@@ -1212,15 +1212,16 @@ bool sra_small_ok(int D, int N, int Nk, int dtype, const void* const* ptrs, int 
   return N <= small_n && sra_fast_ok(D, Nk, dtype, ptrs, nptr, strides, nstr);
 }
 
-// the forward takes the short-sequence kernel only up to CMX_SRA_SMALL_FWD_N queries (default 2048,
-// the backward's limit).  Measured standalone (profiles/r05_e_sra_standalone.txt, Bt = 4, Nk = 300):
-// N = 1200 x 5 heads 16.0 us small vs 11.9 us fast; N = 300 x 8 heads 9.0 vs 10.6 us.  600 (the fast
-// forward at stage 3) is not the default: its different (equally valid) summation order moves the
-// config-4 stage-4 CM-FRM channel-MLP units inside the ReLU band past the parity test's 5 % exclusion
-// cap (tests/test_config_parity.py, r05_f: ratio 18.4 on FRMs.3.channel_weights.mlp.0.bias)
+// the forward takes the short-sequence kernel only up to CMX_SRA_SMALL_FWD_N queries (default 600:
+// stage 4; stage 3's N = 1200 runs the general LDS-resident forward).  Measured standalone
+// (profiles/r05_e_sra_standalone.txt, Bt = 4, Nk = 300): N = 1200 x 5 heads 16.0 us small vs 11.9 us
+// fast; N = 300 x 8 heads 9.0 vs 10.6 us.  Both forwards sit at the same error against fp64 at the
+// B2 / B4 stage-3 / 4 shapes (tests/test_gpu_kernels.py::test_sra_fwd_kernel_choice); the round-5
+// config-4 trip (FRMs.3.channel_weights.mlp.0.bias ratio 18.4) was the parity test's ReLU-band cap,
+// which now excludes exactly the rows whose ReLU decision flipped
 bool sra_small_fwd_ok(int D, int N, int Nk, int dtype, const void* const* ptrs, int nptr, const long* strides,
                       int nstr) {
-  static int& small_fwd_n = cmx_knob("SRA_SMALL_FWD_N", 2048);
+  static int& small_fwd_n = cmx_knob("SRA_SMALL_FWD_N", 600);
   return N <= small_fwd_n && sra_small_ok(D, N, Nk, dtype, ptrs, nptr, strides, nstr);
 }
 

@@ -40,7 +40,7 @@ class BucketedGradSync:
     FusedAdamW.step) joins the side stream into the current one and returns the 1/P scale
     the AdamW kernel applies."""
 
-    def __init__(self, store, group=None, overlap=None, payload=None, chunk_mb=None):
+    def __init__(self, store, group=None, overlap=None, payload=None, chunk_mb=None, groups=None):
         import os
         self.store = store
         self.group = group
@@ -60,21 +60,41 @@ class BucketedGradSync:
         # the vectorized cast / shard-sum kernels (a fractional MB would otherwise misalign)
         self.chunk = max(1024, (int(mb * 2 ** 20) // (2 if self.payload == "bf16" else 4)) // 64 * 64)
         self.ranges = {sid: (a, b) for sid, a, b in store.segments}
+        # CMX_DP_GROUPS (default 2): the backward-completion segments are exchanged in this many
+        # groups of consecutive segments -- each group's queued weight gradients flushed as ONE
+        # grouped launch and all-reduced together once the backward has passed the group's last
+        # stage.  4 = one exchange per segment (round 5: the per-segment flushes cut the grouped
+        # weight-gradient launch in four and the side-stream joins left the CUs idle, 6 % off the
+        # step at world size 1); 2 = decode head + stage 4 + stage 3 mid-backward, stages 2 + 1 at
+        # the end of the backward
+        ng = int(os.environ.get("CMX_DP_GROUPS", "2")) if groups is None else int(groups)
+        sids = sorted(self.ranges)
+        ng = max(1, min(ng, len(sids)))
+        per = -(-len(sids) // ng)
+        self.group_of = {sid: i // per for i, sid in enumerate(sids)}
+        self.group_last = {}
+        for sid in sids:
+            self.group_last[self.group_of[sid]] = sid
         self.works = []
         self.launched = set()
         self._armed = False
         self.side = None
 
     def _launch(self, sid):
-        """Flush the queued gradient work, then all-reduce segment ``sid`` on the side stream:
-        the side stream waits for the backward so far, the blocking all-reduce blocks only the
-        side stream, and the main stream runs on.  (A plain stream fork/join, so it is also
-        captured into the step's HIP graph; async_op works are not capture-safe here.)"""
+        """Flush the queued gradient work, then all-reduce the group of segments ending at
+        ``sid`` on the side stream: the side stream waits for the backward so far, the blocking
+        all-reduce blocks only the side stream, and the main stream runs on.  (A plain stream
+        fork/join, so it is also captured into the step's HIP graph; async_op works are not
+        capture-safe here.)"""
         from . import deferred
         if sid in self.launched or sid not in self.ranges:
             return
+        g = self.group_of[sid]
+        members = [s for s in sorted(self.ranges) if self.group_of[s] == g and s not in self.launched]
         deferred.flush()
-        a, b = self.ranges[sid]
+        # the group's segments are consecutive in the flat buffer: one range
+        a = min(self.ranges[s][0] for s in members)
+        b = max(self.ranges[s][1] for s in members)
         main = torch.cuda.current_stream() if self.store.grad.is_cuda else None
         if main is None:                         # CPU tensors (gloo tests): blocking, in order
             self._reduce(self.store.grad[a:b])
@@ -85,7 +105,7 @@ class BucketedGradSync:
             with torch.cuda.stream(self.side):
                 self._reduce(self.store.grad[a:b])
             self.works.append(self.side)
-        self.launched.add(sid)
+        self.launched.update(members)
 
     def _world(self) -> int:
         return dist.get_world_size(self.group)
@@ -146,8 +166,9 @@ class BucketedGradSync:
             if not self._armed:
                 self._armed = True
                 torch.autograd.Variable._execution_engine.queue_callback(self._finish_backward)
+            # every group whose last segment the backward has passed
             for s in sorted(self.ranges):
-                if s <= sid:
+                if s <= sid and self.group_last[self.group_of[s]] <= sid:
                     self._launch(s)
             return None
         return hook

@@ -1169,8 +1169,8 @@ class FRMF(Function):
         cw = torch.empty(B, 2 * C, dtype=torch.float32, device=x.device)
         # ChannelWeights (net_utils.py:11-30): avg || max pool + both MLP GEMVs
         ws = K._ws(K.query("cmx_frm_pool_workspace", B, N, C), x.device)
-        K.call("cmx_frm_pool_fwd", K.ptr(x), K.ptr(pooled), K.ptr(argmax), K.ptr(ws), K.ptr(pool_tickets(anchor, x, B, C)), B, N, C, dt,
-               K.stream())
+        K.call("cmx_frm_pool_fwd", K.ptr(x), K.ptr(pooled), K.ptr(argmax), K.ptr(ws), K.ptr(pool_tickets(anchor, x, B, C)),
+               B, N, C, dt, K.stream())
         K.call("cmx_small_linear_fwd", K.ptr(pooled), K.ptr(W1), K.ptr(b1), K.ptr(y1), B, 4 * C, 4 * C, 2, K.stream())
         K.call("cmx_small_linear_fwd", K.ptr(y1), K.ptr(W2), K.ptr(b2), K.ptr(cw), B, 4 * C, 2 * C, 3, K.stream())
         if FRM_PROBE is not None:

@@ -5,8 +5,10 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r06
 P="python -u -m pytest -x -v --timeout 900 --timeout-method thread"
+timeout -k 10 240 python -u -m pytest -x -v --timeout 60 --timeout-method thread tests/test_gpu_modules.py -k "frm_channel_one_launch or frm_pool_one_launch" > gpurun_out/r06/b_frm.log 2>&1
+rc=$?; echo "frm rc=$rc"; tail -3 gpurun_out/r06/b_frm.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 $P tests/test_gpu_kernels.py::test_sra_fwd_kernel_choice tests/test_metric_eval.py::test_evaluator_graph_cache_of_one \
-  tests/test_gpu_gemm.py -k "ln or sra or graph_cache" > gpurun_out/r06/b_unit.log 2>&1
+  tests/test_gpu_gemm.py tests/test_gpu_modules.py -k "ln or sra or graph_cache or frm" > gpurun_out/r06/b_unit.log 2>&1
 echo "unit rc=$?"; tail -3 gpurun_out/r06/b_unit.log
 timeout -k 10 300 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_optim.py > gpurun_out/r06/b_optim.log 2>&1
 echo "optim rc=$?"; tail -2 gpurun_out/r06/b_optim.log
