@@ -4,8 +4,8 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r06
-timeout -k 10 300 python -u -m pytest -v -s --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k "sra_fwd_kernel_choice" > gpurun_out/r06/c_sra.log 2>&1
-echo "sra rc=$?"; grep "sra fwd" gpurun_out/r06/c_sra.log | head -8
+timeout -k 10 300 python -u -m pytest -v -s --timeout 120 --timeout-method thread tests/test_gpu_kernels.py tests/test_gpu_gemm.py -k "sra_fwd_kernel_choice or gemm_ln" > gpurun_out/r06/c_sra.log 2>&1
+rc=$?; echo "sra/ln rc=$rc"; grep "sra fwd" gpurun_out/r06/c_sra.log | head -8; tail -3 gpurun_out/r06/c_sra.log; [ $rc -le 1 ] || exit $rc
 CMX_PARITY_OUT=gpurun_out/r06/parity_c timeout -k 10 1500 python -u -m pytest -v -s --timeout 1200 --timeout-method thread tests/test_config_parity.py > gpurun_out/r06/c_par.log 2>&1
 echo "parity rc=$?"; grep -E "PASSED|FAILED|worst" gpurun_out/r06/c_par.log | head -20
 timeout -k 10 400 python -u bench.py --no-cpu-baseline > gpurun_out/r06/c_bench.json 2> gpurun_out/r06/c_bench.err
