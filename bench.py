@@ -26,22 +26,31 @@ import time
 
 
 def _graph_streams_env(argv, env):
-    """The HIP graph executor's stream count for a single-GPU run: 2 (CMX_GRAPH_STREAMS, 0 = the
-    runtime default of 4).  The replayed step has two concurrent chains (the encoder / decoder
-    and the FFM branch on its side stream); with the default four executor streams the main
-    chain's nodes are dealt round-robin over several hardware queues and every hand-over is a
-    cross-queue wait (~9 us each in the kernel traces).  Measured (DESIGN.md round 5, 3
-    interleaved pairs): 272.5 vs 269.5 img/s.  Set before torch loads the HIP runtime (the
-    runtime reads its flags at load); multi-rank runs keep the runtime default."""
-    gpus = 1
-    for i, a in enumerate(argv):
-        if a == "--gpus" and i + 1 < len(argv):
-            gpus = int(argv[i + 1])
-        elif a.startswith("--gpus="):
-            gpus = int(a.split("=", 1)[1])
+    """The HIP graph executor's stream count: 2 (CMX_GRAPH_STREAMS, 0 = the runtime default of 4).
+    The replayed step has two concurrent chains (the encoder / decoder and the FFM branch on its
+    side stream); with the default four executor streams the main chain's nodes are dealt
+    round-robin over several hardware queues and every hand-over is a cross-queue wait (~9 us each
+    in the kernel traces).  Measured (DESIGN.md round 5, 3 interleaved pairs): 272.5 vs 269.5
+    img/s; the data-parallel step (RCCL segment all-reduces on a third captured stream) rehearsed
+    at world size 1 under the same setting (round 6: 246.9 vs 251.0 img/s without the DP path), so
+    every rank of an N-GPU run takes it too.  Never more executor streams than the process has
+    hardware queues (GPU_MAX_HW_QUEUES): the count is clamped to it.  Set before torch loads the
+    HIP runtime (the runtime reads its flags at load)."""
     n = env.get("CMX_GRAPH_STREAMS", "2")
-    if n != "0" and "DEBUG_HIP_FORCE_GRAPH_QUEUES" not in env and gpus == 1 and int(env.get("WORLD_SIZE", "1")) == 1:
-        env["DEBUG_HIP_FORCE_GRAPH_QUEUES"] = n
+    hwq = env.get("GPU_MAX_HW_QUEUES")
+    if "DEBUG_HIP_FORCE_GRAPH_QUEUES" in env:
+        n = env["DEBUG_HIP_FORCE_GRAPH_QUEUES"]
+        if hwq and int(n) > int(hwq):
+            raise SystemExit(f"[bench] DEBUG_HIP_FORCE_GRAPH_QUEUES={n} exceeds GPU_MAX_HW_QUEUES={hwq}: the HIP "
+                             f"graph executor would deal the step over more streams than the process has queues")
+        return
+    if n == "0":
+        n = "4"                                  # the runtime's own choice
+        if not (hwq and int(hwq) < 4):
+            return
+    if hwq and int(n) > int(hwq):
+        n = hwq
+    env["DEBUG_HIP_FORCE_GRAPH_QUEUES"] = n
 
 
 if __name__ == "__main__":
@@ -503,6 +512,7 @@ def main():
                        "image": [args.height, args.width], "classes": args.classes,
                        "parallelism": f"dp{world}", "hip_graph": graph is not None,
                        "hip_graph_streams": os.environ.get("DEBUG_HIP_FORCE_GRAPH_QUEUES", "runtime default"),
+                       "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "runtime default"),
                        "loss_scaling": bool(args.loss_scaling)},
             "step_mfma_roofline": {"train_gflop_per_image": round(fl_img / 1e9, 3),
                                    "achieved_tflops": round((ips / world) * fl_img / 1e12, 2),

@@ -220,20 +220,14 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
   a.kt_per_split = (nk + splitk - 1) / splitk;
   splitk = (nk + a.kt_per_split - 1) / a.kt_per_split;      // no empty splits
   a.nsplit = splitk;
-  // LayerNorm of C's rows in the same launch (tail = 2): one 64 x 64 / 64 x 128 tile spans the row
-  // (N <= 128) and the lanes that store it normalise it; at N = 320 / 512 (stages 3 / 4) a 64 x N
-  // tile, one block per CU, where the row block's whole weight panel (K x N) stays small enough to
-  // stream per block (K * N <= 1280 * 320: proj at stages 3 / 4, fc2 at stage 3; the stage-4 fc2,
-  // K = 2048, keeps its own LayerNorm launch)
+  // LayerNorm of C's rows in the same launch (tail = 2): N <= 128, one 64 x 64 / 64 x 128 tile
+  // spans the row and the lanes that store it normalise it
   const bool row_ln = tail != nullptr;
-  const bool wide_ln = tail && (N == 320 || N == 512);
   if (tail) {
-    CMX_REQUIRE(fast && ((N <= 128 && N % 8 == 0) || (wide_ln && (long)K * N <= 1280L * 320)) && splitk == 1 &&
-                    !transA && !transB && out_mode == 0 && !ones_col && !a.nup && !a.scatter && gh == 1 && !mask &&
-                    a.cvec && dtype != 0,
+    CMX_REQUIRE(fast && N <= 128 && N % 8 == 0 && splitk == 1 && !transA && !transB && out_mode == 0 && !ones_col &&
+                    !a.nup && !a.scatter && gh == 1 && !mask && a.cvec && dtype != 0,
                 CMX_ERR_ARG, "gemm_ln: the LayerNorm epilogue needs the 16-bit path without split-K, forward layouts, a "
-                "plain aligned store and N <= 128 (N %% 8 == 0) or N = 320 / 512 with K * N <= 409600 (G=%d M=%d N=%d "
-                "K=%d)", G, M, N, K);
+                "plain aligned store and N <= 128, N %% 8 == 0 (G=%d M=%d N=%d K=%d)", G, M, N, K);
     CMX_REQUIRE(tail->gamma && tail->beta && tail->y && tail->mean && tail->rstd && ((uintptr_t)tail->y & 15) == 0 &&
                     tail->y != C, CMX_ERR_ARG, "gemm_ln: LayerNorm buffers");
     a.tail = 2; a.ln_gamma = tail->gamma; a.ln_beta = tail->beta; a.ln_sg = tail->sg; a.ln_y = tail->y;
@@ -270,7 +264,7 @@ int gemm_impl(const void* A, const void* A2, const void* B, void* C, const float
   if (fast) {
     int bm, bn;
     plan_tiles(G, M, nb, K, &bm, &bn);
-    if (row_ln || lnb) bm = 64, bn = N <= 64 ? 64 : N <= 128 ? 128 : N;   // one tile spans the row
+    if (row_ln || lnb) bm = 64, bn = N <= 64 ? 64 : 128;   // one tile spans the row
     if (lnb && a.scatter) bn = scC;                         // (one tap's C channels)
     // 64 x 64 tiles that overflow one round of resident blocks by less than CMX_GEMM_MID percent
     // (5 per CU) take 64 x 128 tiles instead: one round of blocks twice as long, not a second

@@ -583,14 +583,14 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
   // refilled was last read in the previous iteration, which every wave has left.
   constexpr int PER = BM / 32 + BN / 32;        // LDS-DMA instructions per stage per wave
   auto wait_keep = [](int keep) {               // all but the `keep` most recent tiles landed
-    if constexpr (NS > 7) { if (keep >= 7) { vm_wait<7 * PER>(); return; } }
-    if constexpr (NS > 6) { if (keep >= 6) { vm_wait<6 * PER>(); return; } }
-    if constexpr (NS > 5) { if (keep == 5) { vm_wait<5 * PER>(); return; } }
-    if constexpr (NS > 4) { if (keep == 4) { vm_wait<4 * PER>(); return; } }
-    if constexpr (NS > 3) { if (keep == 3) { vm_wait<3 * PER>(); return; } }
-    if constexpr (NS > 2) { if (keep >= 2) { vm_wait<2 * PER>(); return; } }
-    if constexpr (NS > 1) { if (keep >= 1) { vm_wait<PER>(); return; } }
-    vm_wait<0>();
+    if (NS > 7 && keep >= 7) vm_wait<7 * PER>();
+    else if (NS > 6 && keep >= 6) vm_wait<6 * PER>();
+    else if (NS > 5 && keep == 5) vm_wait<5 * PER>();
+    else if (NS > 4 && keep == 4) vm_wait<4 * PER>();
+    else if (NS > 3 && keep == 3) vm_wait<3 * PER>();
+    else if (keep >= 2) vm_wait<2 * PER>();
+    else if (keep == 1) vm_wait<PER>();
+    else vm_wait<0>();
   };
   const int pro = min(NS - 1, kt1 - kt0);
 #pragma unroll
@@ -642,10 +642,7 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
   }
   __syncthreads();
   cs = reinterpret_cast<float*>(smem);
-  // lanes per output row: BN / 8 chunks of 8 columns; a row LayerNorm over a wide tile (BN 320 /
-  // 512: stage-3 / 4 rows) takes a whole wave per row (64 lanes, the lanes past BN / 8 hold zeros),
-  // ln_fwd_kernel's lane count for those widths, so its statistics stay bit-identical
-  constexpr int TPR = (EPI >= 2 && BN > 128) ? 64 : BN / 8, RPP = 256 * KW / TPR, NPASS = (BM + RPP - 1) / RPP;
+  constexpr int TPR = BN / 8, RPP = 256 * KW / TPR, NPASS = (BM + RPP - 1) / RPP;
   const int jl = (threadIdx.x % TPR) * 8;
   const int j = j0 + jl;
   const bool live = j < nreal;
@@ -694,10 +691,8 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
     const int rsl = threadIdx.x / TPR;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      if (jl < BN) {
-        red[(rsl * 2) * BN + jl + e] = dga[e];
-        red[(rsl * 2 + 1) * BN + jl + e] = dba[e];
-      }
+      red[(rsl * 2) * BN + jl + e] = dga[e];
+      red[(rsl * 2 + 1) * BN + jl + e] = dba[e];
     }
     __syncthreads();
     const int C = p.scatter ? p.scC : p.N;         // the norm's width (= BN under the scatter)
@@ -716,7 +711,7 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmArgs& p, const int lin,
 // (64 x 64 two-stage blocks take 32 KB of LDS: five fit a CU when the kernel stays within 96
 // VGPRs, which the launch bound asks of the register allocator -- at 97 only four are resident)
 template <int BM, int BN, bool TA, bool TB, int NS, int KW = 1, typename E = bf16, int TAIL = 0>
-__global__ __launch_bounds__(256 * KW, (BM == 64 && BN == 64 && NS == 2 && KW == 1) ? 5 : ((KW == 4 || BN > 128) ? 1 : 2))
+__global__ __launch_bounds__(256 * KW, (BM == 64 && BN == 64 && NS == 2 && KW == 1) ? 5 : (KW == 4 ? 1 : 2))
 void gemm_bf16_kernel(const GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[gemm_smem_bytes<BM, BN, NS, KW>()];
   const int lin = xcd_tile(blockIdx.x, p.tiles_m * p.tiles_n * p.G * p.nsplit);
@@ -1184,7 +1179,6 @@ void launch_bf16(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStream
     }
   }
 #define CMX_GEMM_LAUNCH(TA, TB) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, TA, TB, NS, KW, E>), grid, dim3(256 * KW), 0, s, a)
-  if constexpr (BN > 128) return;     // (wide tiles: the row-LayerNorm epilogue only, launch_ln_wide)
   if (!tA && !tB) CMX_GEMM_LAUNCH(false, false);
   else if (!tA && tB) CMX_GEMM_LAUNCH(false, true);
   else if (tA && tB) CMX_GEMM_LAUNCH(true, true);
@@ -1219,16 +1213,6 @@ void launch_bf16_ns(const GemmArgs& a, int G, int nsplit, int tA, int tB, hipStr
   else launch_bf16<BM, BN, 2, 1, E>(a, G, nsplit, tA, tB, s);
 }
 
-// Row LayerNorm epilogue over a tile as wide as the row (cmx_gemm_ln at N = 320 / 512: Block.norm2
-// after proj, the next norm1 after fc2 at stages 3 / 4, dual_segformer.py:168-169): 64 x N tiles,
-// one 4-wave block per CU (the 2-stage ring is (64 + N) x 64 x 2 x 2 B = 96 / 144 KB of LDS)
-template <typename E>
-void launch_ln_wide(const GemmArgs& a, int G, int bn, hipStream_t s) {
-  dim3 grid(a.tiles_m * G);
-  if (bn == 320) hipLaunchKernelGGL((gemm_bf16_kernel<64, 320, false, false, 2, 1, E, 2>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((gemm_bf16_kernel<64, 512, false, false, 2, 1, E, 2>), grid, dim3(256), 0, s, a);
-}
-
 // the 16-bit fast path for one problem: tile shape (bm, bn), element type from dtype (1 bf16, 2 fp16)
 template <typename E>
 void launch_fast_t(const GemmArgs& a, int bm, int bn, int G, int nsplit, int tA, int tB, hipStream_t s) {
@@ -1238,11 +1222,6 @@ void launch_fast_t(const GemmArgs& a, int bm, int bn, int G, int nsplit, int tA,
   else launch_bf16_ns<128, 128, E>(a, G, nsplit, tA, tB, s);
 }
 inline void launch_fast(const GemmArgs& a, int bm, int bn, int G, int nsplit, int tA, int tB, int dtype, hipStream_t s) {
-  if (bn > 128) {
-    if (dtype == 2) launch_ln_wide<f16>(a, G, bn, s);
-    else launch_ln_wide<bf16>(a, G, bn, s);
-    return;
-  }
   if (dtype == 2) launch_fast_t<f16>(a, bm, bn, G, nsplit, tA, tB, s);
   else launch_fast_t<bf16>(a, bm, bn, G, nsplit, tA, tB, s);
 }

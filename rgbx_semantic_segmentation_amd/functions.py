@@ -131,7 +131,7 @@ def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1
         bg = store.g(bp).view(G, -1)
     ln = None
     N = W.shape[1]
-    if ln_tail is not None and LN_ROW and ((N <= 128 and N % 8 == 0) or (N in (320, 512) and LN_WIDE)):
+    if ln_tail is not None and LN_ROW and N <= 128 and N % 8 == 0:
         m = ln_tail.mod
         ln = (store.w(m.weight, compute=False).view(G, -1), store.w(m.bias, compute=False).view(G, -1), m.eps, ln_tail)
     return GLinear.apply(W, Wg, b, bg, wp, act, res, rscale, rps, x1, x2, tap, ln, dgrad_tap)
@@ -141,10 +141,6 @@ def glinear(store, wp, bp, x1, x2=None, act="none", res=None, rscale=None, rps=1
 # Linear whose output row fits one GEMM tile (C <= 128: stages 1-2) normalises it in its epilogue
 # (cmx_gemm_ln, tail = 2): bit-identical statistics, no tickets, no second pass over the rows
 LN_ROW = os.environ.get("CMX_LN_ROW", "1") != "0"
-# CMX_LN_WIDE=0: stage-3 / 4 rows (C = 320 / 512) keep their own LayerNorm launch (A/B switch);
-# default: proj -> norm2 and fc2 -> next norm1 / stage norm on 64 x C tiles (cmx_gemm_ln), where
-# the library accepts the shape (K * C <= 1280 * 320)
-LN_WIDE = os.environ.get("CMX_LN_WIDE", "1") != "0"
 
 # CMX_MULTI_GEMM=0 launches the grouped Linears of GLinearMulti one by one (A/B switch)
 MULTI_GEMM = os.environ.get("CMX_MULTI_GEMM", "1") != "0"

@@ -182,13 +182,11 @@ def gemm_ln(A, B, C, ln_gamma, ln_beta, ln_eps, bias=None, residual=None, rscale
     """K.gemm's forward form (C = epi(A @ B^T)) plus the LayerNorm of C's rows in the same
     launch (cmx_gemm_ln): returns (y, mean, rstd), y = LN(C) in C's layout, mean / rstd (G, M)
     fp32; None when the problem is not eligible (the caller runs gemm + the LN kernel).
-    N <= 128 (N % 8 == 0), or N = 320 / 512 with K * N <= 1280 * 320: the LayerNorm runs in the
-    GEMM's epilogue (one tile spans a row; the library refuses other shapes)."""
+    N <= 128 (N % 8 == 0): the LayerNorm runs in the GEMM's epilogue (one tile spans a row)."""
     G, M, K1 = A.shape
     Kd = K1 + (A2.shape[2] if A2 is not None else 0)
     N = B.shape[1]
-    if A.dtype not in (torch.bfloat16, torch.float16) or not ((N <= 128 and N % 8 == 0) or N in (320, 512)) \
-            or not C.is_contiguous():
+    if A.dtype not in (torch.bfloat16, torch.float16) or not (N <= 128 and N % 8 == 0) or not C.is_contiguous():
         return None
     tA, lda, sA = _operand(A, "A")
     tB, ldb, sB = _operand(B, "B")

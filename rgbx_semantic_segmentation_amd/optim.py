@@ -46,6 +46,7 @@ class FusedAdamW:
         self.exp_avg = torch.zeros_like(store.flat)
         self.exp_avg_sq = torch.zeros_like(store.flat)
         self.lr_t = torch.full((1,), float(lr), dtype=torch.float32, device=dev)
+        self._lr_written = float(lr)
         self.step_t = torch.zeros(1, dtype=torch.float32, device=dev)
         # this optimizer's own step-count arrival counters (zero; every launch leaves them zero)
         self.tickets = torch.zeros(query("cmx_adamw_tickets"), dtype=torch.int32, device=dev)
@@ -64,7 +65,11 @@ class FusedAdamW:
 
     # ------------------------------------------------------------------ lr
     def _set_lr(self, lr: float):
-        self.lr_t.fill_(lr)          # eager write, outside any captured graph
+        # eager write, outside any captured graph; the reference loop sets the same value on every
+        # param group (train.py:206-207), so only a changed value launches the device write
+        if lr != getattr(self, "_lr_written", None):
+            self.lr_t.fill_(lr)
+            self._lr_written = lr
         for g in self.param_groups:
             dict.__setitem__(g, "lr", lr)
 

@@ -56,19 +56,30 @@ def test_gpus_2_launches_two_ranks_end_to_end():
     assert lines == [{"dry_run": True, "n_gpus": 2, "ranks_seen": 2}]
 
 
-def test_graph_streams_env_single_gpu_only():
-    """bench.py sets the HIP graph executor's stream count (2) only for a one-GPU run, before
-    torch loads the runtime; an explicit setting, CMX_GRAPH_STREAMS=0 or any multi-rank run keeps
-    the runtime's own choice."""
+def test_graph_streams_env():
+    """bench.py sets the HIP graph executor's stream count (2) before torch loads the runtime, for
+    one GPU and for every rank of an N-GPU run; CMX_GRAPH_STREAMS picks another count (0 = the
+    runtime's own), an explicit DEBUG_HIP_FORCE_GRAPH_QUEUES is kept.  The count never exceeds
+    GPU_MAX_HW_QUEUES: clamped, and an explicit larger setting is refused."""
     import bench
-    env = {}
-    bench._graph_streams_env(["--steps", "5"], env)
-    assert env["DEBUG_HIP_FORCE_GRAPH_QUEUES"] == "2"
-    for argv, e in ((["--gpus", "2"], {}), (["--gpus=8"], {}), ([], {"WORLD_SIZE": "4"}),
-                    ([], {"CMX_GRAPH_STREAMS": "0"}), ([], {"DEBUG_HIP_FORCE_GRAPH_QUEUES": "3"})):
-        before = dict(e)
+    for argv, e in ((["--steps", "5"], {}), (["--gpus", "2"], {}), (["--gpus=8"], {}), ([], {"WORLD_SIZE": "4"})):
         bench._graph_streams_env(argv, e)
-        assert e.get("DEBUG_HIP_FORCE_GRAPH_QUEUES") == before.get("DEBUG_HIP_FORCE_GRAPH_QUEUES"), (argv, e)
+        assert e["DEBUG_HIP_FORCE_GRAPH_QUEUES"] == "2", (argv, e)
+    e = {"CMX_GRAPH_STREAMS": "0"}
+    bench._graph_streams_env([], e)
+    assert "DEBUG_HIP_FORCE_GRAPH_QUEUES" not in e
+    e = {"DEBUG_HIP_FORCE_GRAPH_QUEUES": "3"}
+    bench._graph_streams_env([], e)
+    assert e["DEBUG_HIP_FORCE_GRAPH_QUEUES"] == "3"
     e = {"CMX_GRAPH_STREAMS": "3"}
     bench._graph_streams_env([], e)
     assert e["DEBUG_HIP_FORCE_GRAPH_QUEUES"] == "3"
+    for hwq, want in (("1", "1"), ("2", "2"), ("3", "2"), ("8", "2")):
+        e = {"GPU_MAX_HW_QUEUES": hwq}
+        bench._graph_streams_env([], e)
+        assert e["DEBUG_HIP_FORCE_GRAPH_QUEUES"] == want, (hwq, e)
+    e = {"GPU_MAX_HW_QUEUES": "2", "CMX_GRAPH_STREAMS": "0"}
+    bench._graph_streams_env([], e)
+    assert e["DEBUG_HIP_FORCE_GRAPH_QUEUES"] == "2"
+    with pytest.raises(SystemExit):
+        bench._graph_streams_env([], {"GPU_MAX_HW_QUEUES": "1", "DEBUG_HIP_FORCE_GRAPH_QUEUES": "2"})
