@@ -34,7 +34,7 @@ typedef struct ihipStream_t* hipStream_t;
  * from, and the Python binding refuses a library whose revision differs (an older .so with the
  * same symbol names but shifted arguments would otherwise corrupt memory silently).  Bump it
  * on every change of an entry point's argument list. */
-#define CMX_ABI_VERSION 5
+#define CMX_ABI_VERSION 6
 int cmx_abi_version(void);
 const char* cmx_last_error(void);
 /* pinned host -> device copy of a packed record table on `stream` (see grouped launches) */
@@ -175,12 +175,22 @@ int cmx_bilinear_adjoint_1d(const void* in, void* out, int64_t P, int Lo, int Li
 /* DecoderHead.linear_fuse (MLPDecoder.py:66-77) without the (B, N1, 4E) concat: the 1x1 conv commutes with the
  * bilinear upsample (linear, weights sum to 1), so Z = e1 Wf[:, 3E:]^T + bias + up(z4) + up(z3) + up(z2) with the
  * low-resolution products z_i = e_i Wf[:, slot_i]^T (B, h_i, w_i, E) added by the GEMM epilogue (z_i may be NULL).
- * e1 (B*H1*W1, E); Wf_c1 points at column 3E of the (E, ldw) weight; Z (B*H1*W1, E). */
+ * e1 (B*H1*W1, K) with row stride lda; Wf_c1 (E, K) with row stride ldw (column 3E of linear_fuse's weight: K = E);
+ * Z (B*H1*W1, E). */
 /* dx of the SRA spatial-reduction conv Attention.sr (kernel = stride = R, pad 0; dual_segformer.py:95-96): the
  * dgrad GEMM dy (G, NIg*Ho*Wo, N) @ W (G, N, R*R*C) with the col2im folded into its epilogue as an address remap
  * (non-overlapping patches).  dx (G*NIg, H, W, C) NHWC; pixels outside the Ho*R x Wo*R window are not written. */
 int cmx_conv_patch_dgrad(const void* dy, const void* Wt, void* dx, int G, int NIg, int H, int W, int C, int R, int Ho, int Wo, int N, int64_t sdy, int64_t sW, int64_t sdx, int dtype, hipStream_t stream);
-int cmx_decoder_fuse_fwd(const void* e1, const void* Wf_c1, void* Z, const float* bias, const void* z4, const void* z3, const void* z2, int B, int H1, int W1, int h4, int w4, int h3, int w3, int h2, int w2, int E, int64_t ldw, int dtype, hipStream_t stream);
+
+int cmx_decoder_fuse_fwd(const void* e1, const void* Wf_c1, void* Z, const float* bias, const void* z4, const void* z3, const void* z2, int B, int H1, int W1, int h4, int w4, int h3, int w3, int h2, int w2, int E, int K, int64_t lda, int64_t ldw, int dtype, hipStream_t stream);
+/* DecoderHead with linear_c{1..4} folded into linear_fuse (MLPDecoder.py:60-77; default path, functions.DecoderFoldF):
+ * Z = sum_i up_i(x_i M_i^T) + b with M_i = Wf_i Wc_i, b = bf + sum_i Wf_i bc_i (cmx_decoder_fuse_fwd with e1 = x1,
+ * K = C1, Wf_c1 = M_1).  cmx_decoder_fold_bias forms b from Wf (E, ldw) and the four fp32 biases (slot order
+ * c4, c3, c2, c1).  cmx_decoder_fold_bwd_prep, after dM_i = dY_i^T x_i and gb = sum_rows dZ are known: dMh = dtype(dM)
+ * (n elements; dMh NULL: none), WfT (4E, E) = Wf^T, dWf (E, ldg) = gb bcat^T (the dM_i Wc_i^T GEMMs accumulate onto
+ * it), dbc_i = Wf_i^T gb, dbf = gb.  E a multiple of 64. */
+int cmx_decoder_fold_bias(const void* Wf, int64_t ldw, const float* bf, const float* bc4, const float* bc3, const float* bc2, const float* bc1, float* b, int E, int dtype, hipStream_t stream);
+int cmx_decoder_fold_bwd_prep(const float* dM, void* dMh, int64_t n, const float* gb, const void* Wf, int64_t ldw, void* WfT, float* dWf, int64_t ldg, const float* bc4, const float* bc3, const float* bc2, const float* bc1, float* dbc4, float* dbc3, float* dbc2, float* dbc1, float* dbf, int E, int dtype, hipStream_t stream);
 
 /* ---- fused final upsample + CrossEntropyLoss(mean, ignore_index=255) (builder.py:233,249). */
 size_t cmx_upsample_ce_workspace(int B, int H, int W);

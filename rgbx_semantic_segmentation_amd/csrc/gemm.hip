@@ -460,12 +460,15 @@ int cmx_conv_patch_dgrad(const void* dy, const void* Wt, void* dx, int G, int NI
 //   Z = e1 @ Wf[:, 3E:4E]^T + bias + up(z4) + up(z3) + up(z2)
 // where z_i = e_i @ Wf[:, slot_i]^T are the low-resolution products of the upsampled branches
 // (bilinear interpolation is linear with weights summing to 1, so it commutes with the 1x1
-// conv: W up(e) = up(W e)).  e1 (B*H1*W1, E), z_i (B, h_i, w_i, E), Wf (E, ldw) with the c1
-// slice at column 3E; Z (B*H1*W1, E).  The (B, N1, 4E) concat of the reference is never formed.
+// conv: W up(e) = up(W e)).  e1 (B*H1*W1, K) row stride lda, z_i (B, h_i, w_i, E), Wf_c1 (E, K)
+// row stride ldw: the c1 slice of the conv (K = E, DecoderFuseF) or, with linear_c1 folded in,
+// the composed M_1 = Wf_c1 Wc_1 (K = C1, e1 = the stage-1 features; decoder_fold.hip).
+// Z (B*H1*W1, E).  The (B, N1, 4E) concat of the reference is never formed.
 int cmx_decoder_fuse_fwd(const void* e1, const void* Wf_c1, void* Z, const float* bias, const void* z4, const void* z3,
                          const void* z2, int B, int H1, int W1, int h4, int w4, int h3, int w3, int h2, int w2, int E,
-                         int64_t ldw, int dtype, hipStream_t s) {
-  CMX_REQUIRE(B > 0 && H1 > 0 && W1 > 0 && E > 0 && E % 8 == 0, CMX_ERR_SHAPE, "decoder_fuse_fwd: B=%d E=%d", B, E);
+                         int K, int64_t lda, int64_t ldw, int dtype, hipStream_t s) {
+  CMX_REQUIRE(B > 0 && H1 > 0 && W1 > 0 && E > 0 && E % 8 == 0 && K > 0 && lda >= K && ldw >= K, CMX_ERR_SHAPE,
+              "decoder_fuse_fwd: B=%d E=%d K=%d", B, E, K);
   UpSpec up{};
   const void* src[3] = {z4, z3, z2};
   const int hh[3] = {h4, h3, h2}, ww[3] = {w4, w3, w2};
@@ -475,7 +478,7 @@ int cmx_decoder_fuse_fwd(const void* e1, const void* Wf_c1, void* Z, const float
   }
   up.oH = H1; up.oW = W1;
   const int M = B * H1 * W1;
-  return gemm_impl(e1, nullptr, Wf_c1, Z, bias, nullptr, nullptr, nullptr, nullptr, 1, M, E, E, E, E, 0, ldw, E, 0, 0,
+  return gemm_impl(e1, nullptr, Wf_c1, Z, bias, nullptr, nullptr, nullptr, nullptr, 1, M, E, K, K, lda, 0, ldw, E, 0, 0,
                    0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 1, dtype, s, &up);
 }
 

@@ -50,6 +50,7 @@ class _Queue:
         self.keep = []         # tensors the queued work reads or writes
         self.streams = {}      # streams the queued operands were produced on (FFM's side stream)
         self.dtype = 0         # operand dtype code of the queued GEMMs (1 bf16, 2 fp16; 0 = none yet)
+        self.post = []         # callables run right after the next flush (deferred.after)
         self.armed = False
 
 
@@ -135,6 +136,17 @@ def wgrad(dz: torch.Tensor, x: torch.Tensor, Wg: torch.Tensor, bg: torch.Tensor 
     _note_stream()
     arm()
     return True
+
+
+def after(fn) -> None:
+    """Run ``fn`` on the flushing stream right after the next flush, which forms every weight
+    gradient queued so far (the decoder fold's chain rule reads its queued dM_i products);
+    with nothing queued, now."""
+    if pending():
+        _q.post.append(fn)
+        arm()
+    else:
+        fn()
 
 
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, Wg: torch.Tensor, bg, geom) -> bool:
@@ -239,6 +251,9 @@ def flush(max_blocks: int = 0) -> None:
     _q.armed = False
     if _q.gemms or _q.convs or _q.reds:
         _issue(max_blocks)
+    post, _q.post = _q.post, []
+    for fn in post:
+        fn()
 
 
 def _issue(max_blocks: int = 0) -> None:

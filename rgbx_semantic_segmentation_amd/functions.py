@@ -1377,8 +1377,8 @@ class DecoderFuseF(Function):
         Z = torch.empty(B * N1, E, dtype=e1.dtype, device=e1.device)
         Wc1 = W[:, 3 * E:]
         K.call("cmx_decoder_fuse_fwd", K.ptr(_c(e1)), Wc1.data_ptr(), K.ptr(Z), K.ptr(bf), K.ptr(zs[0]), K.ptr(zs[1]),
-               K.ptr(zs[2]), B, H1, W1, hw[2][0], hw[2][1], hw[1][0], hw[1][1], hw[0][0], hw[0][1], E, W.stride(0),
-               K.dtype_code(e1), K.stream())
+               K.ptr(zs[2]), B, H1, W1, hw[2][0], hw[2][1], hw[1][0], hw[1][1], hw[0][0], hw[0][1], E, E, E,
+               W.stride(0), K.dtype_code(e1), K.stream())
         ctx.save_for_backward(e4, e3, e2, e1, Wf)
         ctx.meta = (Wfg, bfg, sizes)
         return Z
@@ -1404,6 +1404,105 @@ class DecoderFuseF(Function):
         _wgrad_into(dZ, e1f, Wfg[:, :, 3 * E:], bfg)
         _gemm_group(jobs)                         # the four branches' input gradients: one launch
         return grads[0], grads[1], grads[2], de1.view(e1.shape), None, None, None, None, None, None
+
+
+# CMX_DECODER_FOLD=0: linear_c{1..4} as their own GEMMs ahead of DecoderFuseF (A/B switch)
+DECODER_FOLD = os.environ.get("CMX_DECODER_FOLD", "1") != "0"
+
+
+class DecoderFoldF(Function):
+    """DecoderHead's four MLP projections, upsample, concat and linear_fuse 1x1 conv
+    (MLPDecoder.py:60-77) with linear_c{1..4} folded into the conv.  Branch i of the reference
+    is Wf_i up_i(x_i Wc_i^T + bc_i) (Wf_i: the conv's column slot of the branch, up_1 = identity);
+    bilinear upsampling is linear with weights summing to 1, so
+
+        Z = sum_i up_i(x_i M_i^T) + b,    M_i = Wf_i Wc_i  (E x C_i),    b = bf + sum_i Wf_i bc_i
+
+    Forward: the four compositions M_i as one multi GEMM (K = E), b (cmx_decoder_fold_bias), the
+    c2..c4 products x_i M_i^T at their own resolution (one multi launch) and the c1 product
+    (K = C1 = 64 instead of the reference's two GEMMs with K = 64 and K = 512) with their
+    bilinear upsample added in its epilogue (cmx_decoder_fuse_fwd).  Neither the (B, N1, 4E)
+    concat nor the four (B, N_i, E) projections exist.  Backward, with dY_i = up_i^T dZ:
+    dx_i = dY_i M_i (one multi launch); dM_i = dY_i^T x_i and gb = sum_rows dZ are queued
+    weight-gradient problems; after the flush that forms them (deferred.after) the chain rule
+
+        dWf_i = dM_i Wc_i^T + gb bc_i^T    dWc_i = Wf_i^T dM_i    dbc_i = Wf_i^T gb    dbf = gb
+
+    is one prep kernel (cmx_decoder_fold_bwd_prep: the 16-bit copy of dM, Wf^T, the rank-1 and
+    bias terms) and two multi GEMMs of 512 x 512-sized products.  Executed per B2 step (bs=2):
+    about 11 GFLOP forward + backward instead of 75 for DecoderFuseF on top of linear_c{1..4};
+    the step roofline keeps the reference's op-by-op count (flops.py)."""
+
+    @staticmethod
+    def forward(ctx, x4, x3, x2, x1, Wf, Wc, bf, bc, grads, sizes, anchor):
+        B, N1, C1 = x1.shape
+        E = Wf.shape[0]
+        (H1, W1), hw = sizes[0], sizes[1:]        # hw: grids of c2, c3, c4
+        xs = (x4, x3, x2, x1)                     # slot order of Wf's columns
+        Cs = [w.shape[1] for w in Wc]
+        Ms = [torch.empty(1, E, C, dtype=Wf.dtype, device=Wf.device) for C in Cs]
+        _gemm_group([dict(A=Wf[None, :, s * E:(s + 1) * E], B=Wc[s][None].transpose(1, 2), C=Ms[s], splitk=1)
+                     for s in range(4)])          # M_i = Wf_i Wc_i: one launch
+        b = torch.empty(E, dtype=torch.float32, device=Wf.device)
+        K.call("cmx_decoder_fold_bias", Wf.data_ptr(), Wf.stride(0), K.ptr(bf), *[K.ptr(t) for t in bc], K.ptr(b), E,
+               K.dtype_code(Wf), K.stream())
+        zs, jobs = [], []
+        for s, (h, w) in enumerate((hw[2], hw[1], hw[0])):
+            z = torch.empty(1, B * h * w, E, dtype=x1.dtype, device=x1.device)
+            jobs.append(dict(A=_c(xs[s]).reshape(1, B * h * w, Cs[s]), B=Ms[s], C=z))
+            zs.append(z)
+        _gemm_group(jobs)                         # the three low-resolution branch products: one launch
+        Z = torch.empty(B * N1, E, dtype=x1.dtype, device=x1.device)
+        K.call("cmx_decoder_fuse_fwd", K.ptr(_c(x1)), K.ptr(Ms[3]), K.ptr(Z), K.ptr(b), K.ptr(zs[0]), K.ptr(zs[1]),
+               K.ptr(zs[2]), B, H1, W1, hw[2][0], hw[2][1], hw[1][0], hw[1][1], hw[0][0], hw[0][1], E, C1, C1, C1,
+               K.dtype_code(x1), K.stream())
+        ctx.save_for_backward(*xs, Wf, *Wc, *Ms)
+        ctx.meta = (bc, grads, sizes)
+        return Z
+
+    @staticmethod
+    def backward(ctx, dZ):
+        t = ctx.saved_tensors
+        xs, Wf, Wc, Ms = t[:4], t[4], t[5:9], t[9:13]
+        bc, grads, sizes = ctx.meta
+        B, N1, C1 = xs[3].shape
+        E = Wf.shape[0]
+        (H1, W1), hw = sizes[0], sizes[1:]
+        Cs = [w.shape[1] for w in Wc]
+        dZ = _c(dZ).view(1, B * N1, E)
+        offs = [0]
+        for C in Cs:
+            offs.append(offs[-1] + E * C)
+        dM = torch.empty(offs[-1], dtype=torch.float32, device=dZ.device)
+        gb = torch.empty(1, E, dtype=torch.float32, device=dZ.device)
+        dxs, jobs = [], []
+        for s in range(4):
+            dY = dZ if s == 3 else _adjoint_to(dZ, B, H1, W1, *hw[2 - s], E).view(1, -1, E)
+            x = xs[s].reshape(1, -1, Cs[s])
+            dx = torch.empty_like(x)
+            jobs.append(dict(A=dY, B=Ms[s].transpose(1, 2), C=dx))
+            dxs.append(dx.view(xs[s].shape))
+            _wgrad_into(dY, x, dM[offs[s]:offs[s + 1]].view(1, E, Cs[s]), gb if s == 3 else None)
+        _gemm_group(jobs)                         # the four branches' input gradients: one launch
+        deferred.after(lambda: _decoder_fold_chain(dM, gb, offs, Wf, Wc, bc, grads, Cs, E))
+        return (*dxs, None, None, None, None, None, None, None)
+
+
+def _decoder_fold_chain(dM, gb, offs, Wf, Wc, bc, grads, Cs, E):
+    """DecoderFoldF's weight and bias gradients from dM_i (fp32, packed) and gb once they exist."""
+    Wfg, bfg, Wcg, bcg = grads
+    h16 = Wf.dtype != torch.float32
+    dMh = torch.empty(dM.shape, dtype=Wf.dtype, device=dM.device) if h16 else None
+    WfT = torch.empty(4 * E, E, dtype=Wf.dtype, device=Wf.device)
+    K.call("cmx_decoder_fold_bwd_prep", K.ptr(dM), K.ptr(dMh), dM.numel(), K.ptr(gb), Wf.data_ptr(), Wf.stride(0),
+           K.ptr(WfT), Wfg.data_ptr(), Wfg.stride(-2), *[K.ptr(t) for t in bc], *[K.ptr(t) for t in bcg], K.ptr(bfg),
+           E, K.dtype_code(Wf), K.stream())
+    src = dMh if h16 else dM
+    D = [src[offs[s]:offs[s + 1]].view(1, E, Cs[s]) for s in range(4)]
+    # dWf_i += dM_i Wc_i^T (onto gb bc_i^T) and dWc_i = Wf_i^T dM_i: one launch each
+    _gemm_group([dict(A=D[s], B=Wc[s][None], C=Wfg[:, :, s * E:(s + 1) * E], out_mode=2, splitk=1) for s in range(4)])
+    _gemm_group([dict(A=WfT[None, s * E:(s + 1) * E], B=D[s].transpose(1, 2), C=Wcg[s], out_mode=1, splitk=1)
+                 for s in range(4)])
 
 
 # ---------------------------------------------------------------------------- final upsample + CE

@@ -41,7 +41,7 @@ def test_header_symbols_exported():
     lib = ctypes.CDLL(_lib.LIB_PATH)
     missing = [n for n in sigs if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.cmx_abi_version() == _lib.header_abi_version() == 5
+    assert lib.cmx_abi_version() == _lib.header_abi_version() == 6
 
 
 def test_abi_rejects_bad_shapes_without_launching():

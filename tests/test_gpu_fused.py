@@ -3,6 +3,8 @@
 * functions.DecoderFuseF (cmx_decoder_fuse_fwd + low-resolution branch GEMMs + bilinear
   adjoints): DecoderHead's upsample + concat + linear_fuse 1x1 conv (MLPDecoder.py:66-77) with
   the conv commuted ahead of the upsample -- forward and every input / weight / bias gradient.
+* functions.DecoderFoldF (linear_c{1..4} folded into linear_fuse, decoder_fold.hip): the whole
+  decode head up to the fuse conv against linear -> upsample -> concat -> conv in fp32.
 * cmx_conv_patch_dgrad: dx of the SRA spatial-reduction conv (kernel = stride = R, pad 0,
   dual_segformer.py:95-96) with the col2im folded into the GEMM epilogue, incl. grids that R
   does not divide (the remainder pixels get zero gradient, as torch's conv backward gives).
@@ -58,6 +60,64 @@ def test_decoder_fuse_matches_upsample_concat_conv(dev, dtype, B, H1, W1, E):
         assert rel(eq[i].grad, er[i].grad) < tol, (i, rel(eq[i].grad, er[i].grad))
     assert rel(Wg, Wr.grad) < tol, rel(Wg, Wr.grad)
     assert rel(bg, br.grad) < tol, rel(bg, br.grad)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,H1,W1,E,Cs", [(2, 120, 160, 512, (64, 128, 320, 512)), (1, 32, 40, 128, (32, 64, 160, 256)),
+                                          (2, 30, 17, 64, (32, 64, 160, 256))])
+def test_decoder_fold_matches_mlp_upsample_concat_conv(dev, dtype, B, H1, W1, E, Cs):
+    """functions.DecoderFoldF against the reference decode head's op sequence in fp32
+    (MLPDecoder.py:60-77: linear_c{1..4} -> upsample -> concat c4, c3, c2, c1 -> 1x1 conv):
+    the output, the four feature gradients and the gradients of all ten weights and biases
+    (the chain-rule terms run after deferred.flush, as in the step)."""
+    from rgbx_semantic_segmentation_amd import deferred
+    from rgbx_semantic_segmentation_amd import functions as Fn
+    torch.manual_seed(0)
+    grids = [(H1, W1), ((H1 + 1) // 2, (W1 + 1) // 2), ((H1 + 3) // 4, (W1 + 3) // 4), ((H1 + 7) // 8, (W1 + 7) // 8)]
+    xs = [torch.randn(B, h * w, C, device=dev) for (h, w), C in zip(grids, Cs)]      # x1..x4
+    Wcs = [torch.randn(E, C, device=dev) * C ** -0.5 for C in Cs]
+    bcs = [torch.randn(E, device=dev) * 0.1 for _ in Cs]
+    Wf = torch.randn(E, 4 * E, device=dev) * (4 * E) ** -0.5
+    bf = torch.randn(E, device=dev) * 0.1
+    dZ = torch.randn(B * H1 * W1, E, device=dev)
+    xr = [x.to(dtype).float().requires_grad_(True) for x in xs]
+    Wcr = [w.to(dtype).float().requires_grad_(True) for w in Wcs]
+    bcr = [b.clone().requires_grad_(True) for b in bcs]
+    Wr = Wf.to(dtype).float().requires_grad_(True)
+    br = bf.clone().requires_grad_(True)
+
+    def nchw(e, hw):
+        return e.view(B, hw[0], hw[1], E).permute(0, 3, 1, 2)
+    cs = [xr[i] @ Wcr[i].t() + bcr[i] for i in range(4)]
+    ups = [TF.interpolate(nchw(cs[i], grids[i]), size=(H1, W1), mode="bilinear", align_corners=False)
+           for i in (3, 2, 1)]
+    cat = torch.cat(ups + [nchw(cs[0], grids[0])], 1)
+    Zr = TF.conv2d(cat, Wr.view(E, 4 * E, 1, 1), br).permute(0, 2, 3, 1).reshape(B * H1 * W1, E)
+    Zr.backward(dZ.to(dtype).float())
+    # product (slot order c4, c3, c2, c1)
+    xq = [x.to(dtype).requires_grad_(True) for x in xs]
+    order = (3, 2, 1, 0)
+    Wq = Wf.to(dtype)
+    Wcq = tuple(Wcs[i].to(dtype) for i in order)
+    Wfg = torch.full((1, E, 4 * E), float("nan"), device=dev)
+    bfg = torch.full((E,), float("nan"), device=dev)
+    Wcg = [torch.full((1, E, C), float("nan"), device=dev) for C in Cs]
+    bcg = [torch.full((E,), float("nan"), device=dev) for _ in Cs]
+    grads = (Wfg, bfg, tuple(Wcg[i] for i in order), tuple(bcg[i] for i in order))
+    anchor = torch.nn.Parameter(torch.zeros(1, device=dev))
+    Z = Fn.DecoderFoldF.apply(xq[3], xq[2], xq[1], xq[0], Wq, Wcq, bf, tuple(bcs[i] for i in order), grads, grids,
+                              anchor)
+    Z.backward(dZ.to(dtype))
+    deferred.flush()
+    torch.cuda.synchronize()
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert rel(Z, Zr) < tol, rel(Z, Zr)
+    for i in range(4):
+        assert rel(xq[i].grad, xr[i].grad) < tol, (i, rel(xq[i].grad, xr[i].grad))
+        assert rel(Wcg[i][0], Wcr[i].grad) < tol, (i, rel(Wcg[i][0], Wcr[i].grad))
+        assert rel(bcg[i], bcr[i].grad) < tol, (i, rel(bcg[i], bcr[i].grad))
+    assert rel(Wfg[0], Wr.grad) < tol, rel(Wfg[0], Wr.grad)
+    assert rel(bfg, br.grad) < tol, rel(bfg, br.grad)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
