@@ -199,6 +199,11 @@ size_t cmx_upsample_ce_workspace(int B, int H, int W);
  * (stats = the forward's out) without materialising any full-resolution tensor. */
 int cmx_upsample_ce_fwd(const void* logits, const int64_t* label, void* grad, float* out, float* workspace, int B, int h, int w, int H, int W, int K, int ignore_index, int dtype, hipStream_t stream);
 int cmx_upsample_ce_bwd(const void* logits, const int64_t* label, const float* dloss, const float* stats, void* dlogits, int B, int h, int w, int H, int W, int K, int ignore_index, int dtype, hipStream_t stream);
+/* Training form (H = 4h, W = 4w, K <= 40): the loss (out, as cmx_upsample_ce_fwd) and adj (B, h, w, K) fp32 = bilinear
+ * adjoint of (softmax - onehot) in one pass over the pixels; the backward is cmx_upsample_ce_bwd_scale:
+ * dlogits (n elements, dtype) = adj * dloss[0] * stats[1]. */
+int cmx_upsample_ce_fwd_adj(const void* logits, const int64_t* label, float* adj, float* out, float* workspace, int B, int h, int w, int H, int W, int K, int ignore_index, int dtype, hipStream_t stream);
+int cmx_upsample_ce_bwd_scale(const float* adj, const float* dloss, const float* stats, void* dlogits, int64_t n, int dtype, hipStream_t stream);
 
 /* ---- dense layers: batched MFMA GEMM with fused epilogues -----------------------------
  * Replaces every nn.Linear and 1x1 Conv2d of the path (dual_segformer.py:42-43, 87-96, 110;

@@ -6,11 +6,13 @@
 //  * forward: a block owns a 16 x 16 full-res tile, stages the low-res logits it reads
 //    (<= 6 x 6 x K, fp32) in LDS once, and each thread does one pixel's interpolation +
 //    log-softmax + NLL.  Only per-block loss / count partials are written.
-//  * backward: a block owns a TY x TX low-res tile of dlogits.  It recomputes the softmax
-//    gradient g = (p - onehot) * dloss / n_valid of every full-res pixel whose bilinear
-//    footprint touches the tile (<= 20 x 20 pixels at scale 4) into LDS, then applies the
-//    separable bilinear adjoint (x, then y) in LDS and writes the tile once.  The 2-pass
-//    adjoint of a materialised (B, H, W, K) gradient (49 MB at 480 x 640, K = 40) is gone.
+//  * gradient (ce_cells): a block owns a CT_Y x CT_X low-res tile of dlogits and recomputes
+//    the softmax gradient of every full-res pixel whose bilinear footprint touches it, a run
+//    of 4 pixels per thread that share their two low-res columns, then applies the separable
+//    bilinear adjoint (x in registers, y through LDS) and writes the tile once.  In training
+//    the forward runs it (with the loss partials) and the backward only scales its fp32
+//    result by dloss / n_valid; cmx_upsample_ce_bwd is the recompute-in-backward form.  The
+//    2-pass adjoint of a materialised (B, H, W, K) gradient (49 MB at 480 x 640, K = 40) is gone.
 #include "cmx_common.h"
 
 namespace {
@@ -114,178 +116,234 @@ __global__ __launch_bounds__(256) void ce_fwd_tiled(const T* __restrict__ logits
   }
 }
 
-// ------------------------------------------------------------------------ backward (fused)
-// full-res rows contributing to low-res rows [y0, y0 + n): the interval of Y whose bilinear
-// source pair (i0, i1) meets it (monotone in Y)
-__device__ __forceinline__ void footprint(int y0, int n, float scale, int in, int out, int& Ya, int& Yb) {
-  int a = (int)floorf((y0 - 1 + 0.5f) / scale - 0.5f) - 2;
-  if (a < 0) a = 0;
-  int i0, i1;
-  float l0, l1;
-  for (;; ++a) {
-    src_idx(a, scale, in, i0, i1, l0, l1);
-    if (i1 >= y0 || a >= out - 1) break;
-  }
-  int bb = (int)ceilf((y0 + n + 0.5f) / scale - 0.5f) + 2;
-  if (bb > out - 1) bb = out - 1;
-  for (;; --bb) {
-    src_idx(bb, scale, in, i0, i1, l0, l1);
-    if (i0 <= y0 + n - 1 || bb <= a) break;
-  }
-  Ya = a;
-  Yb = bb;
-}
+// ------------------------------------------------------------------------ cells (gradient)
+// Exact x4, align_corners=False: full-res X = 4x + r interpolates low-res columns (x - 1, x) for
+// r = 0, 1 and (x, x + 1) for r = 2, 3, so the run X in [4c - 2, 4c + 2) reads columns c - 1 and
+// c only (at the image borders the clamped taps put all weight on one of them) -- and, by the
+// same weights, the adjoint of the x-interpolation sends the run's gradient to those two columns
+// only.  A thread takes one such run of 4 pixels on one full-res row: 4 LDS reads per class give
+// the run's two row-interpolated columns (registers, log2 units), from which the 4 pixels'
+// logits, softmax and gradient follow; the softmax is shifted by the larger of the two columns'
+// maxima (every pixel's logit is a convex combination of the two: an upper bound, no max pass),
+// and the run's x-adjoint is its two column sums.  A workgroup owns a CT_Y x CT_X low-res tile
+// of the output: the runs of full-res rows [4 y0 - 2, 4 y0 + 4 CT_Y + 2) and cells
+// c = x0 .. x0 + CT_X (recompute (CT_X + 1) / CT_X x (CT_Y + 1) / CT_Y of the tile's own pixels);
+// the column sums meet in LDS (the right column's first, the left column's added after a
+// barrier: one fixed summation order), and the y-adjoint (8 full-res rows per low-res row)
+// writes the tile.
+//   FWD = true:  loss partials of the pixels the tile owns, and the unscaled adjoint of
+//                (softmax - onehot) in fp32 (the backward only scales it: cmx_upsample_ce_bwd_scale)
+//   FWD = false: the adjoint of (softmax - onehot) * dloss[0] * stats[1] in T (recompute backward)
+constexpr int CT_Y = 6, CT_X = 8;
+constexpr int CT_R = 4 * CT_Y + 4;                // full-res footprint rows
+constexpr int CT_C = CT_X + 1;                    // runs per footprint row
+constexpr int CT_NT = 256;
+static_assert(CT_R * CT_C <= CT_NT, "one run per thread");
+constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.69314718055994531f;
 
-// eight waves per workgroup: the 400 footprint pixels of phase A take one pass, and 3 resident
-// workgroups (LDS-bound) give six waves per SIMD to hide the LDS / exp latency
-constexpr int CE_BWD_NT = 512;
-template <typename T>
-__global__ __launch_bounds__(CE_BWD_NT) void ce_bwd_fused(const T* __restrict__ logits, const int64_t* __restrict__ label,
-                                                    const float* __restrict__ dloss, const float* __restrict__ stats,
-                                                    T* __restrict__ dlogits, int h, int w, int H, int W, int K,
-                                                    int ignore, int tiles_x, int tiles_y) {
-  // every LDS image is class-major ([k][pixel]): lanes on consecutive pixels touch consecutive
-  // words (a pixel-major [pixel][k] image with K = 40 put 8 lanes on each bank)
-  constexpr int LW = TX + 2, LP = (TY + 2) * LW;
-  __shared__ float lg[KF * LP];                     // low-res logits: tile + 1-pixel halo
-  __shared__ T g[KF * RY * RX];                     // full-res softmax gradient of the footprint
-  constexpr int KP = KF + 1;                        // odd pitch: phase C lanes on consecutive k
-  __shared__ float t1[RY * TX * KP];                // x-adjoint: (full-res row, low-res col, class)
-  __shared__ float wy[TY * RY], wx[TX * RX];        // bilinear adjoint weights of the tile
+template <typename T, bool FWD>
+__global__ __launch_bounds__(CT_NT) void ce_cells(const T* __restrict__ logits, const int64_t* __restrict__ label,
+                                                  const float* __restrict__ dloss, const float* __restrict__ stats,
+                                                  void* __restrict__ dst, float* __restrict__ part, int h, int w, int H,
+                                                  int W, int K, int ignore, int tiles_x, int tiles_y) {
+  constexpr int LH = CT_Y + 2, LW = CT_X + 2, LP = LH * LW;   // low-res tile + 1-pixel halo
+  constexpr int KP = KF + 1;                                   // odd pitch of the column sums
+  __shared__ float lg[KF * LP];                                // class-major [k][row][col]
+  __shared__ float t1[CT_R * CT_X * KP + KP];                  // x-adjoint [row][col][k] + a spare row
+  __shared__ float wtab[CT_Y][8];                              // y-adjoint weights
+  __shared__ float red[2][CT_NT / 64];
+  const int t = threadIdx.x;
   const int bx = blockIdx.x % tiles_x, by = (blockIdx.x / tiles_x) % tiles_y, b = blockIdx.x / (tiles_x * tiles_y);
-  const int y0 = by * TY, x0 = bx * TX;
-  const int ny = min(TY, h - y0), nx = min(TX, w - x0);
+  const int y0 = by * CT_Y, x0 = bx * CT_X;
+  const int ny = min(CT_Y, h - y0), nx = min(CT_X, w - x0);
   const float sh = (float)h / H, sw = (float)w / W;
-  const float gs = dloss[0] * stats[1];               // dloss / n_valid
-  int Ya, Yb, Xa, Xb;
-  footprint(y0, ny, sh, h, H, Ya, Yb);
-  footprint(x0, nx, sw, w, W, Xa, Xb);
-  const int ry = Yb - Ya + 1, rx = Xb - Xa + 1;       // <= RY, RX (exact x4, host-checked)
-  const int np = ry * rx;
+  const int ri = t / CT_C, c = t % CT_C;          // the thread's run: footprint row, cell
+  const bool act = ri < CT_R;
+  const int Y = 4 * y0 - 2 + ri, X0 = 4 * (x0 + c) - 2;
+  const bool rowin = act && Y >= 0 && Y < H;
+  // global loads first: the run's labels, the thread's share of the logits tile
+  long lab[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int X = X0 + j;
+    lab[j] = (rowin && X >= 0 && X < W) ? label[((long)b * H + Y) * W + X] : -1L;
+  }
   const T* base = logits + (long)b * h * w * K;
-  // all global loads first (logits tile + halo, the labels of the thread's footprint pixels),
-  // then the LDS stores: one memory latency per block instead of one per 256 items
-  constexpr int NL = (LP * KF + CE_BWD_NT - 1) / CE_BWD_NT, NPX = (RY * RX + CE_BWD_NT - 1) / CE_BWD_NT;
+  constexpr int NL = (LP * KF + CT_NT - 1) / CT_NT;
   float v[NL];
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
-    const int e = threadIdx.x + i * CE_BWD_NT;
-    const int k = e % K, px = e / K;                  // coalesced global reads along k
+    const int e = t + i * CT_NT;
+    const int k = e % K, px = e / K;                // coalesced along k
     const int yy = y0 - 1 + px / LW, xx = x0 - 1 + px % LW;
     v[i] = (e < LP * K && yy >= 0 && yy < h && xx >= 0 && xx < w) ? to_f32(base[((long)yy * w + xx) * K + k]) : 0.f;
   }
-  long labs[NPX];
+  if (t < CT_Y * 8) {                             // low-res row y0 + yl from footprint row 4 yl + jj
+    const int yl = t >> 3, r = 4 * yl + (t & 7);
+    int ya, yb;
+    float wa, wb;
+    src_idx(4 * y0 - 2 + r, sh, h, ya, yb, wa, wb);
+    wtab[yl][t & 7] = (4 * y0 - 2 + r >= 0 && 4 * y0 - 2 + r < H)
+                          ? (ya == y0 + yl ? wa : 0.f) + (yb == y0 + yl ? wb : 0.f) : 0.f;
+  }
+  int ya, yb;
+  float wya, wyb;
+  src_idx(Y, sh, h, ya, yb, wya, wyb);            // rows outside the image: no valid pixel uses them
+  // the 4 pixels' weights on the run's columns x0 + c - 1 (tile column c) and x0 + c (c + 1);
+  // lv = the label of a valid pixel, -1 otherwise
+  const int xl = x0 + c - 1, xr = x0 + c;
+  float cl[4], cr[4];
+  int lv[4];
 #pragma unroll
-  for (int i = 0; i < NPX; ++i) {
-    const int pi = threadIdx.x + i * CE_BWD_NT;
-    labs[i] = pi < np ? label[((long)b * H + Ya + pi / rx) * W + Xa + pi % rx] : (long)ignore;
+  for (int j = 0; j < 4; ++j) {
+    int i0, i1;
+    float l0, l1;
+    src_idx(X0 + j, sw, w, i0, i1, l0, l1);
+    cl[j] = (i0 == xl ? l0 : 0.f) + (i1 == xl ? l1 : 0.f);
+    cr[j] = (i0 == xr ? l0 : 0.f) + (i1 == xr ? l1 : 0.f);
+    lv[j] = (lab[j] >= 0 && lab[j] < K && lab[j] != ignore) ? (int)lab[j] : -1;
   }
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
-    const int e = threadIdx.x + i * CE_BWD_NT;
+    const int e = t + i * CT_NT;
     if (e < LP * K) lg[(e % K) * LP + e / K] = v[i];
   }
-  for (int e = threadIdx.x; e < TY * RY + TX * RX; e += CE_BWD_NT) {
-    const bool isy = e < TY * RY;
-    const int q = isy ? e : e - TY * RY;
-    const int R = isy ? RY : RX;
-    const int tl = q / R, j = q % R;                  // low-res index within the tile, footprint index
-    float wgt = 0.f;
-    if (j < (isy ? ry : rx)) {
-      int i0, i1;
-      float l0, l1;
-      src_idx((isy ? Ya : Xa) + j, isy ? sh : sw, isy ? h : w, i0, i1, l0, l1);
-      const int t = (isy ? y0 : x0) + tl;
-      if (i0 == t) wgt += l0;
-      if (i1 == t) wgt += l1;
-    }
-    (isy ? wy : wx)[q] = wgt;
-  }
+  // classes K .. KF - 1: a very negative logit (exp2 -> 0, maxima unchanged), so the class loops
+  // below run KF iterations without a test on K (a runtime test became a branch per class)
+  for (int e = t; e < (KF - K) * LP; e += CT_NT) lg[K * LP + e] = -1e30f;
   __syncthreads();
-  // phase A: g for every footprint pixel (one pixel per lane)
+  // pass 1: the run's two row-interpolated columns per class (registers, log2 units), the bound
+  const float* la = lg + (min(max(ya - y0 + 1, 0), LH - 1)) * LW + c;
+  const float* lb = lg + (min(max(yb - y0 + 1, 0), LH - 1)) * LW + c;
+  const float wa2 = wya * LOG2E, wb2 = wyb * LOG2E;
+  float ml[KF], mr[KF];
+  float M = -INFINITY;
 #pragma unroll
-  for (int i = 0; i < NPX; ++i) {
-    const int pi = threadIdx.x + i * CE_BWD_NT;
-    if (pi >= np) break;
-    const int Y = Ya + pi / rx, X = Xa + pi % rx;
-    const long lab = labs[i];
-    if (lab == ignore || lab < 0 || lab >= K) {
-      for (int k = 0; k < K; ++k) g[k * RY * RX + pi] = from_f32<T>(0.f);
-      continue;
-    }
-    int ya, yb, xa, xb;
-    float wy0, wy1, wx0, wx1;
-    src_idx(Y, sh, h, ya, yb, wy0, wy1);
-    src_idx(X, sw, w, xa, xb, wx0, wx1);
-    const int pa = (ya - y0 + 1) * LW + (xa - x0 + 1), pb = (ya - y0 + 1) * LW + (xb - x0 + 1);
-    const int pc = (yb - y0 + 1) * LW + (xa - x0 + 1), pd = (yb - y0 + 1) * LW + (xb - x0 + 1);
-    const float c00 = wy0 * wx0, c01 = wy0 * wx1, c10 = wy1 * wx0, c11 = wy1 * wx1;
-    // compile-time trip counts (predicated on k < K): z stays in registers (a runtime-bound
-    // loop over a register array would spill it to scratch)
-    float z[KF];
-    float m = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < KF; ++k) {
-      const float* l = lg + k * LP;
-      z[k] = k < K ? c00 * l[pa] + c01 * l[pb] + c10 * l[pc] + c11 * l[pd] : -INFINITY;
-      m = fmaxf(m, z[k]);
-    }
-    float se = 0.f;
-#pragma unroll
-    for (int k = 0; k < KF; ++k) {
-      z[k] = __expf(z[k] - m);
-      se += z[k];
-    }
-    const float inv = gs / se;
-#pragma unroll
-    for (int k = 0; k < KF; ++k)
-      if (k < K) g[k * RY * RX + pi] = from_f32<T>(z[k] * inv - (k == lab ? gs : 0.f));
+  for (int k = 0; k < KF; ++k) {
+    ml[k] = __builtin_fmaf(wa2, la[k * LP], wb2 * lb[k * LP]);
+    mr[k] = __builtin_fmaf(wa2, la[k * LP + 1], wb2 * lb[k * LP + 1]);
+    M = fmaxf(M, fmaxf(ml[k], mr[k]));
   }
-  __syncthreads();
-  // phase B: x-adjoint t1[k][row][xl] = sum_X wx[xl][X] g[k][row][X].  The item index runs over
-  // the compile-time box (KF, RY, TX) -- constant divisors -- and skips what the tile lacks; the
-  // 8 taps are unchecked when they lie inside the footprint (every column but the image borders')
-  for (int e = threadIdx.x; e < KF * RY * TX; e += CE_BWD_NT) {
-    const int xl = e % TX, row = (e / TX) % RY, k = e / (TX * RY);
-    if (k >= K || row >= ry || xl >= nx) continue;
-    const T* gr = g + k * RY * RX + row * rx;
-    const float* wr = wx + xl * RX;
-    // exact x4 (align_corners=False): low-res column x takes full-res X in [4x - 2, 4x + 6)
-    // only (the borders' clamped taps included); the other footprint weights are zero
-    const int jb = 4 * (x0 + xl) - 2 - Xa;
-    float acc = 0.f;
-    if (jb >= 0 && jb + 8 <= rx) {
+  // pass 2: the softmax denominators (pixels outside the image: shift 0, unused)
+  float shv[4], sv[4];
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) acc += wr[jb + jj] * to_f32(gr[jb + jj]);
-    } else {
+  for (int j = 0; j < 4; ++j) {
+    shv[j] = (cl[j] + cr[j]) * M;
+    sv[j] = 0.f;
+  }
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        const int j = jb + jj;
-        acc += (j >= 0 && j < rx) ? wr[j] * to_f32(gr[j]) : 0.f;
+  for (int k = 0; k < KF; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      sv[j] += __builtin_amdgcn_exp2f(__builtin_fmaf(cl[j], ml[k], __builtin_fmaf(cr[j], mr[k], -shv[j])));
+  // a pixel whose own maximum lies more than ~100 binary orders below the bound (logits far apart
+  // between neighbouring low-res pixels) underflowed: redo it with its own maximum
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (lv[j] >= 0 && !(sv[j] >= 0x1p-100f)) {
+      float m = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < KF; ++k) m = fmaxf(m, __builtin_fmaf(cl[j], ml[k], cr[j] * mr[k]));
+      shv[j] = m;
+      sv[j] = 0.f;
+#pragma unroll
+      for (int k = 0; k < KF; ++k)
+        sv[j] += __builtin_amdgcn_exp2f(__builtin_fmaf(cl[j], ml[k], __builtin_fmaf(cr[j], mr[k], -m)));
+    }
+  const float gs = FWD ? 1.f : dloss[0] * stats[1];
+  float al[4], ar[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float inv = lv[j] >= 0 ? gs / sv[j] : 0.f;
+    al[j] = cl[j] * inv;
+    ar[j] = cr[j] * inv;
+  }
+  if constexpr (FWD) {
+    // loss of the valid pixels this tile owns (full-res [4 y0, 4 y0 + 4 CT_Y) x [4 x0, 4 x0 + 4 CT_X))
+    float ls = 0.f, lc = 0.f;
+    const bool rown = Y >= 4 * y0 && Y < 4 * (y0 + CT_Y);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int X = X0 + j;
+      if (lv[j] >= 0 && rown && X >= 4 * x0 && X < 4 * (x0 + CT_X)) {
+        const int q = lv[j] * LP;
+        const float zl = __builtin_fmaf(cl[j], __builtin_fmaf(wa2, la[q], wb2 * lb[q]),
+                                        cr[j] * __builtin_fmaf(wa2, la[q + 1], wb2 * lb[q + 1]));
+        ls += (shv[j] + __builtin_amdgcn_logf(sv[j]) - zl) * LN2;
+        lc += 1.f;
       }
     }
-    t1[(row * TX + xl) * KP + k] = acc;
+    ls = wave_sum(ls);
+    lc = wave_sum(lc);
+    if ((t & 63) == 0) {
+      red[0][t >> 6] = ls;
+      red[1][t >> 6] = lc;
+    }
+  }
+  // pass 3: the gradient's x-adjoint, the run's two column sums; the right column's go to LDS at
+  // once (lanes with nothing to write write the spare row: no per-class branch), the left
+  // column's wait in registers for the barrier; then the -onehot terms at the pixels' classes
+  float* trow = t1 + (act ? ri : 0) * CT_X * KP;
+  float* wrow = (act && c < CT_X) ? trow + c * KP : t1 + CT_R * CT_X * KP;
+  float sl[KF];
+#pragma unroll
+  for (int k = 0; k < KF; ++k) {
+    float gl = 0.f, gr = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(cl[j], ml[k], __builtin_fmaf(cr[j], mr[k], -shv[j])));
+      gl = __builtin_fmaf(al[j], e, gl);
+      gr = __builtin_fmaf(ar[j], e, gr);
+    }
+    wrow[k] = gr;                                 // classes >= K: 0, never read
+    sl[k] = gl;
+  }
+  if (act && c < CT_X)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (lv[j] >= 0) trow[c * KP + lv[j]] -= cr[j] * gs;
+  __syncthreads();
+  if (act && c >= 1) {
+#pragma unroll
+    for (int k = 0; k < KF; ++k) trow[(c - 1) * KP + k] += sl[k];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (lv[j] >= 0) trow[(c - 1) * KP + lv[j]] -= cl[j] * gs;
   }
   __syncthreads();
-  // phase C: y-adjoint, write the tile (k fastest: coalesced along the NHWC row)
-  for (int e = threadIdx.x; e < TY * TX * KF; e += CE_BWD_NT) {
-    const int k = e % KF, xl = (e / KF) % TX, yl = e / (KF * TX);
-    if (k >= K || xl >= nx || yl >= ny) continue;
-    const float* wr = wy + yl * RY;
-    const int jb = 4 * (y0 + yl) - 2 - Ya;              // rows [4y - 2, 4y + 6), as above
-    float acc = 0.f;
-    if (jb >= 0 && jb + 8 <= ry) {
+  if constexpr (FWD) {
+    if (t == 0) {
+      float a = 0.f, n = 0.f;
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) acc += wr[jb + jj] * t1[((jb + jj) * TX + xl) * KP + k];
-    } else {
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        const int j = jb + jj;
-        acc += (j >= 0 && j < ry) ? wr[j] * t1[(j * TX + xl) * KP + k] : 0.f;
+      for (int i = 0; i < CT_NT / 64; ++i) {
+        a += red[0][i];
+        n += red[1][i];
       }
+      part[blockIdx.x * 2] = a;
+      part[blockIdx.x * 2 + 1] = n;
     }
-    dlogits[((long)b * h * w + (long)(y0 + yl) * w + x0 + xl) * K + k] = from_f32<T>(acc);
   }
+  // y-adjoint: low-res row y takes full-res rows [4y - 2, 4y + 6) = footprint rows [4 yl, 4 yl + 8)
+  for (int e = t; e < CT_Y * CT_X * KF; e += CT_NT) {
+    const int k = e % KF, xq = (e / KF) % CT_X, yl = e / (KF * CT_X);
+    if (k >= K || xq >= nx || yl >= ny) continue;
+    const float* tc = t1 + (4 * yl * CT_X + xq) * KP + k;
+    float acc = 0.f;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) acc = __builtin_fmaf(wtab[yl][jj], tc[jj * CT_X * KP], acc);
+    const long o = ((long)b * h * w + (long)(y0 + yl) * w + x0 + xq) * K + k;
+    if constexpr (FWD) reinterpret_cast<float*>(dst)[o] = acc;
+    else reinterpret_cast<T*>(dst)[o] = from_f32<T>(acc);
+  }
+}
+
+// dlogits = adj * dloss[0] * stats[1]
+template <typename T>
+__global__ void ce_scale_kernel(const float* __restrict__ adj, const float* __restrict__ dloss,
+                                const float* __restrict__ stats, T* __restrict__ dl, long n) {
+  const float gs = dloss[0] * stats[1];
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    dl[i] = from_f32<T>(adj[i] * gs);
 }
 
 }  // namespace
@@ -306,6 +364,20 @@ int ce_fwd_tiled_launch(const void* logits, const int64_t* label, float* part, i
   return CMX_OK;
 }
 
+int ce_cells_nblk(int B, int h, int w) { return B * ((h + CT_Y - 1) / CT_Y) * ((w + CT_X - 1) / CT_X); }
+
+// loss partials (part: ce_cells_nblk x 2 floats) and adj (B, h, w, K) fp32 = bilinear adjoint of
+// (softmax - onehot), unscaled; exact x4, K <= 40
+int ce_cells_fwd_launch(const void* logits, const int64_t* label, float* adj, float* part, int B, int h, int w, int H,
+                        int W, int K, int ignore, int dtype, hipStream_t s) {
+  const int tx = (w + CT_X - 1) / CT_X, ty = (h + CT_Y - 1) / CT_Y;
+  CMX_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL((ce_cells<T, true>), dim3(B * tx * ty), dim3(CT_NT), 0, s, (const T*)logits, label, nullptr,
+                       nullptr, (void*)adj, part, h, w, H, W, K, ignore, tx, ty);
+  });
+  return cmx_check_launch("ce_cells_fwd");
+}
+
 extern "C" {
 
 // dlogits (B, h, w, K) = bilinear-adjoint of (softmax - onehot) * dloss[0] * stats[1], with
@@ -317,12 +389,24 @@ int cmx_upsample_ce_bwd(const void* logits, const int64_t* label, const float* d
                         hipStream_t s) {
   CMX_REQUIRE(B > 0 && ce_tiled_ok(h, w, H, W, K), CMX_ERR_SHAPE,
               "upsample_ce_bwd: needs K <= %d and an exact x4 upsampling (K=%d, %dx%d -> %dx%d)", KF, K, h, w, H, W);
-  const int tx = (w + TX - 1) / TX, ty = (h + TY - 1) / TY;
+  const int tx = (w + CT_X - 1) / CT_X, ty = (h + CT_Y - 1) / CT_Y;
   CMX_DISPATCH(dtype, T, {
-    hipLaunchKernelGGL(ce_bwd_fused<T>, dim3(B * tx * ty), dim3(CE_BWD_NT), 0, s, (const T*)logits, label, dloss, stats,
-                       (T*)dlogits, h, w, H, W, K, ignore_index, tx, ty);
+    hipLaunchKernelGGL((ce_cells<T, false>), dim3(B * tx * ty), dim3(CT_NT), 0, s, (const T*)logits, label, dloss,
+                       stats, dlogits, nullptr, h, w, H, W, K, ignore_index, tx, ty);
   });
   return cmx_check_launch("upsample_ce_bwd");
+}
+
+// the backward of cmx_upsample_ce_fwd_adj: dlogits = adj * dloss[0] * stats[1] (n elements)
+int cmx_upsample_ce_bwd_scale(const float* adj, const float* dloss, const float* stats, void* dlogits, int64_t n,
+                              int dtype, hipStream_t s) {
+  CMX_REQUIRE(adj && dloss && stats && dlogits && n >= 0, CMX_ERR_ARG, "upsample_ce_bwd_scale: null operand");
+  if (n == 0) return CMX_OK;
+  const unsigned grid = (unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  CMX_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL(ce_scale_kernel<T>, dim3(grid), dim3(256), 0, s, adj, dloss, stats, (T*)dlogits, (long)n);
+  });
+  return cmx_check_launch("upsample_ce_bwd_scale");
 }
 
 }  // extern "C"

@@ -17,18 +17,24 @@ struct FoldBias {
   float* dbc[4];
 };
 
-// b[k] = bf[k] + sum_j Wf[k, j] bcat[j], one wave per row k
+// b[k] = bf[k] + sum_j Wf[k, j] bcat[j], one wave per row k; each lane reads 16-byte runs of
+// the row (8 x 16-bit or 4 x fp32 elements, inside one slot since E % 8 == 0)
 template <typename T>
 __global__ void fold_bias_kernel(const T* __restrict__ Wf, long ldw, const float* __restrict__ bf, FoldBias p,
                                  float* __restrict__ b, int E) {
+  constexpr int V = VecT<T>::N;
   const int lane = threadIdx.x & 63;
   const int k = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (k >= E) return;                                   // whole wave
   const T* row = Wf + (long)k * ldw;
   float acc = 0.f;
-  for (int s = 0; s < 4; ++s) {
-    const float* bc = p.bc[s];
-    for (int e = lane; e < E; e += 64) acc += to_f32(row[s * E + e]) * bc[e];
+  for (int j = lane * V; j < 4 * E; j += 64 * V) {
+    const int s = j / E, e = j - s * E;
+    float w[V];
+    load_vec<T>(row + j, w);
+    const float* bc = p.bc[s] + e;
+#pragma unroll
+    for (int i = 0; i < V; ++i) acc += w[i] * bc[i];
   }
   acc = wave_sum(acc);
   if (lane == 0) b[k] = bf[k] + acc;
@@ -96,8 +102,9 @@ extern "C" {
 
 int cmx_decoder_fold_bias(const void* Wf, int64_t ldw, const float* bf, const float* bc4, const float* bc3,
                           const float* bc2, const float* bc1, float* b, int E, int dtype, hipStream_t s) {
-  CMX_REQUIRE(Wf && bf && bc4 && bc3 && bc2 && bc1 && b && E > 0 && ldw >= 4 * E, CMX_ERR_ARG,
-              "decoder_fold_bias: E=%d ldw=%ld", E, (long)ldw);
+  CMX_REQUIRE(Wf && bf && bc4 && bc3 && bc2 && bc1 && b && E > 0 && E % 8 == 0 && ldw >= 4 * E && ldw % 8 == 0 &&
+              (uintptr_t)Wf % 16 == 0, CMX_ERR_ARG, "decoder_fold_bias: E=%d ldw=%ld (multiples of 8, 16-B aligned)",
+              E, (long)ldw);
   FoldBias p{{bc4, bc3, bc2, bc1}, {nullptr, nullptr, nullptr, nullptr}};
   CMX_DISPATCH(dtype, T, {
     hipLaunchKernelGGL(fold_bias_kernel<T>, dim3(cdiv(E, 4)), dim3(256), 0, s, (const T*)Wf, (long)ldw, bf, p, b, E);

@@ -113,6 +113,9 @@ int ce_fwd_tiled_nblk(int B, int H, int W);
 bool ce_tiled_ok(int h, int w, int H, int W, int K);
 int ce_fwd_tiled_launch(const void* logits, const int64_t* label, float* part, int B, int h, int w, int H, int W,
                         int K, int ignore, int dtype, hipStream_t s);
+int ce_cells_nblk(int B, int h, int w);
+int ce_cells_fwd_launch(const void* logits, const int64_t* label, float* adj, float* part, int B, int h, int w, int H,
+                        int W, int K, int ignore, int dtype, hipStream_t s);
 
 extern "C" {
 
@@ -141,6 +144,19 @@ int cmx_upsample_ce_fwd(const void* logits, const int64_t* label, void* grad, fl
   });
   hipLaunchKernelGGL(ce_finalize_kernel, dim3(1), dim3(256), 0, s, workspace, nb, out);
   return cmx_check_launch("upsample_ce_fwd");
+}
+
+// training form of the x4 path: loss (out, as above) and adj (B, h, w, K) fp32 = bilinear adjoint of
+// (softmax - onehot) in one pass; the backward is cmx_upsample_ce_bwd_scale
+int cmx_upsample_ce_fwd_adj(const void* logits, const int64_t* label, float* adj, float* out, float* workspace, int B,
+                            int h, int w, int H, int W, int K, int ignore_index, int dtype, hipStream_t s) {
+  CMX_REQUIRE(B > 0 && adj && ce_tiled_ok(h, w, H, W, K), CMX_ERR_SHAPE,
+              "upsample_ce_fwd_adj: needs H = 4h, W = 4w, K <= 40 (K=%d, %dx%d -> %dx%d)", K, h, w, H, W);
+  const int nb = ce_cells_nblk(B, h, w);
+  const int st = ce_cells_fwd_launch(logits, label, adj, workspace, B, h, w, H, W, K, ignore_index, dtype, s);
+  if (st) return st;
+  hipLaunchKernelGGL(ce_finalize_kernel, dim3(1), dim3(256), 0, s, workspace, nb, out);
+  return cmx_check_launch("upsample_ce_fwd_adj");
 }
 
 }  // extern "C"

@@ -1513,13 +1513,21 @@ class UpsampleCEF(Function):
     @staticmethod
     def forward(ctx, logits, label, dims, ignore):
         B, h, w, H, W, Kc = dims
-        # exact x4 (every CMX config), K <= 40: loss only here, the gradient is recomputed tile
-        # by tile in the backward (cmx_upsample_ce_bwd); else the materialised-gradient path
+        # exact x4 (every CMX config), K <= 40: with a backward to come, the loss and the bilinear
+        # adjoint of (softmax - onehot) in one pass (cmx_upsample_ce_fwd_adj; the backward scales
+        # it by dloss / n_valid); without one, the loss only.  Else the materialised-gradient path
         fused = H == 4 * h and W == 4 * w and Kc <= 40
         logits = _c(logits)
         grad = None if fused else torch.empty(B, H, W, Kc, dtype=logits.dtype, device=logits.device)
         out = torch.empty(3, dtype=torch.float32, device=logits.device)
         ws = K._ws(K.query("cmx_upsample_ce_workspace", B, H, W), logits.device)
+        if fused and ctx.needs_input_grad[0]:
+            adj = torch.empty(B, h * w, Kc, dtype=torch.float32, device=logits.device)
+            K.call("cmx_upsample_ce_fwd_adj", K.ptr(logits), K.ptr(label), K.ptr(adj), K.ptr(out), K.ptr(ws), B, h, w,
+                   H, W, Kc, ignore, K.dtype_code(logits), K.stream())
+            ctx.save_for_backward(adj, out, label)
+            ctx.fused, ctx.ignore, ctx.ldtype, ctx.lshape = "adj", ignore, logits.dtype, logits.shape
+            return out[0]
         K.call("cmx_upsample_ce_fwd", K.ptr(logits), K.ptr(label), K.ptr(grad), K.ptr(out), K.ptr(ws), B, h, w, H,
                W, Kc, ignore, K.dtype_code(logits), K.stream())
         ctx.save_for_backward(logits if fused else grad, out, label)
@@ -1532,8 +1540,13 @@ class UpsampleCEF(Function):
     @staticmethod
     def backward(ctx, dloss):
         grad, out, label = ctx.saved_tensors
-        B, h, w, H, W, Kc = ctx.dims
         dloss = _c(dloss.reshape(1).to(torch.float32))
+        if ctx.fused == "adj":
+            dl = torch.empty(ctx.lshape, dtype=ctx.ldtype, device=grad.device)
+            K.call("cmx_upsample_ce_bwd_scale", K.ptr(grad), K.ptr(dloss), K.ptr(out), K.ptr(dl), dl.numel(),
+                   K.dtype_code(dl), K.stream())
+            return dl, None, None, None
+        B, h, w, H, W, Kc = ctx.dims
         if ctx.fused:
             logits = grad
             dl = torch.empty(B, h * w, Kc, dtype=ctx.ldtype, device=logits.device)

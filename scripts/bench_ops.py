@@ -37,7 +37,13 @@ def ce():
     fwd()
     bwd = lambda: K.call("cmx_upsample_ce_bwd", K.ptr(logits), K.ptr(label), K.ptr(dloss), K.ptr(out), K.ptr(dl), B, h,
                          w, H, W, Kc, 255, 1, K.stream())
-    return {"ce_fwd": timeit(fwd), "ce_bwd": timeit(bwd)}
+    adj = torch.empty(B, h * w, Kc, device="cuda")
+    fwd_adj = lambda: K.call("cmx_upsample_ce_fwd_adj", K.ptr(logits), K.ptr(label), K.ptr(adj), K.ptr(out), K.ptr(ws),
+                             B, h, w, H, W, Kc, 255, 1, K.stream())
+    scale = lambda: K.call("cmx_upsample_ce_bwd_scale", K.ptr(adj), K.ptr(dloss), K.ptr(out), K.ptr(dl), dl.numel(), 1,
+                           K.stream())
+    return {"ce_fwd (loss only)": timeit(fwd), "ce_bwd (recompute)": timeit(bwd), "ce_fwd_adj (training)": timeit(fwd_adj),
+            "ce_bwd_scale (training)": timeit(scale)}
 
 
 def bn():

@@ -151,15 +151,19 @@ def test_sra_fwd_kernel_choice(dev, dtype, Bt, N, Nk, heads):
 
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("B,h,w,K", [(2, 120, 160, 40), (1, 15, 20, 9), (2, 16, 24, 19)])
-@pytest.mark.parametrize("fused", [True, False])
-def test_upsample_ce(dev, dtype, B, h, w, K, fused):
+@pytest.mark.parametrize("mode", ["adj", "recompute", "materialised"])
+def test_upsample_ce(dev, dtype, B, h, w, K, mode):
     """Final x4 bilinear upsample + CrossEntropyLoss(mean, ignore_index=255) (builder.py:233,249;
-    train.py:72-73): loss and d logits against torch fp64 autograd.  fused=True: loss-only
-    forward + tile-recomputing backward (ce_fused.hip); False: the materialised-gradient path
-    (forced by a non-x4 output size)."""
+    train.py:72-73): loss and d logits against torch fp64 autograd.  adj: the training form
+    (loss + unscaled adjoint in the forward, a scale in the backward: cmx_upsample_ce_fwd_adj /
+    cmx_upsample_ce_bwd_scale); recompute: loss-only forward + tile-recomputing backward
+    (cmx_upsample_ce_fwd with grad = NULL, cmx_upsample_ce_bwd; ce_fused.hip); materialised: the
+    full-resolution gradient path (forced by a non-x4 output size)."""
     import torch.nn.functional as Fn
+    from rgbx_semantic_segmentation_amd import kernels as Kn
     from rgbx_semantic_segmentation_amd.functions import UpsampleCEF
     torch.manual_seed(7)
+    fused = mode != "materialised"
     H, W = (4 * h, 4 * w) if fused else (4 * h - 2, 4 * w + 3)
     lg = torch.randn(B, h, w, K, dtype=torch.float64) * 3
     lab = torch.randint(0, K, (B, H, W))
@@ -169,11 +173,24 @@ def test_upsample_ce(dev, dtype, B, h, w, K, fused):
     loss_ref = Fn.cross_entropy(up, lab, reduction="mean", ignore_index=255)
     (loss_ref * 0.7).backward()
     x = lg.to(dev, dtype).requires_grad_(True)
-    loss = UpsampleCEF.apply(x, lab.to(dev), (B, h, w, H, W, K), 255)
-    (loss * 0.7).backward()
+    if mode == "recompute":
+        xl, labd = x.detach().contiguous(), lab.to(dev)
+        out = torch.empty(3, device=dev)
+        ws = Kn._ws(Kn.query("cmx_upsample_ce_workspace", B, H, W), dev)
+        Kn.call("cmx_upsample_ce_fwd", Kn.ptr(xl), Kn.ptr(labd), 0, Kn.ptr(out), Kn.ptr(ws), B, h, w, H, W, K, 255,
+                Kn.dtype_code(xl), Kn.stream())
+        dloss = torch.full((1,), 0.7, device=dev)
+        grad = torch.empty_like(xl)
+        Kn.call("cmx_upsample_ce_bwd", Kn.ptr(xl), Kn.ptr(labd), Kn.ptr(dloss), Kn.ptr(out), Kn.ptr(grad), B, h, w, H,
+                W, K, 255, Kn.dtype_code(xl), Kn.stream())
+        loss, xg = out[0], grad
+    else:
+        loss = UpsampleCEF.apply(x, lab.to(dev), (B, h, w, H, W, K), 255)
+        (loss * 0.7).backward()
+        xg = x.grad
     torch.cuda.synchronize()
     assert abs(loss.item() - loss_ref.item()) / loss_ref.item() < (1e-5 if dtype == torch.float32 else 1e-2)
-    assert relerr(x.grad, ref.grad) < TOL[dtype] * 2, relerr(x.grad, ref.grad)
+    assert relerr(xg, ref.grad) < TOL[dtype] * 2, relerr(xg, ref.grad)
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
