@@ -171,6 +171,13 @@ int cmx_bn_bwd_apply(const void* dy, const void* x, const float* mean, const flo
  *      and its separable 1-D adjoint (backward). */
 int cmx_bilinear_fwd_nhwc(const void* in, void* out, int NB, int Hi, int Wi, int Ho, int Wo, int C, int64_t out_pix_stride, int dtype, hipStream_t stream);
 int cmx_bilinear_fwd_nchw_f32(const void* in, float* out, int NB, int Hi, int Wi, int Ho, int Wo, int C, int dtype, hipStream_t stream);
+/* U (B, H, W, C) = bias + up(z0) + up(z1) + up(z2) (any source NULL: absent; bias fp32 or NULL): DecoderHead's three
+ * upsampled branch products summed in one pass (the decoder fold's c1 GEMM adds U as its residual).  C % 64 == 0,
+ * the source widths sum to <= 160. */
+int cmx_bilinear_up3_add(const void* z0, const void* z1, const void* z2, int B, int h0, int w0, int h1, int w1, int h2, int w2, const float* bias, void* out, int H, int W, int C, int dtype, hipStream_t stream);
+/* The backward of up to three upsampled branches from one read of dz (B, H, W, C): y_s (B, h_s, w_s, C) = up_s^T dz
+ * (y1 / y2 NULL: absent), through fp32 workspaces t_s (B*H, w_s, C).  Two launches (x pass, y pass); C % 128 == 0 (fp32: C % 64 == 0). */
+int cmx_bilinear_adjoint3(const void* dz, float* t0, float* t1, float* t2, void* y0, void* y1, void* y2, int B, int H, int W, int h0, int w0, int h1, int w1, int h2, int w2, int C, int dtype, hipStream_t stream);
 int cmx_bilinear_adjoint_1d(const void* in, void* out, int64_t P, int Lo, int Li, int Q, int64_t sp, int64_t so, const float* a1, const float* a2, float alpha0, int in_dtype, int out_dtype, hipStream_t stream);
 /* DecoderHead.linear_fuse (MLPDecoder.py:66-77) without the (B, N1, 4E) concat: the 1x1 conv commutes with the
  * bilinear upsample (linear, weights sum to 1), so Z = e1 Wf[:, 3E:]^T + bias + up(z4) + up(z3) + up(z2) with the

@@ -1408,6 +1408,28 @@ class DecoderFuseF(Function):
 
 # CMX_DECODER_FOLD=0: linear_c{1..4} as their own GEMMs ahead of DecoderFuseF (A/B switch)
 DECODER_FOLD = os.environ.get("CMX_DECODER_FOLD", "1") != "0"
+# CMX_DECODER_UP3=1: DecoderFoldF's forward sums the three upsampled branches in a separate pass
+# (cmx_bilinear_up3_add) and runs the c1 GEMM with it as a plain residual, instead of adding them
+# in the c1 GEMM's epilogue (cmx_decoder_fuse_fwd).  Off: 38 + 27 us in the step against 57 for the
+# epilogue form (round 6).  CMX_DECODER_ADJ3=0: the backward takes the three bilinear adjoints one
+# grid at a time (2 launches each, dZ read three times) instead of from one read of dZ
+# (cmx_bilinear_adjoint3: 55 against 79 us in the step)
+DECODER_UP3 = os.environ.get("CMX_DECODER_UP3", "0") == "1"
+DECODER_ADJ3 = os.environ.get("CMX_DECODER_ADJ3", "1") != "0"
+
+
+def _up3_ok(E, ws):
+    """cmx_bilinear_up3_add takes this decoder's shapes (its staging budget)."""
+    return DECODER_UP3 and E % 64 == 0 and sum(ws) <= 160
+
+
+def _adj3_ok(E, W1, ws, dtype):
+    """cmx_bilinear_adjoint3 takes this decoder's shapes (its LDS budget)."""
+    cs, esz = (64, 4) if dtype == torch.float32 else (128, 2)
+    if not DECODER_ADJ3 or E % cs:
+        return False
+    taps = sum(w * ((2 * W1 + w - 1) // w + 3) for w in ws)
+    return (2 * taps + 3) // 4 * 16 + W1 * cs * esz <= 65536
 
 
 class DecoderFoldF(Function):
@@ -1422,7 +1444,8 @@ class DecoderFoldF(Function):
     c2..c4 products x_i M_i^T at their own resolution (one multi launch) and the c1 product
     (K = C1 = 64 instead of the reference's two GEMMs with K = 64 and K = 512) with their
     bilinear upsample added in its epilogue (cmx_decoder_fuse_fwd).  Neither the (B, N1, 4E)
-    concat nor the four (B, N_i, E) projections exist.  Backward, with dY_i = up_i^T dZ:
+    concat nor the four (B, N_i, E) projections exist.  Backward, with dY_i = up_i^T dZ (the three
+    bilinear adjoints from one read of dZ, cmx_bilinear_adjoint3):
     dx_i = dY_i M_i (one multi launch); dM_i = dY_i^T x_i and gb = sum_rows dZ are queued
     weight-gradient problems; after the flush that forms them (deferred.after) the chain rule
 
@@ -1453,18 +1476,25 @@ class DecoderFoldF(Function):
             zs.append(z)
         _gemm_group(jobs)                         # the three low-resolution branch products: one launch
         Z = torch.empty(B * N1, E, dtype=x1.dtype, device=x1.device)
-        K.call("cmx_decoder_fuse_fwd", K.ptr(_c(x1)), K.ptr(Ms[3]), K.ptr(Z), K.ptr(b), K.ptr(zs[0]), K.ptr(zs[1]),
-               K.ptr(zs[2]), B, H1, W1, hw[2][0], hw[2][1], hw[1][0], hw[1][1], hw[0][0], hw[0][1], E, C1, C1, C1,
-               K.dtype_code(x1), K.stream())
+        if _up3_ok(E, [w for (_, w) in hw]):
+            # b + the three upsampled products in one pass, then the c1 GEMM with it as the residual
+            U = torch.empty(1, B * N1, E, dtype=x1.dtype, device=x1.device)
+            K.call("cmx_bilinear_up3_add", K.ptr(zs[0]), K.ptr(zs[1]), K.ptr(zs[2]), B, hw[2][0], hw[2][1], hw[1][0],
+                   hw[1][1], hw[0][0], hw[0][1], K.ptr(b), K.ptr(U), H1, W1, E, K.dtype_code(x1), K.stream())
+            K.gemm(_c(x1).view(1, B * N1, C1), Ms[3], Z.view(1, B * N1, E), residual=U)
+        else:
+            K.call("cmx_decoder_fuse_fwd", K.ptr(_c(x1)), K.ptr(Ms[3]), K.ptr(Z), K.ptr(b), K.ptr(zs[0]), K.ptr(zs[1]),
+                   K.ptr(zs[2]), B, H1, W1, hw[2][0], hw[2][1], hw[1][0], hw[1][1], hw[0][0], hw[0][1], E, C1, C1, C1,
+                   K.dtype_code(x1), K.stream())
         ctx.save_for_backward(*xs, Wf, *Wc, *Ms)
-        ctx.meta = (bc, grads, sizes)
+        ctx.meta = (bc, grads, sizes, _adj3_ok(E, W1, [w for (_, w) in hw], x1.dtype))
         return Z
 
     @staticmethod
     def backward(ctx, dZ):
         t = ctx.saved_tensors
         xs, Wf, Wc, Ms = t[:4], t[4], t[5:9], t[9:13]
-        bc, grads, sizes = ctx.meta
+        bc, grads, sizes, adj3 = ctx.meta
         B, N1, C1 = xs[3].shape
         E = Wf.shape[0]
         (H1, W1), hw = sizes[0], sizes[1:]
@@ -1475,9 +1505,20 @@ class DecoderFoldF(Function):
             offs.append(offs[-1] + E * C)
         dM = torch.empty(offs[-1], dtype=torch.float32, device=dZ.device)
         gb = torch.empty(1, E, dtype=torch.float32, device=dZ.device)
+        if adj3:
+            # the three grids' bilinear adjoints from one read of dZ (cmx_bilinear_adjoint3)
+            dYs = [torch.empty(1, B * h * w, E, dtype=dZ.dtype, device=dZ.device) for (h, w) in (hw[2], hw[1], hw[0])]
+            ts = [torch.empty(B * H1 * w * E, dtype=torch.float32, device=dZ.device) for (h, w) in (hw[2], hw[1], hw[0])]
+            K.call("cmx_bilinear_adjoint3", K.ptr(dZ), *[K.ptr(t) for t in ts], *[K.ptr(y) for y in dYs], B, H1, W1,
+                   hw[2][0], hw[2][1], hw[1][0], hw[1][1], hw[0][0], hw[0][1], E, K.dtype_code(dZ), K.stream())
         dxs, jobs = [], []
         for s in range(4):
-            dY = dZ if s == 3 else _adjoint_to(dZ, B, H1, W1, *hw[2 - s], E).view(1, -1, E)
+            if s == 3:
+                dY = dZ
+            elif adj3:
+                dY = dYs[s]
+            else:
+                dY = _adjoint_to(dZ, B, H1, W1, *hw[2 - s], E).view(1, -1, E)
             x = xs[s].reshape(1, -1, Cs[s])
             dx = torch.empty_like(x)
             jobs.append(dict(A=dY, B=Ms[s].transpose(1, 2), C=dx))

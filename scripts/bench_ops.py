@@ -46,6 +46,36 @@ def ce():
             "ce_bwd_scale (training)": timeit(scale)}
 
 
+def decoder():
+    """The decoder fold's full-resolution passes at the B2 shapes: the upsample-sum (up3) + the c1
+    residual GEMM against the c1 GEMM with the upsample in its epilogue, and the 3-grid adjoint
+    against three 2-pass adjoints."""
+    from rgbx_semantic_segmentation_amd import functions as F
+    B, H, W, E = 2, 120, 160, 512
+    grids = [(15, 20), (30, 40), (60, 80)]
+    bf = torch.bfloat16
+    zs = [torch.randn(1, B * h * w, E, device="cuda").to(bf) for (h, w) in grids]
+    bias = torch.randn(E, device="cuda")
+    x1 = torch.randn(1, B * H * W, 64, device="cuda").to(bf)
+    M1 = torch.randn(1, E, 64, device="cuda").to(bf)
+    U = torch.empty(1, B * H * W, E, device="cuda").to(bf)
+    Z = torch.empty(1, B * H * W, E, device="cuda").to(bf)
+    g = [v for hw in grids for v in hw]
+    up3 = lambda: K.call("cmx_bilinear_up3_add", *[K.ptr(z) for z in zs], B, *g, K.ptr(bias), K.ptr(U), H, W, E, 1,
+                         K.stream())
+    res = lambda: K.gemm(x1, M1, Z, residual=U)
+    epi = lambda: K.call("cmx_decoder_fuse_fwd", K.ptr(x1), K.ptr(M1), K.ptr(Z), K.ptr(bias), *[K.ptr(z) for z in zs],
+                         B, H, W, *g, E, 64, 64, 64, 1, K.stream())
+    dZ = torch.randn(1, B * H * W, E, device="cuda").to(bf)
+    ys = [torch.empty(1, B * h * w, E, device="cuda").to(bf) for (h, w) in grids]
+    ts = [torch.empty(B * H * w * E, device="cuda") for (h, w) in grids]
+    adj3 = lambda: K.call("cmx_bilinear_adjoint3", K.ptr(dZ), *[K.ptr(t) for t in ts], *[K.ptr(y) for y in ys], B, H,
+                          W, *g, E, 1, K.stream())
+    adj1 = lambda: [F._adjoint_to(dZ, B, H, W, h, w, E) for (h, w) in grids]
+    return {"up3_add": timeit(up3), "c1 residual gemm": timeit(res), "c1 gemm + upsample epilogue": timeit(epi),
+            "adjoint3 (x + y)": timeit(adj3), "3 x adjoint_to (6 launches)": timeit(adj1)}
+
+
 def bn():
     res = {}
     for M, C in [(38400, 512), (2400, 320), (600, 512), (38400, 64)]:
@@ -66,7 +96,7 @@ def bn():
 
 
 if __name__ == "__main__":
-    want = sys.argv[1:] or ["ce", "bn"]
+    want = sys.argv[1:] or ["ce", "bn", "decoder"]
     for name in want:
         for k, v in globals()[name]().items():
             print(f"{k:32s} {v:8.2f} us")

@@ -64,7 +64,7 @@ def test_decoder_fuse_matches_upsample_concat_conv(dev, dtype, B, H1, W1, E):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("B,H1,W1,E,Cs", [(2, 120, 160, 512, (64, 128, 320, 512)), (1, 32, 40, 128, (32, 64, 160, 256)),
-                                          (2, 30, 17, 64, (32, 64, 160, 256))])
+                                          (2, 30, 17, 64, (32, 64, 160, 256)), (2, 30, 17, 128, (32, 64, 160, 256))])
 def test_decoder_fold_matches_mlp_upsample_concat_conv(dev, dtype, B, H1, W1, E, Cs):
     """functions.DecoderFoldF against the reference decode head's op sequence in fp32
     (MLPDecoder.py:60-77: linear_c{1..4} -> upsample -> concat c4, c3, c2, c1 -> 1x1 conv):
@@ -118,6 +118,36 @@ def test_decoder_fold_matches_mlp_upsample_concat_conv(dev, dtype, B, H1, W1, E,
         assert rel(bcg[i], bcr[i].grad) < tol, (i, rel(bcg[i], bcr[i].grad))
     assert rel(Wfg[0], Wr.grad) < tol, rel(Wfg[0], Wr.grad)
     assert rel(bfg, br.grad) < tol, rel(bfg, br.grad)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,H,W,C", [(2, 120, 160, 512), (1, 30, 17, 128), (2, 64, 64, 256)])
+def test_bilinear_up3_and_adjoint3(dev, dtype, B, H, W, C):
+    """cmx_bilinear_up3_add (bias + the sum of three bilinear upsamples, MLPDecoder.py:67-73) and
+    cmx_bilinear_adjoint3 (its backward to the three grids from one read of dZ) against
+    F.interpolate and its autograd adjoint in fp32, incl. non-integer scale factors."""
+    from rgbx_semantic_segmentation_amd import kernels as K
+    torch.manual_seed(3)
+    grids = [((H + 7) // 8, (W + 7) // 8), ((H + 3) // 4, (W + 3) // 4), ((H + 1) // 2, (W + 1) // 2)]
+    zs = [torch.randn(B, h, w, C, device=dev).to(dtype) for (h, w) in grids]
+    bias = torch.randn(C, device=dev)
+    U = torch.empty(B, H, W, C, dtype=dtype, device=dev)
+    K.call("cmx_bilinear_up3_add", *[K.ptr(z) for z in zs], B, *[v for g in grids for v in g], K.ptr(bias), K.ptr(U),
+           H, W, C, K.dtype_code(U), K.stream())
+    zr = [z.float().permute(0, 3, 1, 2).requires_grad_(True) for z in zs]
+    Ur = bias.view(1, C, 1, 1) + sum(TF.interpolate(z, size=(H, W), mode="bilinear", align_corners=False) for z in zr)
+    dZ = torch.randn(B, H, W, C, device=dev).to(dtype)
+    Ur.backward(dZ.float().permute(0, 3, 1, 2))
+    ys = [torch.empty(B, h, w, C, dtype=dtype, device=dev) for (h, w) in grids]
+    ts = [torch.empty(B * H * w * C, device=dev) for (h, w) in grids]
+    K.call("cmx_bilinear_adjoint3", K.ptr(dZ), *[K.ptr(t) for t in ts], *[K.ptr(y) for y in ys], B, H, W,
+           *[v for g in grids for v in g], C, K.dtype_code(dZ), K.stream())
+    torch.cuda.synchronize()
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel(U, Ur.detach().permute(0, 2, 3, 1)) < tol, rel(U, Ur.detach().permute(0, 2, 3, 1))
+    for y, z in zip(ys, zr):
+        ref = z.grad.permute(0, 2, 3, 1)
+        assert rel(y, ref) < tol, rel(y, ref)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
