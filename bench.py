@@ -308,15 +308,19 @@ def main():
         from rgbx_semantic_segmentation_amd.optim import GradScaler
         scaler = GradScaler(device=dev)
 
+    # the backward's seed d loss / d loss = 1 as a persistent tensor: loss.backward() would fill a
+    # fresh one with a kernel launch inside every step (same value, same semantics)
+    seed = torch.ones((), device=dev)
+
     def step():
         loss = model(rgb, x, lab)
         opt.zero_grad()                 # train.py:188's order (arms the per-segment update overlap)
         if scaler is not None:
-            scaler.scale(loss).backward()
+            scaler.scale(loss).backward(seed)
             scaler.step(opt)
             scaler.update()
         else:
-            loss.backward()
+            loss.backward(seed)
             opt.step()
         return loss
 
