@@ -477,7 +477,8 @@ def main():
     roof = families = None
     if not skip and graph is not None:
         try:
-            roof, families = measure_in_step(run_one, workload, shape, float(model.store.flat.numel()))
+            roof, families = measure_in_step(run_one, workload, shape, float(model.store.flat.numel()),
+                                             step_us=ms * 1e3)
         except Exception as e:  # pragma: no cover - tracer availability is the box's
             print(f"[bench] in-step kernel trace failed: {e!r}", file=sys.stderr)
     model.backbone.grad_sync = None
