@@ -166,6 +166,11 @@ int cmx_bn_finalize(const double* sums, double count, float eps, float momentum,
 int cmx_bn_apply(const void* x, const float* mean, const float* invstd, const float* gamma, const float* beta, const void* res, const float* dscale, void* y, int64_t M, int C, int64_t rows_per_sample, int act, int dtype, hipStream_t stream);
 int cmx_bn_bwd_reduce(const void* dy, const void* x, const float* mean, const float* invstd, const float* gamma, const float* beta, const void* res, const float* dscale, double* sums, float* dgamma, float* dbeta, double* workspace, int64_t M, int C, int64_t rows_per_sample, int act, int accumulate, int dtype, hipStream_t stream);
 int cmx_bn_bwd_apply(const void* dy, const void* x, const float* mean, const float* invstd, const float* gamma, const float* beta, const void* res, const float* dscale, const double* sums, double count, void* dx, void* dres, int64_t M, int C, int64_t rows_per_sample, int act, int training, int dtype, hipStream_t stream);
+/* Small maps (local statistics, training; the stage-3/4 ChannelEmbed BNs): the forward (sums, finalize incl. running
+ * stats, apply) and the backward (both sums, dgamma / dbeta, dx / dres) each in ONE launch of C / 16 workgroups that
+ * own 16 channels over all M rows.  C % 16 == 0. */
+int cmx_bn_small_fwd(const void* x, const void* res, const float* gamma, const float* beta, const float* dscale, void* y, double* sums, float* mean, float* invstd, float* running_mean, float* running_var, int64_t M, int C, int64_t rows_per_sample, int act, float eps, float momentum, int dtype, hipStream_t stream);
+int cmx_bn_small_bwd(const void* dy, const void* x, const float* mean, const float* invstd, const float* gamma, const float* beta, const void* res, const float* dscale, float* dgamma, float* dbeta, void* dx, void* dres, int64_t M, int C, int64_t rows_per_sample, int act, int accumulate, int dtype, hipStream_t stream);
 
 /* ---- bilinear, align_corners=False (F.interpolate in MLPDecoder.py:67-73, builder.py:233)
  *      and its separable 1-D adjoint (backward). */

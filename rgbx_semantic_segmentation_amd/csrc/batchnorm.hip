@@ -348,6 +348,201 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
   }
 }
 
+// ---------------------------------------------------------------- small maps, one launch
+// Small local-statistics BatchNorms (the stage-4 ChannelEmbed BNs, 600 rows): a workgroup of 1024
+// lanes owns BS_SC = 16 channels over ALL rows, so the statistics, the finalize and the apply
+// (forward), or both backward sums, dgamma / dbeta and dx (backward), are one launch instead of
+// three (each of which costs ~5 us of latency at these sizes).  Lanes: TPR = 16 / V per row, two
+// rows' loads in flight per lane; a wave folds its rows by xor-shuffles, the block folds its 16
+// waves in LDS.  fp64 sums as the multi-launch path (different order: the fp64 sums agree to
+// rounding).  Measured (bench_ops.py bnsmall): 600 x 512 forward 11.9 vs 20.2 us, backward 12.9
+// vs 21.2; at 2400 x 320 the 20 workgroups' row chains lose (15.3 / 19.1 vs 18.2 / 20.4, and one
+// 8-channel chunk per workgroup was slower still: 15.9 / 22.7), hence CMX_BN_SMALL_M = 600.
+constexpr int BS_NT = 1024, BS_SC = 16;
+
+template <int TPR>
+__device__ __forceinline__ double wave_fold_rows(double v) {
+#pragma unroll
+  for (int o = TPR; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T>
+__global__ __launch_bounds__(BS_NT) void bn_small_fwd_kernel(const T* __restrict__ x, const T* __restrict__ res,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta,
+                                                             const float* __restrict__ dscale, T* __restrict__ y,
+                                                             double* __restrict__ sums, float* __restrict__ mean,
+                                                             float* __restrict__ invstd, float* __restrict__ rmean,
+                                                             float* __restrict__ rvar, long M, int C, long rps,
+                                                             int act, float eps, float momentum) {
+  constexpr int V = VecT<T>::N, TPR = BS_SC / V, RS = BS_NT / TPR, NW = BS_NT / 64;
+  __shared__ double part[NW][2 * BS_SC];
+  __shared__ float coef[2][BS_SC];
+  const int lane = threadIdx.x % TPR, row = threadIdx.x / TPR, w = threadIdx.x >> 6;
+  const int c0 = blockIdx.x * BS_SC + lane * V;
+  double s[V], q[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) s[j] = q[j] = 0.0;
+  for (long m = row; m < M; m += 2 * RS) {
+    float v[2][V];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (m + u * RS < M) load_vec<T>(x + (m + u * RS) * C + c0, v[u]);
+      else
+#pragma unroll
+        for (int j = 0; j < V; ++j) v[u][j] = 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int j = 0; j < V; ++j) { s[j] += v[u][j]; q[j] += (double)v[u][j] * v[u][j]; }
+  }
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    s[j] = wave_fold_rows<TPR>(s[j]);
+    q[j] = wave_fold_rows<TPR>(q[j]);
+  }
+  if ((threadIdx.x & 63) < TPR)
+#pragma unroll
+    for (int j = 0; j < V; ++j) { part[w][lane * V + j] = s[j]; part[w][BS_SC + lane * V + j] = q[j]; }
+  __syncthreads();
+  if (threadIdx.x < BS_SC) {
+    const int c = blockIdx.x * BS_SC + threadIdx.x;
+    double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) { s1 += part[i][threadIdx.x]; s2 += part[i][BS_SC + threadIdx.x]; }
+    sums[c] = s1;
+    sums[C + c] = s2;
+    const double cnt = (double)M, mu = s1 / cnt;
+    double var = s2 / cnt - mu * mu;
+    if (var < 0) var = 0;
+    const float is = (float)(1.0 / sqrt(var + (double)eps));
+    mean[c] = (float)mu;
+    invstd[c] = is;
+    if (rmean) {
+      const double unb = cnt > 1 ? var * cnt / (cnt - 1) : var;
+      rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mu);
+      rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+    }
+    const float sc = gamma[c] * is;
+    coef[0][threadIdx.x] = sc;
+    coef[1][threadIdx.x] = beta[c] - (float)mu * sc;
+  }
+  __syncthreads();
+  float sc[V], sh[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) { sc[j] = coef[0][lane * V + j]; sh[j] = coef[1][lane * V + j]; }
+  for (long m0 = row; m0 < M; m0 += 2 * RS) {
+    float v[2][V], r[2][V], ds[2][V];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const long m = m0 + u * RS;
+      if (m < M) {
+        load_vec<T>(x + m * C + c0, v[u]);
+        if (res) load_vec<T>(res + m * C + c0, r[u]);
+        if (dscale) ld_coef<V>(dscale + (m / rps) * C + c0, ds[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const long m = m0 + u * RS;
+      if (m >= M) continue;
+      float o[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        o[j] = act_fwd(v[u][j] * sc[j] + sh[j] + (res ? r[u][j] : 0.f), act);
+        if (dscale) o[j] *= ds[u][j];
+      }
+      store_vec<T>(y + m * C + c0, o);
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(BS_NT) void bn_small_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ invstd,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta, const T* __restrict__ res,
+                                                             const float* __restrict__ dscale,
+                                                             float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                             T* __restrict__ dx, T* __restrict__ dres, long M, int C,
+                                                             long rps, int act, int accumulate) {
+  constexpr int V = VecT<T>::N, TPR = BS_SC / V, RS = BS_NT / TPR, NW = BS_NT / 64;
+  __shared__ double part[NW][2 * BS_SC];
+  __shared__ float coef[2][BS_SC];
+  const int lane = threadIdx.x % TPR, row = threadIdx.x / TPR, w = threadIdx.x >> 6;
+  const int c0 = blockIdx.x * BS_SC + lane * V;
+  float mu[V], is[V], sc[V], sh[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    mu[j] = mean[c0 + j];
+    is[j] = invstd[c0 + j];
+    sc[j] = gamma[c0 + j] * is[j];
+    sh[j] = beta[c0 + j] - mu[j] * sc[j];
+  }
+  double s[V], q[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) s[j] = q[j] = 0.0;
+  for (long m = row; m < M; m += RS) {
+    const long e = m * C + c0;
+    float xv[V], d[V], r[V], ds[V];
+    load_vec<T>(x + e, xv);
+    load_vec<T>(dy + e, d);
+    if (res) load_vec<T>(res + e, r);
+    if (dscale) ld_coef<V>(dscale + (m / rps) * C + c0, ds);
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      float g = d[j] * act_grad(xv[j] * sc[j] + sh[j] + (res ? r[j] : 0.f), act);
+      if (dscale) g *= ds[j];
+      s[j] += g;
+      q[j] += (double)g * ((xv[j] - mu[j]) * is[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    s[j] = wave_fold_rows<TPR>(s[j]);
+    q[j] = wave_fold_rows<TPR>(q[j]);
+  }
+  if ((threadIdx.x & 63) < TPR)
+#pragma unroll
+    for (int j = 0; j < V; ++j) { part[w][lane * V + j] = s[j]; part[w][BS_SC + lane * V + j] = q[j]; }
+  __syncthreads();
+  if (threadIdx.x < BS_SC) {
+    const int c = blockIdx.x * BS_SC + threadIdx.x;
+    double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) { s1 += part[i][threadIdx.x]; s2 += part[i][BS_SC + threadIdx.x]; }
+    const float gb = (float)s1, gg = (float)s2;
+    if (dbeta) dbeta[c] = accumulate ? dbeta[c] + gb : gb;
+    if (dgamma) dgamma[c] = accumulate ? dgamma[c] + gg : gg;
+    coef[0][threadIdx.x] = (float)(s1 / (double)M);
+    coef[1][threadIdx.x] = (float)(s2 / (double)M);
+  }
+  __syncthreads();
+  float mg[V], mx[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) { mg[j] = coef[0][lane * V + j]; mx[j] = coef[1][lane * V + j]; }
+  for (long m = row; m < M; m += RS) {
+    const long e = m * C + c0;
+    float xv[V], d[V], r[V], ds[V], o[V], gr[V];
+    load_vec<T>(x + e, xv);
+    load_vec<T>(dy + e, d);
+    if (res) load_vec<T>(res + e, r);
+    if (dscale) ld_coef<V>(dscale + (m / rps) * C + c0, ds);
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      float g = d[j] * act_grad(xv[j] * sc[j] + sh[j] + (res ? r[j] : 0.f), act);
+      if (dscale) g *= ds[j];
+      gr[j] = g;
+      o[j] = sc[j] * (g - mg[j] - (xv[j] - mu[j]) * is[j] * mx[j]);
+    }
+    store_vec<T>(dx + e, o);
+    if (dres) store_vec<T>(dres + e, gr);
+  }
+}
+
 unsigned ew_grid(long nvec) {
   const unsigned g = cdiv(nvec, 256);
   return g < 2048 ? (g ? g : 1) : 2048;
@@ -470,6 +665,35 @@ int cmx_bn_bwd_apply(const void* dy, const void* x, const float* mean, const flo
                        (T*)dx, (T*)dres, (long)M, C, (long)rows_per_sample, act, training);
   });
   return cmx_check_launch("bn_bwd_apply");
+}
+
+// the small-map forms (local statistics, training): C % 16 == 0, one launch each
+int cmx_bn_small_fwd(const void* x, const void* res, const float* gamma, const float* beta, const float* dscale,
+                     void* y, double* sums, float* mean, float* invstd, float* running_mean, float* running_var,
+                     int64_t M, int C, int64_t rows_per_sample, int act, float eps, float momentum, int dtype,
+                     hipStream_t s) {
+  CMX_REQUIRE(M > 0 && C % BS_SC == 0 && (!dscale || ((uintptr_t)dscale & 15) == 0), CMX_ERR_SHAPE,
+              "bn_small_fwd: C=%d (a multiple of %d)", C, BS_SC);
+  CMX_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL(bn_small_fwd_kernel<T>, dim3(C / BS_SC), dim3(BS_NT), 0, s, (const T*)x, (const T*)res, gamma,
+                       beta, dscale, (T*)y, sums, mean, invstd, running_mean, running_var, (long)M, C,
+                       (long)rows_per_sample, act, eps, momentum);
+  });
+  return cmx_check_launch("bn_small_fwd");
+}
+
+int cmx_bn_small_bwd(const void* dy, const void* x, const float* mean, const float* invstd, const float* gamma,
+                     const float* beta, const void* res, const float* dscale, float* dgamma, float* dbeta, void* dx,
+                     void* dres, int64_t M, int C, int64_t rows_per_sample, int act, int accumulate, int dtype,
+                     hipStream_t s) {
+  CMX_REQUIRE(M > 0 && C % BS_SC == 0 && (!dscale || ((uintptr_t)dscale & 15) == 0), CMX_ERR_SHAPE,
+              "bn_small_bwd: C=%d (a multiple of %d)", C, BS_SC);
+  CMX_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL(bn_small_bwd_kernel<T>, dim3(C / BS_SC), dim3(BS_NT), 0, s, (const T*)dy, (const T*)x, mean,
+                       invstd, gamma, beta, (const T*)res, dscale, dgamma, dbeta, (T*)dx, (T*)dres, (long)M, C,
+                       (long)rows_per_sample, act, accumulate);
+  });
+  return cmx_check_launch("bn_small_bwd");
 }
 
 }  // extern "C"

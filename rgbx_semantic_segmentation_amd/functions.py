@@ -1273,6 +1273,12 @@ def sync_bn_sums(sums: torch.Tensor, count: float, group) -> float:
     return count * dist.get_world_size(group)
 
 
+# local-statistics BatchNorms of at most this many rows (the stage-4 ChannelEmbed BNs: 600 rows at
+# B2 480 x 640) run forward and backward as one launch each (cmx_bn_small_fwd / _bwd) instead of
+# three; at 2400 rows (stage 3) the one-launch form is slower (batchnorm.hip); 0 = off
+BN_SMALL_M = int(os.environ.get("CMX_BN_SMALL_M", "600"))
+
+
 class BatchNormF(Function):
     @staticmethod
     def forward(ctx, x, res, prm, training, act, dscale, rps, group, anchor):
@@ -1282,6 +1288,18 @@ class BatchNormF(Function):
         mean = torch.empty(C, dtype=torch.float32, device=x.device)
         invstd = torch.empty(C, dtype=torch.float32, device=x.device)
         count = float(M)
+        small = training and group is None and M <= BN_SMALL_M and C % 16 == 0
+        if small:
+            sums = torch.empty(2, C, dtype=torch.float64, device=x.device)
+            y = torch.empty_like(x)
+            K.call("cmx_bn_small_fwd", K.ptr(x), K.ptr(res), K.ptr(gamma), K.ptr(beta), K.ptr(dscale), K.ptr(y),
+                   K.ptr(sums), K.ptr(mean), K.ptr(invstd), K.ptr(rm), K.ptr(rv), M, C, rps, K.ACT[act], eps, momentum,
+                   dt, K.stream())
+            ctx.save_for_backward(x, res if res is not None else x, mean, invstd)
+            ctx.meta = (prm, training, act, dscale, rps, group, count, res is not None)
+            ctx.small = True
+            return y
+        ctx.small = False
         if training:
             sums = torch.empty(2, C, dtype=torch.float64, device=x.device)
             ws = torch.empty(max(1, K.query("cmx_bn_workspace", M, C) // 8), dtype=torch.float64, device=x.device)
@@ -1312,6 +1330,13 @@ class BatchNormF(Function):
         M, C = x.shape
         dt = K.dtype_code(x)
         dy = _c(dy)
+        if ctx.small:
+            dx = torch.empty_like(x)
+            dres = torch.empty_like(x) if has_res else None
+            K.call("cmx_bn_small_bwd", K.ptr(dy), K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(gamma), K.ptr(beta),
+                   K.ptr(res), K.ptr(dscale), K.ptr(gg), K.ptr(bg), K.ptr(dx), K.ptr(dres), M, C, rps, K.ACT[act], 0,
+                   dt, K.stream())
+            return dx, dres, None, None, None, None, None, None, None
         sums = torch.empty(2, C, dtype=torch.float64, device=x.device)
         ws = torch.empty(max(1, K.query("cmx_bn_workspace", M, C) // 8), dtype=torch.float64, device=x.device)
         K.call("cmx_bn_bwd_reduce", K.ptr(dy), K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(gamma), K.ptr(beta),

@@ -76,6 +76,46 @@ def decoder():
             "adjoint3 (x + y)": timeit(adj3), "3 x adjoint_to (6 launches)": timeit(adj1)}
 
 
+def bnsmall():
+    """ChannelEmbed-sized BatchNorms (stage 3: 2400 x 320 ReLU, stage 4: 600 x 512 with residual):
+    the one-launch small-map forms against stats + fold + apply / reduce + fold + apply."""
+    out = {}
+    for M, C, act, use_res in ((2400, 320, 2, False), (600, 512, 0, True)):
+        x = torch.randn(M, C, device="cuda").to(torch.bfloat16)
+        dy = torch.randn(M, C, device="cuda").to(torch.bfloat16)
+        res = torch.randn(M, C, device="cuda").to(torch.bfloat16) if use_res else None
+        g, b = torch.ones(C, device="cuda"), torch.zeros(C, device="cuda")
+        rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+        mean, invstd = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+        sums = torch.empty(2, C, dtype=torch.float64, device="cuda")
+        ws = torch.empty(max(1, K.query("cmx_bn_workspace", M, C) // 8), dtype=torch.float64, device="cuda")
+        y, dx = torch.empty_like(x), torch.empty_like(x)
+        dres = torch.empty_like(x) if use_res else None
+        gg, gb = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+        rps = M // 2
+
+        def multi_f():
+            K.call("cmx_bn_stats_finalize", K.ptr(x), K.ptr(sums), K.ptr(ws), M, C, 1e-5, 0.1, K.ptr(rm), K.ptr(rv),
+                   K.ptr(mean), K.ptr(invstd), 1, K.stream())
+            K.call("cmx_bn_apply", K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(g), K.ptr(b), K.ptr(res), 0, K.ptr(y),
+                   M, C, rps, act, 1, K.stream())
+
+        def multi_b():
+            K.call("cmx_bn_bwd_reduce", K.ptr(dy), K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(g), K.ptr(b),
+                   K.ptr(res), 0, K.ptr(sums), K.ptr(gg), K.ptr(gb), K.ptr(ws), M, C, rps, act, 0, 1, K.stream())
+            K.call("cmx_bn_bwd_apply", K.ptr(dy), K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(g), K.ptr(b),
+                   K.ptr(res), 0, K.ptr(sums), float(M), K.ptr(dx), K.ptr(dres), M, C, rps, act, 1, 1, K.stream())
+        small_f = lambda: K.call("cmx_bn_small_fwd", K.ptr(x), K.ptr(res), K.ptr(g), K.ptr(b), 0, K.ptr(y), K.ptr(sums),
+                                 K.ptr(mean), K.ptr(invstd), K.ptr(rm), K.ptr(rv), M, C, rps, act, 1e-5, 0.1, 1,
+                                 K.stream())
+        small_b = lambda: K.call("cmx_bn_small_bwd", K.ptr(dy), K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(g),
+                                 K.ptr(b), K.ptr(res), 0, K.ptr(gg), K.ptr(gb), K.ptr(dx), K.ptr(dres), M, C, rps, act,
+                                 0, 1, K.stream())
+        for n, f in (("multi fwd", multi_f), ("small fwd", small_f), ("multi bwd", multi_b), ("small bwd", small_b)):
+            out[f"bn {M}x{C} {n}"] = timeit(f)
+    return out
+
+
 def bn():
     res = {}
     for M, C in [(38400, 512), (2400, 320), (600, 512), (38400, 64)]:

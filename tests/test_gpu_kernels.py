@@ -200,13 +200,18 @@ def test_upsample_ce(dev, dtype, B, h, w, K, mode):
     (1200, 320, 600, "relu", False, False, True),            # ChannelEmbed channel_embed.4 BN
     (333, 136, 333, "relu", True, True, True),               # ragged rows / channel count
     (4800, 128, 2400, "none", True, False, False),           # eval: running statistics
+    (600, 512, 300, "none", True, False, True),              # stage-4 ChannelEmbed norm (small-map path)
 ])
-def test_batchnorm(dev, dtype, M, C, rps, act, use_res, use_ds, training):
+@pytest.mark.parametrize("path", ["multi", "small"])
+def test_batchnorm(dev, dtype, M, C, rps, act, use_res, use_ds, training, path):
     """BatchNorm2d train / eval forward and backward through the C-ABI (cmx_bn_stats_finalize /
     cmx_bn_apply / cmx_bn_bwd_reduce / cmx_bn_bwd_apply; ChannelEmbed net_utils.py:319-329 and
     the decoder's linear_fuse BN + ReLU + Dropout2d, MLPDecoder.py:51-55) against fp64 torch
-    autograd on token-major (M, C) rows."""
+    autograd on token-major (M, C) rows.  path = small: the one-launch forms
+    (cmx_bn_small_fwd / cmx_bn_small_bwd: local statistics, training, C % 16 == 0)."""
     from rgbx_semantic_segmentation_amd import kernels as K
+    if path == "small" and not (training and C % 16 == 0):
+        pytest.skip("the small-map path takes training BNs with C % 16 == 0")
     torch.manual_seed(5)
     eps, mom = 1e-5, 0.1
     x = (torch.randn(M, C, device=dev) * 2 + 0.5).to(dtype)
@@ -222,25 +227,33 @@ def test_batchnorm(dev, dtype, M, C, rps, act, use_res, use_ds, training):
     sums = torch.empty(2, C, dtype=torch.float64, device=dev)
     ws = torch.empty(max(1, K.query("cmx_bn_workspace", M, C) // 8), dtype=torch.float64, device=dev)
     dt = K.dtype_code(x)
-    if training:
-        K.call("cmx_bn_stats_finalize", K.ptr(x), K.ptr(sums), K.ptr(ws), M, C, eps, mom, K.ptr(rm), K.ptr(rv),
-               K.ptr(mean), K.ptr(invstd), dt, K.stream())
-    else:
-        K.call("cmx_bn_finalize", 0, 1.0, eps, mom, K.ptr(rm), K.ptr(rv), K.ptr(mean), K.ptr(invstd), C, 0, K.stream())
     y = torch.empty_like(x)
-    K.call("cmx_bn_apply", K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(gamma), K.ptr(beta), K.ptr(res), K.ptr(ds),
-           K.ptr(y), M, C, rps, K.ACT[act], dt, K.stream())
     dy = torch.randn(M, C, device=dev).to(dtype)
     gg = torch.full((C,), float("nan"), device=dev)
     gb = torch.full((C,), float("nan"), device=dev)
-    K.call("cmx_bn_bwd_reduce", K.ptr(dy), K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(gamma), K.ptr(beta),
-           K.ptr(res), K.ptr(ds), K.ptr(sums), K.ptr(gg), K.ptr(gb), K.ptr(ws), M, C, rps, K.ACT[act], 0, dt,
-           K.stream())
     dx = torch.empty_like(x)
     dres = torch.empty_like(x) if use_res else None
-    K.call("cmx_bn_bwd_apply", K.ptr(dy), K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(gamma), K.ptr(beta),
-           K.ptr(res), K.ptr(ds), K.ptr(sums), float(M), K.ptr(dx), K.ptr(dres), M, C, rps, K.ACT[act],
-           int(training), dt, K.stream())
+    if path == "small":
+        K.call("cmx_bn_small_fwd", K.ptr(x), K.ptr(res), K.ptr(gamma), K.ptr(beta), K.ptr(ds), K.ptr(y), K.ptr(sums),
+               K.ptr(mean), K.ptr(invstd), K.ptr(rm), K.ptr(rv), M, C, rps, K.ACT[act], eps, mom, dt, K.stream())
+        K.call("cmx_bn_small_bwd", K.ptr(dy), K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(gamma), K.ptr(beta),
+               K.ptr(res), K.ptr(ds), K.ptr(gg), K.ptr(gb), K.ptr(dx), K.ptr(dres), M, C, rps, K.ACT[act], 0, dt,
+               K.stream())
+    else:
+        if training:
+            K.call("cmx_bn_stats_finalize", K.ptr(x), K.ptr(sums), K.ptr(ws), M, C, eps, mom, K.ptr(rm), K.ptr(rv),
+                   K.ptr(mean), K.ptr(invstd), dt, K.stream())
+        else:
+            K.call("cmx_bn_finalize", 0, 1.0, eps, mom, K.ptr(rm), K.ptr(rv), K.ptr(mean), K.ptr(invstd), C, 0,
+                   K.stream())
+        K.call("cmx_bn_apply", K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(gamma), K.ptr(beta), K.ptr(res),
+               K.ptr(ds), K.ptr(y), M, C, rps, K.ACT[act], dt, K.stream())
+        K.call("cmx_bn_bwd_reduce", K.ptr(dy), K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(gamma), K.ptr(beta),
+               K.ptr(res), K.ptr(ds), K.ptr(sums), K.ptr(gg), K.ptr(gb), K.ptr(ws), M, C, rps, K.ACT[act], 0, dt,
+               K.stream())
+        K.call("cmx_bn_bwd_apply", K.ptr(dy), K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(gamma), K.ptr(beta),
+               K.ptr(res), K.ptr(ds), K.ptr(sums), float(M), K.ptr(dx), K.ptr(dres), M, C, rps, K.ACT[act],
+               int(training), dt, K.stream())
     torch.cuda.synchronize()
     # fp64 reference
     xr = x.double().cpu().requires_grad_(True)
