@@ -103,7 +103,7 @@ FAMILY_RE = (
     ("frm", r"pool_|linear_fwd|linear_bwd|combine_|frm_|reduce_partials"),
     ("ffm", r"ffm_"),
     ("ce", r"ce_|upsample"),
-    ("bilinear", r"bilinear"),
+    ("bilinear", r"bilinear|adj3_|up3_"),
     ("im2col", r"im2col|col2im"),
     ("pe1", r"pe1_"),
 )

@@ -61,7 +61,7 @@ FAMILIES = [
     ("FRM (pool, channel MLP, combine)", r"pool_|linear_fwd|linear_bwd|combine_|frm_|reduce_partials"),
     ("FFM context / cross attention", r"ffm_"),
     ("upsample + CE", r"ce_|upsample"),
-    ("bilinear (decoder fuse adjoint)", r"bilinear"),
+    ("bilinear (decoder fuse adjoint)", r"bilinear|adj3_|up3_"),
     ("im2col / col2im", r"im2col|col2im"),
     ("stage-1 patch embed (direct conv fwd, wgrad)", r"pe1_"),
 ]

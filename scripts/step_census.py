@@ -78,7 +78,7 @@ FAMILIES = [
     ("FRM (CM-FRM)", r"^pool_|^linear_|^combine_|^ifrm"),
     ("FFM (cross attention contexts)", r"^ffm_"),
     ("CE loss + upsample", r"^ce_|^upsample_ce"),
-    ("bilinear / col2im / im2col / patch", r"^bilinear|^col2im|^im2col|^patch"),
+    ("bilinear / col2im / im2col / patch", r"^bilinear|^adj3_|^up3_|^col2im|^im2col|^patch"),
     ("optimizer (AdamW, non-finite check, step)", r"^adamw|^nonfinite|^step_"),
     ("elementwise / casts / partial sums", r"^act_|^residual|^scale_|^cast_|^reduce_partials|^partials|^colsum|^mul2"),
     ("torch / runtime", r"^at::|^__amd|^void at::"),
