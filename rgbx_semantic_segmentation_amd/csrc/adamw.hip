@@ -49,21 +49,46 @@ __device__ __forceinline__ void st4(float* a, float x, float y, float z, float w
 }
 
 // S = the weight shadow's 16-bit type (bf16 or f16, the compute dtype's GEMM operand)
-template <typename S, bool NT = false>
+// the step's scalars (bias corrections from the device step count, the decay factor, the unscale):
+// the same fp64 expressions for every lane of the launch
+struct AdamwScalars {
+  float step_size, bc2s, decf, gscale;
+  double t;
+};
+__device__ __forceinline__ AdamwScalars adamw_scalars(const float* lr_ptr, const float* step_ptr, double b1d,
+                                                      double b2d, double wd, float gscale, const float* loss_scale) {
+  AdamwScalars a;
+  const double lr = *lr_ptr;
+  a.t = (double)*step_ptr + 1.0;
+  a.step_size = (float)(lr / (1.0 - pow(b1d, a.t)));
+  a.bc2s = (float)sqrt(1.0 - pow(b2d, a.t));
+  a.decf = (float)(1.0 - lr * wd);
+  a.gscale = loss_scale ? gscale / *loss_scale : gscale;       // unscale
+  return a;
+}
+
+// BS: the scalars computed once per workgroup by lane 0 and shared through LDS (two fp64 pow,
+// a sqrt and divides per lane were each thread's prologue before its single float4 group)
+template <typename S, bool NT = false, bool BS = true>
 __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                              float* __restrict__ v, S* __restrict__ shadow, const uint8_t* __restrict__ decay64,
                              long n, const float* __restrict__ lr_ptr, float* __restrict__ step_ptr, double b1d,
-                             double b2d, float eps, double wd, float gscale, const float* __restrict__ loss_scale,
+                             double b2d, float eps, double wd, float gscale_in, const float* __restrict__ loss_scale,
                              const float* __restrict__ found_inf, int store_step, unsigned* __restrict__ tickets) {
   // GradScaler semantics (train.py:185-198): a step whose gradients held inf / nan is skipped
   if (found_inf && *found_inf != 0.f) return;
-  if (loss_scale) gscale /= *loss_scale;                       // unscale
-  const double lr = *lr_ptr;
-  const double t = (double)*step_ptr + 1.0;
-  const float step_size = (float)(lr / (1.0 - pow(b1d, t)));
-  const float bc2s = (float)sqrt(1.0 - pow(b2d, t));
+  AdamwScalars sc;
+  if constexpr (BS) {
+    __shared__ AdamwScalars ssc;
+    if (threadIdx.x == 0) ssc = adamw_scalars(lr_ptr, step_ptr, b1d, b2d, wd, gscale_in, loss_scale);
+    __syncthreads();
+    sc = ssc;
+  } else {
+    sc = adamw_scalars(lr_ptr, step_ptr, b1d, b2d, wd, gscale_in, loss_scale);
+  }
+  const float step_size = sc.step_size, bc2s = sc.bc2s, decf = sc.decf, gscale = sc.gscale;
+  const double t = sc.t;
   const float omb1 = (float)(1.0 - b1d), b2 = (float)b2d, omb2 = (float)(1.0 - b2d);
-  const float decf = (float)(1.0 - lr * wd);
   const long nv = n / 4;
   auto update = [&](const long e, float4 pp, const float4 gg, float4 mm, float4 vv, const uint8_t flag) {
     if (flag == 2) return;                             // 0: no decay, 1: decay, 2: frozen
@@ -204,10 +229,17 @@ static int adamw_launch(float* p, const float* g, float* m, float* v, void* shad
   CMX_REQUIRE(blocks <= (long)ADAMW_GRP * ADAMW_NGRP, CMX_ERR_SHAPE, "adamw: %ld blocks exceed the ticket groups", blocks);
   // nontemporal p / g / m / v traffic (CMX_ADAMW_NT=0: cached): 375 -> 348 us standalone
   static int& nt = cmx_knob("ADAMW_NT", 1);
-#define CMX_ADAMW(S_, NT_)                                                                                         \
-  hipLaunchKernelGGL((adamw_kernel<S_, NT_>), dim3((unsigned)blocks), dim3(256), 0, s, p, g, m, v, (S_*)shadow, \
-                     decay64, (long)n, lr_ptr, step_ptr, beta1, beta2, eps, weight_decay, grad_scale, loss_scale,    \
-                     found_inf, store_step, tickets)
+  // CMX_ADAMW_BS=0: every lane computes the step's scalars itself (A/B)
+  static int& bs = cmx_knob("ADAMW_BS", 1);
+#define CMX_ADAMW_(S_, NT_, BS_)                                                                                    \
+  hipLaunchKernelGGL((adamw_kernel<S_, NT_, BS_>), dim3((unsigned)blocks), dim3(256), 0, s, p, g, m, v,            \
+                     (S_*)shadow, decay64, (long)n, lr_ptr, step_ptr, beta1, beta2, eps, weight_decay, grad_scale,   \
+                     loss_scale, found_inf, store_step, tickets)
+#define CMX_ADAMW(S_, NT_)                     \
+  do {                                          \
+    if (bs) CMX_ADAMW_(S_, NT_, true);          \
+    else CMX_ADAMW_(S_, NT_, false);            \
+  } while (0)
   if (shadow_dtype == 2) {
     if (nt) CMX_ADAMW(f16, true);
     else CMX_ADAMW(f16, false);
@@ -216,6 +248,7 @@ static int adamw_launch(float* p, const float* g, float* m, float* v, void* shad
     else CMX_ADAMW(bf16, false);
   }
 #undef CMX_ADAMW
+#undef CMX_ADAMW_
   return cmx_check_launch("adamw_step");
 }
 

@@ -1,5 +1,6 @@
 """Time the fused AdamW launch (cmx_adamw_step) on a B2-sized flat buffer (66.58 M fp32
-parameters + bf16 shadow) for several CMX_ADAMW_BLOCKS grid caps, interleaved in one process
+parameters + bf16 shadow) for several CMX_ADAMW_BLOCKS grid caps and the per-workgroup / per-lane
+step scalars (CMX_ADAMW_BS), interleaved in one process
 (cmx_tune), HIP events around 20 launches each.  Prints us per launch and TB/s of the 30 B /
 parameter algorithmic traffic."""
 import os
@@ -28,8 +29,9 @@ def run():
 
 
 for rep in range(2):
-    for cap in (2048, 16384, 0):
+    for cap, bs in ((32768, 1), (16384, 1), (0, 1), (0, 0)):
         K.tune("ADAMW_BLOCKS", cap)
+        K.tune("ADAMW_BS", bs)
         for _ in range(3):
             run()
         torch.cuda.synchronize()
@@ -40,4 +42,4 @@ for rep in range(2):
         e.record()
         torch.cuda.synchronize()
         us = s.elapsed_time(e) / 20 * 1e3
-        print(f"rep {rep} ADAMW_BLOCKS={cap:6d}: {us:7.1f} us  {30.0 * n / us / 1e6:5.2f} TB/s")
+        print(f"rep {rep} ADAMW_BLOCKS={cap:6d} ADAMW_BS={bs}: {us:7.1f} us  {30.0 * n / us / 1e6:5.2f} TB/s")
