@@ -34,8 +34,9 @@ int bn_tpr(int chunks) {
 // M = 600 .. 2400 rows) then spread over 38 .. 150 row blocks instead of 5 .. 19 whose few
 // lanes walked all rows serially (bn_bwd_reduce 600 x 512: 21 -> 12 us, 2400 x 320: 22 -> 13).
 int bn_nblk(long M) {
+  static int& cap = cmx_knob("BN_NBLK", 256);      // row blocks at most (A/B knob)
   long nb = (M + 15) / 16;
-  return (int)(nb < 256 ? (nb > 0 ? nb : 1) : 256);
+  return (int)(nb < cap ? (nb > 0 ? nb : 1) : cap);
 }
 
 constexpr int UNR = 4;            // rows per lane with loads in flight together

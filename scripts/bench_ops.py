@@ -125,13 +125,19 @@ def bn():
         invstd = torch.ones(C, device="cuda")
         gamma = torch.ones(C, device="cuda")
         beta = torch.zeros(C, device="cuda")
-        ws = torch.empty(max(1, K.query("cmx_bn_workspace", M, C) // 8), dtype=torch.float64, device="cuda")
         sums = torch.empty(2, C, dtype=torch.float64, device="cuda")
         dg = torch.empty(C, device="cuda")
         db = torch.empty(C, device="cuda")
-        f = lambda: K.call("cmx_bn_bwd_reduce", K.ptr(dy), K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(gamma),
-                           K.ptr(beta), 0, 0, K.ptr(sums), K.ptr(dg), K.ptr(db), K.ptr(ws), M, C, 1, 0, 0, 1, K.stream())
-        res[f"bn_bwd_reduce {M}x{C}"] = timeit(f)
+        for cap in (256, 512, 1024):
+            K.tune("BN_NBLK", cap)
+            ws = torch.empty(max(1, K.query("cmx_bn_workspace", M, C) // 8), dtype=torch.float64, device="cuda")
+            f = lambda: K.call("cmx_bn_bwd_reduce", K.ptr(dy), K.ptr(x), K.ptr(mean), K.ptr(invstd), K.ptr(gamma),
+                               K.ptr(beta), 0, 0, K.ptr(sums), K.ptr(dg), K.ptr(db), K.ptr(ws), M, C, 1, 0, 0, 1,
+                               K.stream())
+            fs = lambda: K.call("cmx_bn_stats", K.ptr(x), K.ptr(sums), K.ptr(ws), M, C, 1, K.stream())
+            res[f"bn_bwd_reduce {M}x{C} nblk<={cap}"] = timeit(f)
+            res[f"bn_stats {M}x{C} nblk<={cap}"] = timeit(fs)
+        K.tune("BN_NBLK", 256)
     return res
 
 
