@@ -61,11 +61,7 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, 
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
         const long mu = m + u * stride;
-        if (mu < M) load_vec<T>(x + mu * C + ch * V, v[u]);
-        else {
-#pragma unroll
-          for (int j = 0; j < V; ++j) v[u][j] = 0.f;
-        }
+        load_vec_if<T>(x, mu * C + ch * V, ch * V, mu < M, v[u]);   // (all UNR loads in flight)
       }
 #pragma unroll
       for (int u = 0; u < UNR; ++u)
@@ -201,19 +197,25 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x, 
   extern __shared__ float sp[];
   float* ssc = sp;
   float* ssh = sp + C;
+  const int nvec = (int)(M * C / V), stride = gridDim.x * blockDim.x;
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  // the first vector's loads go out before the coefficient prologue and its barrier (they
+  // were a second memory round trip after it), each later one before the previous store
+  using Raw = typename VecT<T>::raw;
+  const T* rp = res ? res : x;                                   // (an absent residual: unused)
+  Raw xr = load_raw<T>(x + (i < nvec ? (long)i * V : 0)), rr = load_raw<T>(rp + (i < nvec ? (long)i * V : 0));
   for (int c = threadIdx.x; c < C; c += 256) {
     const float sc = gamma[c] * invstd[c];
     ssc[c] = sc;
     ssh[c] = beta[c] - mean[c] * sc;
   }
   __syncthreads();
-  const long nvec = M * C / V;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)nvec; i += gridDim.x * blockDim.x) {
+  for (; i < nvec; i += stride) {
     const int e = i * V;
     const int c0 = e % C;
-    float v[V], sc[V], sh[V], r[V], ds[V];
-    load_vec<T>(x + e, v);
-    if (res) load_vec<T>(res + e, r);
+    float v[V], r[V], sc[V], sh[V], ds[V];
+    unpack_raw<T>(xr, v);
+    unpack_raw<T>(rr, r);
     ld_coef<V>(ssc + c0, sc);
     ld_coef<V>(ssh + c0, sh);
     if (dscale) ld_coef<V>(dscale + (long)((e / C) / (int)rps) * C + c0, ds);
@@ -223,6 +225,9 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x, 
       o[j] = act_fwd(v[j] * sc[j] + sh[j] + (res ? r[j] : 0.f), act);
       if (dscale) o[j] *= ds[j];
     }
+    const long nx = i + stride < nvec ? (long)(i + stride) * V : 0;
+    xr = load_raw<T>(x + nx);
+    rr = load_raw<T>(rp + nx);
     store_vec<T>(y + e, o);
   }
 }
@@ -263,15 +268,17 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
 #pragma unroll
       for (int u = 0; u < UNRB; ++u) {
         const long mu_ = m + u * stride;
-        if (mu_ < M) {
-          const long e = mu_ * C + c0;
-          load_vec<T>(x + e, xv[u]);
-          load_vec<T>(dy + e, d[u]);
-          if (res) load_vec<T>(res + e, r[u]);
-          if (dscale) ld_coef<V>(dscale + (mu_ / rps) * C + c0, ds[u]);
-        } else {
+        const bool ok = mu_ < M;
+        const long e = mu_ * C + c0;
+        // unconditional loads of clamped rows (all UNRB rows' operands in flight together); an
+        // absent residual re-reads dy (from cache) and is not used
+        load_vec_if<T>(x, e, c0, ok, xv[u]);
+        load_vec_if<T>(dy, e, c0, ok, d[u]);
+        load_vec_if<T>(res ? res : dy, e, c0, ok, r[u]);
+        if (dscale) ld_coef<V>(dscale + ((ok ? mu_ : 0) / rps) * C + c0, ds[u]);
+        else {
 #pragma unroll
-          for (int j = 0; j < V; ++j) { xv[u][j] = 0.f; d[u][j] = 0.f; r[u][j] = 0.f; ds[u][j] = 0.f; }
+          for (int j = 0; j < V; ++j) ds[u][j] = 0.f;
         }
       }
 #pragma unroll
@@ -310,6 +317,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
   constexpr int V = VecT<T>::N;
   extern __shared__ float sp[];
   float *smu = sp, *sis = sp + C, *ssc = sp + 2 * C, *ssh = sp + 3 * C, *smg = sp + 4 * C, *smx = sp + 5 * C;
+  const int nvec = (int)(M * C / V), stride = gridDim.x * blockDim.x;
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  // the first vector's loads before the coefficient prologue (as bn_apply_kernel)
+  using Raw = typename VecT<T>::raw;
+  const T* rp = res ? res : dy;                                  // (an absent residual: unused)
+  const long f0 = i < nvec ? (long)i * V : 0;
+  Raw xr = load_raw<T>(x + f0), dr = load_raw<T>(dy + f0), rr = load_raw<T>(rp + f0);
   for (int c = threadIdx.x; c < C; c += 256) {
     const float is = invstd[c], sc = gamma[c] * is;
     smu[c] = mean[c];
@@ -320,14 +334,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
     smx[c] = training ? (float)(sums[C + c] * rcount) : 0.f;
   }
   __syncthreads();
-  const long nvec = M * C / V;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)nvec; i += gridDim.x * blockDim.x) {
+  for (; i < nvec; i += stride) {
     const int e = i * V;
     const int c0 = e % C;
     float xv[V], d[V], r[V], ds[V], mu[V], is[V], sc[V], sh[V], mg[V], mx[V];
-    load_vec<T>(x + e, xv);
-    load_vec<T>(dy + e, d);
-    if (res) load_vec<T>(res + e, r);
+    unpack_raw<T>(xr, xv);
+    unpack_raw<T>(dr, d);
+    unpack_raw<T>(rr, r);
     if (dscale) ld_coef<V>(dscale + (long)((e / C) / (int)rps) * C + c0, ds);
     ld_coef<V>(smu + c0, mu);
     ld_coef<V>(sis + c0, is);
@@ -344,6 +357,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
       gr[j] = g;
       o[j] = sc[j] * (g - mg[j] - (xv[j] - mu[j]) * is[j] * mx[j]);
     }
+    const long nx = i + stride < nvec ? (long)(i + stride) * V : 0;
+    xr = load_raw<T>(x + nx);
+    dr = load_raw<T>(dy + nx);
+    rr = load_raw<T>(rp + nx);
     store_vec<T>(dx + e, o);
     if (dres) store_vec<T>(dres + e, gr);
   }

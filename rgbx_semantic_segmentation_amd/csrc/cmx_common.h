@@ -95,13 +95,18 @@ template <> struct VecT<float> { static constexpr int N = 4; typedef float4 raw;
 template <> struct VecT<bf16> { static constexpr int N = 8; typedef uint4 raw; };
 template <> struct VecT<f16> { static constexpr int N = 8; typedef uint4 raw; };
 
+// one 16-B vector as loaded (raw) and its fp32 values: a raw load can be issued well before
+// its values are wanted (across a barrier or a prologue loop, which the compiler does not move
+// the unpacking past, so a load_vec there waits for its data on the spot)
 template <typename T>
-__device__ __forceinline__ void load_vec(const T* p, float* out) {
+__device__ __forceinline__ typename VecT<T>::raw load_raw(const T* p) {
+  return *reinterpret_cast<const typename VecT<T>::raw*>(p);
+}
+template <typename T>
+__device__ __forceinline__ void unpack_raw(const typename VecT<T>::raw& v, float* out) {
   if constexpr (sizeof(T) == 4) {
-    float4 v = *reinterpret_cast<const float4*>(p);
     out[0] = v.x; out[1] = v.y; out[2] = v.z; out[3] = v.w;
   } else {
-    uint4 v = *reinterpret_cast<const uint4*>(p);
     uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -110,6 +115,22 @@ __device__ __forceinline__ void load_vec(const T* p, float* out) {
       out[2 * i + 1] = f.y;
     }
   }
+}
+template <typename T>
+__device__ __forceinline__ void load_vec(const T* p, float* out) {
+  unpack_raw<T>(load_raw<T>(p), out);
+}
+
+// load_vec of p[off] when ok, zeros otherwise -- as an UNCONDITIONAL load of a clamped offset
+// (`safe`: any in-bounds one) and a select.  A load inside `if (ok) ... else zero` makes the
+// compiler wait for it at the branch's join, so loads meant to be in flight together (several
+// rows per lane) became one round trip each.
+template <typename T>
+__device__ __forceinline__ void load_vec_if(const T* p, long off, long safe, bool ok, float* out) {
+  constexpr int N = VecT<T>::N;
+  load_vec<T>(p + (ok ? off : safe), out);
+#pragma unroll
+  for (int j = 0; j < N; ++j) out[j] = ok ? out[j] : 0.f;
 }
 
 template <typename T>
@@ -162,22 +183,63 @@ __device__ __forceinline__ bool last_arrival(unsigned* ticket, unsigned total) {
   return s_last != 0;
 }
 
+// ---------------------------------------------------------------- cross-lane exchange
+// v of lane (lane ^ O), O a power of two < 64, on the VALU instead of the LDS crossbar
+// (__shfl_xor is a ds_bpermute: an address, an LDS-pipe round trip and an lgkmcnt wait per
+// step): DPP quad permutes for O = 1, 2, DPP row rotates for O = 4, 8 (a 16-lane row rotated by
+// 8 is lane ^ 8; by 4 / 12 selected on lane bit 2 is lane ^ 4), gfx950's v_permlane16_swap /
+// v_permlane32_swap for O = 16, 32 (the swap hands each half its partner row / half, one select
+// per lane).  Exact xor semantics: reductions built on it add in the same order as the
+// __shfl_xor butterflies they replace and give the same bits.  Every lane of the group must be
+// active (all callers reduce in uniform control flow or over whole row groups).
+template <int O>
+__device__ __forceinline__ float xor_lane(float v) {
+  const int x = __builtin_bit_cast(int, v);
+  if constexpr (O == 1) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(x, x, 0xB1, 0xF, 0xF, false));   // quad_perm 1,0,3,2
+  } else if constexpr (O == 2) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(x, x, 0x4E, 0xF, 0xF, false));   // quad_perm 2,3,0,1
+  } else if constexpr (O == 4) {
+    const int a = __builtin_amdgcn_update_dpp(x, x, 0x124, 0xF, 0xF, false);                      // row_ror 4
+    const int b = __builtin_amdgcn_update_dpp(x, x, 0x12C, 0xF, 0xF, false);                      // row_ror 12
+    return __builtin_bit_cast(float, (__lane_id() & 4) ? a : b);
+  } else if constexpr (O == 8) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(x, x, 0x128, 0xF, 0xF, false));  // row_ror 8
+  } else if constexpr (O == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)x, (unsigned)x, false, false);
+    return __builtin_bit_cast(float, (__lane_id() & 16) ? r[0] : r[1]);
+  } else {
+    static_assert(O == 32, "xor_lane: O in 1 .. 32");
+    const auto r = __builtin_amdgcn_permlane32_swap((unsigned)x, (unsigned)x, false, false);
+    return __builtin_bit_cast(float, (__lane_id() & 32) ? r[0] : r[1]);
+  }
+}
+// the same for an offset known only after inlining (folds to one case when it is a constant)
+__device__ __forceinline__ float xor_lane(float v, int o) {
+  switch (o) {
+    case 1: return xor_lane<1>(v);
+    case 2: return xor_lane<2>(v);
+    case 4: return xor_lane<4>(v);
+    case 8: return xor_lane<8>(v);
+    case 16: return xor_lane<16>(v);
+    case 32: return xor_lane<32>(v);
+    default: return __shfl_xor(v, o, 64);
+  }
+}
+
 // ---------------------------------------------------------------- reductions
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-// sum across a power-of-two group of `width` lanes (width <= 64)
+// sum across a power-of-two group of `width` lanes (width <= 64): the butterfly from the widest
+// offset down, as the __shfl_xor loop this replaced (same bits)
 __device__ __forceinline__ float group_sum(float v, int width) {
-  for (int o = width >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if (width > 32) v += xor_lane<32>(v);
+  if (width > 16) v += xor_lane<16>(v);
+  if (width > 8) v += xor_lane<8>(v);
+  if (width > 4) v += xor_lane<4>(v);
+  if (width > 2) v += xor_lane<2>(v);
+  if (width > 1) v += xor_lane<1>(v);
   return v;
 }
+__device__ __forceinline__ float wave_sum(float v) { return group_sum(v, 64); }
 
 // Branch-free fp32 erf: x * P(x^2) / Q(x^2) on x clamped to [-4, 4] (the rational minimax
 // form used by Eigen's fast float erf); max |error| 4.2e-7 against libm erf on [-6, 6]

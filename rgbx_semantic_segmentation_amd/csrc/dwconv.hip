@@ -482,7 +482,7 @@ __device__ __forceinline__ void rs_step(const float (&v)[N], float (&o)[N / 2], 
   for (int k = 0; k < N / 2; ++k) {
     const float send = up ? v[k] : v[k + N / 2];
     const float keep = up ? v[k + N / 2] : v[k];
-    o[k] = keep + __shfl_xor(send, off, 64);
+    o[k] = keep + xor_lane(send, off);
   }
 }
 
@@ -748,7 +748,7 @@ __global__ __launch_bounds__(256, 2) void dw2_bwd_kernel(const T* __restrict__ d
   rs_step<10>(r10, r5, s_off, (lane & s_off) != 0); seg = seg * 2 + ((lane & s_off) != 0); s_off >>= 1;
   for (; s_off > 0; s_off >>= 1) {
 #pragma unroll
-    for (int k = 0; k < 5; ++k) r5[k] += __shfl_xor(r5[k], s_off, 64);
+    for (int k = 0; k < 5; ++k) r5[k] += xor_lane(r5[k], s_off);
   }
   if ((lane & (TPC / 16 - 1)) == 0) {              // one lane per 5-value segment
     float* o = part + ((long)t.g * nsp + t.sp) * C * 10 + (long)c0 * 10 + seg * 5;

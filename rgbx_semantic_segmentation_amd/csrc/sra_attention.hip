@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256) void sra_fwd_kernel(const T* __restrict__ q, c
       sacc[i] = x;
       mt = fmaxf(mt, x);
     }
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    mt = fmaxf(mt, xor_lane<32>(mt));
     const float mn = fmaxf(m, mt);
     const float alpha = exp2f(m - mn);
     float rs = 0.f;
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) void sra_fwd_kernel(const T* __restrict__ q, c
       sacc[i] = p;
       rs += p;
     }
-    rs += __shfl_xor(rs, 32, 64);
+    rs += xor_lane<32>(rs);
     l = l * alpha + rs;
     m = mn;
 #pragma unroll
@@ -242,7 +242,7 @@ __global__ __launch_bounds__(256) void sra_bwd_dq_kernel(
       df[s] = zfrag<T>();
     }
   }
-  dot += __shfl_xor(dot, 32, 64);
+  dot += xor_lane<32>(dot);
   const long sidx = ((long)b * heads + head) * N + qi;
   const float Dq = dot;
   const float lse2 = live ? lse[sidx] * 1.4426950408889634f : 0.f;

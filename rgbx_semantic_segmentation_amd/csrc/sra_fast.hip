@@ -199,7 +199,7 @@ __global__ __launch_bounds__(64 * NW) void sra_fwd_fast(const E* __restrict__ q,
 #pragma unroll
         for (int i = 0; i < 16; ++i) mt = fmaxf(mt, sa[u][ks][i]);
       // max on the raw scores (the scale is positive), exponent as one packed FMA per 2 scores
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
+      mt = fmaxf(mt, xor_lane<32>(mt)) * sl2;
       const float mn = fmaxf(m[u], mt);
       const float alpha = fexp2(m[u] - mn);
       const f2 sl2v = {sl2, sl2}, nmn = {-mn, -mn};
@@ -216,7 +216,7 @@ __global__ __launch_bounds__(64 * NW) void sra_fwd_fast(const E* __restrict__ q,
           rs2 += p;
         }
       float rs = rs2.x + rs2.y;
-      rs += __shfl_xor(rs, 32, 64);
+      rs += xor_lane<32>(rs);
       l[u] = l[u] * alpha + rs;
       // rescale the accumulator only when some lane's running max moved: alpha == 1 exactly
       // otherwise, and after the first key tiles the max rarely moves
@@ -301,7 +301,7 @@ __global__ __launch_bounds__(64 * NW) void sra_dq_fast(const E* __restrict__ q, 
         qf[u][s] = df[u][s] = zfrag<E>();
       }
     }
-    dot += __shfl_xor(dot, 32, 64);
+    dot += xor_lane<32>(dot);
     Dq[u] = dot;
     const long sidx = ((long)b * heads + head) * N + qi;
     lse2[u] = live ? lse[sidx] * 1.4426950408889634f : 0.f;
@@ -662,7 +662,7 @@ __global__ __launch_bounds__(64 * SKT) void sra_fwd_small(const E* __restrict__ 
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < 16; ++i) mt = fmaxf(mt, sa[u][ks][i]);
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
+    mt = fmaxf(mt, xor_lane<32>(mt)) * sl2;
     const f2 sl2v = {sl2, sl2}, nmt = {-mt, -mt};
     f2 rs2 = {0.f, 0.f};
 #pragma unroll
@@ -677,7 +677,7 @@ __global__ __launch_bounds__(64 * SKT) void sra_fwd_small(const E* __restrict__ 
       }
     const float rs = rs2.x + rs2.y;
     m[u] = mt;
-    l[u] = rs + __shfl_xor(rs, 32, 64);
+    l[u] = rs + xor_lane<32>(rs);
   }
   // this wave's (max, sum) per query into its K image (K is no longer read)
   float* st = reinterpret_cast<float*>(Ki);
@@ -773,7 +773,7 @@ __global__ __launch_bounds__(64 * SKT) void sra_dq_small(const E* __restrict__ q
         qf[u][s] = df[u][s] = zfrag<E>();
       }
     }
-    dot += __shfl_xor(dot, 32, 64);
+    dot += xor_lane<32>(dot);
     Dq[u] = dot;
     const long sidx = ((long)b * heads + head) * N + qi;
     lse2[u] = live ? lse[sidx] * 1.4426950408889634f : 0.f;
@@ -889,7 +889,7 @@ __global__ __launch_bounds__(64 * SKT, 2) void sra_dq_small_seq(const E* __restr
         qf[s_] = df[s_] = zfrag<E>();
       }
     }
-    dot += __shfl_xor(dot, 32, 64);
+    dot += xor_lane<32>(dot);
     const float Dq = dot;
     const long sidx = ((long)b * heads + head) * N + qi;
     const float lse2 = live ? lse[sidx] * 1.4426950408889634f : 0.f;
