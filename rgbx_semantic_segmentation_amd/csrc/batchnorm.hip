@@ -57,11 +57,20 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, 
   if (live) {
     const long stride = (long)gridDim.x * RS;
     for (long m = (long)blockIdx.x * RS + slot; m < M; m += UNR * stride) {
-      float v[UNR][V];
+      // the UNR rows as raw vectors first, unpacked after (all UNR loads in flight: a load_vec per
+      // row, and before that a load inside `if (mu < M)`, was one round trip per row)
+      typename VecT<T>::raw raw[UNR];
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
         const long mu = m + u * stride;
-        load_vec_if<T>(x, mu * C + ch * V, ch * V, mu < M, v[u]);   // (all UNR loads in flight)
+        raw[u] = load_raw<T>(x + (mu < M ? mu * C : 0) + ch * V);
+      }
+      float v[UNR][V];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        unpack_raw<T>(raw[u], v[u]);
+#pragma unroll
+        for (int j = 0; j < V; ++j) v[u][j] = m + u * stride < M ? v[u][j] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < UNR; ++u)
