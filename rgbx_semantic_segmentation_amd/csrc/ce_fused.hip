@@ -161,23 +161,34 @@ __global__ __launch_bounds__(CT_NT) void ce_cells(const T* __restrict__ logits, 
   const bool act = ri < CT_R;
   const int Y = 4 * y0 - 2 + ri, X0 = 4 * (x0 + c) - 2;
   const bool rowin = act && Y >= 0 && Y < H;
-  // global loads first: the run's labels, the thread's share of the logits tile
+  // global loads first: the run's labels, the thread's share of the logits tile -- all of them
+  // unconditional (an out-of-range element reads the tile's first one and is replaced by a
+  // select), so they are in flight together: a load under `cond ? load : 0` was sunk into its
+  // branch and waited for there, 4 + NL round trips one after another
   long lab[4];
+  bool labok[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int X = X0 + j;
-    lab[j] = (rowin && X >= 0 && X < W) ? label[((long)b * H + Y) * W + X] : -1L;
+    labok[j] = rowin && X >= 0 && X < W;
+    lab[j] = label[labok[j] ? ((long)b * H + Y) * W + X : (long)b * H * W];
   }
   const T* base = logits + (long)b * h * w * K;
   constexpr int NL = (LP * KF + CT_NT - 1) / CT_NT;
   float v[NL];
+  bool vok[NL];
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
     const int e = t + i * CT_NT;
     const int k = e % K, px = e / K;                // coalesced along k
     const int yy = y0 - 1 + px / LW, xx = x0 - 1 + px % LW;
-    v[i] = (e < LP * K && yy >= 0 && yy < h && xx >= 0 && xx < w) ? to_f32(base[((long)yy * w + xx) * K + k]) : 0.f;
+    vok[i] = e < LP * K && yy >= 0 && yy < h && xx >= 0 && xx < w;
+    v[i] = to_f32(base[vok[i] ? ((long)yy * w + xx) * K + k : 0]);
   }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) lab[j] = labok[j] ? lab[j] : -1L;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) v[i] = vok[i] ? v[i] : 0.f;
   if (t < CT_Y * 8) {                             // low-res row y0 + yl from footprint row 4 yl + jj
     const int yl = t >> 3, r = 4 * yl + (t & 7);
     int ya, yb;
