@@ -301,10 +301,19 @@ __global__ __launch_bounds__(256) void combine_fwd_kernel(const T* __restrict__ 
   for (int k = 0; k < MAXCH; ++k)
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      const int c = (lane + k * TPR) * V + j;
+      // unconditional loads (a lane past the row reads chunk 0), zeroed by a select after: under
+      // `ok ? w2[c] : 0` each was sunk into its branch and waited for, 2 V MAXCH round trips
+      const int c = (lane + k * TPR < nch ? lane + k * TPR : 0) * V + j;
+      wa[k][j] = w2[c];
+      wb[k][j] = w2[C + c];
+    }
+#pragma unroll
+  for (int k = 0; k < MAXCH; ++k)
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
       const bool ok = lane + k * TPR < nch;
-      wa[k][j] = ok ? w2[c] : 0.f;
-      wb[k][j] = ok ? w2[C + c] : 0.f;
+      wa[k][j] = ok ? wa[k][j] : 0.f;
+      wb[k][j] = ok ? wb[k][j] : 0.f;
     }
   for (long row = (long)blockIdx.x * RPB + slot; row < rows; row += (long)gridDim.x * RPB) {
     const int b = (int)(row / N);
@@ -380,12 +389,23 @@ __global__ __launch_bounds__(256) void combine_bwd_kernel(const T* __restrict__ 
   for (int k = 0; k < MCH; ++k)
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      const int c = (lane + k * TPR) * V + j;
+      // unconditional loads (a lane past the row reads chunk 0), zeroed by a select after (as
+      // combine_fwd_kernel: conditional loads were one round trip each)
+      const int c = (lane + k * TPR < nch ? lane + k * TPR : 0) * V + j;
+      c0h[k][j] = cw[(long)b * 2 * C + c];
+      c1h[k][j] = cw[(long)b * 2 * C + C + c];
+      wa[k][j] = w2[c];
+      wb[k][j] = w2[C + c];
+    }
+#pragma unroll
+  for (int k = 0; k < MCH; ++k)
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
       const bool ok = lane + k * TPR < nch;
-      c0h[k][j] = ok ? 0.5f * cw[(long)b * 2 * C + c] : 0.f;
-      c1h[k][j] = ok ? 0.5f * cw[(long)b * 2 * C + C + c] : 0.f;
-      wa[k][j] = ok ? w2[c] : 0.f;
-      wb[k][j] = ok ? w2[C + c] : 0.f;
+      c0h[k][j] = ok ? 0.5f * c0h[k][j] : 0.f;
+      c1h[k][j] = ok ? 0.5f * c1h[k][j] : 0.f;
+      wa[k][j] = ok ? wa[k][j] : 0.f;
+      wb[k][j] = ok ? wb[k][j] : 0.f;
     }
   for (int n = blockIdx.x * RPB + slot; n < N; n += nblk * RPB) {
     const long row = (long)b * N + n;
