@@ -519,7 +519,9 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const float* __restrict__
     const float* p = part + b * sm + k;
     float v[PB_SL];
 #pragma unroll
-    for (int q = 0; q < PB_SL; ++q) v[q] = q < nsl ? p[q * ss] : 0.f;
+    for (int q = 0; q < PB_SL; ++q) v[q] = p[(q < nsl ? q : 0) * ss];     // (unconditional: in flight together)
+#pragma unroll
+    for (int q = 0; q < PB_SL; ++q) v[q] = q < nsl ? v[q] : 0.f;
     float t = 0.f;
 #pragma unroll
     for (int q = 0; q < PB_SL; ++q) t += v[q];
@@ -536,8 +538,12 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const float* __restrict__
       const bool ok = lane + k * TPR < nch;
       dav[k][j] = ok ? sdp[c] : 0.f;
       dmx[k][j] = ok ? sdp[C + c] : 0.f;
-      am[k][j] = ok ? argmax[(long)b * 2 * C + g * C + c] : -1;
+      am[k][j] = argmax[(long)b * 2 * C + g * C + (ok ? c : 0)];        // (unconditional, selected below)
     }
+#pragma unroll
+  for (int k = 0; k < MAXCH; ++k)
+#pragma unroll
+    for (int j = 0; j < V; ++j) am[k][j] = lane + k * TPR < nch ? am[k][j] : -1;
   T* base = dx + (long)gb * N * C;
   for (int n = blockIdx.x * RPB + slot; n < N; n += gridDim.x * RPB) {
 #pragma unroll
